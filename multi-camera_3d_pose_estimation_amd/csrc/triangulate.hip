@@ -1,0 +1,332 @@
+// Batched multi-view triangulation for gfx950 — one (frame, joint) problem per lane.
+//
+// Replaces the reference's T*J Python-level calls of utils.triangulate_points
+// (pose_estimation.py:27-53 -> utils.py:1277-1336), whose numerics live in
+// OpenCV 4.9 (cv.undistortPoints, cv.triangulatePoints,
+// cv.convertPointsFromHomogeneous).  Per lane, in fp64 with no FMA contraction
+// so the rounding sequence is OpenCV's:
+//   1. undistort each view's (x, y) with its own K/dist: 5 fixed iterations,
+//      icdist<0 fallback, RR = K, rounded to f32 (cvUndistortPointsInternal);
+//   2. A (2V x 4): rows x·P[2]-P[0], y·P[2]-P[1] per view (icvTriangulatePoints);
+//   3. one-sided Hestenes Jacobi SVD on the rows of Aᵀ, eps = 10·DBL_EPSILON,
+//      descending selection sort, null vector = Vt row 3 (JacobiSVDImpl_);
+//   4. f32 homogeneous divide: s = w != 0 ? 1.f/w : 1.f (convertPointsFromHomogeneous).
+// The reference's camera selection (top-2 by confidence, ascending; parameters
+// keyed by selection position; pose_estimation.py:32-45) is reproduced in
+// MVP_TRI_REFERENCE mode.
+//
+// Roofline: HBM-bound by design at 12·(V+1) B per point (read x,y,conf per view,
+// write xyz) but FP64-issue-heavy (Jacobi ≈ 2-3 kFLOP/point); see DESIGN.md.
+#pragma clang fp contract(off)
+
+#include "mvp_common.h"
+
+#include <cfloat>
+
+namespace {
+
+constexpr int kMaxCams = 8;
+constexpr int kBlock = 256;
+
+struct CamIdx {
+    int v[kMaxCams];
+};
+
+// cvUndistortPointsInternal (OpenCV 4.9), R = I, P = K, 5 iterations, 5 coefficients.
+// The k4..k6 / thin-prism terms are zero and contribute exact zeros; they are
+// omitted (sign-of-zero differences cannot change the f32 result).
+__device__ __forceinline__ void undistort_point(float uf, float vf, const double* __restrict__ c,
+                                                float& ox, float& oy) {
+    const double fx = c[0], fy = c[4];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double cx = c[2], cy = c[5];
+    const double k0 = c[9], k1 = c[10], k2 = c[11], k3 = c[12], k4 = c[13];
+    const double u = uf, v = vf;
+    double x = (u - cx) * ifx;
+    double y = (v - cy) * ify;
+    const double x0 = x, y0 = y;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        double r2 = x * x + y * y;
+        double icdist = 1. / (1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        if (icdist < 0) {
+            x = (u - cx) * ifx;
+            y = (v - cy) * ify;
+            break;
+        }
+        double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+        double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    double xx = c[0] * x + c[1] * y + c[2];
+    double yy = c[3] * x + c[4] * y + c[5];
+    double ww = 1. / (c[6] * x + c[7] * y + c[8]);
+    ox = (float)(xx * ww);
+    oy = (float)(yy * ww);
+}
+
+// JacobiSVDImpl_<double> on At (4 rows of length M); returns Vt row of the
+// smallest singular value after OpenCV's descending selection sort.
+template <int M>
+__device__ __forceinline__ void jacobi_null_vector(double (&At)[4][M], double (&nv)[4]) {
+    double W[4];
+    double Vt[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < M; k++) sd += At[i][k] * At[i][k];
+        W[i] = sd;
+#pragma unroll
+        for (int k = 0; k < 4; k++) Vt[i][k] = (i == k) ? 1.0 : 0.0;
+    }
+    const double eps = DBL_EPSILON * 10;
+    const int max_iter = M > 30 ? M : 30;
+    for (int iter = 0; iter < max_iter; iter++) {
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+#pragma unroll
+            for (int j = i + 1; j < 4; j++) {
+                double a = W[i], b = W[j], p = 0;
+#pragma unroll
+                for (int k = 0; k < M; k++) p += At[i][k] * At[j][k];
+                if (!(fabs(p) <= eps * sqrt(a * b))) {
+                    p *= 2;
+                    double beta = a - b, gamma = hypot(p, beta);
+                    double c, s;
+                    if (beta < 0) {
+                        double delta = (gamma - beta) * 0.5;
+                        s = sqrt(delta / gamma);
+                        c = p / (gamma * s * 2);
+                    } else {
+                        c = sqrt((gamma + beta) / (gamma * 2));
+                        s = p / (gamma * c * 2);
+                    }
+                    a = 0;
+                    b = 0;
+#pragma unroll
+                    for (int k = 0; k < M; k++) {
+                        double t0 = c * At[i][k] + s * At[j][k];
+                        double t1 = -s * At[i][k] + c * At[j][k];
+                        At[i][k] = t0;
+                        At[j][k] = t1;
+                        a += t0 * t0;
+                        b += t1 * t1;
+                    }
+                    W[i] = a;
+                    W[j] = b;
+                    changed = true;
+#pragma unroll
+                    for (int k = 0; k < 4; k++) {
+                        double t0 = c * Vt[i][k] + s * Vt[j][k];
+                        double t1 = -s * Vt[i][k] + c * Vt[j][k];
+                        Vt[i][k] = t0;
+                        Vt[j][k] = t1;
+                    }
+                }
+            }
+        }
+        if (!changed) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < M; k++) sd += At[i][k] * At[i][k];
+        W[i] = sqrt(sd);
+    }
+    // descending selection sort (only the Vt rows matter), compile-time row indices
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        int j = i;
+        double wj = W[i];
+#pragma unroll
+        for (int k = i + 1; k < 4; k++)
+            if (wj < W[k]) {
+                wj = W[k];
+                j = k;
+            }
+#pragma unroll
+        for (int k = i + 1; k < 4; k++)
+            if (j == k) {
+                double t = W[i];
+                W[i] = W[k];
+                W[k] = t;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    double tv = Vt[i][q];
+                    Vt[i][q] = Vt[k][q];
+                    Vt[k][q] = tv;
+                }
+            }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) nv[q] = Vt[3][q];
+}
+
+__device__ __forceinline__ void write_result(const double (&nv)[4], int64_t p, float* __restrict__ out,
+                                             double* __restrict__ out4) {
+    // cvmSet into the f32 points4D, then convertPointsFromHomogeneous in f32.
+    const float X = (float)nv[0], Y = (float)nv[1], Z = (float)nv[2], w = (float)nv[3];
+    const float s = (w != 0.f) ? __frcp_rn(w) : 1.f;
+    out[3 * p + 0] = __fmul_rn(X, s);
+    out[3 * p + 1] = __fmul_rn(Y, s);
+    out[3 * p + 2] = __fmul_rn(Z, s);
+    if (out4) {
+        out4[4 * p + 0] = nv[0];
+        out4[4 * p + 1] = nv[1];
+        out4[4 * p + 2] = nv[2];
+        out4[4 * p + 3] = nv[3];
+    }
+}
+
+__device__ __forceinline__ void add_view_rows(double (*A)[4], int r, float ux, float uy,
+                                              const double* __restrict__ P) {
+    const double x = ux, y = uy;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        A[r][k] = x * P[8 + k] - P[0 + k];
+        A[r + 1][k] = y * P[8 + k] - P[4 + k];
+    }
+}
+
+__device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], const double* __restrict__ cams,
+                                          int n_cams) {
+    const int total = n_cams * MVP_CAM_DOUBLES;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) scam[i / MVP_CAM_DOUBLES][i % MVP_CAM_DOUBLES] = cams[i];
+    __syncthreads();
+}
+
+// MVP_TRI_REFERENCE: top-2 listed cameras by confidence (ascending), params keyed
+// by selection position (reference quirk, pose_estimation.py:36-45).
+__global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
+    CamIdx ci, int n_ci, float* __restrict__ out, double* __restrict__ out4) {
+    __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
+    load_cams(scam, cams, n_cams);
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const float* __restrict__ kp = kpts + p * 3 * V;
+    // stable ascending argsort, NaN last; keep the last two (pose_estimation.py:36)
+    int best = 0, second = -1;
+    float cbest = kp[2 * V + ci.v[0]];
+    float csecond = 0.f;
+#pragma unroll
+    for (int i = 1; i < kMaxCams; i++) {
+        if (i < n_ci) {
+            const float c = kp[2 * V + ci.v[i]];
+            const bool after_best = isnan(c) ? true : (isnan(cbest) ? false : (c >= cbest));
+            if (after_best) {
+                second = best;
+                csecond = cbest;
+                best = i;
+                cbest = c;
+            } else {
+                const bool after_second =
+                    (second < 0) ? true : (isnan(c) ? true : (isnan(csecond) ? false : (c >= csecond)));
+                if (after_second) {
+                    second = i;
+                    csecond = c;
+                }
+            }
+        }
+    }
+    const int pos0 = second, pos1 = best;  // top_indices = [lower-conf, higher-conf]
+    const int col0 = ci.v[pos0], col1 = ci.v[pos1];
+    float u0x, u0y, u1x, u1y;
+    // points come from the selected columns; parameters from camera key = position
+    undistort_point(kp[col0], kp[V + col0], scam[pos0], u0x, u0y);
+    undistort_point(kp[col1], kp[V + col1], scam[pos1], u1x, u1y);
+    double A[4][4];
+    add_view_rows(A, 0, u0x, u0y, scam[pos0] + 26);
+    add_view_rows(A, 2, u1x, u1y, scam[pos1] + 26);
+    double At[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) At[c][r] = A[r][c];
+    double nv[4];
+    jacobi_null_vector<4>(At, nv);
+    write_result(nv, p, out, out4);
+}
+
+// MVP_TRI_ALL_VIEWS: one 2·NV x 4 DLT over the NV listed views.
+template <int NV>
+__global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
+    CamIdx ci, float* __restrict__ out, double* __restrict__ out4) {
+    __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
+    load_cams(scam, cams, n_cams);
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const float* __restrict__ kp = kpts + p * 3 * V;
+    double A[2 * NV][4];
+#pragma unroll
+    for (int j = 0; j < NV; j++) {
+        const int col = ci.v[j];
+        float ux, uy;
+        undistort_point(kp[col], kp[V + col], scam[col], ux, uy);
+        add_view_rows(A, 2 * j, ux, uy, scam[col] + 26);
+    }
+    double At[4][2 * NV];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < 2 * NV; r++) At[c][r] = A[r][c];
+    double nv[4];
+    jacobi_null_vector<2 * NV>(At, nv);
+    write_result(nv, p, out, out4);
+}
+
+}  // namespace
+
+extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const double* cams, int n_cams,
+                               const int* cam_idx, int n_cam_idx, int mode, float* out_xyz, double* out_xyzw,
+                               void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n_points >= 0, "mvp_triangulate: n_points < 0");
+    MVP_REQUIRE(V >= 2 && V <= 64, "mvp_triangulate: V=%d out of range", V);
+    MVP_REQUIRE(n_cams >= 1 && n_cams <= kMaxCams, "mvp_triangulate: n_cams=%d (1..%d)", n_cams, kMaxCams);
+    MVP_REQUIRE(cam_idx != nullptr, "mvp_triangulate: cam_idx is NULL");
+    MVP_REQUIRE(n_cam_idx >= 2 && n_cam_idx <= kMaxCams, "mvp_triangulate: n_cam_idx=%d (2..%d)", n_cam_idx,
+                kMaxCams);
+    CamIdx ci{};
+    for (int i = 0; i < n_cam_idx; i++) {
+        MVP_REQUIRE(cam_idx[i] >= 0 && cam_idx[i] < V && cam_idx[i] < n_cams,
+                    "mvp_triangulate: cam_idx[%d]=%d out of range (V=%d, n_cams=%d)", i, cam_idx[i], V, n_cams);
+        ci.v[i] = cam_idx[i];
+    }
+    if (n_points == 0) return MVP_OK;
+    MVP_REQUIRE(kpts && cams && out_xyz, "mvp_triangulate: null device pointer");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t blocks = (n_points + kBlock - 1) / kBlock;
+    MVP_REQUIRE(blocks < (1LL << 31), "mvp_triangulate: too many points");
+    if (mode == MVP_TRI_REFERENCE) {
+        MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
+                    "n_cam_idx <= n_cams");
+        hipLaunchKernelGGL(triangulate_reference_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, n_points,
+                           V, cams, n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
+    } else if (mode == MVP_TRI_ALL_VIEWS) {
+#define MVP_TRI_CASE(NV)                                                                                    \
+    case NV:                                                                                                \
+        hipLaunchKernelGGL(triangulate_all_views_kernel<NV>, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, \
+                           n_points, V, cams, n_cams, ci, out_xyz, out_xyzw);                              \
+        break;
+        switch (n_cam_idx) {
+            MVP_TRI_CASE(2)
+            MVP_TRI_CASE(3)
+            MVP_TRI_CASE(4)
+            MVP_TRI_CASE(5)
+            MVP_TRI_CASE(6)
+            MVP_TRI_CASE(7)
+            MVP_TRI_CASE(8)
+        }
+#undef MVP_TRI_CASE
+    } else {
+        mvp::fail(MVP_ERR_ARG, "mvp_triangulate: unknown mode %d", mode);
+    }
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}

@@ -1,0 +1,238 @@
+"""Generate the golden vectors under tests/golden/ by importing the REFERENCE
+itself (sashapersonxyz/Multi-camera_3D_Pose_Estimation at /root/reference).
+
+Runs ONLY in the build container (the reference never travels to the GPU box):
+    python tests/golden/make_golden.py
+The reference needs cv2 and mmpose, which are absent here; they are replaced by
+stub modules.  The stub cv2 is populated with the oracle's OpenCV-4.9
+restatement (oracle/cv_ref.py), so fixtures that go through cv2
+(pose3d_select) pin the reference's selection / ordering / reshape / dtype
+orchestration, not cv2's numerics.  Every other fixture calls reference
+functions that are pure numpy / torch and is pinned to the reference's own
+arithmetic.  Each fixture records its generator seeds.
+
+Only data (inputs and expected outputs) is written; no reference source.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd"))
+
+from mvpose import synthetic as syn  # noqa: E402
+from oracle import cv_ref  # noqa: E402
+from oracle import heatmap_ref  # noqa: E402
+
+REF = "/root/reference"
+
+
+def _install_stubs():
+    cv2 = types.ModuleType("cv2")
+    cv2.undistortPoints = cv_ref.undistort_points
+    cv2.triangulatePoints = cv_ref.triangulate_points_cv
+    cv2.convertPointsFromHomogeneous = cv_ref.convert_points_from_homogeneous
+    sys.modules["cv2"] = cv2
+    for name in ("mmpose", "mmpose.apis", "mmpose.structures", "mmpose.utils"):
+        sys.modules[name] = types.ModuleType(name)
+    sys.modules["mmpose.apis"].inference_topdown = None
+    sys.modules["mmpose.apis"].init_model = None
+    sys.modules["mmpose.structures"].merge_data_samples = None
+    sys.modules["mmpose.utils"].adapt_mmdet_pipeline = None
+    sys.path.insert(0, REF)
+
+
+def _save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path)} B)")
+
+
+def gen_dlt(ref_utils):
+    """utils.DLT known answers (utils.py:19-34), zero distortion."""
+    rig_seed, pose_seed, kp_seed = 11, 12, 13
+    cams = syn.make_rig(2, seed=rig_seed, distortion=False)
+    poses = syn.make_poses(6, seed=pose_seed)
+    k = syn.make_kpts_2d(poses, cams, seed=kp_seed)
+    P0 = cv_ref.projection_matrix(cams[0]["K"], cams[0]["R"], cams[0]["T"])
+    P1 = cv_ref.projection_matrix(cams[1]["K"], cams[1]["R"], cams[1]["T"])
+    pts = k[:, :, :2, :].reshape(-1, 2, 2).astype(np.float64)  # (n, xy, view)
+    out = np.array([ref_utils.DLT(P0, P1, p[:, 0], p[:, 1]) for p in pts])
+    _save("dlt_kat.npz", P0=P0, P1=P1, kpts=k, out=out,
+          K=np.stack([c["K"] for c in cams]), R=np.stack([c["R"] for c in cams]),
+          T=np.stack([c["T"] for c in cams]), dist=np.stack([c["dist"] for c in cams]),
+          seeds=np.array([rig_seed, pose_seed, kp_seed]))
+
+
+def gen_pose3d(pose_estimation):
+    """pose_estimation.get_pose_3D selection / ordering (pose_estimation.py:11-65)."""
+    rig_seed, pose_seed, kp_seed = 21, 22, 23
+    cams = syn.make_rig(3, seed=rig_seed)
+    poses = syn.make_poses(8, seed=pose_seed)
+    k = syn.make_kpts_2d(poses, cams, seed=kp_seed)
+    # planted exact confidence ties and NaN confidences
+    k[0, :5, 2, 1] = k[0, :5, 2, 0]
+    k[1, 3, 2, :] = 0.5
+    k[2, 4, 2, 0] = np.nan
+    k[2, 5, 2, 1] = np.nan
+    k[2, 6, 2, :] = np.nan
+    k[3, 7, 2, 2] = np.nan
+    cp = syn.reference_camera_params(cams)
+    outs = {}
+    for tag, ci, ign in (("01", [0, 1], False), ("012", [0, 1, 2], False), ("12", [1, 2], False),
+                         ("01_nodist", [0, 1], True)):
+        outs["out_" + tag] = pose_estimation.get_pose_3D(dict(cp), k, camera_indices=ci,
+                                                        ignore_nonlinear_distortions=ign)
+    _save("pose3d_select.npz", kpts=k, K=np.stack([c["K"] for c in cams]),
+          R=np.stack([c["R"] for c in cams]), T=np.stack([c["T"] for c in cams]),
+          dist=np.stack([c["dist"] for c in cams]), seeds=np.array([rig_seed, pose_seed, kp_seed]),
+          **outs)
+
+
+def _synthetic_heatmaps(rng, K, H, W, scale=1.0):
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    hm = np.empty((K, H, W), np.float32)
+    for j in range(K):
+        cx, cy = rng.uniform(0.1 * W, 0.9 * W), rng.uniform(0.1 * H, 0.9 * H)
+        sx, sy = rng.uniform(1.5, 4.0) * scale, rng.uniform(1.5, 4.0) * scale
+        rho = rng.uniform(-0.5, 0.5)
+        dx, dy = (xx - cx) / sx, (yy - cy) / sy
+        g = np.exp(-0.5 * (dx * dx - 2 * rho * dx * dy + dy * dy) / (1 - rho * rho))
+        hm[j] = (rng.uniform(0.3, 1.0) * g + rng.normal(0, 0.01, (H, W))).astype(np.float32)
+    hm[K - 1] = rng.uniform(-0.05, 0.0099, (H, W)).astype(np.float32)  # all below threshold -> zeros
+    return hm
+
+
+def gen_moments(PoseEstimator):
+    """PoseEstimator.get_heatmap_means_cov (mmpose_pose_estimation.py:163-215) on
+    (a) a full-resolution heatmap directly, (b) a 64x48 heatmap reverted to a
+    small image with the oracle's cv2.warpAffine restatement (revert_heatmap)."""
+    seed = 31
+    rng = np.random.default_rng(seed)
+    hm_full = _synthetic_heatmaps(rng, 17, 72, 128, scale=3.0)
+    out_full = PoseEstimator.get_heatmap_means_cov(None, hm_full.copy())
+    hm_low = _synthetic_heatmaps(rng, 17, 64, 48)
+    img_h, img_w = 90, 160
+    center, scale = heatmap_ref.whole_image_cs(img_w, img_h)
+    scale = heatmap_ref.fix_aspect_ratio(scale, 192 / 256)
+    M_inv = heatmap_ref.get_warp_matrix(center, scale, 0.0, (48, 64), inv=True)
+    reverted = heatmap_ref.warp_affine_linear_f32(hm_low, M_inv, img_h, img_w)
+    out_rev = PoseEstimator.get_heatmap_means_cov(None, reverted.copy())
+    _save("moments.npz", hm_full=hm_full, out_full=out_full, hm_low=hm_low, M_inv=M_inv,
+          img_hw=np.array([img_h, img_w]), out_rev=out_rev, seeds=np.array([seed]))
+
+
+def gen_project(pr):
+    """project_points_torch (pose_refinement.py:94-179)."""
+    seed = 41
+    cams = syn.make_rig(3, seed=seed)
+    poses = syn.make_poses(5, seed=seed + 1)
+    pts = torch.tensor(poses, dtype=torch.float32)
+    outs = {}
+    for v, c in enumerate(cams):
+        for ign in (False, True):
+            outs[f"out_c{v}_{int(ign)}"] = pr.project_points_torch(pts, c["K"], c["R"], c["T"], c["dist"],
+                                                                   ignore_distortions=ign).numpy()
+    rvec = np.array([0.1, -0.2, 0.05])
+    outs["out_axisangle"] = pr.project_points_torch(pts, cams[1]["K"], torch.tensor(rvec, dtype=torch.float32),
+                                                    cams[1]["T"], cams[1]["dist"]).numpy()
+    _save("project.npz", points=poses.astype(np.float32), K=np.stack([c["K"] for c in cams]),
+          R=np.stack([c["R"] for c in cams]), T=np.stack([c["T"] for c in cams]),
+          dist=np.stack([c["dist"] for c in cams]), rvec=rvec, seeds=np.array([seed]), **outs)
+
+
+def gen_bodylen(ref_utils):
+    seed = 51
+    poses = torch.tensor(syn.make_poses(7, seed=seed), dtype=torch.float32)
+    L = ref_utils.get_body_part_lengths(poses)
+    names = list(L.keys())
+    _save("bodylen.npz", poses=poses.numpy(), names=np.array(names),
+          lengths=np.stack([L[n].numpy() for n in names]), seeds=np.array([seed]))
+
+
+MY_LENGTHS = {  # reference examples/body_part_lengths.yaml:my_lengths (key order kept)
+    "left_shoulder_left_elbow": 38, "left_elbow_left_wrist": 27,
+    "right_shoulder_right_elbow": 38, "right_elbow_right_wrist": 27,
+    "left_hip_left_knee": 51, "left_knee_left_ankle": 40,
+    "right_hip_right_knee": 51, "right_knee_right_ankle": 40,
+    "left_hip_right_hip": 31, "left_shoulder_left_hip": 54,
+    "right_shoulder_right_hip": 54, "left_shoulder_right_shoulder": 47,
+}
+
+
+def sgd_inputs(V, T, seed):
+    """Synthetic heatmaps_2d (T,V,17,6) f64 Gaussians + kpts_3d (T,17,3) f32 init."""
+    rng = np.random.default_rng(seed)
+    cams = syn.make_rig(V, seed=seed)
+    poses = syn.make_poses(T, seed=seed + 1)
+    gauss = np.zeros((T, V, 17, 6))
+    for v, c in enumerate(cams):
+        uv = syn.project(poses, c) + rng.normal(0, 2.0, (T, 17, 2))
+        sx = rng.uniform(2.0, 6.0, (T, 17))
+        sy = rng.uniform(2.0, 6.0, (T, 17))
+        rho = rng.uniform(-0.4, 0.4, (T, 17))
+        gauss[:, v, :, 0:2] = uv
+        gauss[:, v, :, 2] = sx * sx
+        gauss[:, v, :, 3] = rho * sx * sy
+        gauss[:, v, :, 4] = rho * sx * sy
+        gauss[:, v, :, 5] = sy * sy
+    init = (poses + rng.normal(0, 3.0, poses.shape)).astype(np.float32)
+    return cams, gauss, init
+
+
+def gen_sgd(pr):
+    """Optimized_3d_Pose_Estimation.sgd_optimize (pose_refinement.py:894-1096),
+    trajectory-only path, as the CLI drives it (pose_refinement.py:1210-1214)."""
+    cases = [
+        # name, V, T, seed, kwargs
+        ("sgd_V2_T40", 2, 40, 61, dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100,
+                                       max_iter=10, batch_size=None)),
+        ("sgd_V2_T40_b8", 2, 40, 62, dict(lr=0.01, lambda_smooth=1e-3, lambda_body_length=0.5, patience=100,
+                                          max_iter=5, batch_size=8)),
+        ("sgd_V8_T20", 8, 20, 63, dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100,
+                                       max_iter=60, batch_size=None)),
+        ("sgd_V2_T24_stop", 2, 24, 64, dict(lr=0.05, lambda_smooth=1e-6, lambda_body_length=1.0, patience=3,
+                                            max_iter=400, batch_size=None, tolerance=0.2)),
+    ]
+    for name, V, T, seed, kw in cases:
+        cams, gauss, init = sgd_inputs(V, T, seed)
+        params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+        torch.manual_seed(0)
+        opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                              body_lengths=dict(MY_LENGTHS))
+        full_kw = dict(print_frequency=10 ** 9)
+        full_kw.update(kw)
+        opt.sgd_optimize(**full_kw)
+        hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
+        _save(f"{name}.npz", gauss=gauss, init=init, K=np.stack([c["K"] for c in cams]),
+              R=np.stack([c["R"] for c in cams]), T=np.stack([c["T"] for c in cams]),
+              dist=np.stack([c["dist"] for c in cams]), best=opt.best_trajectory.numpy(),
+              final=opt.trajectory.detach().numpy(),
+              kw_names=np.array(list(kw.keys())), kw_vals=np.array([np.nan if v is None else float(v)
+                                                                  for v in kw.values()]),
+              seeds=np.array([seed]), **{"hist_" + k: v for k, v in hist.items()})
+
+
+def main():
+    _install_stubs()
+    import utils as ref_utils  # noqa: E402  (reference utils.py)
+    import pose_estimation  # noqa: E402
+    import pose_refinement as pr  # noqa: E402
+    from mmpose_pose_estimation import PoseEstimator  # noqa: E402
+    gen_dlt(ref_utils)
+    gen_pose3d(pose_estimation)
+    gen_moments(PoseEstimator)
+    gen_project(pr)
+    gen_bodylen(ref_utils)
+    gen_sgd(pr)
+
+
+if __name__ == "__main__":
+    main()

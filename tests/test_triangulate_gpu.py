@@ -1,0 +1,120 @@
+"""GPU parity: HIP triangulation (mvp_triangulate) vs the oracle and the
+reference's golden vectors.  Tolerance: 1e-4 world units (BASELINE north_star),
+on float32 outputs of ~350 cm magnitude (~3 ulp)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import cv_ref
+from mvpose import synthetic as syn
+
+pytestmark = pytest.mark.gpu
+ATOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ops():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import ops as _ops
+    return _ops
+
+
+def _cams(d):
+    return {i: [d["K"][i], d["R"][i], d["T"][i], d["dist"][i]] for i in range(d["K"].shape[0])}
+
+
+def _run(ops, cp, kpts, ci, mode=0, ignore_dist=False):
+    if ignore_dist:
+        cp = {k: [K, R, T, np.asarray(dist) * 0] for k, (K, R, T, dist) in cp.items()}
+    cams = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    k = torch.tensor(np.ascontiguousarray(kpts), device="cuda")
+    out = ops.triangulate(k, cams, ci, mode=mode)
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _check(out, ref, min_exact=0.95):
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    np.testing.assert_allclose(out, ref, rtol=0, atol=ATOL, equal_nan=True)
+    exact = np.mean((out == ref) | (np.isnan(out) & np.isnan(ref)))
+    assert exact >= min_exact, f"only {exact:.3f} of outputs bit-identical to the oracle"
+
+
+@pytest.mark.parametrize("tag,ci,ign", [("01", [0, 1], False), ("012", [0, 1, 2], False),
+                                        ("12", [1, 2], False), ("01_nodist", [0, 1], True)])
+def test_golden_get_pose_3D(ops, tag, ci, ign):
+    d = np.load(os.path.join(GOLDEN, "pose3d_select.npz"))
+    out = _run(ops, _cams(d), d["kpts"], ci, ignore_dist=ign)
+    _check(out, d["out_" + tag])
+
+
+def test_golden_dlt(ops):
+    d = np.load(os.path.join(GOLDEN, "dlt_kat.npz"))
+    out = _run(ops, _cams(d), d["kpts"], [0, 1]).reshape(-1, 3)
+    np.testing.assert_allclose(out, d["out"], rtol=0, atol=ATOL)
+
+
+@pytest.mark.parametrize("V,T,seed", [(2, 300, 1), (3, 100, 2), (8, 50, 3)])
+def test_seeded_vs_oracle(ops, V, T, seed):
+    cams = syn.make_rig(V, seed=seed)
+    k = syn.make_kpts_2d(syn.make_poses(T, seed=seed + 10), cams, seed=seed + 20)
+    cp = syn.reference_camera_params(cams)
+    ref = cv_ref.get_pose_3D(cp, k, camera_indices=[0, 1])
+    _check(_run(ops, cp, k, [0, 1]), ref)
+
+
+def test_top2_of_many(ops):
+    cams = syn.make_rig(5, seed=4)
+    k = syn.make_kpts_2d(syn.make_poses(40, seed=5), cams, seed=6)
+    k[::3, ::2, 2, 3] = k[::3, ::2, 2, 1]  # ties
+    k[5, 3, 2, 2] = np.nan
+    cp = syn.reference_camera_params(cams)
+    ci = [0, 1, 2, 3, 4]
+    ref = cv_ref.get_pose_3D(cp, k, camera_indices=ci)
+    _check(_run(ops, cp, k, ci), ref)
+
+
+def test_nan_and_empty(ops):
+    cams = syn.make_rig(2, seed=7)
+    k = syn.make_kpts_2d(syn.make_poses(4, seed=8), cams, seed=9)
+    k[1, 2, 0, 0] = np.nan
+    k[2, 5, 1, 1] = np.nan
+    cp = syn.reference_camera_params(cams)
+    ref = cv_ref.get_pose_3D(cp, k, camera_indices=[0, 1])
+    out = _run(ops, cp, k, [0, 1])
+    assert np.isnan(out[1, 2]).all() and np.isnan(ref[1, 2]).all()
+    _check(out, ref)
+    empty = _run(ops, cp, np.zeros((0, 17, 3, 2), np.float32), [0, 1])
+    assert empty.shape == (0, 17, 3)
+
+
+@pytest.mark.parametrize("V", [2, 4, 8])
+def test_all_views_vs_oracle(ops, V):
+    cams = syn.make_rig(V, seed=11 + V)
+    k = syn.make_kpts_2d(syn.make_poses(60, seed=12), cams, seed=13)
+    cp = [(c["K"], c["R"], c["T"], c["dist"]) for c in cams]
+    ci = list(range(V))
+    ref = cv_ref.triangulate_all_views(cp, k, ci)
+    _check(_run(ops, syn.reference_camera_params(cams), k, ci, mode=ops.TRI_ALL_VIEWS), ref)
+
+
+def test_full_size_roundtrip_property(ops):
+    """BASELINE config 4 size (100k frames x 17 joints, V=2): noise-free
+    projections must triangulate back to the poses; order of the two cameras
+    must not matter beyond f32 rounding."""
+    cams = syn.make_rig(2, seed=21)
+    T = 100_000
+    poses = syn.make_poses(T, seed=22)
+    k = syn.make_kpts_2d(poses, cams, seed=23, noise_px=0.0)
+    cp = syn.reference_camera_params(cams)
+    out = _run(ops, cp, k, [0, 1])
+    assert np.isfinite(out).all()
+    np.testing.assert_allclose(out, poses, atol=2e-3)
+    k2 = k.copy()
+    k2[:, :, 2, :] = k[:, :, 2, ::-1]  # flip the confidence order -> swapped camera order
+    out2 = _run(ops, cp, k2, [0, 1])
+    np.testing.assert_allclose(out2, out, atol=ATOL)
