@@ -77,6 +77,91 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
                     int n_cams, const int* cam_idx_host, int n_cam_idx, int mode,
                     float* out_xyz_dev, double* out_xyzw_dev, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * 2D stage around the backbone (replaces, per camera frame, what
+ * PoseEstimator.predict gets from mmpose at mmpose_pose_estimation.py:253-267).
+ *
+ * mvp_preprocess: TopdownAffine for a whole-image bbox + PoseDataPreprocessor.
+ *   frames_dev [n][H][W][3] uint8 (as the reference hands them to the model);
+ *   minv_dev [n][6] float64 = the crop -> image map cv2.warpAffine uses
+ *   internally (inverse of mmpose get_warp_matrix); mean3/std3 host f32;
+ *   swap_rb = bgr_to_rgb.  out_dev [(1+with_flip)*n][out_h][out_w][4] bf16
+ *   (RGB + zero channel); the flipped copies (flip test) follow the n originals.
+ * mvp_heatmap_decode: flip-test average (flip_mode='heatmap', shift_heatmap)
+ *   + MSRAHeatmap decode + restore to image pixels.  hm_dev/hm_flip_dev
+ *   [N][K][H][W] f32 (hm_flip may be NULL: no flip test); flip_idx_host [K];
+ *   center_scale_dev [N][4] f32 (cx, cy, sw, sh); outputs avg_dev (nullable)
+ *   [N][K][H][W], kpts_dev [N][K][2] f32, scores_dev [N][K] f32, argmax_dev
+ *   (nullable) [N][K] int32 flat index into H*W; kpts_tkv_dev (nullable)
+ *   [N/V][K][3][V] f32 = the reference kpts_2d layout (crops ordered (t, v)).
+ * mvp_heatmap_moments: revert_heatmap (warp of each map to the img_h x img_w
+ *   image, float bilinear) fused with get_heatmap_means_cov
+ *   (mmpose_pose_estimation.py:163-215): out_dev [N][K][6] float64
+ *   (mx, my, vxx, vxy, vxy, vyy); minv_dev [N][6] = image -> heatmap map.
+ * ------------------------------------------------------------------------- */
+int mvp_preprocess(const uint8_t* frames_dev, int n, int H, int W, const double* minv_dev, int out_h, int out_w,
+                   const float* mean3_host, const float* std3_host, int swap_rb, int with_flip, uint16_t* out_dev,
+                   void* stream);
+int mvp_heatmap_decode(const float* hm_dev, const float* hm_flip_dev, int N, int K, int H, int W,
+                       const int* flip_idx_host, int shift, const float* center_scale_dev, int input_w, int input_h,
+                       float* avg_dev, float* kpts_dev, float* scores_dev, int32_t* argmax_dev, float* kpts_tkv_dev,
+                       int V, void* stream);
+int mvp_heatmap_moments(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
+                        int img_w, float thr, double* out_dev, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Backbone graph runtime (replaces the HRNet-W32 forward inside mmpose's
+ * inference_topdown, called at mmpose_pose_estimation.py:253 once per camera
+ * frame, batch 1, on the CPU).  A static graph of convolutions on bf16 NHWC
+ * activations, BN folded into the weights, executed batch-wide on one stream.
+ * The graph (topology + packed weights) is built by the host
+ * (mvpose/hrnet.py); the runtime validates it, plans one activation arena by
+ * tensor liveness (buffers reused across the ~330 ops), and launches the HIP
+ * kernels.
+ *
+ * Tensors: per-crop shape (h, w, c); dtype MVP_DT_BF16_NHWC or
+ * MVP_DT_F32_NCHW.  The batch dimension is given at forward time.
+ * Ops:
+ *   MVP_OP_STEM : 3x3/s2 conv of a 4-channel (RGB+0) bf16 input to 64 ch, BN+ReLU
+ *                 folded; w_off/b_off index the f32 blob ([64][3][3][4], [64]).
+ *   MVP_OP_CONV : y = act(conv(in[0]) + bias [+ in[1]]), ks 1|3, stride 1|2;
+ *                 w_off indexes the bf16 blob ([cout_pad][ks][ks][cin]),
+ *                 b_off the f32 blob ([cout_pad]); cout_pad = cout <= 32 ? 32 :
+ *                 round_up(cout, 64).  An F32_NCHW output tensor makes it the
+ *                 heatmap head.
+ *   MVP_OP_FUSE : out = act(sum_k nearest_upsample(in[k], up[k])), n_in <= 4
+ *                 (HRModule multi-scale fuse).
+ * ------------------------------------------------------------------------- */
+#define MVP_DT_BF16_NHWC 0
+#define MVP_DT_F32_NCHW 1
+
+#define MVP_OP_STEM 0
+#define MVP_OP_CONV 1
+#define MVP_OP_FUSE 2
+
+typedef struct mvp_tensor_desc {
+    int h, w, c, dtype;
+} mvp_tensor_desc;
+
+typedef struct mvp_op_desc {
+    int kind;
+    int out;
+    int n_in;
+    int in[4];
+    int up[4];
+    int cin, cout, ks, stride, relu;
+    int64_t w_off;
+    int64_t b_off;
+} mvp_op_desc;
+
+int mvp_graph_create(const mvp_tensor_desc* tensors_host, int n_tensors, const mvp_op_desc* ops_host, int n_ops,
+                     int input_tensor, int output_tensor, const uint16_t* w_bf16_dev, int64_t w_elems,
+                     const float* f32_dev, int64_t f32_elems, int max_batch, void** handle_out);
+/* input_dev: [batch][h][w][c] of the input tensor; output_dev: the output tensor. */
+int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* output_dev, void* stream);
+int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);
+int mvp_graph_destroy(void* handle);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,40 @@
+// Internal (not part of the C-ABI): convolution / fuse launchers used by the
+// HRNet graph runtime (hrnet.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mvp {
+
+// One NHWC bf16 convolution with BN folded into (w, bias):
+//   y = act( conv(x, w) + bias [+ res] )
+// w: [Cout_pad][KS][KS][Cin] bf16 (Cout_pad = Cout rounded up to the tile),
+// bias: [Cout_pad] f32.  out_f32_nchw: write f32 [N][Cout][Ho][Wo] instead of
+// bf16 NHWC (HeatmapHead output).
+struct ConvLaunch {
+    const uint16_t* x;
+    const uint16_t* w;
+    const float* bias;
+    const uint16_t* res;  // nullable, same shape as y
+    uint16_t* y;          // bf16 NHWC [N][Ho][Wo][Cout]
+    float* yf;            // f32 NCHW (when out_f32_nchw)
+    int N, H, W, Cin, Cout;
+    int ks, stride, relu, out_f32_nchw;
+};
+
+void launch_conv(const ConvLaunch& c, hipStream_t s);
+
+// 3x3/s2 stem conv on 4-channel (RGB + zero) bf16 crops, BN folded, ReLU.
+// w: [64][3][3][4] f32, bias [64] f32.  x [N][H][W][4] -> y [N][H/2][W/2][64].
+void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,
+                 hipStream_t s);
+
+// HRModule fuse: out = relu( sum_i up_i(in_i) ), nearest upsample factor up_i
+// (1, 2, 4, 8); all tensors bf16 NHWC with C channels, out at resolution H x W.
+void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_t* out, int N, int H, int W,
+                     int C, int relu, hipStream_t s);
+
+// Conv weight padding rule shared with the host packer.
+int conv_cout_pad(int cout);
+
+}  // namespace mvp

@@ -1,0 +1,395 @@
+// HRNet-W32 convolutions for gfx950: implicit GEMM on bf16 MFMA (v_mfma_f32_16x16x32_bf16).
+//
+// GEMM view per conv:  Y[cout][pix] = sum_k W[cout][k] * X[k][pix],  k = (kh, kw, cin),
+// activations NHWC bf16 so 8 consecutive k of one tap are 16 contiguous bytes.
+// A = weights (rows = couts), B = im2col activations (cols = output pixels); the
+// accumulator lane layout (col = lane&15 -> pixel, rows (lane>>4)*4+r -> 4
+// consecutive couts) gives an 8-byte NHWC store per lane.
+//
+// Each 256-thread workgroup (4 waves) owns an output tile of NB crops x TH x TW
+// pixels x BM couts.  Per 32-channel input chunk it stages the input HALO of the
+// tile ((TH-1)*S+KS) x ((TW-1)*S+KS) and the BM x KS*KS x 32 weight slice in LDS,
+// so every input pixel is fetched from L2/HBM once per tile instead of KS*KS times
+// (im2col happens in the LDS addressing).  Rows are padded by 16 B to break the
+// 64-B-stride bank pattern of the ds_read_b128 fragment reads.  Epilogue fuses
+// folded-BN bias, optional residual add (BasicBlock/Bottleneck), ReLU and bf16
+// pack; the head variant writes f32 NCHW heatmaps.
+#include "conv.h"
+#include "mvp_common.h"
+
+namespace mvp {
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    __bf16 b = (__bf16)f;  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN preserved
+    return __builtin_bit_cast(uint16_t, b);
+}
+
+struct ConvParams {
+    const uint16_t* __restrict__ x;
+    const uint16_t* __restrict__ w;
+    const float* __restrict__ bias;
+    const uint16_t* __restrict__ res;
+    uint16_t* __restrict__ y;
+    float* __restrict__ yf;
+    int N, H, W, Cin, Ho, Wo, Cout, Cout_pad;
+    int relu, out_f32;
+    int tiles_w, tiles_h;
+};
+
+template <int KS, int S, int BM, int TH, int TW, int NB>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
+    constexpr int PAD = KS / 2;
+    constexpr int HH = (TH - 1) * S + KS;
+    constexpr int HW = (TW - 1) * S + KS;
+    constexpr int PS = 40;  // halo pixel stride in bf16: 32 ch + 8 pad (80 B)
+    constexpr int KK = KS * KS;
+    constexpr int WS = KK * 32 + 8;  // weight row stride in bf16 (+16 B pad)
+    constexpr int P = NB * TH * TW;
+    static_assert(P % 64 == 0, "tile must hold a multiple of 64 pixels");
+    constexpr int NPT = P / 16;
+    constexpr int NCT = BM / 16;
+    constexpr int PTW = NPT / 4;  // pixel tiles per wave
+    constexpr int HALO_PIX = NB * HH * HW;
+    constexpr int HALO_ELEMS = HALO_PIX * PS;
+    constexpr int W_ELEMS = BM * WS;
+    __shared__ __attribute__((aligned(16))) uint16_t lds[HALO_ELEMS + W_ELEMS];
+    uint16_t* sh = lds;
+    uint16_t* sw = lds + HALO_ELEMS;
+
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int t = blockIdx.x;
+    const int tw_i = t % p.tiles_w;
+    t /= p.tiles_w;
+    const int th_i = t % p.tiles_h;
+    const int tn_i = t / p.tiles_h;
+    const int n0 = tn_i * NB, ho0 = th_i * TH, wo0 = tw_i * TW;
+    const int hi0 = ho0 * S - PAD, wi0 = wo0 * S - PAD;
+    const int co0 = blockIdx.y * BM;
+
+    int hbase[PTW];
+#pragma unroll
+    for (int i = 0; i < PTW; i++) {
+        const int pp = (wave * PTW + i) * 16 + (lane & 15);
+        const int nb = pp / (TH * TW);
+        const int r = pp - nb * (TH * TW);
+        const int th = r / TW, tw = r - (r / TW) * TW;
+        hbase[i] = ((nb * HH + th * S) * HW + tw * S) * PS + (lane >> 4) * 8;
+    }
+    f32x4 acc[PTW][NCT];
+#pragma unroll
+    for (int i = 0; i < PTW; i++)
+#pragma unroll
+        for (int c = 0; c < NCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int c0 = 0; c0 < p.Cin; c0 += 32) {
+        // ---- stage the input halo (zero outside the image / batch)
+        for (int idx = tid; idx < HALO_PIX * 4; idx += 256) {
+            const int ch = idx & 3;
+            const int pix = idx >> 2;
+            const int nb = pix / (HH * HW);
+            const int r = pix - nb * (HH * HW);
+            const int hh = r / HW, ww = r - (r / HW) * HW;
+            const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
+            uint4 v = {0u, 0u, 0u, 0u};
+            if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                v = *reinterpret_cast<const uint4*>(p.x + (((size_t)n * p.H + hi) * p.W + wi) * p.Cin + c0 + ch * 8);
+            *reinterpret_cast<uint4*>(sh + pix * PS + ch * 8) = v;
+        }
+        // ---- stage the weight slice [BM][KK][32]
+        for (int idx = tid; idx < BM * KK * 4; idx += 256) {
+            const int ch = idx & 3;
+            const int r = idx >> 2;
+            const int co = r / KK, tap = r - (r / KK) * KK;
+            const uint4 v =
+                *reinterpret_cast<const uint4*>(p.w + ((size_t)(co0 + co) * KK + tap) * p.Cin + c0 + ch * 8);
+            *reinterpret_cast<uint4*>(sw + co * WS + tap * 32 + ch * 8) = v;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int kh = 0; kh < KS; kh++) {
+#pragma unroll
+            for (int kw = 0; kw < KS; kw++) {
+                const int tap = kh * KS + kw;
+                const int toff = (kh * HW + kw) * PS;
+                bf16x8 a[NCT];
+#pragma unroll
+                for (int c = 0; c < NCT; c++)
+                    a[c] = *reinterpret_cast<const bf16x8*>(sw + (c * 16 + (lane & 15)) * WS + tap * 32 + (lane >> 4) * 8);
+#pragma unroll
+                for (int i = 0; i < PTW; i++) {
+                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(sh + hbase[i] + toff);
+#pragma unroll
+                    for (int c = 0; c < NCT; c++)
+                        acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b, acc[i][c], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head)
+#pragma unroll
+    for (int i = 0; i < PTW; i++) {
+        const int pp = (wave * PTW + i) * 16 + (lane & 15);
+        const int nb = pp / (TH * TW);
+        const int r = pp - nb * (TH * TW);
+        const int th = r / TW, tw = r - (r / TW) * TW;
+        const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
+        if (n >= p.N || ho >= p.Ho || wo >= p.Wo) continue;
+        const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
+#pragma unroll
+        for (int c = 0; c < NCT; c++) {
+            const int co = co0 + c * 16 + (lane >> 4) * 4;
+            const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
+            float v0 = acc[i][c][0] + bv.x, v1 = acc[i][c][1] + bv.y;
+            float v2 = acc[i][c][2] + bv.z, v3 = acc[i][c][3] + bv.w;
+            if (p.out_f32) {
+                const size_t plane = (size_t)p.Ho * p.Wo;
+                float vv[4] = {v0, v1, v2, v3};
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (co + q < p.Cout) p.yf[((size_t)n * p.Cout + co + q) * plane + (size_t)ho * p.Wo + wo] = vv[q];
+                continue;
+            }
+            if (p.res) {
+                const uint2 rv = *reinterpret_cast<const uint2*>(p.res + pix * p.Cout + co);
+                v0 += bf16_to_f32(rv.x & 0xffff);
+                v1 += bf16_to_f32(rv.x >> 16);
+                v2 += bf16_to_f32(rv.y & 0xffff);
+                v3 += bf16_to_f32(rv.y >> 16);
+            }
+            if (p.relu) {
+                v0 = fmaxf(v0, 0.f);
+                v1 = fmaxf(v1, 0.f);
+                v2 = fmaxf(v2, 0.f);
+                v3 = fmaxf(v3, 0.f);
+            }
+            if (co < p.Cout) {
+                uint2 o;
+                o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+                *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
+            }
+        }
+    }
+}
+
+template <int KS, int S, int BM, int TH, int TW, int NB>
+void launch_cfg(const ConvParams& p0, hipStream_t s) {
+    ConvParams p = p0;
+    p.tiles_w = (p.Wo + TW - 1) / TW;
+    p.tiles_h = (p.Ho + TH - 1) / TH;
+    const long tiles_n = (p.N + NB - 1) / NB;
+    const long gx = tiles_n * p.tiles_h * p.tiles_w;
+    MVP_REQUIRE(gx < (1L << 31), "conv grid too large");
+    dim3 grid((unsigned)gx, (unsigned)(p.Cout_pad / BM));
+    hipLaunchKernelGGL((conv_mfma_kernel<KS, S, BM, TH, TW, NB>), grid, dim3(256), 0, s, p);
+}
+
+// Tile shape per output plane width; BM per Cout.
+template <int KS, int S, int BM>
+void launch_plane(const ConvParams& p, hipStream_t s) {
+    if (p.Wo == 48 && p.Ho % 8 == 0) {
+        if constexpr (S == 1)
+            launch_cfg<KS, S, BM, 8, 48, 1>(p, s);
+        else
+            launch_cfg<KS, S, BM, 4, 48, 1>(p, s);
+    } else if (p.Wo == 24 && p.Ho % 8 == 0) {
+        launch_cfg<KS, S, BM, 8, 24, 1>(p, s);
+    } else if (p.Wo == 12 && p.Ho == 16) {
+        launch_cfg<KS, S, BM, 16, 12, 1>(p, s);
+    } else if (p.Wo == 6 && p.Ho == 8) {
+        launch_cfg<KS, S, BM, 8, 6, 4>(p, s);
+    } else {
+        launch_cfg<KS, S, BM, 4, 16, 1>(p, s);  // generic masked tiling
+    }
+}
+
+template <int KS, int S>
+void launch_bm(const ConvParams& p, hipStream_t s) {
+    if (p.Cout_pad == 32)
+        launch_plane<KS, S, 32>(p, s);
+    else
+        launch_plane<KS, S, 64>(p, s);
+}
+
+// ---------------------------------------------------------------- stem conv
+// 3x3/s2, 4 -> 64 channels, direct (VALU fp32): 0.3% of the network's MACs.
+// One thread = one output pixel x 16 output channels (4 threads per pixel).
+__global__ __launch_bounds__(256) void stem_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                   const float* __restrict__ bias, uint16_t* __restrict__ y, int N,
+                                                   int H, int W, int Ho, int Wo) {
+    __shared__ float sw[36][64];
+    __shared__ float sb[64];
+    for (int i = threadIdx.x; i < 36 * 64; i += 256) {
+        const int co = i / 36, k = i % 36;  // w layout [co][tap][c]
+        sw[k][co] = w[i];
+    }
+    if (threadIdx.x < 64) sb[threadIdx.x] = bias[threadIdx.x];
+    __syncthreads();
+    const long gid = (long)blockIdx.x * 256 + threadIdx.x;
+    const int grp = gid & 3;
+    const long pix = gid >> 2;
+    if (pix >= (long)N * Ho * Wo) return;
+    const int wo = pix % Wo;
+    const int ho = (pix / Wo) % Ho;
+    const int n = pix / ((long)Wo * Ho);
+    const int cb = grp * 16;
+    float acc[16];
+#pragma unroll
+    for (int c = 0; c < 16; c++) acc[c] = sb[cb + c];
+    for (int kh = 0; kh < 3; kh++) {
+        const int hi = ho * 2 - 1 + kh;
+        for (int kw = 0; kw < 3; kw++) {
+            const int wi = wo * 2 - 1 + kw;
+            float xin[3] = {0.f, 0.f, 0.f};
+            if (hi >= 0 && hi < H && wi >= 0 && wi < W) {
+                const uint2 v = *reinterpret_cast<const uint2*>(x + (((size_t)n * H + hi) * W + wi) * 4);
+                xin[0] = bf16_to_f32(v.x & 0xffff);
+                xin[1] = bf16_to_f32(v.x >> 16);
+                xin[2] = bf16_to_f32(v.y & 0xffff);
+            }
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const float* wr = &sw[(kh * 3 + kw) * 4 + c][cb];
+#pragma unroll
+                for (int co = 0; co < 16; co++) acc[co] = fmaf(xin[c], wr[co], acc[co]);
+            }
+        }
+    }
+    uint16_t* out = y + (size_t)pix * 64 + cb;
+#pragma unroll
+    for (int co = 0; co < 16; co += 8) {
+        uint4 o;
+        o.x = (uint32_t)f32_to_bf16(fmaxf(acc[co + 0], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 1], 0.f)) << 16);
+        o.y = (uint32_t)f32_to_bf16(fmaxf(acc[co + 2], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 3], 0.f)) << 16);
+        o.z = (uint32_t)f32_to_bf16(fmaxf(acc[co + 4], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 5], 0.f)) << 16);
+        o.w = (uint32_t)f32_to_bf16(fmaxf(acc[co + 6], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 7], 0.f)) << 16);
+        *reinterpret_cast<uint4*>(out + co) = o;
+    }
+}
+
+// ---------------------------------------------------------------- fuse sum
+struct FuseParams {
+    const uint16_t* in[4];
+    int up[4];
+    int n_in;
+    uint16_t* out;
+    int N, H, W, C, relu;
+};
+
+__global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
+    const int chunks = p.C / 8;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    const long total = (long)p.N * p.H * p.W * chunks;
+    if (i >= total) return;
+    const int ch = i % chunks;
+    const long pix = i / chunks;
+    const int w = pix % p.W;
+    const int h = (pix / p.W) % p.H;
+    const int n = pix / ((long)p.W * p.H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < p.n_in; k++) {
+        const int u = p.up[k];
+        const int hs = p.H / u, ws = p.W / u;
+        const uint4 v = *reinterpret_cast<const uint4*>(p.in[k] + (((size_t)n * hs + h / u) * ws + w / u) * p.C + ch * 8);
+        acc[0] += bf16_to_f32(v.x & 0xffff);
+        acc[1] += bf16_to_f32(v.x >> 16);
+        acc[2] += bf16_to_f32(v.y & 0xffff);
+        acc[3] += bf16_to_f32(v.y >> 16);
+        acc[4] += bf16_to_f32(v.z & 0xffff);
+        acc[5] += bf16_to_f32(v.z >> 16);
+        acc[6] += bf16_to_f32(v.w & 0xffff);
+        acc[7] += bf16_to_f32(v.w >> 16);
+    }
+    if (p.relu)
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc[q] = fmaxf(acc[q], 0.f);
+    uint4 o;
+    o.x = (uint32_t)f32_to_bf16(acc[0]) | ((uint32_t)f32_to_bf16(acc[1]) << 16);
+    o.y = (uint32_t)f32_to_bf16(acc[2]) | ((uint32_t)f32_to_bf16(acc[3]) << 16);
+    o.z = (uint32_t)f32_to_bf16(acc[4]) | ((uint32_t)f32_to_bf16(acc[5]) << 16);
+    o.w = (uint32_t)f32_to_bf16(acc[6]) | ((uint32_t)f32_to_bf16(acc[7]) << 16);
+    *reinterpret_cast<uint4*>(p.out + pix * p.C + ch * 8) = o;
+}
+
+}  // namespace
+
+int conv_cout_pad(int cout) { return cout <= 32 ? 32 : ((cout + 63) / 64) * 64; }
+
+void launch_conv(const ConvLaunch& c, hipStream_t s) {
+    MVP_REQUIRE(c.Cin % 32 == 0, "conv: Cin=%d must be a multiple of 32", c.Cin);
+    MVP_REQUIRE(c.ks == 1 || c.ks == 3, "conv: ks=%d", c.ks);
+    MVP_REQUIRE(c.stride == 1 || c.stride == 2, "conv: stride=%d", c.stride);
+    MVP_REQUIRE(c.out_f32_nchw || c.Cout % 4 == 0, "conv: Cout=%d must be a multiple of 4", c.Cout);
+    ConvParams p{};
+    p.x = c.x;
+    p.w = c.w;
+    p.bias = c.bias;
+    p.res = c.res;
+    p.y = c.y;
+    p.yf = c.yf;
+    p.N = c.N;
+    p.H = c.H;
+    p.W = c.W;
+    p.Cin = c.Cin;
+    const int pad = c.ks / 2;
+    p.Ho = (c.H + 2 * pad - c.ks) / c.stride + 1;
+    p.Wo = (c.W + 2 * pad - c.ks) / c.stride + 1;
+    p.Cout = c.Cout;
+    p.Cout_pad = conv_cout_pad(c.Cout);
+    p.relu = c.relu;
+    p.out_f32 = c.out_f32_nchw;
+    if (c.N == 0) return;
+    if (c.ks == 3 && c.stride == 1)
+        launch_bm<3, 1>(p, s);
+    else if (c.ks == 3 && c.stride == 2)
+        launch_bm<3, 2>(p, s);
+    else if (c.ks == 1 && c.stride == 1)
+        launch_bm<1, 1>(p, s);
+    else
+        fail(MVP_ERR_ARG, "conv: unsupported ks=%d stride=%d", c.ks, c.stride);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,
+                 hipStream_t s) {
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    const long total = (long)N * Ho * Wo * 4;
+    if (total == 0) return;
+    hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, w, bias, y, N, H, W,
+                       Ho, Wo);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_t* out, int N, int H, int W, int C,
+                     int relu, hipStream_t s) {
+    MVP_REQUIRE(n_in >= 1 && n_in <= 4, "fuse: n_in=%d", n_in);
+    MVP_REQUIRE(C % 8 == 0, "fuse: C=%d", C);
+    FuseParams p{};
+    for (int k = 0; k < n_in; k++) {
+        p.in[k] = in[k];
+        p.up[k] = up[k];
+        MVP_REQUIRE(up[k] >= 1 && H % up[k] == 0 && W % up[k] == 0, "fuse: bad upsample factor %d", up[k]);
+    }
+    p.n_in = n_in;
+    p.out = out;
+    p.N = N;
+    p.H = H;
+    p.W = W;
+    p.C = C;
+    p.relu = relu;
+    const long total = (long)N * H * W * (C / 8);
+    if (total == 0) return;
+    hipLaunchKernelGGL(fuse_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+}  // namespace mvp

@@ -1,0 +1,239 @@
+// Backbone graph runtime: validation, liveness-based arena planning, launch.
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "conv.h"
+#include "mvp_common.h"
+
+namespace mvp {
+namespace {
+
+struct Graph {
+    std::vector<mvp_tensor_desc> tensors;
+    std::vector<mvp_op_desc> ops;
+    int input = -1, output = -1;
+    const uint16_t* wb = nullptr;
+    const float* fb = nullptr;
+    int max_batch = 0;
+    std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
+    int64_t arena_bytes = 0;
+    char* arena = nullptr;
+};
+
+int64_t elem_size(int dtype) { return dtype == MVP_DT_F32_NCHW ? 4 : 2; }
+
+int64_t tensor_bytes(const mvp_tensor_desc& t, int batch) {
+    return (int64_t)batch * t.h * t.w * t.c * elem_size(t.dtype);
+}
+
+void validate(Graph& g, int64_t w_elems, int64_t f_elems) {
+    const int nt = (int)g.tensors.size();
+    auto T = [&](int id) -> const mvp_tensor_desc& {
+        MVP_REQUIRE(id >= 0 && id < nt, "graph: tensor id %d out of range", id);
+        return g.tensors[id];
+    };
+    std::vector<int> defined(nt, 0);
+    defined[g.input] = 1;
+    for (size_t k = 0; k < g.ops.size(); k++) {
+        const mvp_op_desc& op = g.ops[k];
+        const mvp_tensor_desc& o = T(op.out);
+        MVP_REQUIRE(op.n_in >= 1 && op.n_in <= 4, "graph op %zu: n_in=%d", k, op.n_in);
+        for (int i = 0; i < op.n_in; i++) {
+            if (op.kind == MVP_OP_CONV && i == 1 && op.in[1] < 0) continue;
+            T(op.in[i]);
+            MVP_REQUIRE(defined[op.in[i]], "graph op %zu reads tensor %d before it is produced", k, op.in[i]);
+        }
+        MVP_REQUIRE(!defined[op.out], "graph op %zu: tensor %d produced twice", k, op.out);
+        if (op.kind == MVP_OP_STEM) {
+            const mvp_tensor_desc& x = T(op.in[0]);
+            MVP_REQUIRE(x.c == 4 && x.dtype == MVP_DT_BF16_NHWC, "stem: input must be bf16 NHWC with 4 channels");
+            MVP_REQUIRE(o.c == 64 && o.h == (x.h - 1) / 2 + 1 && o.w == (x.w - 1) / 2 + 1, "stem: output shape");
+            MVP_REQUIRE(op.w_off >= 0 && op.w_off + 64 * 36 <= f_elems && op.b_off >= 0 && op.b_off + 64 <= f_elems,
+                        "stem: weights out of the f32 blob");
+        } else if (op.kind == MVP_OP_CONV) {
+            const mvp_tensor_desc& x = T(op.in[0]);
+            const int pad = op.ks / 2;
+            MVP_REQUIRE(op.ks == 1 || op.ks == 3, "conv op %zu: ks", k);
+            MVP_REQUIRE(op.stride == 1 || (op.stride == 2 && op.ks == 3), "conv op %zu: stride", k);
+            MVP_REQUIRE(x.c == op.cin && x.dtype == MVP_DT_BF16_NHWC && op.cin % 32 == 0,
+                        "conv op %zu: input channels %d vs cin %d", k, x.c, op.cin);
+            MVP_REQUIRE(o.c == op.cout && o.h == (x.h + 2 * pad - op.ks) / op.stride + 1 &&
+                            o.w == (x.w + 2 * pad - op.ks) / op.stride + 1,
+                        "conv op %zu: output shape", k);
+            MVP_REQUIRE(o.dtype == MVP_DT_F32_NCHW || op.cout % 4 == 0, "conv op %zu: cout %% 4", k);
+            if (op.n_in > 1 && op.in[1] >= 0) {
+                const mvp_tensor_desc& r = T(op.in[1]);
+                MVP_REQUIRE(r.h == o.h && r.w == o.w && r.c == o.c && r.dtype == MVP_DT_BF16_NHWC &&
+                                o.dtype == MVP_DT_BF16_NHWC,
+                            "conv op %zu: residual shape", k);
+            }
+            const int64_t cp = conv_cout_pad(op.cout);
+            MVP_REQUIRE(op.w_off >= 0 && op.w_off % 8 == 0 && op.w_off + cp * op.ks * op.ks * op.cin <= w_elems,
+                        "conv op %zu: weights out of the bf16 blob", k);
+            MVP_REQUIRE(op.b_off >= 0 && op.b_off % 4 == 0 && op.b_off + cp <= f_elems,
+                        "conv op %zu: bias out of the f32 blob", k);
+        } else if (op.kind == MVP_OP_FUSE) {
+            MVP_REQUIRE(o.dtype == MVP_DT_BF16_NHWC && o.c % 8 == 0, "fuse op %zu: output", k);
+            for (int i = 0; i < op.n_in; i++) {
+                const mvp_tensor_desc& x = T(op.in[i]);
+                const int u = op.up[i];
+                MVP_REQUIRE(u >= 1 && x.c == o.c && x.h * u == o.h && x.w * u == o.w, "fuse op %zu: input %d shape",
+                            k, i);
+            }
+        } else {
+            fail(MVP_ERR_ARG, "graph op %zu: unknown kind %d", k, op.kind);
+        }
+        defined[op.out] = 1;
+    }
+    MVP_REQUIRE(defined[g.output], "graph: output tensor never produced");
+}
+
+// Greedy first-fit placement of tensors in one arena by lifetime [def, last use].
+void plan(Graph& g) {
+    const int nt = (int)g.tensors.size();
+    std::vector<int> first(nt, -1), last(nt, -1);
+    for (int k = 0; k < (int)g.ops.size(); k++) {
+        const mvp_op_desc& op = g.ops[k];
+        first[op.out] = k;
+        if (last[op.out] < k) last[op.out] = k;
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0) last[op.in[i]] = std::max(last[op.in[i]], k);
+    }
+    std::vector<int> order;
+    for (int t = 0; t < nt; t++)
+        if (t != g.input && t != g.output && first[t] >= 0) order.push_back(t);
+    std::sort(order.begin(), order.end(), [&](int a, int b) {
+        return tensor_bytes(g.tensors[a], 1) > tensor_bytes(g.tensors[b], 1);
+    });
+    g.offset.assign(nt, -1);
+    struct Placed {
+        int64_t off, size;
+        int first, last;
+    };
+    std::vector<Placed> placed;
+    int64_t top = 0;
+    for (int t : order) {
+        const int64_t size = (tensor_bytes(g.tensors[t], g.max_batch) + 255) / 256 * 256;
+        // candidate offsets: 0 and the end of every lifetime-overlapping block
+        std::vector<Placed> live;
+        for (const Placed& p : placed)
+            if (!(p.last < first[t] || last[t] < p.first)) live.push_back(p);
+        std::sort(live.begin(), live.end(), [](const Placed& a, const Placed& b) { return a.off < b.off; });
+        int64_t off = 0;
+        for (const Placed& p : live) {
+            if (off + size <= p.off) break;
+            off = std::max(off, p.off + p.size);
+        }
+        placed.push_back({off, size, first[t], last[t]});
+        g.offset[t] = off;
+        top = std::max(top, off + size);
+    }
+    g.arena_bytes = top;
+}
+
+}  // namespace
+}  // namespace mvp
+
+using mvp::Graph;
+
+extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, const mvp_op_desc* ops, int n_ops,
+                                int input_tensor, int output_tensor, const uint16_t* w_dev, int64_t w_elems,
+                                const float* f_dev, int64_t f_elems, int max_batch, void** handle_out) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(handle_out != nullptr, "mvp_graph_create: handle_out is NULL");
+    *handle_out = nullptr;
+    MVP_REQUIRE(tensors && n_tensors > 0 && ops && n_ops > 0, "mvp_graph_create: empty graph");
+    MVP_REQUIRE(input_tensor >= 0 && input_tensor < n_tensors && output_tensor >= 0 && output_tensor < n_tensors &&
+                    input_tensor != output_tensor,
+                "mvp_graph_create: bad input/output tensor ids");
+    MVP_REQUIRE(max_batch > 0, "mvp_graph_create: max_batch must be > 0");
+    Graph* g = new Graph();
+    try {
+        g->tensors.assign(tensors, tensors + n_tensors);
+        g->ops.assign(ops, ops + n_ops);
+        g->input = input_tensor;
+        g->output = output_tensor;
+        g->wb = w_dev;
+        g->fb = f_dev;
+        g->max_batch = max_batch;
+        mvp::validate(*g, w_elems, f_elems);
+        mvp::plan(*g);
+        if (g->arena_bytes > 0) {
+            hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
+            if (e != hipSuccess)
+                mvp::fail(MVP_ERR_NOMEM, "mvp_graph_create: arena of %lld bytes: %s", (long long)g->arena_bytes,
+                          hipGetErrorString(e));
+        }
+    } catch (...) {
+        delete g;
+        throw;
+    }
+    *handle_out = g;
+    MVP_ABI_END
+}
+
+extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* output_dev, void* stream) {
+    MVP_ABI_BEGIN
+    Graph* g = static_cast<Graph*>(handle);
+    MVP_REQUIRE(g != nullptr, "mvp_graph_forward: NULL handle");
+    MVP_REQUIRE(batch >= 0 && batch <= g->max_batch, "mvp_graph_forward: batch %d exceeds max_batch %d", batch,
+                g->max_batch);
+    MVP_REQUIRE(input_dev && output_dev, "mvp_graph_forward: NULL input/output");
+    if (batch == 0) return MVP_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    auto ptr = [&](int t) -> void* {
+        if (t == g->input) return const_cast<void*>(input_dev);
+        if (t == g->output) return output_dev;
+        return g->arena + g->offset[t];
+    };
+    for (const mvp_op_desc& op : g->ops) {
+        const mvp_tensor_desc& o = g->tensors[op.out];
+        if (op.kind == MVP_OP_STEM) {
+            const mvp_tensor_desc& x = g->tensors[op.in[0]];
+            mvp::launch_stem((const uint16_t*)ptr(op.in[0]), g->fb + op.w_off, g->fb + op.b_off,
+                             (uint16_t*)ptr(op.out), batch, x.h, x.w, s);
+        } else if (op.kind == MVP_OP_CONV) {
+            const mvp_tensor_desc& x = g->tensors[op.in[0]];
+            mvp::ConvLaunch c{};
+            c.x = (const uint16_t*)ptr(op.in[0]);
+            c.w = g->wb + op.w_off;
+            c.bias = g->fb + op.b_off;
+            c.res = (op.n_in > 1 && op.in[1] >= 0) ? (const uint16_t*)ptr(op.in[1]) : nullptr;
+            c.out_f32_nchw = o.dtype == MVP_DT_F32_NCHW;
+            c.y = c.out_f32_nchw ? nullptr : (uint16_t*)ptr(op.out);
+            c.yf = c.out_f32_nchw ? (float*)ptr(op.out) : nullptr;
+            c.N = batch;
+            c.H = x.h;
+            c.W = x.w;
+            c.Cin = op.cin;
+            c.Cout = op.cout;
+            c.ks = op.ks;
+            c.stride = op.stride;
+            c.relu = op.relu;
+            mvp::launch_conv(c, s);
+        } else {
+            const uint16_t* ins[4];
+            for (int i = 0; i < op.n_in; i++) ins[i] = (const uint16_t*)ptr(op.in[i]);
+            mvp::launch_fuse_sum(ins, op.up, op.n_in, (uint16_t*)ptr(op.out), batch, o.h, o.w, o.c, op.relu, s);
+        }
+    }
+    MVP_ABI_END
+}
+
+extern "C" int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(handle && bytes_out, "mvp_graph_arena_bytes: NULL argument");
+    *bytes_out = static_cast<Graph*>(handle)->arena_bytes;
+    MVP_ABI_END
+}
+
+extern "C" int mvp_graph_destroy(void* handle) {
+    MVP_ABI_BEGIN
+    Graph* g = static_cast<Graph*>(handle);
+    if (g) {
+        if (g->arena) (void)hipFree(g->arena);
+        delete g;
+    }
+    MVP_ABI_END
+}

@@ -1,0 +1,381 @@
+// 2D-stage kernels around the backbone (gfx950):
+//
+//  * preprocess_kernel — mmpose TopdownAffine + PoseDataPreprocessor for the
+//    whole-frame bbox (reference mmpose_pose_estimation.py:253, bboxes=None
+//    fallback at :246-250): cv2.warpAffine(INTER_LINEAR) of the uint8 frame to
+//    256x192 with OpenCV's fixed-point mapping (AB_BITS 10, INTER_BITS 5) and
+//    integer bilinear weights, then bgr_to_rgb + (x - mean) / std in f32 ->
+//    bf16 NHWC with a zero 4th channel; the horizontally flipped crop for the
+//    flip test is written in the same pass.
+//  * decode_kernel — flip-test average (flip_mode='heatmap', shift_heatmap),
+//    MSRAHeatmap decode (first-occurrence argmax, val<=0 -> -1, +-0.25 sign
+//    refinement inside 1<px<W-1, 1<py<H-1, x4) and the keypoint restore to image
+//    pixels (TopdownPoseEstimator.add_pred_to_datasample).  One wave per map.
+//  * moments_kernel — revert_heatmap (cv2.warpAffine of the 64x48 map to the
+//    full image, float weights) fused with PoseEstimator.get_heatmap_means_cov
+//    (mmpose_pose_estimation.py:163-215): h<0.01 -> 0, normalised mean and
+//    covariance.  The 17 x H x W reverted heatmap is never written: each lane
+//    evaluates the warp for its image pixels from the LDS-resident map and
+//    accumulates fp64 raw moments.
+#include "mvp_common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(uint16_t, b);
+}
+
+// ---------------------------------------------------------------- preprocess
+struct PreParams {
+    const uint8_t* __restrict__ frames;
+    const double* __restrict__ minv;  // [n][6] crop -> image (warpAffine's inverted map)
+    uint16_t* __restrict__ out;
+    int n, H, W, oh, ow, swap_rb, flip;
+    float mean[3], stdv[3];
+};
+
+__global__ __launch_bounds__(kBlock) void preprocess_kernel(PreParams p) {
+    const long gid = (long)blockIdx.x * kBlock + threadIdx.x;
+    const long total = (long)p.n * p.oh * p.ow;
+    if (gid >= total) return;
+    const int x = gid % p.ow;
+    const int y = (gid / p.ow) % p.oh;
+    const int n = gid / ((long)p.ow * p.oh);
+    const double* M = p.minv + 6 * n;
+    // WarpAffineInvoker: X0/Y0 per row, adelta/bdelta per column (cvRound = rint)
+    const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
+    const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
+    const int X = (X0 + (int)rint(M[0] * x * 1024.0)) >> 5;
+    const int Y = (Y0 + (int)rint(M[3] * x * 1024.0)) >> 5;
+    const int sx = X >> 5, sy = Y >> 5, tx = X & 31, ty = Y & 31;
+    const int w[4] = {(32 - ty) * (32 - tx) * 32, (32 - ty) * tx * 32, ty * (32 - tx) * 32, ty * tx * 32};
+    int acc[3] = {0, 0, 0};
+    const uint8_t* img = p.frames + (size_t)n * p.H * p.W * 3;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int xx = sx + (q & 1), yy = sy + (q >> 1);
+        if (xx >= 0 && xx < p.W && yy >= 0 && yy < p.H) {
+            const uint8_t* px = img + ((size_t)yy * p.W + xx) * 3;
+            acc[0] += px[0] * w[q];
+            acc[1] += px[1] * w[q];
+            acc[2] += px[2] * w[q];
+        }
+    }
+    float v[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        int u = (acc[c] + (1 << 14)) >> 15;
+        u = u < 0 ? 0 : (u > 255 ? 255 : u);
+        v[c] = (float)u;
+    }
+    uint16_t o[4];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        const float src = p.swap_rb ? v[2 - c] : v[c];
+        o[c] = f32_to_bf16(__fdiv_rn(src - p.mean[c], p.stdv[c]));
+    }
+    o[3] = 0;
+    uint2 packed;
+    packed.x = (uint32_t)o[0] | ((uint32_t)o[1] << 16);
+    packed.y = (uint32_t)o[2] | ((uint32_t)o[3] << 16);
+    *reinterpret_cast<uint2*>(p.out + (((size_t)n * p.oh + y) * p.ow + x) * 4) = packed;
+    if (p.flip)
+        *reinterpret_cast<uint2*>(p.out + (((size_t)(n + p.n) * p.oh + y) * p.ow + (p.ow - 1 - x)) * 4) = packed;
+}
+
+// ---------------------------------------------------------------- decode
+struct DecodeParams {
+    const float* __restrict__ hm;
+    const float* __restrict__ hmf;  // nullable: flipped-input heatmaps
+    const float* __restrict__ cs;   // [N][4] center x, y, scale w, h
+    float* __restrict__ avg;        // nullable
+    float* __restrict__ kpts;
+    float* __restrict__ scores;
+    int* __restrict__ amax;
+    float* __restrict__ tkv;        // nullable: [N/V][K][3][V] (reference kpts_2d layout)
+    int N, K, H, W, shift, V;
+    int flip_idx[32];
+    double in_w, in_h;
+};
+
+// value of the (flip-averaged) map at (y, x): (h + shifted flipped h) * 0.5 in f32
+__device__ __forceinline__ float avg_at(const DecodeParams& p, const float* h, const float* hf, int y, int x) {
+    const float a = h[y * p.W + x];
+    if (!hf) return a;
+    int xs = x;
+    if (p.shift && x >= 1) xs = x - 1;  // heatmaps[..., 1:] = heatmaps[..., :-1]
+    const float b = hf[y * p.W + (p.W - 1 - xs)];
+    return __fmul_rn(__fadd_rn(a, b), 0.5f);
+}
+
+__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+    // np.argmax: first occurrence of the max; NaN counts as the max (first NaN wins)
+    const bool vn = isnan(v), bn = isnan(bv);
+    if (bn) return vn && i < bi;
+    if (vn) return true;
+    return v > bv || (v == bv && i < bi);
+}
+
+__global__ __launch_bounds__(kBlock) void decode_kernel(DecodeParams p) {
+    const int lane = threadIdx.x & 63;
+    const long map = (long)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (map >= (long)p.N * p.K) return;
+    const int n = map / p.K, k = map % p.K;
+    const int HW = p.H * p.W;
+    const float* h = p.hm + map * HW;
+    const float* hf = p.hmf ? p.hmf + ((long)n * p.K + p.flip_idx[k]) * HW : nullptr;
+    float* av = p.avg ? p.avg + map * HW : nullptr;
+    float bv = 0.f;
+    int bi = 0x7fffffff;
+    for (int i = lane; i < HW; i += 64) {
+        const int y = i / p.W, x = i - (i / p.W) * p.W;
+        const float v = avg_at(p, h, hf, y, x);
+        if (av) av[i] = v;
+        if (bi == 0x7fffffff || better(v, i, bv, bi)) {
+            bv = v;
+            bi = i;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const float ov = __shfl_xor(bv, off);
+        const int oi = __shfl_xor(bi, off);
+        if (oi != 0x7fffffff && (bi == 0x7fffffff || better(ov, oi, bv, bi))) {
+            bv = ov;
+            bi = oi;
+        }
+    }
+    if (lane != 0) return;
+    const int py = bi / p.W, px = bi - (bi / p.W) * p.W;
+    float kx = (float)px, ky = (float)py;
+    if (!(bv > 0.f)) {  // locs[vals <= 0.] = -1 (NaN > 0 is false but NaN <= 0 is false too)
+        if (!isnan(bv)) {
+            kx = -1.f;
+            ky = -1.f;
+        }
+    }
+    const int ipx = (int)kx, ipy = (int)ky;
+    if (1 < ipx && ipx < p.W - 1 && 1 < ipy && ipy < p.H - 1) {
+        const float dx = __fsub_rn(avg_at(p, h, hf, ipy, ipx + 1), avg_at(p, h, hf, ipy, ipx - 1));
+        const float dy = __fsub_rn(avg_at(p, h, hf, ipy + 1, ipx), avg_at(p, h, hf, ipy - 1, ipx));
+        const float sgx = dx > 0.f ? 1.f : (dx < 0.f ? -1.f : (isnan(dx) ? dx : 0.f));
+        const float sgy = dy > 0.f ? 1.f : (dy < 0.f ? -1.f : (isnan(dy) ? dy : 0.f));
+        kx = __fadd_rn(kx, __fmul_rn(sgx, 0.25f));
+        ky = __fadd_rn(ky, __fmul_rn(sgy, 0.25f));
+    }
+    // * scale_factor (input_size / heatmap_size, f32)
+    kx = __fmul_rn(kx, (float)(p.in_w / p.W));
+    ky = __fmul_rn(ky, (float)(p.in_h / p.H));
+    // keypoints / input_size * input_scale + input_center - 0.5 * input_scale (f64, stored f32)
+    const float* cs = p.cs + 4 * n;
+    const double ox = (double)kx / p.in_w * (double)cs[2] + (double)cs[0] - 0.5 * (double)cs[2];
+    const double oy = (double)ky / p.in_h * (double)cs[3] + (double)cs[1] - 0.5 * (double)cs[3];
+    p.kpts[2 * map + 0] = (float)ox;
+    p.kpts[2 * map + 1] = (float)oy;
+    p.scores[map] = bv;
+    if (p.amax) p.amax[map] = bi;
+    if (p.tkv) {  // crops ordered (t, v): pose_estimation.py:135 stacks [x, y, score] per camera on the last axis
+        const int t = n / p.V, v = n - (n / p.V) * p.V;
+        float* o = p.tkv + (((long)t * p.K + k) * 3) * p.V + v;
+        o[0] = (float)ox;
+        o[p.V] = (float)oy;
+        o[2 * p.V] = bv;
+    }
+}
+
+// ---------------------------------------------------------------- moments
+struct MomParams {
+    const float* __restrict__ hm;     // [N][K][h][w] (flip-averaged)
+    const double* __restrict__ minv;  // [N][6] image -> heatmap (warpAffine's inverted map)
+    double* __restrict__ out;         // [N][K][6]
+    int N, K, h, w, img_h, img_w;
+    float thr;
+};
+
+constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
+
+__global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
+    extern __shared__ __attribute__((aligned(16))) float mom_lds[];
+    float* shm = mom_lds;
+    int* sad = reinterpret_cast<int*>(mom_lds + ((p.h * p.w + 3) & ~3));
+    int* sbd = sad + p.img_w;
+    __shared__ double red[6][kBlock / 64];
+    const long map = blockIdx.x;
+    const int n = map / p.K;
+    const double* M = p.minv + 6 * n;
+    const float* src = p.hm + map * p.h * p.w;
+    for (int i = threadIdx.x; i < p.h * p.w; i += kBlock) shm[i] = src[i];
+    for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
+        sad[x] = (int)rint(M[0] * x * 1024.0);
+        sbd[x] = (int)rint(M[3] * x * 1024.0);
+    }
+    __syncthreads();
+    const double cx = 0.5 * p.img_w, cy = 0.5 * p.img_h;  // centred coordinates (cancellation)
+    double s0 = 0, sx = 0, sy = 0, sxx = 0, sxy = 0, syy = 0;
+    for (int y = 0; y < p.img_h; y++) {
+        const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
+        const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
+        const double yc = y - cy;
+        for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
+            const int X = (X0 + sad[x]) >> 5;
+            const int Y = (Y0 + sbd[x]) >> 5;
+            const int ix = X >> 5, iy = Y >> 5;
+            if (ix >= p.w || ix + 1 < 0 || iy >= p.h || iy + 1 < 0) continue;  // border value 0
+            const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+            const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
+            const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
+            const bool x0 = ix >= 0, x1 = ix + 1 < p.w, y0 = iy >= 0, y1 = iy + 1 < p.h;
+            const float v0 = (x0 && y0) ? shm[iy * p.w + ix] : 0.f;
+            const float v1 = (x1 && y0) ? shm[iy * p.w + ix + 1] : 0.f;
+            const float v2 = (x0 && y1) ? shm[(iy + 1) * p.w + ix] : 0.f;
+            const float v3 = (x1 && y1) ? shm[(iy + 1) * p.w + ix + 1] : 0.f;
+            float v = __fmul_rn(v0, w0);
+            v = __fadd_rn(v, __fmul_rn(v1, w1));
+            v = __fadd_rn(v, __fmul_rn(v2, w2));
+            v = __fadd_rn(v, __fmul_rn(v3, w3));
+            if (!(v >= p.thr)) continue;  // heatmaps[heatmaps < 0.01] = 0
+            const double dv = v, xc = x - cx;
+            s0 += dv;
+            sx += xc * dv;
+            sy += yc * dv;
+            sxx += xc * xc * dv;
+            sxy += xc * yc * dv;
+            syy += yc * yc * dv;
+        }
+    }
+    double vals[6] = {s0, sx, sy, sxx, sxy, syy};
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        double v = vals[q];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        vals[q] = v;
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < 6; q++) red[q][wv] = vals[q];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double t[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        t[q] = 0;
+        for (int k = 0; k < kBlock / 64; k++) t[q] += red[q][k];
+    }
+    double* o = p.out + 6 * map;
+    if (t[0] == 0.0) {
+        for (int q = 0; q < 6; q++) o[q] = 0.0;
+        return;
+    }
+    const double mxc = t[1] / t[0], myc = t[2] / t[0];
+    const double vxx = t[3] / t[0] - mxc * mxc;
+    const double vxy = t[4] / t[0] - mxc * myc;
+    const double vyy = t[5] / t[0] - myc * myc;
+    o[0] = mxc + cx;
+    o[1] = myc + cy;
+    o[2] = vxx;
+    o[3] = vxy;
+    o[4] = vxy;
+    o[5] = vyy;
+}
+
+}  // namespace
+
+extern "C" int mvp_preprocess(const uint8_t* frames, int n, int H, int W, const double* minv, int out_h, int out_w,
+                              const float* mean3, const float* std3, int swap_rb, int with_flip, uint16_t* out,
+                              void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n >= 0 && H > 0 && W > 0 && out_h > 0 && out_w > 0, "mvp_preprocess: bad sizes");
+    MVP_REQUIRE(mean3 && std3, "mvp_preprocess: mean/std are NULL");
+    if (n == 0) return MVP_OK;
+    MVP_REQUIRE(frames && minv && out, "mvp_preprocess: NULL device pointer");
+    PreParams p{};
+    p.frames = frames;
+    p.minv = minv;
+    p.out = out;
+    p.n = n;
+    p.H = H;
+    p.W = W;
+    p.oh = out_h;
+    p.ow = out_w;
+    p.swap_rb = swap_rb;
+    p.flip = with_flip;
+    for (int c = 0; c < 3; c++) {
+        p.mean[c] = mean3[c];
+        p.stdv[c] = std3[c];
+    }
+    const long total = (long)n * out_h * out_w;
+    hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), p);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_heatmap_decode(const float* hm, const float* hm_flip, int N, int K, int H, int W,
+                                  const int* flip_idx, int shift, const float* center_scale, int input_w,
+                                  int input_h, float* avg_out, float* kpts, float* scores, int32_t* argmax,
+                                  float* kpts_tkv, int V, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(N >= 0 && K > 0 && K <= 32 && H > 2 && W > 2, "mvp_heatmap_decode: bad sizes");
+    MVP_REQUIRE(input_w > 0 && input_h > 0, "mvp_heatmap_decode: bad input size");
+    if (N == 0) return MVP_OK;
+    MVP_REQUIRE(hm && center_scale && kpts && scores, "mvp_heatmap_decode: NULL device pointer");
+    DecodeParams p{};
+    p.hm = hm;
+    p.hmf = hm_flip;
+    p.cs = center_scale;
+    p.avg = avg_out;
+    p.kpts = kpts;
+    p.scores = scores;
+    p.amax = argmax;
+    p.tkv = kpts_tkv;
+    p.V = V;
+    MVP_REQUIRE(!kpts_tkv || (V > 0 && N % V == 0), "mvp_heatmap_decode: N=%d not a multiple of V=%d", N, V);
+    p.N = N;
+    p.K = K;
+    p.H = H;
+    p.W = W;
+    p.shift = shift;
+    p.in_w = input_w;
+    p.in_h = input_h;
+    for (int k = 0; k < K; k++) {
+        const int f = flip_idx ? flip_idx[k] : k;
+        MVP_REQUIRE(f >= 0 && f < K, "mvp_heatmap_decode: flip_idx[%d]=%d", k, f);
+        p.flip_idx[k] = f;
+    }
+    const long maps = (long)N * K;
+    hipLaunchKernelGGL(decode_kernel, dim3((unsigned)((maps + 3) / 4)), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), p);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, const double* minv, int img_h,
+                                   int img_w, float thr, double* out, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
+    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8;
+    MVP_REQUIRE(lds <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image width %d exceed the LDS budget", h, w,
+                img_w);
+    if (N == 0) return MVP_OK;
+    MVP_REQUIRE(hm && minv && out, "mvp_heatmap_moments: NULL device pointer");
+    MomParams p{};
+    p.hm = hm;
+    p.minv = minv;
+    p.out = out;
+    p.N = N;
+    p.K = K;
+    p.h = h;
+    p.w = w;
+    p.img_h = img_h;
+    p.img_w = img_w;
+    p.thr = thr;
+    hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * K)), dim3(kBlock), lds,
+                       reinterpret_cast<hipStream_t>(stream), p);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}

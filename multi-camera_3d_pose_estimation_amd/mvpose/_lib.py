@@ -40,12 +40,25 @@ SIGNATURES = {
     "mvp_camera_pack": (c_int, [P(c_double), P(c_double), P(c_double), P(c_double), P(c_double)]),
     "mvp_triangulate": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, P(c_int), c_int, c_int,
                                 c_void_p, c_void_p, c_void_p]),
+    "mvp_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, P(c_float), P(c_float),
+                               c_int, c_int, c_void_p, c_void_p]),
+    "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,
+                                   c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                   c_void_p]),
+    "mvp_heatmap_moments": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float,
+                                    c_void_p, c_void_p]),
+    # graph argtypes with struct pointers are (re)declared in mvpose/hrnet.py
+    "mvp_graph_create": (c_int, None),
+    "mvp_graph_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
+    "mvp_graph_arena_bytes": (c_int, None),
+    "mvp_graph_destroy": (c_int, [c_void_p]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
     _fn = getattr(lib, _name)  # AttributeError = library does not export a declared symbol
     _fn.restype = _res
-    _fn.argtypes = _args
+    if _args is not None:
+        _fn.argtypes = _args
 
 ABI_VERSION = 1
 if lib.mvp_abi_version() != ABI_VERSION:

@@ -1,0 +1,107 @@
+"""Batched GPU top-down 2D pose estimation (the reference's PoseEstimator.predict,
+mmpose_pose_estimation.py:222-272, for all cameras x frames of a batch at once).
+
+Per batch of N camera-frames (uint8, device-resident):
+    mvp_preprocess      crop (whole-image bbox) + normalise, original + flipped
+    mvp_graph_forward   HRNet-W32 + HeatmapHead on 2N crops (bf16 MFMA)
+    mvp_heatmap_decode  flip-test average + MSRAHeatmap decode + restore
+    mvp_heatmap_moments revert_heatmap + get_heatmap_means_cov
+All on one stream; no host synchronisation inside `run`.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import geometry
+from ._lib import call
+from .hrnet import HEATMAP_HW, INPUT_HW, N_JOINTS, HRNetBackbone
+
+MEAN = np.array([123.675, 116.28, 103.53], np.float32)   # PoseDataPreprocessor (RGB order)
+STD = np.array([58.395, 57.12, 57.375], np.float32)
+COCO_FLIP_INDICES = [0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15]
+HEATMAP_THR = 0.01  # get_heatmap_means_cov threshold (mmpose_pose_estimation.py:166)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+class BatchPoseEstimator:
+    """GPU equivalent of PoseEstimator (mmpose_pose_estimation.py:81-272) without
+    the detector: every frame uses the whole-image bbox, which is what the
+    reference falls back to when RTMDet finds no person (:246-250)."""
+
+    def __init__(self, state_dict=None, seed: int = 0, max_frames: int = 256, frame_hw=(720, 1280),
+                 flip_test: bool = True, device="cuda"):
+        self.device = torch.device(device)
+        self.flip_test = flip_test
+        self.max_frames = int(max_frames)
+        self.frame_h, self.frame_w = frame_hw
+        self.backbone = HRNetBackbone(state_dict, seed=seed,
+                                      max_batch=self.max_frames * (2 if flip_test else 1), device=device)
+        geo = geometry.CropGeometry.whole_image(self.frame_w, self.frame_h)
+        self.geometry = geo
+        n = self.max_frames
+        self.crop_minv = torch.tensor(np.tile(geo.crop_minv, (n, 1)), dtype=torch.float64, device=self.device)
+        self.revert_minv = torch.tensor(np.tile(geo.revert_minv, (n, 1)), dtype=torch.float64, device=self.device)
+        self.center_scale = torch.tensor(np.tile(geo.center_scale, (n, 1)), dtype=torch.float32, device=self.device)
+        nc = n * (2 if flip_test else 1)
+        self.crops = torch.empty((nc, INPUT_HW[0], INPUT_HW[1], 4), dtype=torch.bfloat16, device=self.device)
+        self.heatmaps = torch.empty((nc, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=self.device)
+        self.avg = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=self.device)
+        self._mean = (ctypes.c_float * 3)(*MEAN)
+        self._std = (ctypes.c_float * 3)(*STD)
+        self._flip = (ctypes.c_int * N_JOINTS)(*COCO_FLIP_INDICES)
+
+    def run(self, frames: torch.Tensor, n_views: int = 1, kpts_tkv: torch.Tensor | None = None,
+            argmax: bool = False):
+        """frames: (N, H, W, 3) uint8 on the GPU, ordered (t, v) when n_views > 1.
+        Returns dict: keypoints (N,17,2) f32 image px, scores (N,17) f32,
+        gaussians (N,17,6) f64 [mx,my,vxx,vxy,vxy,vyy], and optionally argmax."""
+        if frames.dtype != torch.uint8 or not frames.is_cuda or not frames.is_contiguous():
+            raise ValueError("frames must be a contiguous uint8 CUDA tensor (N, H, W, 3)")
+        n, h, w, c = frames.shape
+        if (h, w, c) != (self.frame_h, self.frame_w, 3):
+            raise ValueError(f"frames must be (N, {self.frame_h}, {self.frame_w}, 3), got {tuple(frames.shape)}")
+        if n > self.max_frames:
+            raise ValueError(f"{n} frames > max_frames {self.max_frames}")
+        dev, s = self.device, _stream(self.device)
+        nc = n * (2 if self.flip_test else 1)
+        crops = self.crops[:nc]
+        call("mvp_preprocess", _ptr(frames), n, h, w, _ptr(self.crop_minv), INPUT_HW[0], INPUT_HW[1], self._mean,
+             self._std, 1, int(self.flip_test), _ptr(crops), s)
+        hm = self.backbone.forward(crops, out=self.heatmaps[:nc])
+        kp = torch.empty((n, N_JOINTS, 2), dtype=torch.float32, device=dev)
+        sc = torch.empty((n, N_JOINTS), dtype=torch.float32, device=dev)
+        am = torch.empty((n, N_JOINTS), dtype=torch.int32, device=dev) if argmax else None
+        avg = self.avg[:n]
+        call("mvp_heatmap_decode", _ptr(hm[:n]), _ptr(hm[n:]) if self.flip_test else None, n, N_JOINTS,
+             HEATMAP_HW[0], HEATMAP_HW[1], self._flip, 1, _ptr(self.center_scale), INPUT_HW[1], INPUT_HW[0],
+             _ptr(avg), _ptr(kp), _ptr(sc), _ptr(am), _ptr(kpts_tkv), int(n_views), s)
+        gauss = torch.empty((n, N_JOINTS, 6), dtype=torch.float64, device=dev)
+        call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(self.revert_minv),
+             h, w, ctypes.c_float(HEATMAP_THR), _ptr(gauss), s)
+        out = {"keypoints": kp, "scores": sc, "gaussians": gauss, "heatmaps": avg}
+        if argmax:
+            out["argmax"] = am
+        return out
+
+    # ---- the reference's per-frame callable contract (pose_estimation.py:88, :104-110)
+    def predict(self, frame, return_full_heatmaps=False):
+        """Single frame (H, W, 3) uint8 numpy/tensor -> (pred_instances, heatmaps (17,6) f64)
+        with pred_instances['keypoints'] (1,17,2) f32 and ['keypoint_scores'] (1,17) f32."""
+        f = torch.as_tensor(np.ascontiguousarray(frame), device=self.device).reshape(1, *np.shape(frame))
+        r = self.run(f.contiguous())
+        inst = {"keypoints": r["keypoints"].cpu().numpy(), "keypoint_scores": r["scores"].cpu().numpy()}
+        if return_full_heatmaps:
+            return inst, r["heatmaps"][0].cpu().numpy()
+        return inst, r["gaussians"][0].cpu().numpy()
+
+    __call__ = predict

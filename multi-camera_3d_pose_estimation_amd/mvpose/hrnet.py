@@ -1,0 +1,337 @@
+"""HRNet-W32 (COCO, 256x192) as a static op graph for the libmvpose backbone runtime.
+
+The reference runs this network inside mmpose's inference_topdown
+(mmpose_pose_estimation.py:253, config td-hm_hrnet-w32_8xb64-210e_coco-256x192,
+built at pose_estimation.py:290-297) on the CPU at batch 1.  Here the host
+walks the same topology (mmpose HRNet: stem, layer1 Bottlenecks, transitions,
+HRModules with BasicBlock branches and multi-scale fuse layers, HeatmapHead),
+folds every BatchNorm into its conv (fp64, then bf16 weights / f32 biases),
+packs all weights into two device blobs and hands the graph to
+mvp_graph_create.  Parameter names are mmpose's, so a converted mmpose
+checkpoint (state dict) loads directly; without network access the bench uses
+`random_state_dict(seed)` (He-normal convs, randomised BN statistics).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call
+
+BN_EPS = 1e-5
+STAGES = ((1, (32, 64)), (4, (32, 64, 128)), (3, (32, 64, 128, 256)))
+N_JOINTS = 17
+INPUT_HW = (256, 192)
+HEATMAP_HW = (64, 48)
+DT_BF16, DT_F32 = 0, 1
+OP_STEM, OP_CONV, OP_FUSE = 0, 1, 2
+
+
+class TensorDesc(ctypes.Structure):
+    _fields_ = [("h", ctypes.c_int), ("w", ctypes.c_int), ("c", ctypes.c_int), ("dtype", ctypes.c_int)]
+
+
+class OpDesc(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("out", ctypes.c_int), ("n_in", ctypes.c_int),
+                ("in_", ctypes.c_int * 4), ("up", ctypes.c_int * 4), ("cin", ctypes.c_int),
+                ("cout", ctypes.c_int), ("ks", ctypes.c_int), ("stride", ctypes.c_int), ("relu", ctypes.c_int),
+                ("w_off", ctypes.c_int64), ("b_off", ctypes.c_int64)]
+
+
+_lib.lib.mvp_graph_create.argtypes = [ctypes.POINTER(TensorDesc), ctypes.c_int, ctypes.POINTER(OpDesc), ctypes.c_int,
+                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+_lib.lib.mvp_graph_arena_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
+
+
+def cout_pad(c: int) -> int:
+    return 32 if c <= 32 else (c + 63) // 64 * 64
+
+
+# ------------------------------------------------------------------ weights --
+def _conv_shapes():
+    """(conv_key, bn_key or None, cout, cin, k) for every conv, mmpose naming."""
+    out = [("backbone.conv1", "backbone.bn1", 64, 3, 3), ("backbone.conv2", "backbone.bn2", 64, 64, 3)]
+    cin = 64
+    for b in range(4):
+        p = f"backbone.layer1.{b}"
+        out += [(f"{p}.conv1", f"{p}.bn1", 64, cin, 1), (f"{p}.conv2", f"{p}.bn2", 64, 64, 3),
+                (f"{p}.conv3", f"{p}.bn3", 256, 64, 1)]
+        if b == 0:
+            out.append((f"{p}.downsample.0", f"{p}.downsample.1", 256, cin, 1))
+        cin = 256
+    pre = [256]
+    for s, (n_mod, chans) in enumerate(STAGES):
+        for i, c in enumerate(chans):
+            if i < len(pre):
+                if c != pre[i]:
+                    out.append((f"backbone.transition{s + 1}.{i}.0", f"backbone.transition{s + 1}.{i}.1", c, pre[i], 3))
+            else:
+                out.append((f"backbone.transition{s + 1}.{i}.0.0", f"backbone.transition{s + 1}.{i}.0.1", c, pre[-1], 3))
+        for m in range(n_mod):
+            p = f"backbone.stage{s + 2}.{m}"
+            for bi, c in enumerate(chans):
+                for k in range(4):
+                    q = f"{p}.branches.{bi}.{k}"
+                    out += [(f"{q}.conv1", f"{q}.bn1", c, c, 3), (f"{q}.conv2", f"{q}.bn2", c, c, 3)]
+            last = s == len(STAGES) - 1 and m == n_mod - 1
+            n_out = 1 if last else len(chans)
+            for i in range(n_out):
+                for j in range(len(chans)):
+                    if j > i:
+                        out.append((f"{p}.fuse_layers.{i}.{j}.0", f"{p}.fuse_layers.{i}.{j}.1", chans[i], chans[j], 1))
+                    elif j < i:
+                        for k in range(i - j):
+                            co = chans[i] if k == i - j - 1 else chans[j]
+                            out.append((f"{p}.fuse_layers.{i}.{j}.{k}.0", f"{p}.fuse_layers.{i}.{j}.{k}.1", co,
+                                        chans[j], 3))
+        pre = list(chans)
+    out.append(("head.final_layer", None, N_JOINTS, 32, 1))
+    return out
+
+
+def random_state_dict(seed: int = 0):
+    """Seeded weights in mmpose naming: He-normal convs, BN with randomised affine
+    and running statistics (so folding is exercised), head bias ~ N(0, 0.1)."""
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for conv, bn, cout, cin, k in _conv_shapes():
+        std = (2.0 / (cin * k * k)) ** 0.5
+        sd[conv + ".weight"] = torch.randn((cout, cin, k, k), generator=g) * std
+        if bn is None:
+            sd[conv + ".bias"] = torch.randn((cout,), generator=g) * 0.1
+        else:
+            sd[bn + ".weight"] = 1.0 + 0.1 * torch.randn((cout,), generator=g)
+            sd[bn + ".bias"] = 0.1 * torch.randn((cout,), generator=g)
+            sd[bn + ".running_mean"] = 0.1 * torch.randn((cout,), generator=g)
+            sd[bn + ".running_var"] = 1.0 + 0.2 * torch.rand((cout,), generator=g)
+            sd[bn + ".num_batches_tracked"] = torch.tensor(0)
+    return sd
+
+
+def fold_bn(sd, conv, bn):
+    """conv weight (cout,cin,k,k) + eval BatchNorm -> (w (cout,k,k,cin) f64, b (cout,) f64)."""
+    w = sd[conv + ".weight"].double().numpy()
+    if bn is None:
+        scale = np.ones(w.shape[0])
+        shift = sd[conv + ".bias"].double().numpy()
+    else:
+        gamma = sd[bn + ".weight"].double().numpy()
+        beta = sd[bn + ".bias"].double().numpy()
+        mean = sd[bn + ".running_mean"].double().numpy()
+        var = sd[bn + ".running_var"].double().numpy()
+        scale = gamma / np.sqrt(var + BN_EPS)
+        shift = beta - mean * scale
+    w = w * scale[:, None, None, None]
+    return np.ascontiguousarray(w.transpose(0, 2, 3, 1)), shift
+
+
+def to_bf16_bits(a: np.ndarray) -> np.ndarray:
+    """fp64/fp32 -> bf16 bit patterns, round to nearest even."""
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+
+
+# ------------------------------------------------------------------ graph --
+class GraphSpec:
+    """Host-side description: tensors, ops, weight blobs (numpy)."""
+
+    def __init__(self):
+        self.tensors: list[tuple[int, int, int, int]] = []
+        self.ops: list[dict] = []
+        self._w: list[np.ndarray] = []
+        self._f: list[np.ndarray] = []
+        self._w_len = 0
+        self._f_len = 0
+
+    def tensor(self, h, w, c, dtype=DT_BF16) -> int:
+        self.tensors.append((h, w, c, dtype))
+        return len(self.tensors) - 1
+
+    def _push_w(self, a_bits: np.ndarray) -> int:
+        off = self._w_len
+        self._w.append(a_bits.ravel())
+        self._w_len += a_bits.size
+        return off
+
+    def _push_f(self, a: np.ndarray) -> int:
+        off = self._f_len
+        a = np.asarray(a, np.float32).ravel()
+        pad = (-a.size) % 4
+        if pad:
+            a = np.concatenate([a, np.zeros(pad, np.float32)])
+        self._f.append(a)
+        self._f_len += a.size
+        return off
+
+    def stem(self, sd, conv, bn, x) -> int:
+        w, b = fold_bn(sd, conv, bn)  # (64, 3, 3, 3)
+        w4 = np.zeros((64, 3, 3, 4))
+        w4[..., :3] = w
+        h, ww, _, _ = self.tensors[x]
+        y = self.tensor((h - 1) // 2 + 1, (ww - 1) // 2 + 1, 64)
+        self.ops.append(dict(kind=OP_STEM, out=y, ins=[x], up=[1], cin=4, cout=64, ks=3, stride=2, relu=1,
+                             w_off=self._push_f(w4), b_off=self._push_f(b)))
+        return y
+
+    def conv(self, sd, conv, bn, x, stride, relu, res=None, out_dtype=DT_BF16) -> int:
+        w, b = fold_bn(sd, conv, bn)
+        cout, k, _, cin = w.shape
+        cp = cout_pad(cout)
+        wp = np.zeros((cp, k, k, cin))
+        wp[:cout] = w
+        bp = np.zeros(cp)
+        bp[:cout] = b
+        h, ww, c, _ = self.tensors[x]
+        assert c == cin, (conv, c, cin)
+        pad = k // 2
+        y = self.tensor((h + 2 * pad - k) // stride + 1, (ww + 2 * pad - k) // stride + 1, cout, out_dtype)
+        self.ops.append(dict(kind=OP_CONV, out=y, ins=[x] + ([res] if res is not None else []), up=[1, 1],
+                             cin=cin, cout=cout, ks=k, stride=stride, relu=int(relu),
+                             w_off=self._push_w(to_bf16_bits(wp)), b_off=self._push_f(bp)))
+        return y
+
+    def fuse(self, terms, relu=True) -> int:
+        (x0, u0) = terms[0]
+        h, w, c, _ = self.tensors[x0]
+        y = self.tensor(h * u0, w * u0, c)
+        self.ops.append(dict(kind=OP_FUSE, out=y, ins=[t for t, _ in terms], up=[u for _, u in terms], cin=c,
+                             cout=c, ks=0, stride=0, relu=int(relu), w_off=0, b_off=0))
+        return y
+
+    def blobs(self):
+        w = np.concatenate(self._w) if self._w else np.zeros(8, np.uint16)
+        f = np.concatenate(self._f) if self._f else np.zeros(4, np.float32)
+        return w, f
+
+
+def build_hrnet_w32(sd) -> tuple[GraphSpec, int, int]:
+    """Walk mmpose's HRNet-W32 + HeatmapHead forward order; returns (spec, input id, output id)."""
+    g = GraphSpec()
+    x_in = g.tensor(INPUT_HW[0], INPUT_HW[1], 4)
+    x = g.stem(sd, "backbone.conv1", "backbone.bn1", x_in)
+    x = g.conv(sd, "backbone.conv2", "backbone.bn2", x, 2, True)
+    for b in range(4):
+        p = f"backbone.layer1.{b}"
+        idn = g.conv(sd, f"{p}.downsample.0", f"{p}.downsample.1", x, 1, False) if b == 0 else x
+        y = g.conv(sd, f"{p}.conv1", f"{p}.bn1", x, 1, True)
+        y = g.conv(sd, f"{p}.conv2", f"{p}.bn2", y, 1, True)
+        x = g.conv(sd, f"{p}.conv3", f"{p}.bn3", y, 1, True, res=idn)
+    ys = [x]
+    pre = [256]
+    for s, (n_mod, chans) in enumerate(STAGES):
+        xs = []
+        for i, c in enumerate(chans):
+            if i < len(pre) and c == pre[i]:
+                xs.append(ys[i])
+            elif i < len(pre):
+                xs.append(g.conv(sd, f"backbone.transition{s + 1}.{i}.0", f"backbone.transition{s + 1}.{i}.1",
+                                 ys[-1], 1, True))
+            else:
+                xs.append(g.conv(sd, f"backbone.transition{s + 1}.{i}.0.0", f"backbone.transition{s + 1}.{i}.0.1",
+                                 ys[-1], 2, True))
+        for m in range(n_mod):
+            p = f"backbone.stage{s + 2}.{m}"
+            for bi in range(len(chans)):
+                for k in range(4):
+                    q = f"{p}.branches.{bi}.{k}"
+                    y = g.conv(sd, f"{q}.conv1", f"{q}.bn1", xs[bi], 1, True)
+                    xs[bi] = g.conv(sd, f"{q}.conv2", f"{q}.bn2", y, 1, True, res=xs[bi])
+            last = s == len(STAGES) - 1 and m == n_mod - 1
+            n_out = 1 if last else len(chans)
+            outs = []
+            for i in range(n_out):
+                terms = []
+                for j in range(len(chans)):
+                    if j == i:
+                        terms.append((xs[j], 1))
+                    elif j > i:
+                        t = g.conv(sd, f"{p}.fuse_layers.{i}.{j}.0", f"{p}.fuse_layers.{i}.{j}.1", xs[j], 1, False)
+                        terms.append((t, 2 ** (j - i)))
+                    else:
+                        t = xs[j]
+                        for k in range(i - j):
+                            t = g.conv(sd, f"{p}.fuse_layers.{i}.{j}.{k}.0", f"{p}.fuse_layers.{i}.{j}.{k}.1", t, 2,
+                                       k != i - j - 1)
+                        terms.append((t, 1))
+                outs.append(g.fuse(terms))
+            xs = outs
+        ys = xs
+        pre = list(chans)
+    out = g.conv(sd, "head.final_layer", None, ys[0], 1, False, out_dtype=DT_F32)
+    return g, x_in, out
+
+
+class HRNetBackbone:
+    """Device-resident HRNet-W32 + head on the libmvpose graph runtime.
+
+    forward(crops (N,256,192,4) bf16 on GPU) -> heatmaps (N,17,64,48) f32."""
+
+    def __init__(self, state_dict=None, seed: int = 0, max_batch: int = 256, device="cuda"):
+        if state_dict is None:
+            state_dict = random_state_dict(seed)
+        spec, self.input_id, self.output_id = build_hrnet_w32(state_dict)
+        self.spec = spec
+        w, f = spec.blobs()
+        self.device = torch.device(device)
+        self.w_dev = torch.from_numpy(w.view(np.int16).copy()).to(self.device)
+        self.f_dev = torch.from_numpy(f).to(self.device)
+        self.max_batch = int(max_batch)
+        tens = (TensorDesc * len(spec.tensors))(*[TensorDesc(*t) for t in spec.tensors])
+        ops = (OpDesc * len(spec.ops))()
+        for k, op in enumerate(spec.ops):
+            d = ops[k]
+            d.kind, d.out, d.n_in = op["kind"], op["out"], len(op["ins"])
+            for i in range(4):
+                d.in_[i] = op["ins"][i] if i < len(op["ins"]) else -1
+                d.up[i] = op["up"][i] if i < len(op["up"]) else 1
+            d.cin, d.cout, d.ks, d.stride, d.relu = op["cin"], op["cout"], op["ks"], op["stride"], op["relu"]
+            d.w_off, d.b_off = op["w_off"], op["b_off"]
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            call("mvp_graph_create", tens, len(spec.tensors), ops, len(spec.ops), self.input_id, self.output_id,
+                 ctypes.c_void_p(self.w_dev.data_ptr()), self.w_dev.numel(), ctypes.c_void_p(self.f_dev.data_ptr()),
+                 self.f_dev.numel(), self.max_batch, ctypes.byref(h))
+        self._h = h
+
+    @property
+    def arena_bytes(self) -> int:
+        b = ctypes.c_int64()
+        call("mvp_graph_arena_bytes", self._h, ctypes.byref(b))
+        return b.value
+
+    def macs_per_crop(self) -> int:
+        macs = 0
+        for op in self.spec.ops:
+            if op["kind"] in (OP_STEM, OP_CONV):
+                h, w, _, _ = self.spec.tensors[op["out"]]
+                cin = 3 if op["kind"] == OP_STEM else op["cin"]
+                macs += h * w * op["cout"] * cin * op["ks"] ** 2
+        return macs
+
+    def forward(self, crops: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if crops.dtype != torch.bfloat16 or not crops.is_cuda or not crops.is_contiguous():
+            raise ValueError("crops must be a contiguous bf16 CUDA tensor (N,256,192,4)")
+        if tuple(crops.shape[1:]) != (INPUT_HW[0], INPUT_HW[1], 4):
+            raise ValueError(f"crops must be (N,{INPUT_HW[0]},{INPUT_HW[1]},4), got {tuple(crops.shape)}")
+        n = crops.shape[0]
+        if n > self.max_batch:
+            raise ValueError(f"batch {n} > max_batch {self.max_batch}")
+        if out is None:
+            out = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=crops.device)
+        call("mvp_graph_forward", self._h, ctypes.c_void_p(crops.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+             ctypes.c_void_p(torch.cuda.current_stream(crops.device).cuda_stream))
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            call("mvp_graph_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,54 @@
+"""Multi-view 2D -> 3D pipeline on one GPU: the reference's
+estimate_pose_from_video / run_pose_est / get_pose_2D / get_pose_3D loop
+(pose_estimation.py:157-327) for a whole batch of synchronised frames at once.
+
+process(frames (T, V, H, W, 3) uint8 on GPU) returns, device-resident:
+    kpts_2d     (T, 17, 3, V) float32   [x, y, score] per camera   (pose_estimation.py:135)
+    heatmaps_2d (T, V, 17, 6) float64   [mx, my, vxx, vxy, vxy, vyy] (mmpose_pose_estimation.py:208-210)
+    kpts_3d     (T, 17, 3)    float32   triangulated                 (pose_estimation.py:319-322)
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import ops
+from .estimator import BatchPoseEstimator
+from .hrnet import N_JOINTS
+
+
+class MultiViewPipeline:
+    def __init__(self, camera_params, estimator: BatchPoseEstimator | None = None, camera_indices=(0, 1),
+                 mode: int = ops.TRI_REFERENCE, device="cuda", **estimator_kw):
+        """camera_params: {camera key: [K, R, T, dist]} (utils.get_params_from_name order),
+        keys 0..V-1 as the reference assumes (pose_estimation.py:276-280)."""
+        self.device = torch.device(device)
+        self.n_views = len(camera_params)
+        self.cams = torch.tensor(ops.pack_cameras(camera_params), device=self.device)
+        self.camera_indices = list(camera_indices)
+        self.mode = mode
+        self.estimator = estimator or BatchPoseEstimator(device=device, **estimator_kw)
+
+    @property
+    def max_frames(self) -> int:
+        return self.estimator.max_frames // self.n_views
+
+    def process(self, frames: torch.Tensor, out: dict | None = None) -> dict:
+        T, V = frames.shape[:2]
+        if V != self.n_views:
+            raise ValueError(f"frames carry {V} views, pipeline has {self.n_views} cameras")
+        flat = frames.reshape(T * V, *frames.shape[2:])
+        if out is None:
+            out = {"kpts_2d": torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)}
+        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"])
+        out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
+        out["kpts_3d"] = ops.triangulate(out["kpts_2d"], self.cams, self.camera_indices, mode=self.mode,
+                                         out=out.get("kpts_3d"))
+        return out
+
+    def process_stream(self, frames: torch.Tensor) -> dict:
+        """Arbitrary-length sequence (T, V, H, W, 3): chunked to the estimator's batch."""
+        T = frames.shape[0]
+        step = self.max_frames
+        parts = [self.process(frames[t:t + step]) for t in range(0, T, step)]
+        return {k: torch.cat([p[k] for p in parts]) for k in parts[0]}

@@ -19,6 +19,7 @@ World units are cm (the reference's calibration units).
 from __future__ import annotations
 
 import numpy as np
+from scipy.signal import lfilter
 
 FRAME_W, FRAME_H = 1280, 720
 N_JOINTS = 17
@@ -84,8 +85,11 @@ def make_rig(n_cams: int, seed: int = 0, distortion: bool = True):
 def make_poses(n_frames: int, seed: int = 0, jitter: float = 5.0):
     """(T, 17, 3) float64 world-space poses (cm)."""
     rng = np.random.default_rng(seed)
-    root = SUBJECT_CENTER + np.cumsum(rng.normal(0.0, 1.0, (n_frames, 3)), axis=0) * np.array([1.0, 0.2, 1.0])
-    yaw = np.cumsum(rng.normal(0.0, 0.02, n_frames))
+    # mean-reverting (AR(1)) root walk: stays within ~+-40 cm of the subject centre
+    # for any sequence length, so long benches keep the same geometry
+    steps = rng.normal(0.0, 2.0, (n_frames, 3)) * np.array([1.0, 0.2, 1.0])
+    root = SUBJECT_CENTER + lfilter([1.0], [1.0, -0.98], steps, axis=0)
+    yaw = lfilter([1.0], [1.0, -0.995], rng.normal(0.0, 0.02, n_frames))
     out = np.empty((n_frames, N_JOINTS, 3))
     for t in range(n_frames):
         c, s = np.cos(yaw[t]), np.sin(yaw[t])

@@ -1,0 +1,146 @@
+"""GPU parity of the 2D-stage kernels vs the oracle / golden vectors:
+preprocess (bit-exact bf16), heatmap decode (argmax bit-exact), moments
+(reference get_heatmap_means_cov golden, fp32-summation tolerance)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import heatmap_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import _lib, geometry
+    return _lib, geometry
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def test_preprocess_bit_exact(lib):
+    _lib, geometry = lib
+    rng = np.random.default_rng(0)
+    frames = rng.integers(0, 256, (3, 720, 1280, 3), dtype=np.uint8)
+    g = geometry.CropGeometry.whole_image(1280, 720)
+    fd = torch.tensor(frames, device="cuda")
+    minv = torch.tensor(np.tile(g.crop_minv, (3, 1)), device="cuda")
+    out = torch.empty((6, 256, 192, 4), dtype=torch.bfloat16, device="cuda")
+    mean = (ctypes.c_float * 3)(*heatmap_ref.MEAN_RGB)
+    std = (ctypes.c_float * 3)(*heatmap_ref.STD_RGB)
+    _lib.call("mvp_preprocess", _p(fd), 3, 720, 1280, _p(minv), 256, 192, mean, std, 1, 1, _p(out), _s())
+    torch.cuda.synchronize()
+    M, _, _ = heatmap_ref.topdown_crop_matrix(1280, 720)
+    o = out.float().cpu().numpy()
+    for i in range(3):
+        ref = heatmap_ref.preprocess(frames[i], M)  # (3, 256, 192) f32
+        ref_bf = torch.tensor(ref).bfloat16().float().numpy()
+        np.testing.assert_array_equal(o[i, :, :, :3], np.moveaxis(ref_bf, 0, -1))
+        np.testing.assert_array_equal(o[i + 3, :, :, :3], np.moveaxis(ref_bf, 0, -1)[:, ::-1])
+        assert (o[i, :, :, 3] == 0).all()
+
+
+def _planted_heatmaps(rng, n, K=17, H=64, W=48):
+    hm = rng.normal(0, 0.05, (n, K, H, W)).astype(np.float32)
+    for i in range(n):
+        for k in range(K):
+            y, x = rng.integers(0, H), rng.integers(0, W)
+            hm[i, k, y, x] += rng.uniform(0.5, 1.0)
+    hm[0, 0] = 0.25                      # all-equal map -> first occurrence
+    hm[0, 1, 10, 10] = hm[0, 1, 20, 5] = 5.0  # exact tie
+    hm[0, 2] = -0.5                      # max <= 0 -> (-1, -1)
+    hm[0, 3, 0, 0] = 9.0                 # max on the border -> no refinement
+    return hm
+
+
+def test_decode_vs_oracle(lib):
+    _lib, geometry = lib
+    rng = np.random.default_rng(1)
+    n = 8
+    hm = _planted_heatmaps(rng, n)
+    hmf = _planted_heatmaps(rng, n)
+    g = geometry.CropGeometry.whole_image(1280, 720)
+    cs = torch.tensor(np.tile(g.center_scale, (n, 1)), device="cuda")
+    hd, hfd = torch.tensor(hm, device="cuda"), torch.tensor(hmf, device="cuda")
+    avg = torch.empty_like(hd)
+    kp = torch.empty((n, 17, 2), device="cuda")
+    sc = torch.empty((n, 17), device="cuda")
+    am = torch.empty((n, 17), dtype=torch.int32, device="cuda")
+    tkv = torch.empty((n // 2, 17, 3, 2), device="cuda")
+    flip = (ctypes.c_int * 17)(*heatmap_ref.COCO_FLIP_INDICES)
+    _lib.call("mvp_heatmap_decode", _p(hd), _p(hfd), n, 17, 64, 48, flip, 1, _p(cs), 192, 256, _p(avg), _p(kp),
+              _p(sc), _p(am), _p(tkv), 2, _s())
+    torch.cuda.synchronize()
+    ref_avg = heatmap_ref.flip_test_average(hm, hmf)
+    np.testing.assert_array_equal(avg.cpu().numpy(), ref_avg)
+    for i in range(n):
+        rk, rs, ri = heatmap_ref.msra_decode(ref_avg[i])
+        np.testing.assert_array_equal(am[i].cpu().numpy(), ri)
+        np.testing.assert_array_equal(sc[i].cpu().numpy(), rs)
+        img = heatmap_ref.keypoints_to_image(rk, g.center, g.scale)
+        np.testing.assert_array_equal(kp[i].cpu().numpy(), img)
+    t = tkv.cpu().numpy()
+    k_np, s_np = kp.cpu().numpy(), sc.cpu().numpy()
+    for i in range(n):
+        np.testing.assert_array_equal(t[i // 2, :, :2, i % 2], k_np[i])
+        np.testing.assert_array_equal(t[i // 2, :, 2, i % 2], s_np[i])
+
+
+def _moments(_lib, hm, minv, img_h, img_w):
+    N, K, h, w = hm.shape
+    hd = torch.tensor(np.ascontiguousarray(hm), device="cuda")
+    md = torch.tensor(np.tile(minv, (N, 1)), device="cuda")
+    out = torch.empty((N, K, 6), dtype=torch.float64, device="cuda")
+    _lib.call("mvp_heatmap_moments", _p(hd), N, K, h, w, _p(md), img_h, img_w, ctypes.c_float(0.01), _p(out), _s())
+    torch.cuda.synchronize()
+    return out.cpu().numpy()
+
+
+def _check_moments(out, ref):
+    # reference sums 1e4-1e6 f32 terms (numpy / torch pairwise): ~1e-6 relative
+    np.testing.assert_allclose(out[:, :2], ref[:, :2], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(out[:, 2:], ref[:, 2:], rtol=2e-4, atol=2e-3)
+
+
+def test_moments_golden_identity_warp(lib):
+    _lib, _ = lib
+    d = np.load(os.path.join(GOLDEN, "moments.npz"))
+    hm = d["hm_full"][None]  # (1,17,72,128) used directly as the image-space map
+    out = _moments(_lib, hm, np.array([1.0, 0, 0, 0, 1.0, 0]), 72, 128)
+    _check_moments(out[0], d["out_full"])
+    assert (out[0, -1] == 0).all()  # all-below-threshold joint -> zeros
+
+
+def test_moments_golden_revert(lib):
+    _lib, geometry = lib
+    d = np.load(os.path.join(GOLDEN, "moments.npz"))
+    img_h, img_w = [int(v) for v in d["img_hw"]]
+    minv = geometry.inverse_map(d["M_inv"])
+    out = _moments(_lib, d["hm_low"][None], minv, img_h, img_w)
+    _check_moments(out[0], d["out_rev"])
+
+
+def test_moments_full_frame_vs_oracle(lib):
+    """1280x720 revert of a 64x48 map against oracle warp + fp64 moments."""
+    _lib, geometry = lib
+    rng = np.random.default_rng(3)
+    hm = _planted_heatmaps(rng, 1)
+    hm = np.abs(hm)
+    g = geometry.CropGeometry.whole_image(1280, 720)
+    out = _moments(_lib, hm, g.revert_minv, 720, 1280)
+    Mh = heatmap_ref.get_warp_matrix(g.center, g.scale, 0.0, (48, 64), inv=True)
+    rev = heatmap_ref.warp_affine_linear_f32(hm[0], Mh, 720, 1280)
+    ref = heatmap_ref.heatmap_means_cov_f64(rev)
+    np.testing.assert_allclose(out[0], ref, rtol=1e-9, atol=1e-7)
