@@ -38,40 +38,61 @@ struct ConvParams {
     const uint16_t* __restrict__ res;
     uint16_t* __restrict__ y;
     float* __restrict__ yf;
+    const uint16_t* __restrict__ zero;  // >= 16 zero bytes: source of padding / out-of-image slots
     int N, H, W, Cin, Ho, Wo, Cout, Cout_pad;
     int relu, out_f32;
-    int tiles_w, tiles_h;
+    int tiles_w, tiles_h, n_tiles;
 };
 
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+template <int KS, int S, int BM, int TH, int TW, int NB>
+struct ConvCfg {
+    static constexpr int HH = (TH - 1) * S + KS;
+    static constexpr int HW = (TW - 1) * S + KS;
+    static constexpr int KK = KS * KS;
+    static constexpr int HALO_PIX = NB * HH * HW;
+    static constexpr int H_SLOTS = HALO_PIX * 5;       // 16-B slots: 4 data + 1 pad per pixel
+    static constexpr int W_ROW = KK * 4 + 1;           // slots per cout row (+1 pad)
+    static constexpr int W_SLOTS = BM * W_ROW;
+    static constexpr int H_BYTES = (H_SLOTS + 63) / 64 * 1024;  // whole 1-KiB DMA pieces
+    static constexpr int W_BYTES = (W_SLOTS + 63) / 64 * 1024;
+    static int lds_bytes(bool multi_chunk) { return 2 * H_BYTES + (multi_chunk ? 2 : 1) * W_BYTES; }
+};
+
+// Persistent implicit-GEMM conv with an LDS-DMA double buffer.  A workgroup walks
+// its work items (tile, 32-channel chunk); at the top of each item one barrier
+// retires the item's DMA (issued one item earlier) and frees the other buffer,
+// then the NEXT item's halo (+ weight slice when the chunk changes) is issued by
+// global_load_lds straight into that buffer and lands while this item's MFMAs
+// run.  Rows are padded by one 16-B slot (dummy DMA from a zero page) so the
+// ds_read_b128 fragment reads of consecutive pixels / couts do not collide.
 template <int KS, int S, int BM, int TH, int TW, int NB>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
+    using C = ConvCfg<KS, S, BM, TH, TW, NB>;
     constexpr int PAD = KS / 2;
-    constexpr int HH = (TH - 1) * S + KS;
-    constexpr int HW = (TW - 1) * S + KS;
-    constexpr int PS = 40;  // halo pixel stride in bf16: 32 ch + 8 pad (80 B)
-    constexpr int KK = KS * KS;
-    constexpr int WS = KK * 32 + 8;  // weight row stride in bf16 (+16 B pad)
+    constexpr int HH = C::HH, HW = C::HW, KK = C::KK;
+    constexpr int PS = 40;           // halo pixel stride in bf16 (80 B)
+    constexpr int WS = C::W_ROW * 8;  // weight row stride in bf16
     constexpr int P = NB * TH * TW;
     static_assert(P % 64 == 0, "tile must hold a multiple of 64 pixels");
     constexpr int NPT = P / 16;
     constexpr int NCT = BM / 16;
     constexpr int PTW = NPT / 4;  // pixel tiles per wave
-    constexpr int HALO_PIX = NB * HH * HW;
-    constexpr int HALO_ELEMS = HALO_PIX * PS;
-    constexpr int W_ELEMS = BM * WS;
-    __shared__ __attribute__((aligned(16))) uint16_t lds[HALO_ELEMS + W_ELEMS];
-    uint16_t* sh = lds;
-    uint16_t* sw = lds + HALO_ELEMS;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    int t = blockIdx.x;
-    const int tw_i = t % p.tiles_w;
-    t /= p.tiles_w;
-    const int th_i = t % p.tiles_h;
-    const int tn_i = t / p.tiles_h;
-    const int n0 = tn_i * NB, ho0 = th_i * TH, wo0 = tw_i * TW;
-    const int hi0 = ho0 * S - PAD, wi0 = wo0 * S - PAD;
     const int co0 = blockIdx.y * BM;
+    const int n_chunks = p.Cin >> 5;
+    const bool multi = n_chunks > 1;
+    const size_t plane_in = (size_t)p.H * p.W;
+    auto halo_buf = [&](int b) -> uint8_t* { return lds + b * C::H_BYTES; };
+    auto w_buf = [&](int b) -> uint8_t* { return lds + 2 * C::H_BYTES + (multi ? b : 0) * C::W_BYTES; };
 
     int hbase[PTW];
 #pragma unroll
@@ -82,36 +103,104 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
         const int th = r / TW, tw = r - (r / TW) * TW;
         hbase[i] = ((nb * HH + th * S) * HW + tw * S) * PS + (lane >> 4) * 8;
     }
+    float4 bias[NCT];
+#pragma unroll
+    for (int c = 0; c < NCT; c++) bias[c] = *reinterpret_cast<const float4*>(p.bias + co0 + c * 16 + (lane >> 4) * 4);
+
+    auto tile_origin = [&](int tile, int& n0, int& ho0, int& wo0) {
+        const int tw_i = tile % p.tiles_w;
+        const int t2 = tile / p.tiles_w;
+        n0 = (t2 / p.tiles_h) * NB;
+        ho0 = (t2 % p.tiles_h) * TH;
+        wo0 = tw_i * TW;
+    };
+    auto issue = [&](int tile, int chunk, int buf, bool with_w) {
+        int n0, ho0, wo0;
+        tile_origin(tile, n0, ho0, wo0);
+        const int hi0 = ho0 * S - PAD, wi0 = wo0 * S - PAD;
+        const uint16_t* xb = p.x + chunk * 32;
+        uint8_t* hb = halo_buf(buf);
+#pragma unroll
+        for (int s0 = 0; s0 < C::H_SLOTS; s0 += 256) {
+            const int sw0 = s0 + wave * 64;  // this wave's 64-slot piece
+            if (sw0 < C::H_SLOTS) {
+                const int sl = sw0 + lane;
+                const int pix = sl / 5, q = sl - (sl / 5) * 5;
+                const void* src = p.zero;
+                if (sl < C::H_SLOTS && q < 4) {
+                    const int nb = pix / (HH * HW);
+                    const int r = pix - nb * (HH * HW);
+                    const int hh = r / HW, ww = r - (r / HW) * HW;
+                    const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
+                    if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                        src = xb + ((size_t)n * plane_in + (size_t)hi * p.W + wi) * p.Cin + q * 8;
+                }
+                glds16(src, hb + sw0 * 16);
+            }
+        }
+        if (with_w) {
+            uint8_t* wb = w_buf(buf);
+            const uint16_t* wsrc = p.w + (size_t)co0 * KK * p.Cin + chunk * 32;
+#pragma unroll
+            for (int s0 = 0; s0 < C::W_SLOTS; s0 += 256) {
+                const int sw0 = s0 + wave * 64;
+                if (sw0 < C::W_SLOTS) {
+                    const int sl = sw0 + lane;
+                    const int row = sl / C::W_ROW, r = sl - (sl / C::W_ROW) * C::W_ROW;
+                    const void* src = p.zero;
+                    if (sl < C::W_SLOTS && r < KK * 4) src = wsrc + ((size_t)row * KK + (r >> 2)) * p.Cin + (r & 3) * 8;
+                    glds16(src, wb + sw0 * 16);
+                }
+            }
+        }
+    };
+
     f32x4 acc[PTW][NCT];
 #pragma unroll
     for (int i = 0; i < PTW; i++)
 #pragma unroll
         for (int c = 0; c < NCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    for (int c0 = 0; c0 < p.Cin; c0 += 32) {
-        // ---- stage the input halo (zero outside the image / batch)
-        for (int idx = tid; idx < HALO_PIX * 4; idx += 256) {
-            const int ch = idx & 3;
-            const int pix = idx >> 2;
-            const int nb = pix / (HH * HW);
-            const int r = pix - nb * (HH * HW);
-            const int hh = r / HW, ww = r - (r / HW) * HW;
-            const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
-            uint4 v = {0u, 0u, 0u, 0u};
-            if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                v = *reinterpret_cast<const uint4*>(p.x + (((size_t)n * p.H + hi) * p.W + wi) * p.Cin + c0 + ch * 8);
-            *reinterpret_cast<uint4*>(sh + pix * PS + ch * 8) = v;
-        }
-        // ---- stage the weight slice [BM][KK][32]
-        for (int idx = tid; idx < BM * KK * 4; idx += 256) {
-            const int ch = idx & 3;
-            const int r = idx >> 2;
-            const int co = r / KK, tap = r - (r / KK) * KK;
-            const uint4 v =
-                *reinterpret_cast<const uint4*>(p.w + ((size_t)(co0 + co) * KK + tap) * p.Cin + c0 + ch * 8);
-            *reinterpret_cast<uint4*>(sw + co * WS + tap * 32 + ch * 8) = v;
-        }
+    int tile = blockIdx.x, chunk = 0, buf = 0;
+    if (tile >= p.n_tiles) return;
+    issue(tile, 0, 0, true);
+    for (;;) {
+        // retire this item's DMA (vmcnt) and make every wave's view of it valid (barrier);
+        // also guarantees all waves finished reading buffer buf^1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        int ntile = tile, nchunk = chunk + 1;
+        if (nchunk == n_chunks) {
+            nchunk = 0;
+            ntile += gridDim.x;
+        }
+        const bool has_next = ntile < p.n_tiles;
+        const bool last_chunk = chunk == n_chunks - 1;
+        // residual rows of this tile: issued before the next DMA so they land under the MFMAs
+        uint2 resv[PTW][NCT];
+        if (last_chunk && p.res) {
+            int n0, ho0, wo0;
+            tile_origin(tile, n0, ho0, wo0);
+#pragma unroll
+            for (int i = 0; i < PTW; i++) {
+                const int pp = (wave * PTW + i) * 16 + (lane & 15);
+                const int nb = pp / (TH * TW);
+                const int r = pp - nb * (TH * TW);
+                const int th = r / TW, tw = r - (r / TW) * TW;
+                const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
+                const bool valid = n < p.N && ho < p.Ho && wo < p.Wo;
+                const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
+#pragma unroll
+                for (int c = 0; c < NCT; c++) {
+                    const int co = co0 + c * 16 + (lane >> 4) * 4;
+                    resv[i][c] = (valid && co < p.Cout) ? *reinterpret_cast<const uint2*>(p.res + pix * p.Cout + co)
+                                                        : uint2{0u, 0u};
+                }
+            }
+        }
+        if (has_next) issue(ntile, nchunk, buf ^ 1, multi);
+        const uint16_t* sh = reinterpret_cast<const uint16_t*>(halo_buf(buf));
+        const uint16_t* sw = reinterpret_cast<const uint16_t*>(w_buf(buf));
 #pragma unroll
         for (int kh = 0; kh < KS; kh++) {
 #pragma unroll
@@ -131,84 +220,134 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
                 }
             }
         }
-        __syncthreads();
-    }
-
-    // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head)
+        if (last_chunk) {
+            // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head)
+            int n0, ho0, wo0;
+            tile_origin(tile, n0, ho0, wo0);
 #pragma unroll
-    for (int i = 0; i < PTW; i++) {
-        const int pp = (wave * PTW + i) * 16 + (lane & 15);
-        const int nb = pp / (TH * TW);
-        const int r = pp - nb * (TH * TW);
-        const int th = r / TW, tw = r - (r / TW) * TW;
-        const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
-        if (n >= p.N || ho >= p.Ho || wo >= p.Wo) continue;
-        const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
+            for (int i = 0; i < PTW; i++) {
+                const int pp = (wave * PTW + i) * 16 + (lane & 15);
+                const int nb = pp / (TH * TW);
+                const int r = pp - nb * (TH * TW);
+                const int th = r / TW, tw = r - (r / TW) * TW;
+                const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
+                const bool valid = n < p.N && ho < p.Ho && wo < p.Wo;
+                const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
 #pragma unroll
-        for (int c = 0; c < NCT; c++) {
-            const int co = co0 + c * 16 + (lane >> 4) * 4;
-            const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
-            float v0 = acc[i][c][0] + bv.x, v1 = acc[i][c][1] + bv.y;
-            float v2 = acc[i][c][2] + bv.z, v3 = acc[i][c][3] + bv.w;
-            if (p.out_f32) {
-                const size_t plane = (size_t)p.Ho * p.Wo;
-                float vv[4] = {v0, v1, v2, v3};
+                for (int c = 0; c < NCT; c++) {
+                    const int co = co0 + c * 16 + (lane >> 4) * 4;
+                    float v0 = acc[i][c][0] + bias[c].x, v1 = acc[i][c][1] + bias[c].y;
+                    float v2 = acc[i][c][2] + bias[c].z, v3 = acc[i][c][3] + bias[c].w;
+                    acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+                    if (!valid) continue;
+                    if (p.out_f32) {
+                        const size_t plane = (size_t)p.Ho * p.Wo;
+                        const float vv[4] = {v0, v1, v2, v3};
 #pragma unroll
-                for (int q = 0; q < 4; q++)
-                    if (co + q < p.Cout) p.yf[((size_t)n * p.Cout + co + q) * plane + (size_t)ho * p.Wo + wo] = vv[q];
-                continue;
-            }
-            if (p.res) {
-                const uint2 rv = *reinterpret_cast<const uint2*>(p.res + pix * p.Cout + co);
-                v0 += bf16_to_f32(rv.x & 0xffff);
-                v1 += bf16_to_f32(rv.x >> 16);
-                v2 += bf16_to_f32(rv.y & 0xffff);
-                v3 += bf16_to_f32(rv.y >> 16);
-            }
-            if (p.relu) {
-                v0 = fmaxf(v0, 0.f);
-                v1 = fmaxf(v1, 0.f);
-                v2 = fmaxf(v2, 0.f);
-                v3 = fmaxf(v3, 0.f);
-            }
-            if (co < p.Cout) {
-                uint2 o;
-                o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-                o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-                *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
+                        for (int q = 0; q < 4; q++)
+                            if (co + q < p.Cout)
+                                p.yf[((size_t)n * p.Cout + co + q) * plane + (size_t)ho * p.Wo + wo] = vv[q];
+                        continue;
+                    }
+                    if (co >= p.Cout) continue;
+                    if (p.res) {
+                        const uint2 rv = resv[i][c];
+                        v0 += bf16_to_f32(rv.x & 0xffff);
+                        v1 += bf16_to_f32(rv.x >> 16);
+                        v2 += bf16_to_f32(rv.y & 0xffff);
+                        v3 += bf16_to_f32(rv.y >> 16);
+                    }
+                    if (p.relu) {
+                        v0 = fmaxf(v0, 0.f);
+                        v1 = fmaxf(v1, 0.f);
+                        v2 = fmaxf(v2, 0.f);
+                        v3 = fmaxf(v3, 0.f);
+                    }
+                    uint2 o;
+                    o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                    o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+                    *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
+                }
             }
         }
+        if (!has_next) break;
+        tile = ntile;
+        chunk = nchunk;
+        buf ^= 1;
     }
+}
+
+int g_num_cus = 0;
+uint16_t* g_zero = nullptr;
+
+int num_cus() {
+    if (g_num_cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_num_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    return g_num_cus;
+}
+
+const uint16_t* zero_page() {
+    if (!g_zero) {
+        MVP_HIP(hipMalloc(&g_zero, 256));
+        MVP_HIP(hipMemset(g_zero, 0, 256));
+    }
+    return g_zero;
 }
 
 template <int KS, int S, int BM, int TH, int TW, int NB>
 void launch_cfg(const ConvParams& p0, hipStream_t s) {
+    using C = ConvCfg<KS, S, BM, TH, TW, NB>;
     ConvParams p = p0;
     p.tiles_w = (p.Wo + TW - 1) / TW;
     p.tiles_h = (p.Ho + TH - 1) / TH;
     const long tiles_n = (p.N + NB - 1) / NB;
-    const long gx = tiles_n * p.tiles_h * p.tiles_w;
-    MVP_REQUIRE(gx < (1L << 31), "conv grid too large");
-    dim3 grid((unsigned)gx, (unsigned)(p.Cout_pad / BM));
-    hipLaunchKernelGGL((conv_mfma_kernel<KS, S, BM, TH, TW, NB>), grid, dim3(256), 0, s, p);
+    const long nt = tiles_n * p.tiles_h * p.tiles_w;
+    MVP_REQUIRE(nt < (1L << 31), "conv: too many tiles");
+    p.n_tiles = (int)nt;
+    p.zero = zero_page();
+    const bool multi = p.Cin > 32;
+    const int lds = C::lds_bytes(multi);
+    MVP_REQUIRE(lds <= 160 * 1024, "conv: LDS %d B over budget", lds);
+    auto kern = conv_mfma_kernel<KS, S, BM, TH, TW, NB>;
+    static int per_cu[2] = {-1, -1};  // resident workgroups per CU (single / multi chunk LDS footprint)
+    if (per_cu[multi] < 0) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        int b = 0;
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 256, lds));
+        per_cu[multi] = b > 0 ? b : 1;
+    }
+    const int y_blocks = p.Cout_pad / BM;
+    long gx = ((long)num_cus() * per_cu[multi] + y_blocks - 1) / y_blocks;
+    if (gx > nt) gx = nt;
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)y_blocks), dim3(256), lds, s, p);
 }
 
-// Tile shape per output plane width; BM per Cout.
+// Tile shape per output plane; BM per Cout.
 template <int KS, int S, int BM>
 void launch_plane(const ConvParams& p, hipStream_t s) {
-    if (p.Wo == 48 && p.Ho % 8 == 0) {
-        if constexpr (S == 1)
-            launch_cfg<KS, S, BM, 8, 48, 1>(p, s);
-        else
+    if constexpr (S == 1) {
+        if (p.Wo == 48 && p.Ho % 4 == 0)
             launch_cfg<KS, S, BM, 4, 48, 1>(p, s);
-    } else if (p.Wo == 24 && p.Ho % 8 == 0) {
-        launch_cfg<KS, S, BM, 8, 24, 1>(p, s);
-    } else if (p.Wo == 12 && p.Ho == 16) {
-        launch_cfg<KS, S, BM, 16, 12, 1>(p, s);
-    } else if (p.Wo == 6 && p.Ho == 8) {
-        launch_cfg<KS, S, BM, 8, 6, 4>(p, s);
+        else if (p.Wo == 24 && p.Ho % 8 == 0)
+            launch_cfg<KS, S, BM, 8, 24, 1>(p, s);
+        else if (p.Wo == 12 && p.Ho == 16)
+            launch_cfg<KS, S, BM, 16, 12, 1>(p, s);
+        else if (p.Wo == 6 && p.Ho == 8)
+            launch_cfg<KS, S, BM, 8, 6, 4>(p, s);
+        else
+            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);  // generic masked tiling
     } else {
-        launch_cfg<KS, S, BM, 4, 16, 1>(p, s);  // generic masked tiling
+        if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
+            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);
+        else if (p.Wo % 8 == 0 && p.Ho % 8 == 0)
+            launch_cfg<KS, S, BM, 8, 8, 1>(p, s);
+        else if (p.Wo % 4 == 0 && p.Ho % 16 == 0)
+            launch_cfg<KS, S, BM, 16, 4, 1>(p, s);
+        else
+            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);
     }
 }
 

@@ -39,7 +39,10 @@ class MultiViewPipeline:
             raise ValueError(f"frames carry {V} views, pipeline has {self.n_views} cameras")
         flat = frames.reshape(T * V, *frames.shape[2:])
         if out is None:
-            out = {"kpts_2d": torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)}
+            out = {}
+        if "kpts_2d" not in out or tuple(out["kpts_2d"].shape) != (T, N_JOINTS, 3, V):
+            out["kpts_2d"] = torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)
+            out.pop("kpts_3d", None)
         r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"])
         out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
         out["kpts_3d"] = ops.triangulate(out["kpts_2d"], self.cams, self.camera_indices, mode=self.mode,

@@ -262,9 +262,16 @@ def msra_decode(heatmaps):
 
 
 def keypoints_to_image(kpts_input, center, scale, input_size=(192, 256)):
-    """TopdownPoseEstimator.add_pred_to_datasample restore."""
-    input_size = np.array(input_size, np.float32)
-    return (kpts_input / input_size * scale + center - 0.5 * scale).astype(np.float32)
+    """TopdownPoseEstimator.add_pred_to_datasample restore:
+    keypoints / input_size * input_scale + input_center - 0.5 * input_scale.
+    input_size is TopdownAffine's (w, h) tuple of Python ints, so the f32
+    keypoints promote to float64 (int64 array operand); the result is stored
+    back into the float32 keypoint array."""
+    size = np.asarray(tuple(int(v) for v in input_size))  # int64
+    center = np.asarray(center, np.float32)
+    scale = np.asarray(scale, np.float32)
+    out = np.asarray(kpts_input, np.float32) / size * scale + center - 0.5 * scale
+    return out.astype(np.float32)
 
 
 # ---------------------------------------------------------------- moments --
