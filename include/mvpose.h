@@ -97,7 +97,10 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
  * mvp_heatmap_moments: revert_heatmap (warp of each map to the img_h x img_w
  *   image, float bilinear) fused with get_heatmap_means_cov
  *   (mmpose_pose_estimation.py:163-215): out_dev [N][K][6] float64
- *   (mx, my, vxx, vxy, vxy, vyy); minv_dev [N][6] = image -> heatmap map.
+ *   (mx, my, vxx, vxy, vxy, vyy); minv_dev [N][6] = image -> heatmap map;
+ *   separable != 0 asserts (host-checked with mvp_warp_is_separable) that every
+ *   map's fixed-point source column depends on x only and source row on y only,
+ *   enabling the column-resident fast path.
  * ------------------------------------------------------------------------- */
 int mvp_preprocess(const uint8_t* frames_dev, int n, int H, int W, const double* minv_dev, int out_h, int out_w,
                    const float* mean3_host, const float* std3_host, int swap_rb, int with_flip, uint16_t* out_dev,
@@ -106,8 +109,9 @@ int mvp_heatmap_decode(const float* hm_dev, const float* hm_flip_dev, int N, int
                        const int* flip_idx_host, int shift, const float* center_scale_dev, int input_w, int input_h,
                        float* avg_dev, float* kpts_dev, float* scores_dev, int32_t* argmax_dev, float* kpts_tkv_dev,
                        int V, void* stream);
+int mvp_warp_is_separable(const double* minv_host, int img_h, int img_w, int* separable_out);
 int mvp_heatmap_moments(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
-                        int img_w, float thr, double* out_dev, void* stream);
+                        int img_w, float thr, int separable, double* out_dev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Backbone graph runtime (replaces the HRNet-W32 forward inside mmpose's
@@ -131,6 +135,12 @@ int mvp_heatmap_moments(const float* hm_dev, int N, int K, int h, int w, const d
  *                 heatmap head.
  *   MVP_OP_FUSE : out = act(sum_k nearest_upsample(in[k], up[k])), n_in <= 4
  *                 (HRModule multi-scale fuse).
+ * Segments: every op carries a segment id; the ops of a segment are
+ * contiguous.  seg_micro_batch_host[g] > 0 runs segment g in micro-batches of
+ * that many crops (0 = whole batch at once): tensors produced and consumed only
+ * inside a micro-batched segment are allocated for one micro-batch, so a chain
+ * of layers keeps its intermediates in the 256 MiB Infinity Cache instead of
+ * HBM.
  * ------------------------------------------------------------------------- */
 #define MVP_DT_BF16_NHWC 0
 #define MVP_DT_F32_NCHW 1
@@ -150,13 +160,15 @@ typedef struct mvp_op_desc {
     int in[4];
     int up[4];
     int cin, cout, ks, stride, relu;
+    int segment;
     int64_t w_off;
     int64_t b_off;
 } mvp_op_desc;
 
 int mvp_graph_create(const mvp_tensor_desc* tensors_host, int n_tensors, const mvp_op_desc* ops_host, int n_ops,
-                     int input_tensor, int output_tensor, const uint16_t* w_bf16_dev, int64_t w_elems,
-                     const float* f32_dev, int64_t f32_elems, int max_batch, void** handle_out);
+                     const int* seg_micro_batch_host, int n_segments, int input_tensor, int output_tensor,
+                     const uint16_t* w_bf16_dev, int64_t w_elems, const float* f32_dev, int64_t f32_elems,
+                     int max_batch, void** handle_out);
 /* input_dev: [batch][h][w][c] of the input tensor; output_dev: the output tensor. */
 int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* output_dev, void* stream);
 int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);

@@ -1,6 +1,7 @@
 // C-ABI plumbing of libmvpose.so: version, thread-local last error, host helpers.
 #include "mvp_common.h"
 
+#include <cmath>
 #include <cstring>
 
 namespace mvp {
@@ -52,5 +53,22 @@ extern "C" int mvp_camera_pack(const double* K, const double* dist5, const doubl
             acc += K[i * 3 + 2] * Rt[2][j];
             out[26 + i * 4 + j] = acc;
         }
+    MVP_ABI_END
+}
+
+// Host helper: does OpenCV's fixed-point warp (WarpAffineInvoker) of an img_h x
+// img_w destination through minv (dst -> src, 6 doubles) have a source column
+// that depends on x only and a source row that depends on y only?
+extern "C" int mvp_warp_is_separable(const double* M, int img_h, int img_w, int* out) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(M && out && img_h > 0 && img_w > 0, "mvp_warp_is_separable: bad arguments");
+    int sep = 1;
+    const int X00 = (int)std::rint((M[1] * 0 + M[2]) * 1024.0);
+    for (int y = 1; y < img_h && sep; y++)
+        if ((int)std::rint((M[1] * y + M[2]) * 1024.0) != X00) sep = 0;
+    const int b0 = (int)std::rint(M[3] * 0 * 1024.0);
+    for (int x = 1; x < img_w && sep; x++)
+        if ((int)std::rint(M[3] * x * 1024.0) != b0) sep = 0;
+    *out = sep;
     MVP_ABI_END
 }

@@ -15,6 +15,8 @@
 // folded-BN bias, optional residual add (BasicBlock/Bottleneck), ReLU and bf16
 // pack; the head variant writes f32 NCHW heatmaps.
 #include "conv.h"
+
+#include <cstdlib>
 #include "mvp_common.h"
 
 namespace mvp {
@@ -42,7 +44,13 @@ struct ConvParams {
     int N, H, W, Cin, Ho, Wo, Cout, Cout_pad;
     int relu, out_f32;
     int tiles_w, tiles_h, n_tiles;
+    int wmode;  // WM_ONCE / WM_RESIDENT / WM_STREAM
+    int ablate; // diagnostics only (MVPOSE_CONV_ABLATE): 1 no stores, 2 no DMA
 };
+
+// Weight staging modes: one 32-channel chunk staged once (Cin = 32); every chunk
+// resident in LDS for the whole launch (fits); or a per-chunk double buffer.
+enum { WM_ONCE = 0, WM_RESIDENT = 1, WM_STREAM = 2 };
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
@@ -57,12 +65,14 @@ struct ConvCfg {
     static constexpr int HW = (TW - 1) * S + KS;
     static constexpr int KK = KS * KS;
     static constexpr int HALO_PIX = NB * HH * HW;
-    static constexpr int H_SLOTS = HALO_PIX * 5;       // 16-B slots: 4 data + 1 pad per pixel
-    static constexpr int W_ROW = KK * 4 + 1;           // slots per cout row (+1 pad)
-    static constexpr int W_SLOTS = BM * W_ROW;
-    static constexpr int H_BYTES = (H_SLOTS + 63) / 64 * 1024;  // whole 1-KiB DMA pieces
+    static constexpr int HPIX = (HALO_PIX + 63) / 64 * 64;  // pixels per chunk plane (whole 1-KiB DMA pieces)
+    static constexpr int H_SLOTS = 4 * HPIX;                // 16-B slots, layout [chunk q][pixel]
+    static constexpr int W_SLOTS = KK * 4 * BM;             // layout [tap][chunk q][cout]
+    static constexpr int H_BYTES = H_SLOTS * 16;
     static constexpr int W_BYTES = (W_SLOTS + 63) / 64 * 1024;
-    static int lds_bytes(bool multi_chunk) { return 2 * H_BYTES + (multi_chunk ? 2 : 1) * W_BYTES; }
+    static int lds_bytes(int wmode, int n_chunks) {
+        return 2 * H_BYTES + (wmode == WM_ONCE ? 1 : wmode == WM_RESIDENT ? n_chunks : 2) * W_BYTES;
+    }
 };
 
 // Persistent implicit-GEMM conv with an LDS-DMA double buffer.  A workgroup walks
@@ -70,15 +80,14 @@ struct ConvCfg {
 // retires the item's DMA (issued one item earlier) and frees the other buffer,
 // then the NEXT item's halo (+ weight slice when the chunk changes) is issued by
 // global_load_lds straight into that buffer and lands while this item's MFMAs
-// run.  Rows are padded by one 16-B slot (dummy DMA from a zero page) so the
-// ds_read_b128 fragment reads of consecutive pixels / couts do not collide.
+// run.  LDS images are chunk-major ([q][pixel] for the halo, [tap][q][cout] for
+// the weights) so each 16-lane ds_read_b128 group of a fragment read touches 16
+// distinct 16-B bank slots (conflict-free for row-contiguous pixel tiles).
 template <int KS, int S, int BM, int TH, int TW, int NB>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
     using C = ConvCfg<KS, S, BM, TH, TW, NB>;
     constexpr int PAD = KS / 2;
-    constexpr int HH = C::HH, HW = C::HW, KK = C::KK;
-    constexpr int PS = 40;           // halo pixel stride in bf16 (80 B)
-    constexpr int WS = C::W_ROW * 8;  // weight row stride in bf16
+    constexpr int HH = C::HH, HW = C::HW, KK = C::KK, HPIX = C::HPIX;
     constexpr int P = NB * TH * TW;
     static_assert(P % 64 == 0, "tile must hold a multiple of 64 pixels");
     constexpr int NPT = P / 16;
@@ -89,11 +98,15 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int co0 = blockIdx.y * BM;
     const int n_chunks = p.Cin >> 5;
-    const bool multi = n_chunks > 1;
+    const int wmode = p.wmode;
     const size_t plane_in = (size_t)p.H * p.W;
     auto halo_buf = [&](int b) -> uint8_t* { return lds + b * C::H_BYTES; };
-    auto w_buf = [&](int b) -> uint8_t* { return lds + 2 * C::H_BYTES + (multi ? b : 0) * C::W_BYTES; };
+    auto w_buf = [&](int b, int chunk) -> uint8_t* {
+        const int slot = wmode == WM_ONCE ? 0 : wmode == WM_RESIDENT ? chunk : b;
+        return lds + 2 * C::H_BYTES + slot * C::W_BYTES;
+    };
 
+    // B fragment: lane reads pixel (lane & 15) of its pixel tile, chunk q = lane >> 4
     int hbase[PTW];
 #pragma unroll
     for (int i = 0; i < PTW; i++) {
@@ -101,8 +114,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
         const int nb = pp / (TH * TW);
         const int r = pp - nb * (TH * TW);
         const int th = r / TW, tw = r - (r / TW) * TW;
-        hbase[i] = ((nb * HH + th * S) * HW + tw * S) * PS + (lane >> 4) * 8;
+        hbase[i] = ((lane >> 4) * HPIX + (nb * HH + th * S) * HW + tw * S) * 8;
     }
+    const int abase = ((lane >> 4) * BM + (lane & 15)) * 8;
     float4 bias[NCT];
 #pragma unroll
     for (int c = 0; c < NCT; c++) bias[c] = *reinterpret_cast<const float4*>(p.bias + co0 + c * 16 + (lane >> 4) * 4);
@@ -114,6 +128,22 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
         ho0 = (t2 % p.tiles_h) * TH;
         wo0 = tw_i * TW;
     };
+    auto issue_w = [&](int chunk, uint8_t* wb) {
+        const uint16_t* wsrc = p.w + (size_t)co0 * KK * p.Cin + chunk * 32;
+#pragma unroll
+        for (int s0 = 0; s0 < C::W_SLOTS; s0 += 256) {
+            const int sw0 = s0 + wave * 64;
+            if (sw0 < C::W_SLOTS) {
+                const int sl = sw0 + lane;
+                const void* src = p.zero;
+                if (sl < C::W_SLOTS) {
+                    const int co = sl % BM, tq = sl / BM;  // tq = tap * 4 + q
+                    src = wsrc + ((size_t)co * KK + (tq >> 2)) * p.Cin + (tq & 3) * 8;
+                }
+                glds16(src, wb + sw0 * 16);
+            }
+        }
+    };
     auto issue = [&](int tile, int chunk, int buf, bool with_w) {
         int n0, ho0, wo0;
         tile_origin(tile, n0, ho0, wo0);
@@ -122,38 +152,23 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
         uint8_t* hb = halo_buf(buf);
 #pragma unroll
         for (int s0 = 0; s0 < C::H_SLOTS; s0 += 256) {
-            const int sw0 = s0 + wave * 64;  // this wave's 64-slot piece
-            if (sw0 < C::H_SLOTS) {
-                const int sl = sw0 + lane;
-                const int pix = sl / 5, q = sl - (sl / 5) * 5;
-                const void* src = p.zero;
-                if (sl < C::H_SLOTS && q < 4) {
-                    const int nb = pix / (HH * HW);
-                    const int r = pix - nb * (HH * HW);
-                    const int hh = r / HW, ww = r - (r / HW) * HW;
-                    const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
-                    if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                        src = xb + ((size_t)n * plane_in + (size_t)hi * p.W + wi) * p.Cin + q * 8;
-                }
-                glds16(src, hb + sw0 * 16);
+            const int sw0 = s0 + wave * 64;  // this wave's 64-slot piece (one chunk plane)
+            const int q = sw0 / HPIX;
+            const int pix = sw0 - q * HPIX + lane;
+            const void* src = p.zero;
+            if (pix < C::HALO_PIX) {
+                const int nb = pix / (HH * HW);
+                const int r = pix - nb * (HH * HW);
+                const int hh = r / HW, ww = r - (r / HW) * HW;
+                const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
+                if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                    src = xb + ((size_t)n * plane_in + (size_t)hi * p.W + wi) * p.Cin + q * 8;
             }
+            glds16(src, hb + sw0 * 16);
         }
-        if (with_w) {
-            uint8_t* wb = w_buf(buf);
-            const uint16_t* wsrc = p.w + (size_t)co0 * KK * p.Cin + chunk * 32;
-#pragma unroll
-            for (int s0 = 0; s0 < C::W_SLOTS; s0 += 256) {
-                const int sw0 = s0 + wave * 64;
-                if (sw0 < C::W_SLOTS) {
-                    const int sl = sw0 + lane;
-                    const int row = sl / C::W_ROW, r = sl - (sl / C::W_ROW) * C::W_ROW;
-                    const void* src = p.zero;
-                    if (sl < C::W_SLOTS && r < KK * 4) src = wsrc + ((size_t)row * KK + (r >> 2)) * p.Cin + (r & 3) * 8;
-                    glds16(src, wb + sw0 * 16);
-                }
-            }
-        }
+        if (with_w) issue_w(chunk, w_buf(buf, chunk));
     };
+    const bool do_dma = !(p.ablate & 2), do_store = !(p.ablate & 1);
 
     f32x4 acc[PTW][NCT];
 #pragma unroll
@@ -163,7 +178,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
 
     int tile = blockIdx.x, chunk = 0, buf = 0;
     if (tile >= p.n_tiles) return;
-    issue(tile, 0, 0, true);
+    if (do_dma) issue(tile, 0, 0, true);
+    if (wmode == WM_RESIDENT && do_dma)
+        for (int c = 1; c < n_chunks; c++) issue_w(c, w_buf(0, c));
     for (;;) {
         // retire this item's DMA (vmcnt) and make every wave's view of it valid (barrier);
         // also guarantees all waves finished reading buffer buf^1
@@ -198,27 +215,32 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
                 }
             }
         }
-        if (has_next) issue(ntile, nchunk, buf ^ 1, multi);
+        if (has_next && do_dma) issue(ntile, nchunk, buf ^ 1, wmode == WM_STREAM);
         const uint16_t* sh = reinterpret_cast<const uint16_t*>(halo_buf(buf));
-        const uint16_t* sw = reinterpret_cast<const uint16_t*>(w_buf(buf));
+        const uint16_t* sw = reinterpret_cast<const uint16_t*>(w_buf(buf, chunk));
+        // fragment reads of tap t+1 are issued before the MFMAs of tap t (two static
+        // register sets), so LDS latency hides under the matrix work
+        bf16x8 fa[2][NCT], fb[2][PTW];
+        auto load_tap = [&](int tap, bf16x8 (&a)[NCT], bf16x8 (&b)[PTW]) {
+            const int toff = ((tap / KS) * HW + (tap % KS)) * 8;
 #pragma unroll
-        for (int kh = 0; kh < KS; kh++) {
+            for (int c = 0; c < NCT; c++)
+                a[c] = *reinterpret_cast<const bf16x8*>(sw + tap * 4 * BM * 8 + abase + c * 16 * 8);
 #pragma unroll
-            for (int kw = 0; kw < KS; kw++) {
-                const int tap = kh * KS + kw;
-                const int toff = (kh * HW + kw) * PS;
-                bf16x8 a[NCT];
+            for (int i = 0; i < PTW; i++) b[i] = *reinterpret_cast<const bf16x8*>(sh + hbase[i] + toff);
+        };
+        load_tap(0, fa[0], fb[0]);
+#pragma unroll
+        for (int tap = 0; tap < KK; tap++) {
+            const int cur = tap & 1;
+            if (tap + 1 < KK) load_tap(tap + 1, fa[cur ^ 1], fb[cur ^ 1]);
+            __builtin_amdgcn_sched_barrier(0);  // keep tap t+1's reads ahead of tap t's MFMAs
+#pragma unroll
+            for (int i = 0; i < PTW; i++)
 #pragma unroll
                 for (int c = 0; c < NCT; c++)
-                    a[c] = *reinterpret_cast<const bf16x8*>(sw + (c * 16 + (lane & 15)) * WS + tap * 32 + (lane >> 4) * 8);
-#pragma unroll
-                for (int i = 0; i < PTW; i++) {
-                    const bf16x8 b = *reinterpret_cast<const bf16x8*>(sh + hbase[i] + toff);
-#pragma unroll
-                    for (int c = 0; c < NCT; c++)
-                        acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b, acc[i][c], 0, 0, 0);
-                }
-            }
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][c], fb[cur][i], acc[i][c], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (last_chunk) {
             // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head)
@@ -266,7 +288,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
                     uint2 o;
                     o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
                     o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-                    *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
+                    if (do_store) *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
+                    else if ((o.x ^ o.y) == 0x12345678u) p.y[0] = 0;  // keep the epilogue live
                 }
             }
         }
@@ -308,55 +331,76 @@ void launch_cfg(const ConvParams& p0, hipStream_t s) {
     MVP_REQUIRE(nt < (1L << 31), "conv: too many tiles");
     p.n_tiles = (int)nt;
     p.zero = zero_page();
-    const bool multi = p.Cin > 32;
-    const int lds = C::lds_bytes(multi);
-    MVP_REQUIRE(lds <= 160 * 1024, "conv: LDS %d B over budget", lds);
+    const int n_chunks = p.Cin / 32;
+    constexpr int kLdsMax = 160 * 1024;
+    p.wmode = n_chunks == 1 ? WM_ONCE
+              : C::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax ? WM_RESIDENT : WM_STREAM;
+    const int lds = C::lds_bytes(p.wmode, n_chunks);
+    MVP_REQUIRE(lds <= kLdsMax, "conv: LDS %d B over budget", lds);
     auto kern = conv_mfma_kernel<KS, S, BM, TH, TW, NB>;
-    static int per_cu[2] = {-1, -1};  // resident workgroups per CU (single / multi chunk LDS footprint)
-    if (per_cu[multi] < 0) {
-        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        int b = 0;
-        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, kern, 256, lds));
-        per_cu[multi] = b > 0 ? b : 1;
+    static bool attr_set = false;
+    if (!attr_set) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+        attr_set = true;
+    }
+    static int per_cu_cache[kLdsMax / 1024 + 1] = {0};  // resident workgroups per CU by LDS footprint
+    int& per_cu = per_cu_cache[(lds + 1023) / 1024];
+    if (per_cu == 0) {
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds));
+        if (per_cu < 1) per_cu = 1;
     }
     const int y_blocks = p.Cout_pad / BM;
-    long gx = ((long)num_cus() * per_cu[multi] + y_blocks - 1) / y_blocks;
+    long gx = ((long)num_cus() * per_cu + y_blocks - 1) / y_blocks;
     if (gx > nt) gx = nt;
     hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)y_blocks), dim3(256), lds, s, p);
 }
 
-// Tile shape per output plane; BM per Cout.
-template <int KS, int S, int BM>
-void launch_plane(const ConvParams& p, hipStream_t s) {
-    if constexpr (S == 1) {
-        if (p.Wo == 48 && p.Ho % 4 == 0)
-            launch_cfg<KS, S, BM, 4, 48, 1>(p, s);
-        else if (p.Wo == 24 && p.Ho % 8 == 0)
-            launch_cfg<KS, S, BM, 8, 24, 1>(p, s);
-        else if (p.Wo == 12 && p.Ho == 16)
-            launch_cfg<KS, S, BM, 16, 12, 1>(p, s);
-        else if (p.Wo == 6 && p.Ho == 8)
-            launch_cfg<KS, S, BM, 8, 6, 4>(p, s);
-        else
-            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);  // generic masked tiling
-    } else {
-        if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
-            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);
-        else if (p.Wo % 8 == 0 && p.Ho % 8 == 0)
-            launch_cfg<KS, S, BM, 8, 8, 1>(p, s);
-        else if (p.Wo % 4 == 0 && p.Ho % 16 == 0)
-            launch_cfg<KS, S, BM, 16, 4, 1>(p, s);
-        else
-            launch_cfg<KS, S, BM, 4, 16, 1>(p, s);
-    }
+// Cout tile: 64 couts when the weights can stay LDS-resident (or Cin = 32),
+// else 32 couts if that makes them resident, else 64 couts streamed per chunk.
+template <int KS, int S, int TH, int TW, int NB>
+void launch_tile(const ConvParams& p, hipStream_t s) {
+    constexpr int kLdsMax = 160 * 1024;
+    const int n_chunks = p.Cin / 32;
+    if (p.Cout_pad == 32) return launch_cfg<KS, S, 32, TH, TW, NB>(p, s);
+    if (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax)
+        return launch_cfg<KS, S, 64, TH, TW, NB>(p, s);
+    if (ConvCfg<KS, S, 32, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax)
+        return launch_cfg<KS, S, 32, TH, TW, NB>(p, s);
+    launch_cfg<KS, S, 64, TH, TW, NB>(p, s);
 }
 
+// Tile shape per output plane.
 template <int KS, int S>
-void launch_bm(const ConvParams& p, hipStream_t s) {
-    if (p.Cout_pad == 32)
-        launch_plane<KS, S, 32>(p, s);
-    else
-        launch_plane<KS, S, 64>(p, s);
+void launch_plane(const ConvParams& p, hipStream_t s) {
+    if constexpr (S == 1) {
+        static const int th48 = [] {
+            const char* e = getenv("MVPOSE_TILE_TH48");  // tuning experiments only
+            return e ? atoi(e) : 4;
+        }();
+        if (p.Wo == 48 && p.Ho % 8 == 0 && th48 == 8)
+            launch_tile<KS, S, 8, 48, 1>(p, s);
+        else if (p.Wo == 48 && p.Ho % 4 == 0 && th48 == 2)
+            launch_tile<KS, S, 2, 32, 1>(p, s);
+        else if (p.Wo == 48 && p.Ho % 4 == 0)
+            launch_tile<KS, S, 4, 48, 1>(p, s);
+        else if (p.Wo == 24 && p.Ho % 8 == 0)
+            launch_tile<KS, S, 8, 24, 1>(p, s);
+        else if (p.Wo == 12 && p.Ho == 16)
+            launch_tile<KS, S, 16, 12, 1>(p, s);
+        else if (p.Wo == 6 && p.Ho == 8)
+            launch_tile<KS, S, 8, 6, 4>(p, s);
+        else
+            launch_tile<KS, S, 4, 16, 1>(p, s);  // generic masked tiling
+    } else {
+        if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
+            launch_tile<KS, S, 4, 16, 1>(p, s);
+        else if (p.Wo % 8 == 0 && p.Ho % 8 == 0)
+            launch_tile<KS, S, 8, 8, 1>(p, s);
+        else if (p.Wo % 4 == 0 && p.Ho % 16 == 0)
+            launch_tile<KS, S, 16, 4, 1>(p, s);
+        else
+            launch_tile<KS, S, 4, 16, 1>(p, s);
+    }
 }
 
 // ---------------------------------------------------------------- stem conv
@@ -486,13 +530,18 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.Cout_pad = conv_cout_pad(c.Cout);
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
+    static const int ablate = [] {
+        const char* e = getenv("MVPOSE_CONV_ABLATE");
+        return e ? atoi(e) : 0;
+    }();
+    p.ablate = ablate;
     if (c.N == 0) return;
     if (c.ks == 3 && c.stride == 1)
-        launch_bm<3, 1>(p, s);
+        launch_plane<3, 1>(p, s);
     else if (c.ks == 3 && c.stride == 2)
-        launch_bm<3, 2>(p, s);
+        launch_plane<3, 2>(p, s);
     else if (c.ks == 1 && c.stride == 1)
-        launch_bm<1, 1>(p, s);
+        launch_plane<1, 1>(p, s);
     else
         fail(MVP_ERR_ARG, "conv: unsupported ks=%d stride=%d", c.ks, c.stride);
     MVP_HIP(hipGetLastError());

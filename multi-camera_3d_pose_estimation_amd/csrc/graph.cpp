@@ -9,9 +9,16 @@
 namespace mvp {
 namespace {
 
+struct Segment {
+    int first_op = 0, last_op = -1;  // inclusive op range
+    int micro_batch = 0;             // 0 = whole batch
+};
+
 struct Graph {
     std::vector<mvp_tensor_desc> tensors;
     std::vector<mvp_op_desc> ops;
+    std::vector<Segment> segs;
+    std::vector<int> local_seg;  // segment a tensor is local to (micro-batch sized), -1 = full batch
     int input = -1, output = -1;
     const uint16_t* wb = nullptr;
     const float* fb = nullptr;
@@ -87,25 +94,74 @@ void validate(Graph& g, int64_t w_elems, int64_t f_elems) {
         defined[op.out] = 1;
     }
     MVP_REQUIRE(defined[g.output], "graph: output tensor never produced");
+    // segments: contiguous op ranges in increasing order
+    const int ns = (int)g.segs.size();
+    int prev = -1;
+    for (int k = 0; k < (int)g.ops.size(); k++) {
+        const int sg = g.ops[k].segment;
+        MVP_REQUIRE(sg >= 0 && sg < ns, "graph op %d: segment %d out of range", k, sg);
+        MVP_REQUIRE(sg >= prev, "graph op %d: segments must be contiguous and ordered", k);
+        if (sg != prev) g.segs[sg].first_op = k;
+        g.segs[sg].last_op = k;
+        prev = sg;
+    }
 }
 
 // Greedy first-fit placement of tensors in one arena by lifetime [def, last use].
+// A tensor produced and consumed only inside one micro-batched segment is
+// "local": it is sized for one micro-batch and re-used by every micro-batch.
+// Every other tensor a micro-batched segment touches is sliced per micro-batch,
+// so its lifetime is widened to the whole segment (later micro-batches replay
+// the segment's ops).
 void plan(Graph& g) {
     const int nt = (int)g.tensors.size();
+    const int no = (int)g.ops.size();
     std::vector<int> first(nt, -1), last(nt, -1);
-    for (int k = 0; k < (int)g.ops.size(); k++) {
+    std::vector<int> seg_of_def(nt, -1);
+    std::vector<int> multi_seg(nt, 0);  // used by more than one segment
+    std::vector<int> use_seg(nt, -1);
+    for (int k = 0; k < no; k++) {
         const mvp_op_desc& op = g.ops[k];
         first[op.out] = k;
         if (last[op.out] < k) last[op.out] = k;
+        seg_of_def[op.out] = op.segment;
+        auto touch = [&](int t) {
+            if (use_seg[t] < 0) use_seg[t] = op.segment;
+            else if (use_seg[t] != op.segment) multi_seg[t] = 1;
+        };
+        touch(op.out);
         for (int i = 0; i < op.n_in; i++)
-            if (op.in[i] >= 0) last[op.in[i]] = std::max(last[op.in[i]], k);
+            if (op.in[i] >= 0) {
+                last[op.in[i]] = std::max(last[op.in[i]], k);
+                touch(op.in[i]);
+            }
+    }
+    g.local_seg.assign(nt, -1);
+    for (int t = 0; t < nt; t++) {
+        if (t == g.input || t == g.output || first[t] < 0) continue;
+        const int sg = seg_of_def[t];
+        if (!multi_seg[t] && g.segs[sg].micro_batch > 0 && g.segs[sg].micro_batch < g.max_batch) g.local_seg[t] = sg;
+    }
+    for (int k = 0; k < no; k++) {
+        const mvp_op_desc& op = g.ops[k];
+        const Segment& sg = g.segs[op.segment];
+        if (sg.micro_batch <= 0 || sg.micro_batch >= g.max_batch) continue;
+        auto widen = [&](int t) {
+            if (t < 0 || g.local_seg[t] >= 0) return;
+            first[t] = std::min(first[t] < 0 ? sg.first_op : first[t], sg.first_op);
+            last[t] = std::max(last[t], sg.last_op);
+        };
+        widen(op.out);
+        for (int i = 0; i < op.n_in; i++) widen(op.in[i]);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
         if (t != g.input && t != g.output && first[t] >= 0) order.push_back(t);
-    std::sort(order.begin(), order.end(), [&](int a, int b) {
-        return tensor_bytes(g.tensors[a], 1) > tensor_bytes(g.tensors[b], 1);
-    });
+    auto alloc_bytes = [&](int t) {
+        const int b = g.local_seg[t] >= 0 ? g.segs[g.local_seg[t]].micro_batch : g.max_batch;
+        return (tensor_bytes(g.tensors[t], b) + 255) / 256 * 256;
+    };
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return alloc_bytes(a) > alloc_bytes(b); });
     g.offset.assign(nt, -1);
     struct Placed {
         int64_t off, size;
@@ -114,8 +170,7 @@ void plan(Graph& g) {
     std::vector<Placed> placed;
     int64_t top = 0;
     for (int t : order) {
-        const int64_t size = (tensor_bytes(g.tensors[t], g.max_batch) + 255) / 256 * 256;
-        // candidate offsets: 0 and the end of every lifetime-overlapping block
+        const int64_t size = alloc_bytes(t);
         std::vector<Placed> live;
         for (const Placed& p : placed)
             if (!(p.last < first[t] || last[t] < p.first)) live.push_back(p);
@@ -138,8 +193,9 @@ void plan(Graph& g) {
 using mvp::Graph;
 
 extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, const mvp_op_desc* ops, int n_ops,
-                                int input_tensor, int output_tensor, const uint16_t* w_dev, int64_t w_elems,
-                                const float* f_dev, int64_t f_elems, int max_batch, void** handle_out) {
+                                const int* seg_micro_batch, int n_segments, int input_tensor, int output_tensor,
+                                const uint16_t* w_dev, int64_t w_elems, const float* f_dev, int64_t f_elems,
+                                int max_batch, void** handle_out) {
     MVP_ABI_BEGIN
     MVP_REQUIRE(handle_out != nullptr, "mvp_graph_create: handle_out is NULL");
     *handle_out = nullptr;
@@ -148,6 +204,7 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
                     input_tensor != output_tensor,
                 "mvp_graph_create: bad input/output tensor ids");
     MVP_REQUIRE(max_batch > 0, "mvp_graph_create: max_batch must be > 0");
+    MVP_REQUIRE(seg_micro_batch && n_segments > 0, "mvp_graph_create: segments missing");
     Graph* g = new Graph();
     try {
         g->tensors.assign(tensors, tensors + n_tensors);
@@ -157,6 +214,11 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         g->wb = w_dev;
         g->fb = f_dev;
         g->max_batch = max_batch;
+        g->segs.resize(n_segments);
+        for (int i = 0; i < n_segments; i++) {
+            MVP_REQUIRE(seg_micro_batch[i] >= 0, "mvp_graph_create: negative micro-batch");
+            g->segs[i].micro_batch = seg_micro_batch[i];
+        }
         mvp::validate(*g, w_elems, f_elems);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
@@ -182,17 +244,21 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
     MVP_REQUIRE(input_dev && output_dev, "mvp_graph_forward: NULL input/output");
     if (batch == 0) return MVP_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int64_t slice = 0;  // first crop of the current micro-batch
     auto ptr = [&](int t) -> void* {
-        if (t == g->input) return const_cast<void*>(input_dev);
-        if (t == g->output) return output_dev;
-        return g->arena + g->offset[t];
+        const mvp_tensor_desc& d = g->tensors[t];
+        if (g->local_seg[t] >= 0) return g->arena + g->offset[t];
+        char* base = t == g->input ? (char*)const_cast<void*>(input_dev)
+                     : t == g->output ? (char*)output_dev
+                                      : g->arena + g->offset[t];
+        return base + slice * mvp::tensor_bytes(d, 1);
     };
-    for (const mvp_op_desc& op : g->ops) {
+    auto run_op = [&](const mvp_op_desc& op, int nb) {
         const mvp_tensor_desc& o = g->tensors[op.out];
         if (op.kind == MVP_OP_STEM) {
             const mvp_tensor_desc& x = g->tensors[op.in[0]];
             mvp::launch_stem((const uint16_t*)ptr(op.in[0]), g->fb + op.w_off, g->fb + op.b_off,
-                             (uint16_t*)ptr(op.out), batch, x.h, x.w, s);
+                             (uint16_t*)ptr(op.out), nb, x.h, x.w, s);
         } else if (op.kind == MVP_OP_CONV) {
             const mvp_tensor_desc& x = g->tensors[op.in[0]];
             mvp::ConvLaunch c{};
@@ -203,7 +269,7 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             c.out_f32_nchw = o.dtype == MVP_DT_F32_NCHW;
             c.y = c.out_f32_nchw ? nullptr : (uint16_t*)ptr(op.out);
             c.yf = c.out_f32_nchw ? (float*)ptr(op.out) : nullptr;
-            c.N = batch;
+            c.N = nb;
             c.H = x.h;
             c.W = x.w;
             c.Cin = op.cin;
@@ -215,8 +281,18 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         } else {
             const uint16_t* ins[4];
             for (int i = 0; i < op.n_in; i++) ins[i] = (const uint16_t*)ptr(op.in[i]);
-            mvp::launch_fuse_sum(ins, op.up, op.n_in, (uint16_t*)ptr(op.out), batch, o.h, o.w, o.c, op.relu, s);
+            mvp::launch_fuse_sum(ins, op.up, op.n_in, (uint16_t*)ptr(op.out), nb, o.h, o.w, o.c, op.relu, s);
         }
+    };
+    for (const mvp::Segment& sg : g->segs) {
+        if (sg.last_op < sg.first_op) continue;
+        const int mb = (sg.micro_batch > 0 && sg.micro_batch < batch) ? sg.micro_batch : batch;
+        for (int64_t b0 = 0; b0 < batch; b0 += mb) {
+            slice = b0;
+            const int nb = (int)std::min<int64_t>(mb, batch - b0);
+            for (int k = sg.first_op; k <= sg.last_op; k++) run_op(g->ops[k], nb);
+        }
+        slice = 0;
     }
     MVP_ABI_END
 }

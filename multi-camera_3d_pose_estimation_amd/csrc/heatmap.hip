@@ -193,88 +193,208 @@ struct MomParams {
     double* __restrict__ out;         // [N][K][6]
     int N, K, h, w, img_h, img_w;
     float thr;
+    int separable;  // host-verified: source column depends on x only, source row on y only
 };
 
 constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
+constexpr int kMomCols = 8;            // image columns per lane (separable path)
 
+// One workgroup per (crop, joint) map.  The fixed-point warp of an image pixel
+// (OpenCV WarpAffineInvoker) is X = (X0(y) + adelta(x)) >> 5, Y = (Y0(y) + bdelta(x)) >> 5.
+// Separable path (axis-aligned crops, the only ones the pipeline makes): each
+// lane owns image columns (source column ix and weight fx fixed), walks the rows,
+// keeps the 4 taps in registers while the source row iy stays the same (~33
+// image rows per heatmap row), and accumulates per column S, S·y, S·y² in fp64;
+// x-moments are applied per column at the end.  Rows / columns whose taps are
+// all below thr·(1-1e-6) contribute exact zeros and are skipped (bounding box
+// of active heatmap cells).
 __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
     extern __shared__ __attribute__((aligned(16))) float mom_lds[];
     float* shm = mom_lds;
     int* sad = reinterpret_cast<int*>(mom_lds + ((p.h * p.w + 3) & ~3));
     int* sbd = sad + p.img_w;
     __shared__ double red[6][kBlock / 64];
+    __shared__ int bbox[4];
     const long map = blockIdx.x;
     const int n = map / p.K;
     const double* M = p.minv + 6 * n;
     const float* src = p.hm + map * p.h * p.w;
-    for (int i = threadIdx.x; i < p.h * p.w; i += kBlock) shm[i] = src[i];
+    if (threadIdx.x == 0) {
+        bbox[0] = p.w;
+        bbox[1] = -1;
+        bbox[2] = p.h;
+        bbox[3] = -1;
+    }
+    __syncthreads();
+    const float thr_lo = p.thr * (1.f - 1e-6f);
+    int c0 = p.w, c1 = -1, r0 = p.h, r1 = -1;
+    for (int i = threadIdx.x; i < p.h * p.w; i += kBlock) {
+        const float v = src[i];
+        shm[i] = v;
+        if (!(v < thr_lo)) {  // active (or NaN)
+            const int r = i / p.w, c = i - (i / p.w) * p.w;
+            c0 = min(c0, c);
+            c1 = max(c1, c);
+            r0 = min(r0, r);
+            r1 = max(r1, r);
+        }
+    }
     for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
         sad[x] = (int)rint(M[0] * x * 1024.0);
         sbd[x] = (int)rint(M[3] * x * 1024.0);
     }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        c0 = min(c0, __shfl_xor(c0, off));
+        c1 = max(c1, __shfl_xor(c1, off));
+        r0 = min(r0, __shfl_xor(r0, off));
+        r1 = max(r1, __shfl_xor(r1, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&bbox[0], c0);
+        atomicMax(&bbox[1], c1);
+        atomicMin(&bbox[2], r0);
+        atomicMax(&bbox[3], r1);
+    }
     __syncthreads();
+    c0 = bbox[0];
+    c1 = bbox[1];
+    r0 = bbox[2];
+    r1 = bbox[3];
     const double cx = 0.5 * p.img_w, cy = 0.5 * p.img_h;  // centred coordinates (cancellation)
-    double s0 = 0, sx = 0, sy = 0, sxx = 0, sxy = 0, syy = 0;
-    for (int y = 0; y < p.img_h; y++) {
-        const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
-        const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
-        const double yc = y - cy;
-        for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
-            const int X = (X0 + sad[x]) >> 5;
-            const int Y = (Y0 + sbd[x]) >> 5;
-            const int ix = X >> 5, iy = Y >> 5;
-            if (ix >= p.w || ix + 1 < 0 || iy >= p.h || iy + 1 < 0) continue;  // border value 0
-            const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
-            const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
-            const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
-            const bool x0 = ix >= 0, x1 = ix + 1 < p.w, y0 = iy >= 0, y1 = iy + 1 < p.h;
-            const float v0 = (x0 && y0) ? shm[iy * p.w + ix] : 0.f;
-            const float v1 = (x1 && y0) ? shm[iy * p.w + ix + 1] : 0.f;
-            const float v2 = (x0 && y1) ? shm[(iy + 1) * p.w + ix] : 0.f;
-            const float v3 = (x1 && y1) ? shm[(iy + 1) * p.w + ix + 1] : 0.f;
-            float v = __fmul_rn(v0, w0);
-            v = __fadd_rn(v, __fmul_rn(v1, w1));
-            v = __fadd_rn(v, __fmul_rn(v2, w2));
-            v = __fadd_rn(v, __fmul_rn(v3, w3));
-            if (!(v >= p.thr)) continue;  // heatmaps[heatmaps < 0.01] = 0
-            const double dv = v, xc = x - cx;
-            s0 += dv;
-            sx += xc * dv;
-            sy += yc * dv;
-            sxx += xc * xc * dv;
-            sxy += xc * yc * dv;
-            syy += yc * yc * dv;
+    double t[6] = {0, 0, 0, 0, 0, 0};
+    if (c1 >= 0) {
+        if (p.separable) {
+            // columns whose taps (ix, ix+1) touch [c0, c1]; rows whose (iy, iy+1) touch [r0, r1]
+            const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
+            for (int xb = threadIdx.x; xb < p.img_w; xb += kBlock * kMomCols) {
+                int ix[kMomCols];
+                float fx[kMomCols], gx[kMomCols];
+                bool on[kMomCols];
+                double S[kMomCols], Sy[kMomCols], Syy[kMomCols];
+                float v00[kMomCols], v01[kMomCols], v10[kMomCols], v11[kMomCols];
+                bool any = false;
+#pragma unroll
+                for (int j = 0; j < kMomCols; j++) {
+                    const int x = xb + j * kBlock;
+                    const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
+                    ix[j] = X >> 5;
+                    fx[j] = (float)(X & 31) * (1.f / 32.f);
+                    gx[j] = 1.f - fx[j];
+                    on[j] = x < p.img_w && ix[j] + 1 >= c0 && ix[j] <= c1;
+                    any |= on[j];
+                    S[j] = Sy[j] = Syy[j] = 0.0;
+                    v00[j] = v01[j] = v10[j] = v11[j] = 0.f;
+                }
+                if (__any(any)) {
+                    int cur_iy = -0x7fffffff;
+                    const int Y0b = sbd[0];
+                    for (int y = 0; y < p.img_h; y++) {
+                        const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + Y0b) >> 5;
+                        const int iy = Yq >> 5;
+                        if (iy + 1 < r0 || iy > r1) continue;  // whole row inactive (uniform)
+                        const float fy = (float)(Yq & 31) * (1.f / 32.f), gy = 1.f - fy;
+                        if (iy != cur_iy) {
+                            cur_iy = iy;
+                            const bool ry0 = iy >= 0 && iy < p.h, ry1 = iy + 1 >= 0 && iy + 1 < p.h;
+#pragma unroll
+                            for (int j = 0; j < kMomCols; j++) {
+                                const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
+                                v00[j] = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
+                                v01[j] = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
+                                v10[j] = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
+                                v11[j] = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                            }
+                        }
+                        const double yc = y - cy, yc2 = yc * yc;
+#pragma unroll
+                        for (int j = 0; j < kMomCols; j++) {
+                            // OpenCV float remap: ((v0 w0 + v1 w1) + v2 w2) + v3 w3, w from the 32x32 table
+                            float v = __fmul_rn(v00[j], __fmul_rn(gy, gx[j]));
+                            v = __fadd_rn(v, __fmul_rn(v01[j], __fmul_rn(gy, fx[j])));
+                            v = __fadd_rn(v, __fmul_rn(v10[j], __fmul_rn(fy, gx[j])));
+                            v = __fadd_rn(v, __fmul_rn(v11[j], __fmul_rn(fy, fx[j])));
+                            const double dv = (v >= p.thr) ? (double)v : 0.0;  // heatmaps[heatmaps < thr] = 0
+                            S[j] += dv;
+                            Sy[j] = fma(yc, dv, Sy[j]);
+                            Syy[j] = fma(yc2, dv, Syy[j]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < kMomCols; j++) {
+                    const double xc = (double)(xb + j * kBlock) - cx;
+                    t[0] += S[j];
+                    t[1] = fma(xc, S[j], t[1]);
+                    t[2] += Sy[j];
+                    t[3] = fma(xc * xc, S[j], t[3]);
+                    t[4] = fma(xc, Sy[j], t[4]);
+                    t[5] += Syy[j];
+                }
+            }
+        } else {
+            for (int y = 0; y < p.img_h; y++) {
+                const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
+                const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
+                const double yc = y - cy;
+                for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
+                    const int X = (X0 + sad[x]) >> 5;
+                    const int Y = (Y0 + sbd[x]) >> 5;
+                    const int ix = X >> 5, iy = Y >> 5;
+                    if (ix >= p.w || ix + 1 < 0 || iy >= p.h || iy + 1 < 0) continue;  // border value 0
+                    const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+                    const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
+                    const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
+                    const bool x0 = ix >= 0, x1 = ix + 1 < p.w, y0 = iy >= 0, y1 = iy + 1 < p.h;
+                    const float v0 = (x0 && y0) ? shm[iy * p.w + ix] : 0.f;
+                    const float v1 = (x1 && y0) ? shm[iy * p.w + ix + 1] : 0.f;
+                    const float v2 = (x0 && y1) ? shm[(iy + 1) * p.w + ix] : 0.f;
+                    const float v3 = (x1 && y1) ? shm[(iy + 1) * p.w + ix + 1] : 0.f;
+                    float v = __fmul_rn(v0, w0);
+                    v = __fadd_rn(v, __fmul_rn(v1, w1));
+                    v = __fadd_rn(v, __fmul_rn(v2, w2));
+                    v = __fadd_rn(v, __fmul_rn(v3, w3));
+                    if (!(v >= p.thr)) continue;
+                    const double dv = v, xc = x - cx;
+                    t[0] += dv;
+                    t[1] += xc * dv;
+                    t[2] += yc * dv;
+                    t[3] += xc * xc * dv;
+                    t[4] += xc * yc * dv;
+                    t[5] += yc * yc * dv;
+                }
+            }
         }
     }
-    double vals[6] = {s0, sx, sy, sxx, sxy, syy};
+    // t = {S, Sx, Sy, Sxx, Sxy, Syy}
 #pragma unroll
     for (int q = 0; q < 6; q++) {
-        double v = vals[q];
+        double v = t[q];
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-        vals[q] = v;
+        t[q] = v;
     }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < 6; q++) red[q][wv] = vals[q];
+        for (int q = 0; q < 6; q++) red[q][wv] = t[q];
     __syncthreads();
     if (threadIdx.x != 0) return;
-    double t[6];
+    double a[6];
 #pragma unroll
     for (int q = 0; q < 6; q++) {
-        t[q] = 0;
-        for (int k = 0; k < kBlock / 64; k++) t[q] += red[q][k];
+        a[q] = 0;
+        for (int k = 0; k < kBlock / 64; k++) a[q] += red[q][k];
     }
     double* o = p.out + 6 * map;
-    if (t[0] == 0.0) {
+    if (a[0] == 0.0) {
         for (int q = 0; q < 6; q++) o[q] = 0.0;
         return;
     }
-    const double mxc = t[1] / t[0], myc = t[2] / t[0];
-    const double vxx = t[3] / t[0] - mxc * mxc;
-    const double vxy = t[4] / t[0] - mxc * myc;
-    const double vyy = t[5] / t[0] - myc * myc;
+    const double mxc = a[1] / a[0], myc = a[2] / a[0];
+    const double vxx = a[3] / a[0] - mxc * mxc;
+    const double vxy = a[4] / a[0] - mxc * myc;
+    const double vyy = a[5] / a[0] - myc * myc;
     o[0] = mxc + cx;
     o[1] = myc + cy;
     o[2] = vxx;
@@ -355,7 +475,7 @@ extern "C" int mvp_heatmap_decode(const float* hm, const float* hm_flip, int N, 
 }
 
 extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, const double* minv, int img_h,
-                                   int img_w, float thr, double* out, void* stream) {
+                                   int img_w, float thr, int separable, double* out, void* stream) {
     MVP_ABI_BEGIN
     MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
     const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8;
@@ -374,6 +494,7 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     p.img_h = img_h;
     p.img_w = img_w;
     p.thr = thr;
+    p.separable = separable;
     hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * K)), dim3(kBlock), lds,
                        reinterpret_cast<hipStream_t>(stream), p);
     MVP_HIP(hipGetLastError());

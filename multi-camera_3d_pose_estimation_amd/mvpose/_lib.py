@@ -45,8 +45,9 @@ SIGNATURES = {
     "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,
                                    c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p]),
+    "mvp_warp_is_separable": (c_int, [P(c_double), c_int, c_int, P(c_int)]),
     "mvp_heatmap_moments": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float,
-                                    c_void_p, c_void_p]),
+                                    c_int, c_void_p, c_void_p]),
     # graph argtypes with struct pointers are (re)declared in mvpose/hrnet.py
     "mvp_graph_create": (c_int, None),
     "mvp_graph_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

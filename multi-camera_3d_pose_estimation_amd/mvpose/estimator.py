@@ -25,6 +25,15 @@ COCO_FLIP_INDICES = [0, 2, 1, 4, 3, 6, 5, 8, 7, 10, 9, 12, 11, 14, 13, 16, 15]
 HEATMAP_THR = 0.01  # get_heatmap_means_cov threshold (mmpose_pose_estimation.py:166)
 
 
+def warp_is_separable(minv, img_h, img_w) -> bool:
+    """mvp_warp_is_separable on a (6,) image -> heatmap map (enables the fast moments path)."""
+    m = np.ascontiguousarray(minv, dtype=np.float64)
+    out = ctypes.c_int()
+    call("mvp_warp_is_separable", m.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(img_h), int(img_w),
+         ctypes.byref(out))
+    return bool(out.value)
+
+
 def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
@@ -48,6 +57,7 @@ class BatchPoseEstimator:
                                       max_batch=self.max_frames * (2 if flip_test else 1), device=device)
         geo = geometry.CropGeometry.whole_image(self.frame_w, self.frame_h)
         self.geometry = geo
+        self.separable = warp_is_separable(geo.revert_minv, self.frame_h, self.frame_w)
         n = self.max_frames
         self.crop_minv = torch.tensor(np.tile(geo.crop_minv, (n, 1)), dtype=torch.float64, device=self.device)
         self.revert_minv = torch.tensor(np.tile(geo.revert_minv, (n, 1)), dtype=torch.float64, device=self.device)
@@ -87,7 +97,7 @@ class BatchPoseEstimator:
              _ptr(avg), _ptr(kp), _ptr(sc), _ptr(am), _ptr(kpts_tkv), int(n_views), s)
         gauss = torch.empty((n, N_JOINTS, 6), dtype=torch.float64, device=dev)
         call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(self.revert_minv),
-             h, w, ctypes.c_float(HEATMAP_THR), _ptr(gauss), s)
+             h, w, ctypes.c_float(HEATMAP_THR), int(self.separable), _ptr(gauss), s)
         out = {"keypoints": kp, "scores": sc, "gaussians": gauss, "heatmaps": avg}
         if argmax:
             out["argmax"] = am

@@ -14,6 +14,7 @@ checkpoint (state dict) loads directly; without network access the bench uses
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -38,12 +39,32 @@ class OpDesc(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("out", ctypes.c_int), ("n_in", ctypes.c_int),
                 ("in_", ctypes.c_int * 4), ("up", ctypes.c_int * 4), ("cin", ctypes.c_int),
                 ("cout", ctypes.c_int), ("ks", ctypes.c_int), ("stride", ctypes.c_int), ("relu", ctypes.c_int),
-                ("w_off", ctypes.c_int64), ("b_off", ctypes.c_int64)]
+                ("segment", ctypes.c_int), ("w_off", ctypes.c_int64), ("b_off", ctypes.c_int64)]
 
 
 _lib.lib.mvp_graph_create.argtypes = [ctypes.POINTER(TensorDesc), ctypes.c_int, ctypes.POINTER(OpDesc), ctypes.c_int,
-                                      ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                      ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+                                      ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p)]
+
+# Micro-batch (crops) per graph segment: keeps a chain's intermediates inside the
+# 256 MiB Infinity Cache (MI355X_MICROARCH.md) instead of round-tripping HBM.
+#   stem    : stem + layer1 + transition1 (256-ch 64x48 tensors, 1.5 MB / crop)
+#   branch0 : each HRModule's 4 BasicBlocks on the 64x48x32 branch
+#   branch1 : same on the 32x24x64 branch
+# 0 = whole batch.  Override: MVPOSE_MICRO_BATCH="stem:64,branch0:256,branch1:0".
+DEFAULT_MICRO_BATCH = {"stem": 0, "branch0": 0, "branch1": 0}  # measured: no gain yet
+
+
+def micro_batch_config():
+    cfg = dict(DEFAULT_MICRO_BATCH)
+    env = os.environ.get("MVPOSE_MICRO_BATCH", "")
+    for item in filter(None, env.split(",")):
+        k, v = item.split(":")
+        cfg[k.strip()] = int(v)
+    return cfg
+
+
 _lib.lib.mvp_graph_arena_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
 
 
@@ -141,10 +162,20 @@ class GraphSpec:
     def __init__(self):
         self.tensors: list[tuple[int, int, int, int]] = []
         self.ops: list[dict] = []
+        self.seg_micro_batch: list[int] = [0]
+        self._seg = 0
         self._w: list[np.ndarray] = []
         self._f: list[np.ndarray] = []
         self._w_len = 0
         self._f_len = 0
+
+    def segment(self, micro_batch: int = 0) -> None:
+        """Start a new segment (contiguous ops run in micro-batches of `micro_batch` crops)."""
+        if self.ops and self.ops[-1]["segment"] == self._seg:
+            self.seg_micro_batch.append(int(micro_batch))
+            self._seg += 1
+        else:
+            self.seg_micro_batch[self._seg] = int(micro_batch)
 
     def tensor(self, h, w, c, dtype=DT_BF16) -> int:
         self.tensors.append((h, w, c, dtype))
@@ -172,7 +203,7 @@ class GraphSpec:
         w4[..., :3] = w
         h, ww, _, _ = self.tensors[x]
         y = self.tensor((h - 1) // 2 + 1, (ww - 1) // 2 + 1, 64)
-        self.ops.append(dict(kind=OP_STEM, out=y, ins=[x], up=[1], cin=4, cout=64, ks=3, stride=2, relu=1,
+        self.ops.append(dict(kind=OP_STEM, segment=self._seg, out=y, ins=[x], up=[1], cin=4, cout=64, ks=3, stride=2, relu=1,
                              w_off=self._push_f(w4), b_off=self._push_f(b)))
         return y
 
@@ -188,7 +219,7 @@ class GraphSpec:
         assert c == cin, (conv, c, cin)
         pad = k // 2
         y = self.tensor((h + 2 * pad - k) // stride + 1, (ww + 2 * pad - k) // stride + 1, cout, out_dtype)
-        self.ops.append(dict(kind=OP_CONV, out=y, ins=[x] + ([res] if res is not None else []), up=[1, 1],
+        self.ops.append(dict(kind=OP_CONV, segment=self._seg, out=y, ins=[x] + ([res] if res is not None else []), up=[1, 1],
                              cin=cin, cout=cout, ks=k, stride=stride, relu=int(relu),
                              w_off=self._push_w(to_bf16_bits(wp)), b_off=self._push_f(bp)))
         return y
@@ -197,7 +228,7 @@ class GraphSpec:
         (x0, u0) = terms[0]
         h, w, c, _ = self.tensors[x0]
         y = self.tensor(h * u0, w * u0, c)
-        self.ops.append(dict(kind=OP_FUSE, out=y, ins=[t for t, _ in terms], up=[u for _, u in terms], cin=c,
+        self.ops.append(dict(kind=OP_FUSE, segment=self._seg, out=y, ins=[t for t, _ in terms], up=[u for _, u in terms], cin=c,
                              cout=c, ks=0, stride=0, relu=int(relu), w_off=0, b_off=0))
         return y
 
@@ -207,9 +238,11 @@ class GraphSpec:
         return w, f
 
 
-def build_hrnet_w32(sd) -> tuple[GraphSpec, int, int]:
+def build_hrnet_w32(sd, micro_batch=None) -> tuple[GraphSpec, int, int]:
     """Walk mmpose's HRNet-W32 + HeatmapHead forward order; returns (spec, input id, output id)."""
+    mb = micro_batch_config() if micro_batch is None else micro_batch
     g = GraphSpec()
+    g.segment(mb.get("stem", 0))
     x_in = g.tensor(INPUT_HW[0], INPUT_HW[1], 4)
     x = g.stem(sd, "backbone.conv1", "backbone.bn1", x_in)
     x = g.conv(sd, "backbone.conv2", "backbone.bn2", x, 2, True)
@@ -222,6 +255,8 @@ def build_hrnet_w32(sd) -> tuple[GraphSpec, int, int]:
     ys = [x]
     pre = [256]
     for s, (n_mod, chans) in enumerate(STAGES):
+        if s > 0:
+            g.segment(0)
         xs = []
         for i, c in enumerate(chans):
             if i < len(pre) and c == pre[i]:
@@ -235,10 +270,12 @@ def build_hrnet_w32(sd) -> tuple[GraphSpec, int, int]:
         for m in range(n_mod):
             p = f"backbone.stage{s + 2}.{m}"
             for bi in range(len(chans)):
+                g.segment(mb.get(f"branch{bi}", 0))
                 for k in range(4):
                     q = f"{p}.branches.{bi}.{k}"
                     y = g.conv(sd, f"{q}.conv1", f"{q}.bn1", xs[bi], 1, True)
                     xs[bi] = g.conv(sd, f"{q}.conv2", f"{q}.bn2", y, 1, True, res=xs[bi])
+            g.segment(0)
             last = s == len(STAGES) - 1 and m == n_mod - 1
             n_out = 1 if last else len(chans)
             outs = []
@@ -269,10 +306,10 @@ class HRNetBackbone:
 
     forward(crops (N,256,192,4) bf16 on GPU) -> heatmaps (N,17,64,48) f32."""
 
-    def __init__(self, state_dict=None, seed: int = 0, max_batch: int = 256, device="cuda"):
+    def __init__(self, state_dict=None, seed: int = 0, max_batch: int = 256, device="cuda", micro_batch=None):
         if state_dict is None:
             state_dict = random_state_dict(seed)
-        spec, self.input_id, self.output_id = build_hrnet_w32(state_dict)
+        spec, self.input_id, self.output_id = build_hrnet_w32(state_dict, micro_batch)
         self.spec = spec
         w, f = spec.blobs()
         self.device = torch.device(device)
@@ -288,10 +325,13 @@ class HRNetBackbone:
                 d.in_[i] = op["ins"][i] if i < len(op["ins"]) else -1
                 d.up[i] = op["up"][i] if i < len(op["up"]) else 1
             d.cin, d.cout, d.ks, d.stride, d.relu = op["cin"], op["cout"], op["ks"], op["stride"], op["relu"]
+            d.segment = op["segment"]
             d.w_off, d.b_off = op["w_off"], op["b_off"]
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
-            call("mvp_graph_create", tens, len(spec.tensors), ops, len(spec.ops), self.input_id, self.output_id,
+            segs = (ctypes.c_int * len(spec.seg_micro_batch))(*spec.seg_micro_batch)
+            call("mvp_graph_create", tens, len(spec.tensors), ops, len(spec.ops), segs, len(spec.seg_micro_batch),
+                 self.input_id, self.output_id,
                  ctypes.c_void_p(self.w_dev.data_ptr()), self.w_dev.numel(), ctypes.c_void_p(self.f_dev.data_ptr()),
                  self.f_dev.numel(), self.max_batch, ctypes.byref(h))
         self._h = h

@@ -53,6 +53,25 @@ def test_backbone_batch_consistency(models):
     assert torch.equal(full[3], one[0])
 
 
+def test_micro_batched_segments_bitwise_equal(models):
+    """Segment micro-batching (Infinity-Cache residency) must not change a bit."""
+    dev, _ = models
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(7)
+    plain = hrnet.HRNetBackbone(sd, max_batch=8, micro_batch={"stem": 0, "branch0": 0, "branch1": 0})
+    split = hrnet.HRNetBackbone(sd, max_batch=8, micro_batch={"stem": 3, "branch0": 2, "branch1": 5, "branch2": 3})
+    g = torch.Generator().manual_seed(2)
+    x = torch.zeros((7, 256, 192, 4))
+    x[..., :3] = torch.randn((7, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = split.forward(xb)
+    c = dev.forward(xb)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c)
+    assert split.arena_bytes < plain.arena_bytes
+
+
 def test_arena_is_reused(models):
     dev, _ = models
     per_crop = dev.arena_bytes / dev.max_batch

@@ -98,12 +98,16 @@ def test_decode_vs_oracle(lib):
         np.testing.assert_array_equal(t[i // 2, :, 2, i % 2], s_np[i])
 
 
-def _moments(_lib, hm, minv, img_h, img_w):
+def _moments(_lib, hm, minv, img_h, img_w, separable=None):
+    from mvpose.estimator import warp_is_separable
+    if separable is None:
+        separable = warp_is_separable(minv, img_h, img_w)
     N, K, h, w = hm.shape
     hd = torch.tensor(np.ascontiguousarray(hm), device="cuda")
     md = torch.tensor(np.tile(minv, (N, 1)), device="cuda")
     out = torch.empty((N, K, 6), dtype=torch.float64, device="cuda")
-    _lib.call("mvp_heatmap_moments", _p(hd), N, K, h, w, _p(md), img_h, img_w, ctypes.c_float(0.01), _p(out), _s())
+    _lib.call("mvp_heatmap_moments", _p(hd), N, K, h, w, _p(md), img_h, img_w, ctypes.c_float(0.01), int(separable),
+              _p(out), _s())
     torch.cuda.synchronize()
     return out.cpu().numpy()
 
@@ -132,14 +136,26 @@ def test_moments_golden_revert(lib):
     _check_moments(out[0], d["out_rev"])
 
 
-def test_moments_full_frame_vs_oracle(lib):
-    """1280x720 revert of a 64x48 map against oracle warp + fp64 moments."""
+@pytest.mark.parametrize("kind", ["dense", "peaked"])
+@pytest.mark.parametrize("separable", [True, False])
+def test_moments_full_frame_vs_oracle(lib, kind, separable):
+    """1280x720 revert of a 64x48 map against oracle warp + fp64 moments, on both
+    kernel paths (the separable column-resident path with bbox culling, and the
+    general per-pixel path); dense maps (every pixel above threshold) and peaked
+    maps (small active region, culling exercised)."""
     _lib, geometry = lib
     rng = np.random.default_rng(3)
     hm = _planted_heatmaps(rng, 1)
-    hm = np.abs(hm)
+    if kind == "dense":
+        hm = np.abs(hm) + 0.02
+    else:
+        yy, xx = np.mgrid[0:64, 0:48]
+        for k in range(17):
+            cy, cx = rng.uniform(5, 59), rng.uniform(5, 43)
+            hm[0, k] = np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * 2.0 ** 2)) - 0.005
     g = geometry.CropGeometry.whole_image(1280, 720)
-    out = _moments(_lib, hm, g.revert_minv, 720, 1280)
+    assert geometry is not None
+    out = _moments(_lib, hm, g.revert_minv, 720, 1280, separable=separable)
     Mh = heatmap_ref.get_warp_matrix(g.center, g.scale, 0.0, (48, 64), inv=True)
     rev = heatmap_ref.warp_affine_linear_f32(hm[0], Mh, 720, 1280)
     ref = heatmap_ref.heatmap_means_cov_f64(rev)
