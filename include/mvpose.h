@@ -174,6 +174,52 @@ int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* outp
 int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);
 int mvp_graph_destroy(void* handle);
 
+/* ---------------------------------------------------------------------------
+ * Reprojection-error trajectory refinement (Optimized_3d_Pose_Estimation,
+ * reference pose_refinement.py:579-668 + sgd_optimize :894-1096, trajectory-only
+ * path the CLI runs at :1210-1214).
+ *
+ * One workgroup refines one trajectory: the whole optimisation (every
+ * iteration, every overlapping window, forward costs, analytic gradient,
+ * clip_grad_norm_, Adam, running-mean early stop, best-trajectory snapshot)
+ * runs inside ONE launch.  M independent trajectories run as M workgroups.
+ *
+ * Camera record (MVP_SGD_CAM_FLOATS f32): [K 9 | R 9 (matrix) | T 3 | dist 5].
+ * ------------------------------------------------------------------------- */
+#define MVP_SGD_CAM_FLOATS 26
+#define MVP_SGD_N_COSTS 4 /* total, likelihood, smoothness, body_length */
+
+typedef struct mvp_sgd_params {
+    /* Python floats in the reference: kept in double so the f32 casts match torch's. */
+    double lr, beta1, beta2, adam_eps;        /* torch.optim.Adam (eps 1e-8) */
+    double lambda_smooth, lambda_body_length; /* a cost is skipped when its lambda <= 0 (:978-983) */
+    double tolerance;                         /* running-mean improvement threshold (:1073) */
+    double max_grad_norm;                     /* clip_grad_norm_ max_norm (1.0 at :1045) */
+    int patience, max_iter;                  /* loop runs while no_improve < patience && it <= max_iter */
+    int batch_size;                          /* window length; windows start every batch_size/2 (:786-796) */
+    int ignore_distortions;
+    int own_camera_gaussians;                /* 0 = reference: all cameras vs camera-0 Gaussians (:663, :885) */
+} mvp_sgd_params;
+
+/* Float workspace needed by mvp_sgd_refine for M trajectories of T x J points seen by V cameras. */
+int mvp_sgd_workspace_floats(int M, int T, int V, int J, int64_t* out);
+
+/* gauss [M][T][V][J][6] f32 (mx,my,cxx,cxy,cyx,cyy), traj0 [M][T][J][3] f32 (T already sliced by
+ * time_interval; windows cover the first floor(T/batch_size)*batch_size rows), cams [V][26] f32, seg [n_seg][2] int
+ * joint pairs (a -> b, length |X_b - X_a|) with seg_len [n_seg] f32 in the body-length YAML order.
+ * Outputs: final [M][T][J][3], best [M][T][J][3] (NaN if never improved),
+ * batch_costs [M][max_iter+1][n_windows][4], iter_means [M][max_iter+1][4] (the reference's
+ * running means), iters [M] (iterations executed).  All pointers are device pointers except p. */
+int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J,
+                   const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p, float* workspace,
+                   float* final_traj, float* best_traj, float* batch_costs, float* iter_means, int* iters,
+                   void* stream);
+
+/* project_points_torch (pose_refinement.py:94-179): pts [n][3] f32 -> uv [n][2] f32 for one camera
+ * record (R as a 3x3 matrix). */
+int mvp_project_points(const float* pts, int64_t n, const float* cam, int ignore_distortions, float* uv,
+                       void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,554 @@
+// Reprojection-error trajectory refinement for gfx950 — one workgroup per trajectory,
+// the whole optimisation in one launch.
+//
+// Replaces Optimized_3d_Pose_Estimation.sgd_optimize (reference
+// pose_refinement.py:894-1096, trajectory-only path run by the CLI at :1210-1214).
+// Per overlapping window (create_batch_indices, :786-796) and per iteration:
+//   pass A  forward costs   likelihood  0.5·dᵀΣ⁻¹d of every camera's projection
+//                                       (project_points_torch :94-179) against the
+//                                       camera-0 Gaussian (:863-889, quirk F7),
+//                                       nan_mean (:221-229);
+//                           smoothness  λs·mean‖x_t − 2x_{t−1} + x_{t−2}‖² (:836-845);
+//                           body length λb·‖a − μb‖²/‖a‖², μ = a·b/b·b (:848-860)
+//           + the likelihood gradient through the projection Jacobian (radial +
+//           tangential distortion), unscaled, into a per-point buffer
+//   pass B  scale it by 1/n and add the stencil and segment-length adjoints,
+//           pulled per owned point; ‖g‖₂ for clip_grad_norm_ (:1045)
+//   pass C  Adam over the WHOLE trajectory (torch single-tensor Adam; rows outside
+//           the window keep moving with their momentum)
+// then the reference's running-mean early stop, where the cost list doubles as
+// the running-mean list (:987, :1070-1089, quirk F6), and the best snapshot.
+//
+// Rounding follows torch's f32 op order (contraction off); reductions are
+// fp64 — results agree with the reference to f32 rounding, not bit-for-bit
+// (its BLAS/pairwise summation order is not reproducible here).
+#pragma clang fp contract(off)
+
+#include "mvp_common.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kMaxSgdCams = 16;
+constexpr int kMaxSeg = 32;
+constexpr int kMaxJ = 64;
+
+struct SgdArgs {
+    const float* gauss;
+    const float* traj0;
+    const float* cams;
+    const int* seg;
+    const float* seg_len;
+    float* ws;
+    float* final_traj;
+    float* best_traj;
+    float* batch_costs;
+    float* iter_means;
+    int* iters;
+    int T, V, J, n_seg;
+    int B, stride, n_win;
+    int traj_in_lds;
+    mvp_sgd_params p;
+};
+
+struct Proj {
+    float u, v;                 // pixel
+    float x, y;                 // normalised (undistorted) coordinates
+    float P2;                   // camera-frame depth
+    float r2, rad, h2;
+    float xd, yd;
+};
+
+// project_points_torch (pose_refinement.py:118-177) for one point, torch op order.
+__device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, float X1, float X2, bool ign) {
+    const float* K = c;
+    const float* R = c + 9;
+    const float* T = c + 18;
+    const float* d = c + 21;
+    Proj o;
+    const float P0 = X0 * R[0] + X1 * R[1] + X2 * R[2] + T[0];
+    const float P1 = X0 * R[3] + X1 * R[4] + X2 * R[5] + T[1];
+    const float P2 = X0 * R[6] + X1 * R[7] + X2 * R[8] + T[2];
+    o.P2 = P2;
+    o.x = P0 / P2;
+    o.y = P1 / P2;
+    if (!ign) {
+        const float x = o.x, y = o.y;
+        const float r2 = x * x + y * y;
+        const float k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3], k3 = d[4];
+        const float rad = 1.f + k1 * r2 + k2 * (r2 * r2) + k3 * (r2 * r2 * r2);
+        float xd = x * rad, yd = y * rad;
+        xd = xd + (2.f * p1 * x * y + p2 * (r2 + 2.f * (x * x)));
+        yd = yd + (p1 * (r2 + 2.f * (y * y)) + 2.f * p2 * x * y);
+        o.r2 = r2;
+        o.rad = rad;
+        o.xd = xd;
+        o.yd = yd;
+    } else {
+        o.r2 = 0.f;
+        o.rad = 1.f;
+        o.xd = o.x;
+        o.yd = o.y;
+    }
+    const float h0 = o.xd * K[0] + o.yd * K[1] + K[2];
+    const float h1 = o.xd * K[3] + o.yd * K[4] + K[5];
+    const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
+    o.h2 = h2;
+    o.u = h0 / h2;
+    o.v = h1 / h2;
+    return o;
+}
+
+// d(u,v)/dX transposed applied to (gu, gv): the adjoint of project().
+__device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const Proj& o, bool ign, float gu,
+                                                float gv, float& g0, float& g1, float& g2) {
+    const float* K = c;
+    const float* R = c + 9;
+    const float* d = c + 21;
+    // (u, v) = (h0, h1) / h2, h = K·[xd, yd, 1]
+    const float ih2 = 1.f / o.h2;
+    const float gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
+    const float gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
+    float gx = gxd, gy = gyd;
+    if (!ign) {
+        const float x = o.x, y = o.y, r2 = o.r2, rad = o.rad;
+        const float k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3], k3 = d[4];
+        const float drad = k1 + 2.f * k2 * r2 + 3.f * k3 * r2 * r2;
+        const float dxx = rad + 2.f * x * x * drad + 2.f * p1 * y + 6.f * p2 * x;
+        const float dxy = 2.f * x * y * drad + 2.f * p1 * x + 2.f * p2 * y;
+        const float dyy = rad + 2.f * y * y * drad + 6.f * p1 * y + 2.f * p2 * x;
+        gx = dxx * gxd + dxy * gyd;   // d(xd,yd)/dx is symmetric in its off-diagonal
+        gy = dxy * gxd + dyy * gyd;
+    }
+    // x = P0/P2, y = P1/P2, P = R·X + T
+    const float iP2 = 1.f / o.P2;
+    const float a = gx * iP2, b = gy * iP2, cz = -(gx * o.x + gy * o.y) * iP2;
+    g0 = R[0] * a + R[3] * b + R[6] * cz;
+    g1 = R[1] * a + R[4] * b + R[7] * cz;
+    g2 = R[2] * a + R[5] * b + R[8] * cz;
+}
+
+// Σ⁻¹ of (cov + 1e-6·I) (pose_refinement.py:663-668), cov = [g2 g3; g4 g5].
+__device__ __forceinline__ void cov_inverse(const float* __restrict__ g, float& a00, float& a01, float& a10,
+                                            float& a11) {
+    const float c00 = g[2] + 1e-6f, c01 = g[3], c10 = g[4], c11 = g[5] + 1e-6f;
+    const float det = c00 * c11 - c01 * c10;
+    a00 = c11 / det;
+    a01 = -c01 / det;
+    a10 = -c10 / det;
+    a11 = c00 / det;
+}
+
+// Per (frame, camera, joint): the Gaussian mean and Σ⁻¹, computed once per launch.
+struct Target {
+    float m0, m1, a00, a01, a10, a11;
+};
+
+__device__ __forceinline__ Target load_target(const float* __restrict__ tg) {
+    const float2 p = *reinterpret_cast<const float2*>(tg);
+    const float2 q = *reinterpret_cast<const float2*>(tg + 2);
+    const float2 r = *reinterpret_cast<const float2*>(tg + 4);
+    return {p.x, p.y, q.x, q.y, r.x, r.y};
+}
+
+// 0.5·dᵀΣ⁻¹d (the negated gaussian_likelihood quadratic term, :741-758)
+__device__ __forceinline__ float quad_cost(const Target& g, float d0, float d1) {
+    return 0.5f * ((d0 * g.a00 + d1 * g.a10) * d0 + (d0 * g.a01 + d1 * g.a11) * d1);
+}
+
+constexpr int kU = 4;   // points per thread in flight (independent loads issued together)
+
+template <int BS, int NV>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[8]) {
+#pragma unroll
+    for (int i = 0; i < NV; i++)
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v[i] += __shfl_xor(v[i], off, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0)
+#pragma unroll
+        for (int i = 0; i < NV; i++) red[w][i] = v[i];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < BS / 64; k++) s += red[k][i];
+        v[i] = s;
+    }
+}
+
+__device__ __forceinline__ bool finite(float x) { return !(isnan(x) || isinf(x)); }
+
+template <int BS>
+__global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
+    extern __shared__ float lds_traj[];
+    __shared__ float cam_s[kMaxSgdCams * MVP_SGD_CAM_FLOATS];
+    __shared__ int seg_s[kMaxSeg * 2];
+    __shared__ float seglen_s[kMaxSeg];
+    __shared__ double red_s[BS / 64][8];
+
+    const int m = blockIdx.x, tid = threadIdx.x;
+    const int T = a.T, V = a.V, J = a.J, B = a.B, NS = a.n_seg;
+    const int TJ = T * J, n3 = TJ * 3;
+    const bool ign = a.p.ignore_distortions != 0;
+    const bool own = a.p.own_camera_gaussians != 0;
+    const bool use_s = a.p.lambda_smooth > 0, use_b = a.p.lambda_body_length > 0;
+    const float lam_s = (float)a.p.lambda_smooth, lam_b = (float)a.p.lambda_body_length;
+
+    const int Vg = own ? V : 1;                     // cameras with their own Gaussian
+    float* ws = a.ws + (size_t)m * ((size_t)4 * n3 + T + (size_t)T * V * J * 6);
+    float* X = a.traj_in_lds ? lds_traj : ws;
+    float* mo = ws + n3;
+    float* ve = ws + 2 * (size_t)n3;
+    float* gb = ws + 3 * (size_t)n3;
+    float* sterm = ws + 4 * (size_t)n3;            // per-window smoothness terms ‖D‖²
+    float* tgt = sterm + T;                         // [T][Vg][J][6] Target records
+    const float* G = a.gauss + (size_t)m * T * V * J * 6;
+    const float* X0 = a.traj0 + (size_t)m * n3;
+    float* best = a.best_traj + (size_t)m * n3;
+
+    for (int i = tid; i < V * MVP_SGD_CAM_FLOATS; i += BS) cam_s[i] = a.cams[i];
+    for (int i = tid; i < NS; i += BS) {
+        seg_s[2 * i] = a.seg[2 * i];
+        seg_s[2 * i + 1] = a.seg[2 * i + 1];
+        seglen_s[i] = a.seg_len[i];
+    }
+    for (int r = tid; r < T * Vg * J; r += BS) {
+        const int j = r % J, tc = r / J, c = tc % Vg, t = tc / Vg;
+        const float* g = G + (((size_t)t * V + c) * J + j) * 6;
+        float A00, A01, A10, A11;
+        cov_inverse(g, A00, A01, A10, A11);
+        float* o = tgt + (size_t)r * 6;
+        o[0] = g[0];
+        o[1] = g[1];
+        o[2] = A00;
+        o[3] = A01;
+        o[4] = A10;
+        o[5] = A11;
+    }
+    for (int e = tid; e < n3; e += BS) {
+        X[e] = X0[e];
+        mo[e] = 0.f;
+        ve[e] = 0.f;
+        best[e] = __builtin_nanf("");
+    }
+    __syncthreads();
+
+    // ‖a‖² of the repeated body-length vector (create_body_length_vect, :765-781)
+    double aa = 0.0;
+    for (int s = 0; s < NS; s++) aa += (double)seglen_s[s] * seglen_s[s];
+    aa *= B;
+
+    const float w1 = (float)(1.0 - a.p.beta1);
+    const float b2 = (float)a.p.beta2, w2 = (float)(1.0 - a.p.beta2);
+    const float eps = (float)a.p.adam_eps;
+    const int n_win = a.n_win;
+
+    double hist_sum[MVP_SGD_N_COSTS] = {0, 0, 0, 0};
+    long hist_cnt = 0;
+    float best_total = INFINITY;
+    int no_imp = 0, it = 0, step = 0;
+
+    while (no_imp < a.p.patience && it <= a.p.max_iter) {
+        for (int w = 0; w < n_win; w++) {
+            const int t0 = w * a.stride;
+            const int nq = B * J;
+            // ---- pass A: forward costs
+            double acc[6] = {0, 0, 0, 0, 0, 0};   // lsum, lcnt, ssum, scnt, ab, bb
+            // likelihood value AND its (not yet 1/n-scaled) gradient: one projection per
+            // (point, camera) per step; the scale needs the global finite count.
+            for (int q0 = tid; q0 < nq; q0 += kU * BS) {
+                float xs[kU][3];
+                Target tg[kU];
+                int tq[kU], jq[kU];
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const int q = min(q0 + u * BS, nq - 1);
+                    tq[u] = t0 + q / J;
+                    jq[u] = q - (q / J) * J;
+                    const float* x = X + 3 * (tq[u] * J + jq[u]);
+                    xs[u][0] = x[0];
+                    xs[u][1] = x[1];
+                    xs[u][2] = x[2];
+                    tg[u] = load_target(tgt + ((size_t)tq[u] * Vg * J + jq[u]) * 6);
+                }
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const int q = q0 + u * BS;
+                    if (q >= nq) break;
+                    float lsum = 0.f, g0 = 0.f, g1 = 0.f, g2 = 0.f;
+                    int lcnt = 0;
+                    for (int c = 0; c < V; c++) {
+                        const float* cam = cam_s + c * MVP_SGD_CAM_FLOATS;
+                        const Proj o = project(cam, xs[u][0], xs[u][1], xs[u][2], ign);
+                        const Target g =
+                            own ? load_target(tgt + (((size_t)tq[u] * Vg + c) * J + jq[u]) * 6) : tg[u];
+                        const float d0 = o.u - g.m0, d1 = o.v - g.m1;
+                        const float val = quad_cost(g, d0, d1);
+                        if (!finite(val)) continue;
+                        lsum += val;
+                        lcnt++;
+                        const float s01 = g.a01 + g.a10;
+                        const float gu = 0.5f * (2.f * g.a00 * d0 + s01 * d1);
+                        const float gv = 0.5f * (s01 * d0 + 2.f * g.a11 * d1);
+                        float h0, h1, h2;
+                        project_adjoint(cam, o, ign, gu, gv, h0, h1, h2);
+                        g0 += h0;
+                        g1 += h1;
+                        g2 += h2;
+                    }
+                    acc[0] += lsum;
+                    acc[1] += lcnt;
+                    gb[3 * q + 0] = g0;
+                    gb[3 * q + 1] = g1;
+                    gb[3 * q + 2] = g2;
+                }
+            }
+            if (use_s)
+                for (int i = 2 + tid; i < B; i += BS) {
+                    const int t = t0 + i;
+                    const float* xa = X + 3 * t * J;
+                    const float* xb = xa - 3 * J;
+                    const float* xc = xb - 3 * J;
+                    float ss = 0.f;
+                    for (int e = 0; e < 3 * J; e++) {
+                        const float D = (xa[e] - xb[e]) - (xb[e] - xc[e]);
+                        ss += D * D;
+                    }
+                    const float nrm = sqrtf(ss);
+                    const float term = nrm * nrm;
+                    sterm[i] = term;
+                    if (finite(term)) {
+                        acc[2] += term;
+                        acc[3] += 1.0;
+                    }
+                }
+            if (use_b)
+                for (int r = tid; r < NS * B; r += BS) {
+                    const int s = r / B, t = t0 + (r - s * B);
+                    const float* xa = X + 3 * (t * J + seg_s[2 * s]);
+                    const float* xb = X + 3 * (t * J + seg_s[2 * s + 1]);
+                    const float e0 = xb[0] - xa[0], e1 = xb[1] - xa[1], e2 = xb[2] - xa[2];
+                    const float len = sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
+                    acc[4] += (double)seglen_s[s] * len;
+                    acc[5] += (double)len * len;
+                }
+            block_sum<BS>(acc, red_s);
+            const float L = (float)(acc[0] / acc[1]);
+            const float S = lam_s * (float)(acc[2] / acc[3]);
+            const float mu = (float)acc[4] / (float)acc[5];
+            const float lscale = acc[1] > 0 ? (float)(1.0 / acc[1]) : 0.f;
+            const float sscale = acc[3] > 0 ? 2.f * lam_s * (float)(1.0 / acc[3]) : 0.f;
+            const float bscale = -2.f * lam_b * mu / (float)aa;
+
+            // ---- pass B: gradient of the window's total cost, pulled per owned point
+            double acc2[2] = {0, 0};   // ‖g‖², Σ r²
+            for (int q = tid; q < nq; q += BS) {
+                const int i = q / J, j = q - i * J, t = t0 + i;
+                float g0 = gb[3 * q + 0] * lscale, g1 = gb[3 * q + 1] * lscale, g2 = gb[3 * q + 2] * lscale;
+                if (use_s) {
+                    // terms centred at t (coef +1), t+1 (-2), t+2 (+1), each 2·λs/n·D
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        const int ic = i + k;
+                        if (ic < 2 || ic >= B || !finite(sterm[ic])) continue;
+                        const float coef = (k == 1 ? -2.f : 1.f) * sscale;
+                        const float* xa = X + 3 * ((t + k) * J + j);
+                        const float* xb = xa - 3 * J;
+                        const float* xc = xb - 3 * J;
+                        g0 += coef * ((xa[0] - xb[0]) - (xb[0] - xc[0]));
+                        g1 += coef * ((xa[1] - xb[1]) - (xb[1] - xc[1]));
+                        g2 += coef * ((xa[2] - xb[2]) - (xb[2] - xc[2]));
+                    }
+                }
+                if (use_b)
+                    for (int s = 0; s < NS; s++) {
+                        const int ja = seg_s[2 * s], jb = seg_s[2 * s + 1];
+                        if (ja != j && jb != j) continue;
+                        const float* xa = X + 3 * (t * J + ja);
+                        const float* xb = X + 3 * (t * J + jb);
+                        const float e0 = xb[0] - xa[0], e1 = xb[1] - xa[1], e2 = xb[2] - xa[2];
+                        const float len = sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
+                        if (!(len > 0.f)) continue;
+                        const float r = seglen_s[s] - mu * len;
+                        float dl = bscale * r / len;
+                        if (ja == j) dl = -dl;
+                        if (ja == jb) dl = 0.f;
+                        g0 += dl * e0;
+                        g1 += dl * e1;
+                        g2 += dl * e2;
+                    }
+                gb[3 * q + 0] = g0;
+                gb[3 * q + 1] = g1;
+                gb[3 * q + 2] = g2;
+                acc2[0] += (double)g0 * g0 + (double)g1 * g1 + (double)g2 * g2;
+            }
+            if (use_b)
+                for (int r = tid; r < NS * B; r += BS) {
+                    const int s = r / B, t = t0 + (r - s * B);
+                    const float* xa = X + 3 * (t * J + seg_s[2 * s]);
+                    const float* xb = X + 3 * (t * J + seg_s[2 * s + 1]);
+                    const float e0 = xb[0] - xa[0], e1 = xb[1] - xa[1], e2 = xb[2] - xa[2];
+                    const float len = sqrtf(e0 * e0 + e1 * e1 + e2 * e2);
+                    const float rr = seglen_s[s] - mu * len;
+                    acc2[1] += (double)rr * rr;
+                }
+            block_sum<BS>(acc2, red_s);
+            const float gnorm = (float)sqrt(acc2[0]);
+            const float coef = fminf((float)a.p.max_grad_norm / (gnorm + 1e-6f), 1.f);
+            const float Bc = lam_b * (float)acc2[1] / (float)aa;
+
+            // ---- pass C: Adam over the whole trajectory (torch _single_tensor_adam)
+            step++;
+            const double bc1 = 1.0 - pow(a.p.beta1, (double)step);
+            const double bc2 = 1.0 - pow(a.p.beta2, (double)step);
+            const float nstep = (float)(-(a.p.lr / bc1));
+            const float bc2s = (float)sqrt(bc2);
+            const int wlo = t0 * J * 3, whi = (t0 + B) * J * 3;
+            for (int e = tid; e < n3; e += BS) {
+                const float g = (e >= wlo && e < whi) ? gb[e - wlo] * coef : 0.f;
+                float mv = mo[e];
+                mv = (w1 < 0.5f) ? mv + w1 * (g - mv) : g - (g - mv) * (1.f - w1);
+                float vv = ve[e] * b2;
+                vv = vv + w2 * g * g;
+                mo[e] = mv;
+                ve[e] = vv;
+                const float denom = sqrtf(vv) / bc2s + eps;
+                X[e] = X[e] + nstep * mv / denom;
+            }
+            __syncthreads();
+
+            float total = L;
+            if (use_s) total = total + S;
+            if (use_b) total = total + Bc;
+            const float rec[MVP_SGD_N_COSTS] = {total, L, use_s ? S : 0.f, use_b ? Bc : 0.f};
+#pragma unroll
+            for (int k = 0; k < MVP_SGD_N_COSTS; k++) hist_sum[k] += rec[k];
+            hist_cnt++;
+            if (tid == 0) {
+                float* bc = a.batch_costs + (((size_t)m * (a.p.max_iter + 1) + it) * n_win + w) * MVP_SGD_N_COSTS;
+#pragma unroll
+                for (int k = 0; k < MVP_SGD_N_COSTS; k++) bc[k] = rec[k];
+            }
+        }
+        // running mean over the shared list (F6): append the mean to the same list
+        float mean[MVP_SGD_N_COSTS];
+#pragma unroll
+        for (int k = 0; k < MVP_SGD_N_COSTS; k++) mean[k] = (float)(hist_sum[k] / (double)hist_cnt);
+#pragma unroll
+        for (int k = 0; k < MVP_SGD_N_COSTS; k++) hist_sum[k] += mean[k];
+        hist_cnt++;
+        if (tid == 0) {
+            float* im = a.iter_means + ((size_t)m * (a.p.max_iter + 1) + it) * MVP_SGD_N_COSTS;
+#pragma unroll
+            for (int k = 0; k < MVP_SGD_N_COSTS; k++) im[k] = mean[k];
+        }
+        if (mean[0] < best_total - (float)a.p.tolerance) {
+            best_total = mean[0];
+            for (int e = tid; e < n3; e += BS) best[e] = X[e];
+            no_imp = 0;
+        } else {
+            no_imp++;
+        }
+        it++;
+        if (no_imp >= a.p.patience) break;
+    }
+    float* fin = a.final_traj + (size_t)m * n3;
+    for (int e = tid; e < n3; e += BS) fin[e] = X[e];
+    if (tid == 0) a.iters[m] = it;
+}
+
+__global__ void project_kernel(const float* __restrict__ pts, long n, const float* __restrict__ cam, int ign,
+                               float* __restrict__ uv) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float c[MVP_SGD_CAM_FLOATS];
+#pragma unroll
+    for (int k = 0; k < MVP_SGD_CAM_FLOATS; k++) c[k] = cam[k];
+    const Proj o = project(c, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], ign != 0);
+    uv[2 * i] = o.u;
+    uv[2 * i + 1] = o.v;
+}
+
+}  // namespace
+
+extern "C" int mvp_sgd_workspace_floats(int M, int T, int V, int J, int64_t* out) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(out && M > 0 && T > 0 && V > 0 && J > 0, "mvp_sgd_workspace_floats: bad arguments");
+    *out = (int64_t)M * ((int64_t)4 * T * J * 3 + T + (int64_t)T * V * J * 6);
+    MVP_ABI_END
+}
+
+extern "C" int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J,
+                              const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p,
+                              float* workspace, float* final_traj, float* best_traj, float* batch_costs,
+                              float* iter_means, int* iters, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(p && gauss && traj0 && cams && workspace && final_traj && best_traj && batch_costs && iter_means &&
+                    iters,
+                "mvp_sgd_refine: null pointer");
+    MVP_REQUIRE(M > 0 && T > 0 && V > 0 && J > 0, "mvp_sgd_refine: M, T, V, J must be positive");
+    MVP_REQUIRE(V <= kMaxSgdCams, "mvp_sgd_refine: V=%d > %d cameras", V, kMaxSgdCams);
+    MVP_REQUIRE(J <= kMaxJ, "mvp_sgd_refine: J=%d > %d joints", J, kMaxJ);
+    MVP_REQUIRE(n_seg >= 0 && n_seg <= kMaxSeg, "mvp_sgd_refine: n_seg=%d outside [0, %d]", n_seg, kMaxSeg);
+    MVP_REQUIRE(n_seg == 0 || (seg && seg_len), "mvp_sgd_refine: segments missing");
+    MVP_REQUIRE(p->lambda_body_length <= 0 || n_seg > 0,
+                "mvp_sgd_refine: lambda_body_length > 0 needs body lengths (reference create_body_length_vect)");
+    MVP_REQUIRE(p->batch_size >= 2 && p->batch_size <= T, "mvp_sgd_refine: batch_size=%d outside [2, T=%d]",
+                p->batch_size, T);
+    MVP_REQUIRE(p->max_iter >= 0 && p->patience >= 0, "mvp_sgd_refine: max_iter/patience must be >= 0");
+    SgdArgs a;
+    a.gauss = gauss;
+    a.traj0 = traj0;
+    a.cams = cams;
+    a.seg = seg;
+    a.seg_len = seg_len;
+    a.ws = workspace;
+    a.final_traj = final_traj;
+    a.best_traj = best_traj;
+    a.batch_costs = batch_costs;
+    a.iter_means = iter_means;
+    a.iters = iters;
+    a.T = T;
+    a.V = V;
+    a.J = J;
+    a.n_seg = n_seg;
+    a.B = p->batch_size;
+    a.stride = p->batch_size / 2;
+    // windows cover the first floor(T/B)*B rows (sgd_optimize :900-905); later rows only see Adam
+    // with zero gradient, i.e. stay where they started.
+    const int t_win = (T / a.B) * a.B;
+    a.n_win = (t_win - a.B) / a.stride + 1;
+    a.p = *p;
+    const size_t traj_bytes = (size_t)T * J * 3 * sizeof(float);
+    constexpr size_t kLdsBudget = 120 * 1024;
+    a.traj_in_lds = traj_bytes <= kLdsBudget;
+    const size_t lds = a.traj_in_lds ? traj_bytes : 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (T * J > 1024) {
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kLdsBudget));
+        hipLaunchKernelGGL(sgd_kernel<512>, dim3(M), dim3(512), lds, s, a);
+    } else {
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kLdsBudget));
+        hipLaunchKernelGGL(sgd_kernel<256>, dim3(M), dim3(256), lds, s, a);
+    }
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_project_points(const float* pts, int64_t n, const float* cam, int ignore_distortions, float* uv,
+                                  void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n >= 0 && (n == 0 || (pts && cam && uv)), "mvp_project_points: bad arguments");
+    if (n == 0) return MVP_OK;
+    constexpr int kBlock = 256;
+    hipLaunchKernelGGL(project_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, pts, (long)n, cam, ignore_distortions, uv);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}

@@ -1,0 +1,278 @@
+"""Reprojection-error trajectory refinement on the GPU (mvp_sgd_refine).
+
+Host mirror of the reference's refinement API (pose_refinement.py):
+
+* ``Optimized_3d_Pose_Estimation(gaussians, initial_trajectory,
+  decomposed_cam_params_initial, body_lengths, camera_IDs, ...)`` (:579) and
+  its ``sgd_optimize(**kwargs)`` (:894) with the same keywords and defaults;
+  afterwards ``best_trajectory``, ``trajectory``, ``all_costs_total`` and
+  ``best_decomposed_cam_params`` read like the reference's.  The whole
+  optimisation (every iteration and window) is ONE kernel launch.
+* ``refine_trajectories(...)``: M independent trajectories (same rig) in one
+  launch, one workgroup each — the throughput form (SGD shards as replicas).
+* ``project_points_torch`` (:94-179) on the GPU.
+
+Scope: the trajectory-only path the CLI runs (:1210-1214).  Extrinsic learning
+from samples (:684-706, :800-831), the NN trajectory parameterisation
+(``use_NN``) and ``randomize_params`` are outside the hot path and raise
+NotImplementedError.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call
+
+CAM_FLOATS = 26
+N_COSTS = 4
+COST_NAMES = ("total_cost", "likelihood_cost", "smoothness_cost", "body_length_cost")
+
+# reference utils.py:1067 CONNECTIVITY_DICT['coco'], joint names utils.py:1071-1155;
+# segment names are generate_connectivity_names' "<start>_<end>" (utils.py:1055-1062).
+COCO_JOINTS = ("nose", "left_eye", "right_eye", "left_ear", "right_ear", "left_shoulder", "right_shoulder",
+               "left_elbow", "right_elbow", "left_wrist", "right_wrist", "left_hip", "right_hip", "left_knee",
+               "right_knee", "left_ankle", "right_ankle")
+COCO_CONNECTIONS = ((0, 1), (0, 2), (1, 3), (2, 4), (5, 7), (7, 9), (6, 8), (8, 10), (11, 13), (13, 15),
+                    (12, 14), (14, 16), (5, 6), (5, 11), (6, 12), (11, 12))
+SEGMENTS = {f"{COCO_JOINTS[a]}_{COCO_JOINTS[b]}": (a, b) for a, b in COCO_CONNECTIONS}
+
+
+class SgdParams(ctypes.Structure):
+    """mvp_sgd_params (include/mvpose.h)."""
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("adam_eps", ctypes.c_double), ("lambda_smooth", ctypes.c_double),
+                ("lambda_body_length", ctypes.c_double), ("tolerance", ctypes.c_double),
+                ("max_grad_norm", ctypes.c_double), ("patience", ctypes.c_int), ("max_iter", ctypes.c_int),
+                ("batch_size", ctypes.c_int), ("ignore_distortions", ctypes.c_int),
+                ("own_camera_gaussians", ctypes.c_int)]
+
+
+_lib.lib.mvp_sgd_refine.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                    ctypes.POINTER(SgdParams), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _device(device):
+    dev = torch.device(device if device is not None else "cuda")
+    if dev.type != "cuda":
+        raise ValueError("mvpose refinement runs on the GPU only (no CPU fallback)")
+    return dev
+
+
+def rotation_conversion(rotation_rep, to_vector=True):
+    """utils.py:1219-1268: axis-angle <-> matrix (host, float32 torch like the reference)."""
+    was_np = isinstance(rotation_rep, np.ndarray)
+    r = torch.as_tensor(rotation_rep)
+    if r.shape == (3, 3) and to_vector:
+        theta = torch.acos((torch.trace(r) - 1) / 2)
+        if torch.abs(theta) < 1e-6:
+            return torch.zeros(3)
+        s = 2 * torch.sin(theta)
+        out = theta * torch.tensor([(r[2, 1] - r[1, 2]) / s, (r[0, 2] - r[2, 0]) / s, (r[1, 0] - r[0, 1]) / s])
+    elif r.shape != (3, 3) and not to_vector:
+        theta = torch.norm(r)
+        if torch.abs(theta) < 1e-6:
+            return torch.eye(3)
+        ux, uy, uz = r / theta
+        k = torch.tensor([[0, -uz, uy], [uz, 0, -ux], [-uy, ux, 0]])
+        out = torch.eye(3) + torch.sin(theta) * k + (1 - torch.cos(theta)) * torch.mm(k, k)
+    else:
+        out = r
+    return np.array(out) if was_np else out
+
+
+def camera_record(K, R, T, dist) -> np.ndarray:
+    """One MVP_SGD_CAM_FLOATS f32 record [K | R (matrix) | T | dist] from the reference's
+    decomposed parameters (R may be a 3x3 matrix or an axis-angle vector)."""
+    f32 = (lambda a: torch.as_tensor(np.asarray(a) if not isinstance(a, torch.Tensor) else a).to(torch.float32))
+    Rm = rotation_conversion(f32(R), to_vector=False)
+    d = f32(dist).reshape(-1)
+    if d.numel() != 5:
+        raise ValueError("dist_coeffs must have shape (1, 5)")
+    rec = np.concatenate([f32(K).reshape(9).numpy(), torch.as_tensor(Rm, dtype=torch.float32).reshape(9).numpy(),
+                          f32(T).reshape(3).numpy(), d.numpy()]).astype(np.float32)
+    return rec
+
+
+def segments_for(body_lengths):
+    """body_lengths {segment name: length} (YAML order) -> (pairs int32 (n,2), lengths f32 (n,))."""
+    names = list(body_lengths.keys())
+    unknown = [n for n in names if n not in SEGMENTS]
+    if unknown:
+        raise KeyError(f"unknown body segment(s) {unknown}; expected names from {list(SEGMENTS)}")
+    pairs = np.array([SEGMENTS[n] for n in names], np.int32).reshape(-1, 2)
+    lens = np.array([float(body_lengths[n]) for n in names], np.float32)
+    return pairs, lens
+
+
+def project_points_torch(points, K, R, T, dist_coeffs, indicies=None, torch_dtype=torch.float32,
+                         ignore_distortions=False, device=None):
+    """pose_refinement.py:94-179 on the GPU: (Time, N, 3) -> (len(indicies), N, 2) f32.
+    Returned on the device the points came from (CPU points are copied over and back)."""
+    if torch_dtype != torch.float32:
+        raise NotImplementedError("float32 only (the reference's default)")
+    pts = torch.as_tensor(points).to(torch.float32)
+    if pts.dim() != 3 or pts.shape[2] != 3:
+        raise ValueError("points must have shape (Time, N, 3)")
+    home = pts.device
+    dev = _device(device if device is not None else (home if home.type == "cuda" else "cuda"))
+    rows = list(range(pts.shape[0])) if indicies is None else list(indicies)
+    sel = pts[rows].reshape(-1, 3).to(dev).contiguous()
+    cam = torch.from_numpy(camera_record(K, R, T, dist_coeffs)).to(dev)
+    uv = torch.empty((sel.shape[0], 2), dtype=torch.float32, device=dev)
+    call("mvp_project_points", _ptr(sel), sel.shape[0], _ptr(cam), int(bool(ignore_distortions)), _ptr(uv),
+         _stream(dev))
+    return uv.reshape(len(rows), pts.shape[1], 2).to(home)
+
+
+def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=None, lr=0.001, betas=(0.9, 0.999),
+                        lambda_smooth=1.0, lambda_body_length=1.0, patience=100, tolerance=1e-5, max_iter=1000,
+                        batch_size=None, ignore_distortions=False, own_camera_gaussians=False, max_grad_norm=1.0,
+                        adam_eps=1e-8, device=None):
+    """M trajectories in one launch.  gaussians (M,T,V,J,6), initial_trajectories (M,T,J,3)
+    (already time-sliced), cameras = V x (K, R, T, dist).  Returns device tensors:
+    best (M,T,J,3) (NaN rows if never improved), final, batch_costs (M,max_iter+1,n_win,4),
+    iter_means (M,max_iter+1,4), iters (M,)."""
+    dev = _device(device)
+    G = torch.as_tensor(gaussians).to(device=dev, dtype=torch.float32).contiguous()
+    X0 = torch.as_tensor(initial_trajectories).to(device=dev, dtype=torch.float32).contiguous()
+    if G.dim() != 5 or G.shape[-1] != 6 or X0.dim() != 4 or X0.shape[-1] != 3:
+        raise ValueError("gaussians must be (M,T,V,J,6) and initial_trajectories (M,T,J,3)")
+    M, T, V, J = G.shape[:4]
+    if X0.shape[:3] != (M, T, J):
+        raise ValueError(f"initial_trajectories {tuple(X0.shape)} does not match gaussians {tuple(G.shape)}")
+    if len(cameras) != V:
+        raise ValueError(f"{len(cameras)} cameras for V={V}")
+    B = T if batch_size is None else int(batch_size)
+    if B < 2 or B > T:
+        raise ValueError(f"batch_size {B} must be in [2, T={T}]")
+    if lambda_body_length > 0 and not body_lengths:
+        raise ValueError("lambda_body_length > 0 needs body_lengths (reference create_body_length_vect)")
+    cams = torch.from_numpy(np.stack([camera_record(*c) for c in cameras])).to(dev)
+    if body_lengths:
+        pairs, lens = segments_for(body_lengths)
+        seg = torch.from_numpy(pairs).to(dev)
+        seg_len = torch.from_numpy(lens).to(dev)
+        n_seg = len(lens)
+    else:
+        seg = seg_len = None
+        n_seg = 0
+    p = SgdParams(lr=float(lr), beta1=float(betas[0]), beta2=float(betas[1]), adam_eps=float(adam_eps),
+                  lambda_smooth=float(lambda_smooth), lambda_body_length=float(lambda_body_length),
+                  tolerance=float(tolerance), max_grad_norm=float(max_grad_norm), patience=int(patience),
+                  max_iter=int(max_iter), batch_size=B, ignore_distortions=int(bool(ignore_distortions)),
+                  own_camera_gaussians=int(bool(own_camera_gaussians)))
+    t_win = (T // B) * B
+    n_win = (t_win - B) // (B // 2) + 1
+    nws = ctypes.c_int64()
+    call("mvp_sgd_workspace_floats", M, T, V, J, ctypes.byref(nws))
+    ws = torch.empty(nws.value, dtype=torch.float32, device=dev)
+    best = torch.empty_like(X0)
+    final = torch.empty_like(X0)
+    n_it = int(max_iter) + 1
+    batch_costs = torch.zeros((M, n_it, n_win, N_COSTS), dtype=torch.float32, device=dev)
+    iter_means = torch.zeros((M, n_it, N_COSTS), dtype=torch.float32, device=dev)
+    iters = torch.zeros(M, dtype=torch.int32, device=dev)
+    call("mvp_sgd_refine", _ptr(G), _ptr(X0), _ptr(cams), M, T, V, J, _ptr(seg), _ptr(seg_len), n_seg,
+         ctypes.byref(p), _ptr(ws), _ptr(final), _ptr(best), _ptr(batch_costs), _ptr(iter_means), _ptr(iters),
+         _stream(dev))
+    return {"best": best, "final": final, "batch_costs": batch_costs, "iter_means": iter_means, "iters": iters}
+
+
+class Optimized_3d_Pose_Estimation:
+    """GPU drop-in for pose_refinement.Optimized_3d_Pose_Estimation (:579-668)."""
+
+    def __init__(self, gaussians, initial_trajectory, decomposed_cam_params_initial=None, body_lengths=None,
+                 camera_IDs=None, R_initial=None, T_initial=None, N_sample_points=100, torch_dtype=torch.float32,
+                 device=None):
+        if torch_dtype != torch.float32:
+            raise NotImplementedError("float32 only (the reference's default)")
+        if decomposed_cam_params_initial is None:
+            raise ValueError("decomposed_cam_params_initial is required")
+        for cid, prm in decomposed_cam_params_initial.items():   # :601-606
+            if prm[1] is None:
+                prm[1] = torch.eye(3)
+            if prm[2] is None:
+                prm[2] = torch.zeros(3, 1)
+        self.device = _device(device)
+        self.torch_dtype = torch_dtype
+        self.gaussians = torch.as_tensor(np.asarray(gaussians) if not isinstance(gaussians, torch.Tensor)
+                                         else gaussians).to(torch.float32)
+        self.initial_trajectory = torch.as_tensor(np.asarray(initial_trajectory) if not isinstance(
+            initial_trajectory, torch.Tensor) else initial_trajectory).to(torch.float32)
+        self.decomposed_cam_params_initial = {
+            k: [torch.as_tensor(np.asarray(c) if not isinstance(c, torch.Tensor) else c).to(torch.float32)
+                for c in v] for k, v in decomposed_cam_params_initial.items()}
+        self.decomposed_cam_params = {k: [c.clone() for c in v] for k, v in self.decomposed_cam_params_initial.items()}
+        self.n_cams = self.gaussians.shape[1]
+        self.n_joints = self.gaussians.shape[2]
+        self.n_dims = self.initial_trajectory.shape[2]
+        self.N_sample_points = N_sample_points
+        self.body_lengths = body_lengths
+        self.camera_IDs = camera_IDs if camera_IDs is not None else list(decomposed_cam_params_initial.keys())
+        keys = list(self.decomposed_cam_params.keys())
+        self.camera_indices = [keys.index(i) for i in self.camera_IDs]
+        self.best_trajectory = None
+        self.best_decomposed_cam_params = None
+
+    def sgd_optimize(self, extrinsic_optimization_IDs=[], optimize_trajectory=True, lr=0.001, betas=(0.9, 0.999),
+                     lambda_smooth=1.0, lambda_body_length=1.0, patience=100, tolerance=1e-5, max_iter=1000,
+                     print_frequency=100, batch_size=None, N_sample_points=100, GT_camera_IDs=None,
+                     ignore_distortions=False, reset_camera_params=False, print_compute_times=False,
+                     time_interval=[0, -1], randomize_params=False, use_NN=False, own_camera_gaussians=False):
+        if extrinsic_optimization_IDs or not optimize_trajectory or use_NN or randomize_params:
+            raise NotImplementedError("only the trajectory-only refinement (the CLI's path) runs on the GPU")
+        if self.n_dims != 3:
+            raise NotImplementedError("3D trajectories only")
+        a, b = time_interval
+        G = self.gaussians[a:b]
+        X0 = self.initial_trajectory[a:b]
+        n_t = min(len(G), len(X0))
+        G, X0 = G[:n_t], X0[:n_t]
+        B = n_t if batch_size is None else int(batch_size)
+        cams = [self.decomposed_cam_params[i] for i in self.camera_IDs]
+        G = G[:, self.camera_indices] if own_camera_gaussians else G
+        r = refine_trajectories(G[None], X0[None], cams, body_lengths=self.body_lengths, lr=lr, betas=betas,
+                                lambda_smooth=lambda_smooth, lambda_body_length=lambda_body_length,
+                                patience=patience, tolerance=tolerance, max_iter=max_iter, batch_size=B,
+                                ignore_distortions=ignore_distortions, own_camera_gaussians=own_camera_gaussians,
+                                device=self.device)
+        iters = int(r["iters"][0].item())
+        best = r["best"][0].cpu()
+        self.trajectory = r["final"][0].cpu()
+        self.best_trajectory = None if torch.isnan(best).any() else best
+        if self.best_trajectory is not None:
+            self.best_decomposed_cam_params = {k: [p.clone() for p in v] for k, v in self.decomposed_cam_params.items()}
+        names = ["total_cost", "likelihood_cost"]
+        if lambda_smooth > 0:
+            names.append("smoothness_cost")
+        if lambda_body_length > 0:
+            names.append("body_length_cost")
+        bc = r["batch_costs"][0, :iters].cpu().numpy()
+        im = r["iter_means"][0, :iters].cpu().numpy()
+        hist = {n: [] for n in names}
+        for it in range(iters):           # the reference's shared cost / running-mean list (F6)
+            for n in names:
+                k = COST_NAMES.index(n)
+                hist[n].extend(np.float32(v) for v in bc[it, :, k])
+                hist[n].append(np.float32(im[it, k]))
+        self.all_costs_total = hist
+        self.iterations = iters
+        if print_frequency and print_frequency < 10 ** 8:
+            for it in range(0, iters, print_frequency):
+                print(f"Iteration {it}: " + ", ".join(f"{n}: {im[it, COST_NAMES.index(n)]:.2e}" for n in names))
+        return self
