@@ -37,8 +37,20 @@ def parse():
     ap.add_argument("--frames", type=int, default=256, help="synchronised frames per step per GPU")
     ap.add_argument("--views", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-frames", type=int, default=4)
+    ap.add_argument("--cpu-sample-frames", type=int, default=12)
     return ap.parse_args()
+
+
+def committed_traffic():
+    """HBM bytes per launch from the newest committed PMC pass (profiles/rNN_traffic.json,
+    tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected) — PMC counters cannot be
+    read from inside a normal run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return {}, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
 def setup_dist(args):
@@ -152,6 +164,7 @@ def main():
     tri_gbs = tri_bytes / (tri_ms * 1e-3) / 1e9
 
     if rank == 0:
+        traffic, traffic_src = committed_traffic()
         total_frames = world * B * args.steps
         res = {
             "metric": METRIC,
@@ -171,10 +184,12 @@ def main():
                        "crops_per_step_per_gpu": 2 * B * V, "parallelism": f"dp{world} (frame-sharded)"},
             "roofline": {"bound": "mfma", "kernel": "HRNet-W32 conv graph (conv_mfma_kernel family)",
                          "achieved": bb_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": bb_tflops / BF16_PEAK_TFLOPS, "traffic": None,
-                         "flops_per_launch": flops, "avg_launch_ms": bb_ms},
+                         "frac": bb_tflops / BF16_PEAK_TFLOPS,
+                         "traffic": traffic.get("backbone", {}).get("hbm_bytes_per_launch"),
+                         "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": bb_ms},
             "roofline_triangulate": {"bound": "hbm", "achieved": tri_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": tri_gbs / HBM_PEAK_GBS, "bytes_per_launch": tri_bytes,
+                                     "traffic": traffic.get("triangulate", {}).get("hbm_bytes_per_launch"),
                                      "avg_launch_ms": tri_ms},
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -220,6 +220,15 @@ int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, in
 int mvp_project_points(const float* pts, int64_t n, const float* cam, int ignore_distortions, float* uv,
                        void* stream);
 
+/* ---------------------------------------------------------------------------
+ * linear_interpolation (pose_refinement.py:15-84; always run by the refinement
+ * CLI, :1170-1172): outlier-filtered local linear fit per (t, point, dim).
+ * pts_dev/out_dev [T][P][D] f32; k <= 30; see csrc/interp.hip for the rules.
+ * ------------------------------------------------------------------------- */
+int mvp_linear_interpolation(const float* pts_dev, int T, int P, int D, int k, float k_std, float median_std,
+                             int use_rolling_average, int filter_distance_from_median, float* out_dev,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

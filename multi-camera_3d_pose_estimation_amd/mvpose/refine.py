@@ -10,7 +10,7 @@ Host mirror of the reference's refinement API (pose_refinement.py):
   optimisation (every iteration and window) is ONE kernel launch.
 * ``refine_trajectories(...)``: M independent trajectories (same rig) in one
   launch, one workgroup each — the throughput form (SGD shards as replicas).
-* ``project_points_torch`` (:94-179) on the GPU.
+* ``project_points_torch`` (:94-179) and ``linear_interpolation`` (:15-84) on the GPU.
 
 Scope: the trajectory-only path the CLI runs (:1210-1214).  Extrinsic learning
 from samples (:684-706, :800-831), the NN trajectory parameterisation
@@ -137,6 +137,26 @@ def project_points_torch(points, K, R, T, dist_coeffs, indicies=None, torch_dtyp
     call("mvp_project_points", _ptr(sel), sel.shape[0], _ptr(cam), int(bool(ignore_distortions)), _ptr(uv),
          _stream(dev))
     return uv.reshape(len(rows), pts.shape[1], 2).to(home)
+
+
+def linear_interpolation(points, k=5, k_std=2, median_std=2, use_rolling_average=False,
+                         filter_distance_from_median=True, device=None):
+    """pose_refinement.py:15-84 on the GPU (mvp_linear_interpolation).  points (T, P, D) or
+    (T, P); returns a float32 array of the same shape (numpy in, numpy out; tensors stay tensors)."""
+    was_tensor = isinstance(points, torch.Tensor)
+    x = points if was_tensor else torch.from_numpy(np.ascontiguousarray(np.asarray(points)))
+    home = x.device
+    dev = _device(device if device is not None else (home if home.type == "cuda" else "cuda"))
+    squeeze = x.dim() == 2
+    x = (x[..., None] if squeeze else x).to(device=dev, dtype=torch.float32).contiguous()
+    if x.dim() != 3:
+        raise ValueError("points must be (time, n_points, dim) or (time, n_points)")
+    out = torch.empty_like(x)
+    T, P, D = x.shape
+    call("mvp_linear_interpolation", _ptr(x), T, P, D, int(k), float(k_std), float(median_std),
+         int(bool(use_rolling_average)), int(bool(filter_distance_from_median)), _ptr(out), _stream(dev))
+    out = out[..., 0] if squeeze else out
+    return out.to(home) if was_tensor else out.cpu().numpy()
 
 
 def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=None, lr=0.001, betas=(0.9, 0.999),

@@ -2,7 +2,7 @@
 itself (sashapersonxyz/Multi-camera_3D_Pose_Estimation at /root/reference).
 
 Runs ONLY in the build container (the reference never travels to the GPU box):
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [generator ...]   (default: all)
 The reference needs cv2 and mmpose, which are absent here; they are replaced by
 stub modules.  The stub cv2 is populated with the oracle's OpenCV-4.9
 restatement (oracle/cv_ref.py), so fixtures that go through cv2
@@ -220,18 +220,39 @@ def gen_sgd(pr):
               seeds=np.array([seed]), **{"hist_" + k: v for k, v in hist.items()})
 
 
+def gen_interp(pr):
+    """pose_refinement.linear_interpolation (pose_refinement.py:15-84) on a noisy
+    kpts_3d-like sequence with spikes, a NaN frame and constant stretches."""
+    seed = 71
+    rng = np.random.default_rng(seed)
+    pts = syn.make_poses(40, seed=seed).astype(np.float32)
+    pts += rng.normal(0, 0.5, pts.shape).astype(np.float32)
+    spikes = rng.integers(0, 40, 25)
+    pts[spikes, rng.integers(0, 17, 25), rng.integers(0, 3, 25)] += rng.choice([-40, 40], 25).astype(np.float32)
+    pts[17, 3, :] = np.nan
+    pts[5:12, 8, 1] = 7.25
+    cases = {"default": {}, "rolling": dict(use_rolling_average=True), "nomedian": dict(filter_distance_from_median=False),
+             "k7": dict(k=7, k_std=1.5, median_std=3)}
+    outs = {f"out_{n}": pr.linear_interpolation(pts.copy(), **kw) for n, kw in cases.items()}
+    _save("interp.npz", points=pts, seeds=np.array([seed]), **outs)
+
+
+GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "interp")
+
+
 def main():
+    only = set(sys.argv[1:]) or set(GENERATORS)
     _install_stubs()
     import utils as ref_utils  # noqa: E402  (reference utils.py)
     import pose_estimation  # noqa: E402
     import pose_refinement as pr  # noqa: E402
     from mmpose_pose_estimation import PoseEstimator  # noqa: E402
-    gen_dlt(ref_utils)
-    gen_pose3d(pose_estimation)
-    gen_moments(PoseEstimator)
-    gen_project(pr)
-    gen_bodylen(ref_utils)
-    gen_sgd(pr)
+    gens = {"dlt": lambda: gen_dlt(ref_utils), "pose3d": lambda: gen_pose3d(pose_estimation),
+            "moments": lambda: gen_moments(PoseEstimator), "project": lambda: gen_project(pr),
+            "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr), "interp": lambda: gen_interp(pr)}
+    for name in GENERATORS:
+        if name in only:
+            gens[name]()
 
 
 if __name__ == "__main__":

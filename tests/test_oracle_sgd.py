@@ -67,3 +67,12 @@ def test_sgd_matches_reference(case):
     np.testing.assert_array_equal(r.trajectory.numpy(), d["final"])
     for k, v in r.all_costs_total.items():
         np.testing.assert_array_equal(np.array([float(x) for x in v]), d["hist_" + k])
+
+
+@pytest.mark.parametrize("case,kw", [("default", {}), ("rolling", dict(use_rolling_average=True)),
+                                     ("nomedian", dict(filter_distance_from_median=False)),
+                                     ("k7", dict(k=7, k_std=1.5, median_std=3))])
+def test_linear_interpolation_matches_reference(case, kw):
+    from oracle import interp_ref
+    d = np.load(os.path.join(GOLDEN, "interp.npz"))
+    np.testing.assert_array_equal(interp_ref.linear_interpolation(d["points"], **kw), d["out_" + case])

@@ -129,3 +129,28 @@ def test_sgd_argument_errors(refine):
     with pytest.raises(KeyError):
         refine.refine_trajectories(g[None], x[None], cams, body_lengths={"left_nose_right_toe": 3.0})
     assert issubclass(MvposeError, RuntimeError)
+
+
+@pytest.mark.parametrize("case,kw", [("default", {}), ("rolling", dict(use_rolling_average=True)),
+                                     ("nomedian", dict(filter_distance_from_median=False)),
+                                     ("k7", dict(k=7, k_std=1.5, median_std=3))])
+def test_linear_interpolation_golden(refine, case, kw):
+    """mvp_linear_interpolation vs the reference's output (interp.npz): the f32 window
+    statistics decide the same kept set, the f64 line fit rounds to the same f32."""
+    d = np.load(os.path.join(GOLDEN, "interp.npz"))
+    out = refine.linear_interpolation(d["points"], **kw)
+    assert out.dtype == np.float32 and out.shape == d["points"].shape
+    np.testing.assert_allclose(out, d["out_" + case], rtol=2e-7, atol=1e-6)
+
+
+def test_linear_interpolation_matches_oracle_large(refine):
+    from oracle import interp_ref
+    rng = np.random.default_rng(5)
+    pts = (np.cumsum(rng.normal(0, 1, (120, 17, 3)), axis=0) + rng.normal(0, 0.2, (120, 17, 3))).astype(np.float32)
+    pts[rng.integers(0, 120, 60), rng.integers(0, 17, 60), rng.integers(0, 3, 60)] += 30
+    ref = interp_ref.linear_interpolation(pts)
+    out = refine.linear_interpolation(torch.tensor(pts, device="cuda"))
+    assert out.is_cuda
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=2e-7, atol=1e-6)
+    two_d = refine.linear_interpolation(pts[:, :, 0])
+    np.testing.assert_allclose(two_d, ref[:, :, 0], rtol=2e-7, atol=1e-6)
