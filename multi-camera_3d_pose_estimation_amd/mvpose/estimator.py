@@ -48,9 +48,13 @@ class BatchPoseEstimator:
     reference falls back to when RTMDet finds no person (:246-250)."""
 
     def __init__(self, state_dict=None, seed: int = 0, max_frames: int = 256, frame_hw=(720, 1280),
-                 flip_test: bool = True, device="cuda"):
+                 flip_test: bool = True, swap_rb: bool = True, device="cuda"):
+        """swap_rb: PoseDataPreprocessor(bgr_to_rgb=True) on frames as handed to the model.  The
+        reference hands mmpose cvtColor(RGB2BGR) of the decoded (BGR) frame (utils.py:860/864), so
+        for decoded frames the two swaps cancel: pass swap_rb=False."""
         self.device = torch.device(device)
         self.flip_test = flip_test
+        self.swap_rb = bool(swap_rb)
         self.max_frames = int(max_frames)
         self.frame_h, self.frame_w = frame_hw
         self.backbone = HRNetBackbone(state_dict, seed=seed,
@@ -86,7 +90,7 @@ class BatchPoseEstimator:
         nc = n * (2 if self.flip_test else 1)
         crops = self.crops[:nc]
         call("mvp_preprocess", _ptr(frames), n, h, w, _ptr(self.crop_minv), INPUT_HW[0], INPUT_HW[1], self._mean,
-             self._std, 1, int(self.flip_test), _ptr(crops), s)
+             self._std, int(self.swap_rb), int(self.flip_test), _ptr(crops), s)
         hm = self.backbone.forward(crops, out=self.heatmaps[:nc])
         kp = torch.empty((n, N_JOINTS, 2), dtype=torch.float32, device=dev)
         sc = torch.empty((n, N_JOINTS), dtype=torch.float32, device=dev)
