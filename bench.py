@@ -99,27 +99,24 @@ def cpu_baseline(n_frames, views, seed=0):
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
-    from mvpose import hrnet, ops, synthetic as syn
+    from mvpose import dist as mdist, hrnet, ops, synthetic as syn
     from mvpose.estimator import BatchPoseEstimator
     from mvpose.pipeline import MultiViewPipeline
 
     B, V = args.frames, args.views
     sd = hrnet.random_state_dict(0) if rank == 0 or world == 1 else hrnet.random_state_dict(0)
     est = BatchPoseEstimator(sd, max_frames=B * V, device=dev)
-    if world > 1:  # weights live once on rank 0's host; ship them over RCCL (xGMI)
-        torch.distributed.broadcast(est.backbone.w_dev, 0)
-        torch.distributed.broadcast(est.backbone.f_dev, 0)
+    # weights live once on rank 0; ship them over RCCL (xGMI) — the only start-up collective
+    mdist.broadcast_([est.backbone.w_dev, est.backbone.f_dev], src=0)
     cams = syn.make_rig(V, seed=1)
     pipe = MultiViewPipeline(syn.reference_camera_params(cams), estimator=est, device=dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
     frames = torch.randint(0, 256, (B, V, 720, 1280, 3), dtype=torch.uint8, device=dev, generator=g)
-    gathered = torch.empty((world * B, 17, 3), dtype=torch.float32, device=dev) if rank == 0 else None
     out = {}
 
     def step():
         o = pipe.process(frames, out)
-        if world > 1:
-            torch.distributed.gather(o["kpts_3d"], list(gathered.chunk(world)) if rank == 0 else None, dst=0)
+        mdist.gather_frames(o["kpts_3d"], world * B)   # per-step 3D joints to rank 0 (204 B/frame)
         return o
 
     for _ in range(args.warmup):

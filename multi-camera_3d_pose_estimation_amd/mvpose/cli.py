@@ -191,7 +191,8 @@ def pose_refinement_main(argv=None):
         opt.sgd_optimize(**kw)
         path = os.path.join(args.save_path, "kpts_3d_SGD.npy")
         print(f"saving SGD at {path}")
-        np.save(path, np.array(opt.best_trajectory))
+        best = opt.best_trajectory
+        np.save(path, best.numpy() if best is not None else np.array(None))
         outputs["SGD"] = path
         types.discard("SGD")
     if types:
