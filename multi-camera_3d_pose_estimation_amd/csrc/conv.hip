@@ -17,6 +17,7 @@
 #include "conv.h"
 
 #include <cstdlib>
+#include <type_traits>
 #include "mvp_common.h"
 
 namespace mvp {
@@ -40,13 +41,16 @@ struct ConvParams {
     const uint16_t* __restrict__ res;
     uint16_t* __restrict__ y;
     float* __restrict__ yf;
-    const uint16_t* __restrict__ zero;  // >= 16 zero bytes: source of padding / out-of-image slots
+    const uint16_t* __restrict__ zero;  // kZeroSlots*16 zero bytes: source of padding / out-of-image slots
+    uint16_t* sink;                     // write-only scratch for masked-off lanes' stores
+    float* sinkf;
     int N, H, W, Cin, Ho, Wo, Cout, Cout_pad;
     int relu, out_f32;
     int tiles_w, tiles_h, n_tiles;
     int wmode;  // WM_ONCE / WM_RESIDENT / WM_STREAM
-    int ablate; // diagnostics only (MVPOSE_CONV_ABLATE): 1 no stores, 2 no DMA
 };
+
+constexpr int kZeroSlots = 4096;  // 16-B slots of the zero region (64 KiB)
 
 // Weight staging modes: one 32-channel chunk staged once (Cin = 32); every chunk
 // resident in LDS for the whole launch (fits); or a per-chunk double buffer.
@@ -59,51 +63,83 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
     __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
 }
 
-template <int KS, int S, int BM, int TH, int TW, int NB>
+template <int KS, int S, int BM, int TH, int TW, int NB, int NW = 4>
 struct ConvCfg {
     static constexpr int HH = (TH - 1) * S + KS;
     static constexpr int HW = (TW - 1) * S + KS;
     static constexpr int KK = KS * KS;
     static constexpr int HALO_PIX = NB * HH * HW;
-    static constexpr int HPIX = (HALO_PIX + 63) / 64 * 64;  // pixels per chunk plane (whole 1-KiB DMA pieces)
+    static constexpr int HGRAN = 16 * NW;  // whole 1-KiB DMA pieces for every wave in each round
+    static constexpr int HPIX = (HALO_PIX + HGRAN - 1) / HGRAN * HGRAN;  // pixels per chunk plane
     static constexpr int H_SLOTS = 4 * HPIX;                // 16-B slots, layout [chunk q][pixel]
     static constexpr int W_SLOTS = KK * 4 * BM;             // layout [tap][chunk q][cout]
     static constexpr int H_BYTES = H_SLOTS * 16;
     static constexpr int W_BYTES = (W_SLOTS + 63) / 64 * 1024;
-    static int lds_bytes(int wmode, int n_chunks) {
-        return 2 * H_BYTES + (wmode == WM_ONCE ? 1 : wmode == WM_RESIDENT ? n_chunks : 2) * W_BYTES;
+    static int lds_bytes(int wmode, int n_chunks, int nbuf) {
+        return nbuf * H_BYTES + (wmode == WM_ONCE ? 1 : wmode == WM_RESIDENT ? n_chunks : nbuf) * W_BYTES;
     }
 };
 
-// Persistent implicit-GEMM conv with an LDS-DMA double buffer.  A workgroup walks
-// its work items (tile, 32-channel chunk); at the top of each item one barrier
-// retires the item's DMA (issued one item earlier) and frees the other buffer,
-// then the NEXT item's halo (+ weight slice when the chunk changes) is issued by
-// global_load_lds straight into that buffer and lands while this item's MFMAs
-// run.  LDS images are chunk-major ([q][pixel] for the halo, [tap][q][cout] for
-// the weights) so each 16-lane ds_read_b128 group of a fragment read touches 16
-// distinct 16-B bank slots (conflict-free for row-contiguous pixel tiles).
-template <int KS, int S, int BM, int TH, int TW, int NB>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
-    using C = ConvCfg<KS, S, BM, TH, TW, NB>;
+// s_waitcnt vmcnt(n') for the largest level n' <= n: waits until at most n' of this
+// wave's vector-memory operations are outstanding (rounding down only waits longer).
+__device__ __forceinline__ void wait_vmcnt_le(int n) {
+    if (n >= 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
+    else if (n >= 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+    else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Persistent implicit-GEMM conv with an NBUF-deep LDS-DMA ring.  A workgroup walks
+// its work items k = (tile, 32-channel chunk); the halo (+ weight slice when
+// streamed) of item k+NBUF-1 is issued by global_load_lds straight into the ring
+// slot freed by item k-1, so NBUF-1 items' DMAs are in flight under each item's
+// MFMAs.  Completion is tracked per wave by counting its own vector-memory
+// instructions (DMA pieces, residual loads, stores — every one issued
+// unconditionally, out-of-range lanes pointed at a zero region / a sink), so the
+// top-of-item wait is vmcnt(#ops younger than item k's DMA), never vmcnt(0).
+// LDS images are chunk-major ([q][pixel] halo, [tap][q][cout] weights): each
+// 16-lane ds_read_b128 group of a fragment read touches 16 distinct bank slots.
+template <int KS, int S, int BM, int TH, int TW, int NB, int NBUF, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
+    using C = ConvCfg<KS, S, BM, TH, TW, NB, NW>;
+    constexpr int NT = NW * 64;  // threads
     constexpr int PAD = KS / 2;
     constexpr int HH = C::HH, HW = C::HW, KK = C::KK, HPIX = C::HPIX;
     constexpr int P = NB * TH * TW;
     static_assert(P % 64 == 0, "tile must hold a multiple of 64 pixels");
+    static_assert(NBUF >= 2, "ring needs two slots");
+    constexpr int D = NBUF - 1;  // items in flight ahead of the one computing
     constexpr int NPT = P / 16;
     constexpr int NCT = BM / 16;
-    constexpr int PTW = NPT / 4;  // pixel tiles per wave
+    static_assert(NPT % NW == 0, "pixel tiles must split evenly over the waves");
+    constexpr int PTW = NPT / NW;  // pixel tiles per wave
+    static_assert(C::H_SLOTS % NT == 0, "halo pieces must split evenly over the waves");
+    constexpr int kHaloOps = C::H_SLOTS / NT;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if ((int)blockIdx.x >= p.n_tiles) return;
     const int co0 = blockIdx.y * BM;
     const int n_chunks = p.Cin >> 5;
     const int wmode = p.wmode;
     const size_t plane_in = (size_t)p.H * p.W;
+    const int w_ops = (C::W_SLOTS - wave * 64 + NT - 1) / NT;  // weight-slice DMA pieces issued by this wave
+    const int item_ops = kHaloOps + (wmode == WM_STREAM ? w_ops : 0);
+    const int n_items = ((p.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1) * n_chunks;
     auto halo_buf = [&](int b) -> uint8_t* { return lds + b * C::H_BYTES; };
     auto w_buf = [&](int b, int chunk) -> uint8_t* {
         const int slot = wmode == WM_ONCE ? 0 : wmode == WM_RESIDENT ? chunk : b;
-        return lds + 2 * C::H_BYTES + slot * C::W_BYTES;
+        return lds + NBUF * C::H_BYTES + slot * C::W_BYTES;
     };
 
     // B fragment: lane reads pixel (lane & 15) of its pixel tile, chunk q = lane >> 4
@@ -117,9 +153,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
         hbase[i] = ((lane >> 4) * HPIX + (nb * HH + th * S) * HW + tw * S) * 8;
     }
     const int abase = ((lane >> 4) * BM + (lane & 15)) * 8;
-    float4 bias[NCT];
-#pragma unroll
-    for (int c = 0; c < NCT; c++) bias[c] = *reinterpret_cast<const float4*>(p.bias + co0 + c * 16 + (lane >> 4) * 4);
+    // folded-BN bias of this block's couts, read by the epilogue from LDS (visible after
+    // the first item's barrier); registers would pin a pending load across the loop
+    __shared__ float4 sbias[BM / 4];
+    if (tid < BM / 4) sbias[tid] = *reinterpret_cast<const float4*>(p.bias + co0 + tid * 4);
 
     auto tile_origin = [&](int tile, int& n0, int& ho0, int& wo0) {
         const int tw_i = tile % p.tiles_w;
@@ -131,11 +168,11 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
     auto issue_w = [&](int chunk, uint8_t* wb) {
         const uint16_t* wsrc = p.w + (size_t)co0 * KK * p.Cin + chunk * 32;
 #pragma unroll
-        for (int s0 = 0; s0 < C::W_SLOTS; s0 += 256) {
+        for (int s0 = 0; s0 < C::W_SLOTS; s0 += NT) {
             const int sw0 = s0 + wave * 64;
-            if (sw0 < C::W_SLOTS) {
+            if (sw0 < C::W_SLOTS) {  // wave-uniform: exactly w_ops pieces per call
                 const int sl = sw0 + lane;
-                const void* src = p.zero;
+                const void* src = p.zero + (sl & (kZeroSlots - 1)) * 8;
                 if (sl < C::W_SLOTS) {
                     const int co = sl % BM, tq = sl / BM;  // tq = tap * 4 + q
                     src = wsrc + ((size_t)co * KK + (tq >> 2)) * p.Cin + (tq & 3) * 8;
@@ -144,78 +181,129 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
             }
         }
     };
-    auto issue = [&](int tile, int chunk, int buf, bool with_w) {
+    // Per-lane halo geometry of each of this wave's DMA pieces, fixed for the launch:
+    // pixel (nb, hh, ww) of the halo and its element offset from the halo origin.
+    // Per item only the tile origin moves: bounds = 3 compares, address = one add.
+    int hgeo[kHaloOps], hoff[kHaloOps];
+#pragma unroll
+    for (int j = 0; j < kHaloOps; j++) {
+        const int sw0 = j * NT + wave * 64;
+        const int q = sw0 / HPIX;
+        const int pix = sw0 - q * HPIX + lane;
+        const int nb = pix / (HH * HW);
+        const int r = pix - nb * (HH * HW);
+        const int hh = r / HW, ww = r - (r / HW) * HW;
+        hgeo[j] = pix < C::HALO_PIX ? (hh | (ww << 10) | (nb << 20)) : -1;
+        hoff[j] = (int)(((size_t)nb * plane_in + (size_t)hh * p.W + ww) * p.Cin) + q * 8;
+    }
+    auto issue = [&](int k, int buf) {
+        const int tile = blockIdx.x + (k / n_chunks) * gridDim.x, chunk = k % n_chunks;
         int n0, ho0, wo0;
         tile_origin(tile, n0, ho0, wo0);
         const int hi0 = ho0 * S - PAD, wi0 = wo0 * S - PAD;
-        const uint16_t* xb = p.x + chunk * 32;
+        // element offset of the halo origin (may point before the image; only in-bounds lanes use it)
+        const uint16_t* xb = p.x + ((long)n0 * (long)plane_in + (long)hi0 * p.W + wi0) * p.Cin + chunk * 32;
         uint8_t* hb = halo_buf(buf);
 #pragma unroll
-        for (int s0 = 0; s0 < C::H_SLOTS; s0 += 256) {
-            const int sw0 = s0 + wave * 64;  // this wave's 64-slot piece (one chunk plane)
-            const int q = sw0 / HPIX;
-            const int pix = sw0 - q * HPIX + lane;
-            const void* src = p.zero;
-            if (pix < C::HALO_PIX) {
-                const int nb = pix / (HH * HW);
-                const int r = pix - nb * (HH * HW);
-                const int hh = r / HW, ww = r - (r / HW) * HW;
-                const int n = n0 + nb, hi = hi0 + hh, wi = wi0 + ww;
-                if (n < p.N && hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                    src = xb + ((size_t)n * plane_in + (size_t)hi * p.W + wi) * p.Cin + q * 8;
-            }
+        for (int j = 0; j < kHaloOps; j++) {
+            const int sw0 = j * NT + wave * 64;  // this wave's 64-slot piece (one chunk plane)
+            const int g = hgeo[j];
+            const int hh = g & 1023, ww = (g >> 10) & 1023, nb = g >> 20;
+            const bool in = g >= 0 && (unsigned)(hi0 + hh) < (unsigned)p.H && (unsigned)(wi0 + ww) < (unsigned)p.W &&
+                            n0 + nb < p.N;
+            // out-of-image slots read zeros from a 64-KiB zero region, one distinct 16-B
+            // slot per lane: a single shared zero line is an L2-channel hot spot
+            const void* src = in ? (const void*)(xb + hoff[j]) : (const void*)(p.zero + ((sw0 + lane) & (kZeroSlots - 1)) * 8);
             glds16(src, hb + sw0 * 16);
         }
-        if (with_w) issue_w(chunk, w_buf(buf, chunk));
+        if (wmode == WM_STREAM) issue_w(chunk, w_buf(buf, chunk));
     };
-    const bool do_dma = !(p.ablate & 2), do_store = !(p.ablate & 1);
-
+    // Per-lane output pixel of each pixel tile relative to the tile origin.
+    int eoff[PTW], egeo[PTW];
+#pragma unroll
+    for (int i = 0; i < PTW; i++) {
+        const int pp = (wave * PTW + i) * 16 + (lane & 15);
+        const int nb = pp / (TH * TW);
+        const int r = pp - nb * (TH * TW);
+        const int th = r / TW, tw = r - (r / TW) * TW;
+        egeo[i] = th | (tw << 10) | (nb << 20);
+        eoff[i] = (nb * p.Ho + th) * p.Wo + tw;
+    }
     f32x4 acc[PTW][NCT];
 #pragma unroll
     for (int i = 0; i < PTW; i++)
 #pragma unroll
         for (int c = 0; c < NCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    int tile = blockIdx.x, chunk = 0, buf = 0;
-    if (tile >= p.n_tiles) return;
-    if (do_dma) issue(tile, 0, 0, true);
-    if (wmode == WM_RESIDENT && do_dma)
-        for (int c = 1; c < n_chunks; c++) issue_w(c, w_buf(0, c));
-    for (;;) {
-        // retire this item's DMA (vmcnt) and make every wave's view of it valid (barrier);
-        // also guarantees all waves finished reading buffer buf^1
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        int ntile = tile, nchunk = chunk + 1;
-        if (nchunk == n_chunks) {
-            nchunk = 0;
-            ntile += gridDim.x;
+    // ---- prologue: resident / single weight slices, then the first D items
+    int ops = 0;
+    if (wmode == WM_ONCE) {
+        issue_w(0, w_buf(0, 0));
+        ops += w_ops;
+    } else if (wmode == WM_RESIDENT) {
+        for (int c = 0; c < n_chunks; c++) issue_w(c, w_buf(0, c));
+        ops += w_ops * n_chunks;
+    }
+    int mark[D];  // ops count at the end of item (k + j)'s DMA, j = 0 .. D-1
+#pragma unroll
+    for (int j = 0; j < D; j++) {
+        if (j < n_items) {
+            issue(j, j);
+            ops += item_ops;
         }
-        const bool has_next = ntile < p.n_tiles;
-        const bool last_chunk = chunk == n_chunks - 1;
-        // residual rows of this tile: issued before the next DMA so they land under the MFMAs
+        mark[j] = ops;
+    }
+
+    const int store_ops = p.out_f32 ? 4 * PTW * NCT : PTW * NCT;
+    int buf = 0;
+    for (int k = 0; k < n_items; k++) {
+        // item k's pieces from this wave have landed; the barrier makes every wave's
+        // pieces visible and guarantees all waves are done reading ring slot k-1
+        wait_vmcnt_le(ops - mark[0]);
+        // plain s_barrier, not __syncthreads(): its release fence would drain vmcnt to 0
+        // (every DMA in flight, stores included) and collapse the ring to depth 1
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int j = 0; j + 1 < D; j++) mark[j] = mark[j + 1];
+        const int tile = blockIdx.x + (k / n_chunks) * gridDim.x, chunk = k % n_chunks;
+        int n0, ho0, wo0;
+        tile_origin(tile, n0, ho0, wo0);
+        const int pix0 = (n0 * p.Ho + ho0) * p.Wo + wo0;  // output pixel of the tile origin
+        const int co_l = co0 + (lane >> 4) * 4;
+        // One body per item kind, so residual loads and their use sit on the same
+        // control path (the waitcnt pass merges paths, and a load pending on an
+        // infeasible path would cost a vmcnt(0) at the next item).
+        auto item = [&](auto last_tag) {
+        constexpr bool LAST = decltype(last_tag)::value;
+        // residual rows of this tile (before the next DMA so they land under the MFMAs);
+        // issued for every last-chunk item, from the zero region when there is no residual
         uint2 resv[PTW][NCT];
-        if (last_chunk && p.res) {
-            int n0, ho0, wo0;
-            tile_origin(tile, n0, ho0, wo0);
+        if constexpr (LAST) {
 #pragma unroll
             for (int i = 0; i < PTW; i++) {
-                const int pp = (wave * PTW + i) * 16 + (lane & 15);
-                const int nb = pp / (TH * TW);
-                const int r = pp - nb * (TH * TW);
-                const int th = r / TW, tw = r - (r / TW) * TW;
-                const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
-                const bool valid = n < p.N && ho < p.Ho && wo < p.Wo;
-                const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
+                const int g = egeo[i];
+                const bool valid = n0 + (g >> 20) < p.N && ho0 + (g & 1023) < p.Ho && wo0 + ((g >> 10) & 1023) < p.Wo;
+                const uint16_t* rrow = (p.res ? p.res : p.zero) + (size_t)(pix0 + eoff[i]) * p.Cout;
 #pragma unroll
                 for (int c = 0; c < NCT; c++) {
-                    const int co = co0 + c * 16 + (lane >> 4) * 4;
-                    resv[i][c] = (valid && co < p.Cout) ? *reinterpret_cast<const uint2*>(p.res + pix * p.Cout + co)
-                                                        : uint2{0u, 0u};
+                    const int co = co_l + c * 16;
+                    const uint16_t* src = (p.res && valid && co < p.Cout) ? rrow + co : p.zero + lane * 4;
+                    resv[i][c] = *reinterpret_cast<const uint2*>(src);
                 }
             }
+            ops += PTW * NCT;
         }
-        if (has_next && do_dma) issue(ntile, nchunk, buf ^ 1, wmode == WM_STREAM);
+        asm volatile("" ::: "memory");
+        // issued for every item (past the end: a tile beyond the last crop, i.e. zero-region
+        // reads into the free slot), so the VMEM count between the residual loads and their
+        // use is the same on every path and the epilogue waits vmcnt(pieces), not vmcnt(0)
+        const int nbuf = buf + D >= NBUF ? buf + D - NBUF : buf + D;
+        issue(k + D, nbuf);
+        ops += item_ops;
+        mark[D - 1] = ops;
+        asm volatile("" ::: "memory");
         const uint16_t* sh = reinterpret_cast<const uint16_t*>(halo_buf(buf));
         const uint16_t* sw = reinterpret_cast<const uint16_t*>(w_buf(buf, chunk));
         // fragment reads of tap t+1 are issued before the MFMAs of tap t (two static
@@ -242,37 +330,37 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
                     acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][c], fb[cur][i], acc[i][c], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
-        if (last_chunk) {
-            // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head)
-            int n0, ho0, wo0;
-            tile_origin(tile, n0, ho0, wo0);
+        if constexpr (LAST) {
+            // ---- epilogue: + bias [+ residual] [relu] -> bf16 NHWC (or f32 NCHW for the head);
+            // every store instruction issues (invalid lanes write the sink)
 #pragma unroll
             for (int i = 0; i < PTW; i++) {
-                const int pp = (wave * PTW + i) * 16 + (lane & 15);
-                const int nb = pp / (TH * TW);
-                const int r = pp - nb * (TH * TW);
-                const int th = r / TW, tw = r - (r / TW) * TW;
+                const int g = egeo[i];
+                const int nb = g >> 20, th = g & 1023, tw = (g >> 10) & 1023;
                 const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
                 const bool valid = n < p.N && ho < p.Ho && wo < p.Wo;
-                const size_t pix = ((size_t)n * p.Ho + ho) * p.Wo + wo;
+                const int pix = pix0 + eoff[i];
+                uint16_t* yrow = p.y + (size_t)pix * p.Cout;
 #pragma unroll
                 for (int c = 0; c < NCT; c++) {
-                    const int co = co0 + c * 16 + (lane >> 4) * 4;
-                    float v0 = acc[i][c][0] + bias[c].x, v1 = acc[i][c][1] + bias[c].y;
-                    float v2 = acc[i][c][2] + bias[c].z, v3 = acc[i][c][3] + bias[c].w;
+                    const int co = co_l + c * 16;
+                    const float4 bias = sbias[c * 4 + (lane >> 4)];
+                    float v0 = acc[i][c][0] + bias.x, v1 = acc[i][c][1] + bias.y;
+                    float v2 = acc[i][c][2] + bias.z, v3 = acc[i][c][3] + bias.w;
                     acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-                    if (!valid) continue;
                     if (p.out_f32) {
                         const size_t plane = (size_t)p.Ho * p.Wo;
                         const float vv[4] = {v0, v1, v2, v3};
 #pragma unroll
-                        for (int q = 0; q < 4; q++)
-                            if (co + q < p.Cout)
-                                p.yf[((size_t)n * p.Cout + co + q) * plane + (size_t)ho * p.Wo + wo] = vv[q];
+                        for (int q = 0; q < 4; q++) {
+                            const bool ok = valid && co + q < p.Cout;
+                            float* dst = ok ? p.yf + ((size_t)n * p.Cout + co + q) * plane + (size_t)ho * p.Wo + wo
+                                            : p.sinkf + lane * 4 + q;
+                            *dst = vv[q];
+                        }
                         continue;
                     }
-                    if (co >= p.Cout) continue;
-                    if (p.res) {
+                    {  // + residual (zeros when the conv has none)
                         const uint2 rv = resv[i][c];
                         v0 += bf16_to_f32(rv.x & 0xffff);
                         v1 += bf16_to_f32(rv.x >> 16);
@@ -288,15 +376,18 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvParams p) {
                     uint2 o;
                     o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
                     o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-                    if (do_store) *reinterpret_cast<uint2*>(p.y + pix * p.Cout + co) = o;
-                    else if ((o.x ^ o.y) == 0x12345678u) p.y[0] = 0;  // keep the epilogue live
+                    uint16_t* dst = (valid && co < p.Cout) ? yrow + co : p.sink + lane * 4;
+                    *reinterpret_cast<uint2*>(dst) = o;
                 }
             }
+            ops += store_ops;
         }
-        if (!has_next) break;
-        tile = ntile;
-        chunk = nchunk;
-        buf ^= 1;
+        };
+        if (chunk == n_chunks - 1)
+            item(std::integral_constant<bool, true>{});
+        else
+            item(std::integral_constant<bool, false>{});
+        buf = buf + 1 == NBUF ? 0 : buf + 1;
     }
 }
 
@@ -312,17 +403,62 @@ int num_cus() {
     return g_num_cus;
 }
 
+uint16_t* g_sink = nullptr;
+
 const uint16_t* zero_page() {
     if (!g_zero) {
-        MVP_HIP(hipMalloc(&g_zero, 256));
-        MVP_HIP(hipMemset(g_zero, 0, 256));
+        MVP_HIP(hipMalloc(&g_zero, kZeroSlots * 16));
+        MVP_HIP(hipMemset(g_zero, 0, kZeroSlots * 16));
+        MVP_HIP(hipMalloc(&g_sink, 64 * 16));
     }
     return g_zero;
 }
 
-template <int KS, int S, int BM, int TH, int TW, int NB>
+constexpr int kLdsMax = 160 * 1024 - 1024;  // dynamic LDS budget (static: the bias tile)
+
+// Resident workgroups per CU of one kernel instance at a given LDS footprint (cached).
+template <int KS, int S, int BM, int TH, int TW, int NB, int NBUF, int NW>
+int blocks_per_cu(int lds) {
+    auto kern = conv_mfma_kernel<KS, S, BM, TH, TW, NB, NBUF, NW>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
+        attr_set = true;
+    }
+    static int cache[kLdsMax / 1024 + 1] = {0};
+    int& per_cu = cache[(lds + 1023) / 1024];
+    if (per_cu == 0) {
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, NW * 64, lds));
+        if (per_cu < 1) per_cu = 1;
+    }
+    return per_cu;
+}
+
+template <int KS, int S, int BM, int TH, int TW, int NB, int NBUF, int NW>
+void launch_ring(const ConvParams& p, int lds, int per_cu, hipStream_t s) {
+    const int y_blocks = p.Cout_pad / BM;
+    long gx = ((long)num_cus() * per_cu + y_blocks - 1) / y_blocks;
+    if (gx > p.n_tiles) gx = p.n_tiles;
+    hipLaunchKernelGGL((conv_mfma_kernel<KS, S, BM, TH, TW, NB, NBUF, NW>), dim3((unsigned)gx, (unsigned)y_blocks),
+                       dim3(NW * 64), lds, s, p);
+}
+
+template <int KS, int S, int BM, int TH, int TW, int NB, int NW>
+int wmode_for(int n_chunks) {
+    using C = ConvCfg<KS, S, BM, TH, TW, NB, NW>;
+    return n_chunks == 1 ? WM_ONCE : C::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax ? WM_RESIDENT : WM_STREAM;
+}
+
+// Resident workgroups per CU by LDS alone for the 2-slot ring (tile / wave-count choice).
+template <int KS, int S, int BM, int TH, int TW, int NB, int NW>
+int lds_blocks(int n_chunks) {
+    using C = ConvCfg<KS, S, BM, TH, TW, NB, NW>;
+    return kLdsMax / C::lds_bytes(wmode_for<KS, S, BM, TH, TW, NB, NW>(n_chunks), n_chunks, 2);
+}
+
+template <int KS, int S, int BM, int TH, int TW, int NB, int NW>
 void launch_cfg(const ConvParams& p0, hipStream_t s) {
-    using C = ConvCfg<KS, S, BM, TH, TW, NB>;
+    using C = ConvCfg<KS, S, BM, TH, TW, NB, NW>;
     ConvParams p = p0;
     p.tiles_w = (p.Wo + TW - 1) / TW;
     p.tiles_h = (p.Ho + TH - 1) / TH;
@@ -331,75 +467,107 @@ void launch_cfg(const ConvParams& p0, hipStream_t s) {
     MVP_REQUIRE(nt < (1L << 31), "conv: too many tiles");
     p.n_tiles = (int)nt;
     p.zero = zero_page();
+    p.sink = g_sink;
+    p.sinkf = reinterpret_cast<float*>(g_sink);
     const int n_chunks = p.Cin / 32;
-    constexpr int kLdsMax = 160 * 1024;
-    p.wmode = n_chunks == 1 ? WM_ONCE
-              : C::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax ? WM_RESIDENT : WM_STREAM;
-    const int lds = C::lds_bytes(p.wmode, n_chunks);
-    MVP_REQUIRE(lds <= kLdsMax, "conv: LDS %d B over budget", lds);
-    auto kern = conv_mfma_kernel<KS, S, BM, TH, TW, NB>;
-    static bool attr_set = false;
-    if (!attr_set) {
-        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kLdsMax));
-        attr_set = true;
+    p.wmode = wmode_for<KS, S, BM, TH, TW, NB, NW>(n_chunks);
+    // ring depth: maximise DMA items in flight per CU = resident workgroups x (depth - 1)
+    int best = 0, best_score = -1, best_lds = 0, best_bpc = 0;
+    for (int nbuf = 2; nbuf <= 4; nbuf++) {
+        const int lds = C::lds_bytes(p.wmode, n_chunks, nbuf);
+        if (lds > kLdsMax) break;
+        const int bpc = nbuf == 2   ? blocks_per_cu<KS, S, BM, TH, TW, NB, 2, NW>(lds)
+                        : nbuf == 3 ? blocks_per_cu<KS, S, BM, TH, TW, NB, 3, NW>(lds)
+                                    : blocks_per_cu<KS, S, BM, TH, TW, NB, 4, NW>(lds);
+        const int score = bpc * (nbuf - 1);
+        if (score > best_score) {
+            best = nbuf;
+            best_score = score;
+            best_lds = lds;
+            best_bpc = bpc;
+        }
     }
-    static int per_cu_cache[kLdsMax / 1024 + 1] = {0};  // resident workgroups per CU by LDS footprint
-    int& per_cu = per_cu_cache[(lds + 1023) / 1024];
-    if (per_cu == 0) {
-        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds));
-        if (per_cu < 1) per_cu = 1;
+    MVP_REQUIRE(best > 0, "conv: LDS %d B over budget", C::lds_bytes(p.wmode, n_chunks, 2));
+    static const int force = [] {
+        const char* e = getenv("MVPOSE_CONV_RING");  // tuning experiments only
+        return e ? atoi(e) : 0;
+    }();
+    if (force >= 2 && force <= 4 && C::lds_bytes(p.wmode, n_chunks, force) <= kLdsMax && force != best) {
+        best = force;
+        best_lds = C::lds_bytes(p.wmode, n_chunks, force);
+        best_bpc = force == 2   ? blocks_per_cu<KS, S, BM, TH, TW, NB, 2, NW>(best_lds)
+                   : force == 3 ? blocks_per_cu<KS, S, BM, TH, TW, NB, 3, NW>(best_lds)
+                                : blocks_per_cu<KS, S, BM, TH, TW, NB, 4, NW>(best_lds);
     }
-    const int y_blocks = p.Cout_pad / BM;
-    long gx = ((long)num_cus() * per_cu + y_blocks - 1) / y_blocks;
-    if (gx > nt) gx = nt;
-    hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)y_blocks), dim3(256), lds, s, p);
+    if (best == 2)
+        launch_ring<KS, S, BM, TH, TW, NB, 2, NW>(p, best_lds, best_bpc, s);
+    else if (best == 3)
+        launch_ring<KS, S, BM, TH, TW, NB, 3, NW>(p, best_lds, best_bpc, s);
+    else
+        launch_ring<KS, S, BM, TH, TW, NB, 4, NW>(p, best_lds, best_bpc, s);
 }
 
 // Cout tile: 64 couts when the weights can stay LDS-resident (or Cin = 32),
 // else 32 couts if that makes them resident, else 64 couts streamed per chunk.
-template <int KS, int S, int TH, int TW, int NB>
+template <int KS, int S, int TH, int TW, int NB, int NW>
 void launch_tile(const ConvParams& p, hipStream_t s) {
-    constexpr int kLdsMax = 160 * 1024;
     const int n_chunks = p.Cin / 32;
-    if (p.Cout_pad == 32) return launch_cfg<KS, S, 32, TH, TW, NB>(p, s);
-    if (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax)
-        return launch_cfg<KS, S, 64, TH, TW, NB>(p, s);
-    if (ConvCfg<KS, S, 32, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks) <= kLdsMax)
-        return launch_cfg<KS, S, 32, TH, TW, NB>(p, s);
-    launch_cfg<KS, S, 64, TH, TW, NB>(p, s);
+    if (p.Cout_pad == 32) return launch_cfg<KS, S, 32, TH, TW, NB, NW>(p, s);
+    if (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
+        return launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
+    if (ConvCfg<KS, S, 32, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
+        return launch_cfg<KS, S, 32, TH, TW, NB, NW>(p, s);
+    launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
+}
+
+// 4-wave tile (TH, TW, NB) unless its LDS footprint leaves one workgroup per CU
+// (one wave per SIMD: nothing hides LDS / DMA / barrier latency behind another
+// wave's MFMAs) — then the 8-wave tile (TH8, TW8, NB8), twice the pixels, one
+// workgroup of two waves per SIMD sharing the resident weights.
+template <int KS, int S, int TH, int TW, int NB, int TH8, int TW8, int NB8>
+void launch_tile2(const ConvParams& p, hipStream_t s) {
+    static const int nw_env = [] {
+        const char* e = getenv("MVPOSE_CONV_WAVES");  // tuning experiments only: 4 or 8
+        return e ? atoi(e) : 0;
+    }();
+    const int n_chunks = p.Cin / 32;
+    const int bm = p.Cout_pad == 32                                                               ? 32
+                   : (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
+                       ? 64
+                   : ConvCfg<KS, S, 32, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax ? 32
+                                                                                                    : 64;
+    const int blocks4 = bm == 32 ? lds_blocks<KS, S, 32, TH, TW, NB, 4>(n_chunks)
+                                 : lds_blocks<KS, S, 64, TH, TW, NB, 4>(n_chunks);
+    const bool eight = nw_env == 8 || (nw_env != 4 && blocks4 < 2);
+    if (eight)
+        launch_tile<KS, S, TH8, TW8, NB8, 8>(p, s);
+    else
+        launch_tile<KS, S, TH, TW, NB, 4>(p, s);
 }
 
 // Tile shape per output plane.
 template <int KS, int S>
 void launch_plane(const ConvParams& p, hipStream_t s) {
     if constexpr (S == 1) {
-        static const int th48 = [] {
-            const char* e = getenv("MVPOSE_TILE_TH48");  // tuning experiments only
-            return e ? atoi(e) : 4;
-        }();
-        if (p.Wo == 48 && p.Ho % 8 == 0 && th48 == 8)
-            launch_tile<KS, S, 8, 48, 1>(p, s);
-        else if (p.Wo == 48 && p.Ho % 4 == 0 && th48 == 2)
-            launch_tile<KS, S, 2, 32, 1>(p, s);
-        else if (p.Wo == 48 && p.Ho % 4 == 0)
-            launch_tile<KS, S, 4, 48, 1>(p, s);
-        else if (p.Wo == 24 && p.Ho % 8 == 0)
-            launch_tile<KS, S, 8, 24, 1>(p, s);
+        if (p.Wo == 48 && p.Ho % 8 == 0)
+            launch_tile2<KS, S, 4, 48, 1, 8, 48, 1>(p, s);
+        else if (p.Wo == 24 && p.Ho % 16 == 0)
+            launch_tile2<KS, S, 8, 24, 1, 16, 24, 1>(p, s);
         else if (p.Wo == 12 && p.Ho == 16)
-            launch_tile<KS, S, 16, 12, 1>(p, s);
+            launch_tile2<KS, S, 16, 12, 1, 16, 12, 2>(p, s);
         else if (p.Wo == 6 && p.Ho == 8)
-            launch_tile<KS, S, 8, 6, 4>(p, s);
+            launch_tile2<KS, S, 8, 6, 4, 8, 6, 8>(p, s);
         else
-            launch_tile<KS, S, 4, 16, 1>(p, s);  // generic masked tiling
+            launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
     } else {
         if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
-            launch_tile<KS, S, 4, 16, 1>(p, s);
+            launch_tile<KS, S, 4, 16, 1, 4>(p, s);
         else if (p.Wo % 8 == 0 && p.Ho % 8 == 0)
-            launch_tile<KS, S, 8, 8, 1>(p, s);
+            launch_tile<KS, S, 8, 8, 1, 4>(p, s);
         else if (p.Wo % 4 == 0 && p.Ho % 16 == 0)
-            launch_tile<KS, S, 16, 4, 1>(p, s);
+            launch_tile<KS, S, 16, 4, 1, 4>(p, s);
         else
-            launch_tile<KS, S, 4, 16, 1>(p, s);
+            launch_tile<KS, S, 4, 16, 1, 4>(p, s);
     }
 }
 
@@ -456,6 +624,83 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint16_t* __restrict__ 
         o.z = (uint32_t)f32_to_bf16(fmaxf(acc[co + 4], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 5], 0.f)) << 16);
         o.w = (uint32_t)f32_to_bf16(fmaxf(acc[co + 6], 0.f)) | ((uint32_t)f32_to_bf16(fmaxf(acc[co + 7], 0.f)) << 16);
         *reinterpret_cast<uint4*>(out + co) = o;
+    }
+}
+
+// MFMA stem: the same conv as implicit GEMM on v_mfma_f32_16x16x32_bf16.
+// K = 9 taps x 4 channels = 36, padded to 64 (two K=32 steps; tap 8 alone in the
+// second).  A workgroup computes two output rows (2*WO pixels x 64 couts): the
+// five input rows they need are staged in LDS (1-pixel zero border), weights are
+// converted once into bf16 A fragments held in registers, BN bias + ReLU fused.
+template <int WO>
+__global__ __launch_bounds__(256) void stem_mfma_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                        int H, int Ho) {
+    constexpr int W = 2 * WO;   // input width
+    constexpr int LW = W + 2;   // staged row (pixels) with the zero border
+    constexpr int P = 2 * WO;   // output pixels per workgroup
+    static_assert(P % 64 == 0, "two output rows must split into 16-pixel tiles per wave");
+    constexpr int PTW = P / 64;
+    __shared__ uint2 sx[5 * LW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+    const int tiles = Ho / 2;
+    const int n = blockIdx.x / tiles, ho0 = (blockIdx.x - n * tiles) * 2;
+    const uint2* xin = reinterpret_cast<const uint2*>(x) + (size_t)n * H * W;
+    for (int i = tid; i < 5 * LW; i += 256) {
+        const int r = i / LW, c = i - r * LW;
+        const int hi = 2 * ho0 - 1 + r, wi = c - 1;
+        sx[i] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? xin[(size_t)hi * W + wi] : uint2{0u, 0u};
+    }
+    bf16x8 afr[4][2];
+    float4 b4[4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const int co = c * 16 + (lane & 15);
+#pragma unroll
+        for (int kc = 0; kc < 2; kc++) {
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = kc * 32 + g * 8 + j, tap = k >> 2, ch = k & 3;
+                afr[c][kc][j] = (__bf16)(tap < 9 ? w[(co * 9 + tap) * 4 + ch] : 0.f);
+            }
+        }
+        b4[c] = *reinterpret_cast<const float4*>(bias + c * 16 + g * 4);
+    }
+    __syncthreads();
+    f32x4 acc[PTW][4];
+#pragma unroll
+    for (int i = 0; i < PTW; i++) {
+        const int pix = (wave * PTW + i) * 16 + (lane & 15);
+        const int orow = pix / WO, ocol = pix - (pix / WO) * WO;
+        auto tap_px = [&](int tap) { return sx[(2 * orow + tap / 3) * LW + 2 * ocol + tap % 3]; };
+        const uint2 t0 = tap_px(2 * g), t1 = tap_px(2 * g + 1);
+        const uint2 t8 = g == 0 ? tap_px(8) : uint2{0u, 0u};
+        union {
+            uint4 u;
+            bf16x8 v;
+        } b0, b1;
+        b0.u = uint4{t0.x, t0.y, t1.x, t1.y};
+        b1.u = uint4{t8.x, t8.y, 0u, 0u};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][0], b0.v, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][1], b1.v, acc[i][c], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < PTW; i++) {
+        const int pix = (wave * PTW + i) * 16 + (lane & 15);
+        const int orow = pix / WO, ocol = pix - (pix / WO) * WO;
+        uint16_t* out = y + (((size_t)n * Ho + ho0 + orow) * WO + ocol) * 64;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float v0 = fmaxf(acc[i][c][0] + b4[c].x, 0.f), v1 = fmaxf(acc[i][c][1] + b4[c].y, 0.f);
+            const float v2 = fmaxf(acc[i][c][2] + b4[c].z, 0.f), v3 = fmaxf(acc[i][c][3] + b4[c].w, 0.f);
+            uint2 o;
+            o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+            o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+            *reinterpret_cast<uint2*>(out + c * 16 + g * 4) = o;
+        }
     }
 }
 
@@ -530,11 +775,6 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.Cout_pad = conv_cout_pad(c.Cout);
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
-    static const int ablate = [] {
-        const char* e = getenv("MVPOSE_CONV_ABLATE");
-        return e ? atoi(e) : 0;
-    }();
-    p.ablate = ablate;
     if (c.N == 0) return;
     if (c.ks == 3 && c.stride == 1)
         launch_plane<3, 1>(p, s);
@@ -552,6 +792,12 @@ void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t*
     const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
     const long total = (long)N * Ho * Wo * 4;
     if (total == 0) return;
+    if (Wo == 96 && H % 2 == 0 && Ho % 2 == 0) {  // the 256x192 crop: MFMA path
+        hipLaunchKernelGGL(stem_mfma_kernel<96>, dim3((unsigned)((long)N * Ho / 2)), dim3(256), 0, s, x, w, bias, y,
+                           H, Ho);
+        MVP_HIP(hipGetLastError());
+        return;
+    }
     hipLaunchKernelGGL(stem_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, x, w, bias, y, N, H, W,
                        Ho, Wo);
     MVP_HIP(hipGetLastError());
