@@ -37,4 +37,14 @@ void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_
 // Conv weight padding rule shared with the host packer.
 int conv_cout_pad(int cout);
 
+// 64 KiB of device zeros (out-of-image DMA source), allocated on first use.
+const uint16_t* conv_zero_region();
+
+// Fused BasicBlock on 32 channels (block.hip):
+//   y = relu(conv3x3(relu(conv3x3(x, w1) + b1), w2) + b2 + x), all bf16 NHWC [N][H][W][32],
+// w1/w2 [32][3][3][32] bf16, b1/b2 [32] f32.  Bit-identical to the two convs run separately.
+bool basic_block_c32_supported(int H, int W);
+void launch_basic_block_c32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
+                            const float* b2, uint16_t* y, int N, int H, int W, hipStream_t s);
+
 }  // namespace mvp

@@ -750,6 +750,8 @@ __global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
 
 }  // namespace
 
+const uint16_t* conv_zero_region() { return zero_page(); }
+
 int conv_cout_pad(int cout) { return cout <= 32 ? 32 : ((cout + 63) / 64) * 64; }
 
 void launch_conv(const ConvLaunch& c, hipStream_t s) {

@@ -1,5 +1,6 @@
 // Backbone graph runtime: validation, liveness-based arena planning, launch.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -23,6 +24,8 @@ struct Graph {
     const uint16_t* wb = nullptr;
     const float* fb = nullptr;
     int max_batch = 0;
+    std::vector<int> absorbed;    // op folded into the next op (fused BasicBlock), not run on its own
+    std::vector<int> block_head;  // op runs the fused BasicBlock of (op - 1, op)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -107,6 +110,37 @@ void validate(Graph& g, int64_t w_elems, int64_t f_elems) {
     }
 }
 
+// Fusion pass: a 3x3 conv pair conv1 (relu) -> conv2 (+ conv1's input as residual,
+// relu) on 32 channels whose intermediate feeds nothing else becomes one fused
+// BasicBlock launch; the intermediate tensor is then never allocated.
+void fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.absorbed.assign(no, 0);
+    g.block_head.assign(no, 0);
+    if (!enable) return;
+    std::vector<int> uses(nt, 0);
+    for (const mvp_op_desc& op : g.ops)
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0) uses[op.in[i]]++;
+    auto is_c32_conv3 = [&](const mvp_op_desc& op) {
+        return op.kind == MVP_OP_CONV && op.ks == 3 && op.stride == 1 && op.cin == 32 && op.cout == 32 && op.relu &&
+               g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    for (int k = 0; k + 1 < no; k++) {
+        const mvp_op_desc& a = g.ops[k];
+        const mvp_op_desc& b = g.ops[k + 1];
+        if (g.absorbed[k] || g.block_head[k] || !is_c32_conv3(a) || !is_c32_conv3(b)) continue;
+        const bool a_plain = a.n_in == 1 || a.in[1] < 0;
+        const bool b_res = b.n_in > 1 && b.in[1] == a.in[0];
+        const mvp_tensor_desc& t = g.tensors[a.out];
+        if (!a_plain || !b_res || b.in[0] != a.out || uses[a.out] != 1 || a.out == g.output) continue;
+        if (a.segment != b.segment || !basic_block_c32_supported(t.h, t.w)) continue;
+        g.absorbed[k] = 1;
+        g.block_head[k + 1] = 1;
+        k++;
+    }
+}
+
 // Greedy first-fit placement of tensors in one arena by lifetime [def, last use].
 // A tensor produced and consumed only inside one micro-batched segment is
 // "local": it is sized for one micro-batch and re-used by every micro-batch.
@@ -121,6 +155,7 @@ void plan(Graph& g) {
     std::vector<int> multi_seg(nt, 0);  // used by more than one segment
     std::vector<int> use_seg(nt, -1);
     for (int k = 0; k < no; k++) {
+        if (g.absorbed[k]) continue;  // its output lives only in the fused kernel's LDS
         const mvp_op_desc& op = g.ops[k];
         first[op.out] = k;
         if (last[op.out] < k) last[op.out] = k;
@@ -130,11 +165,11 @@ void plan(Graph& g) {
             else if (use_seg[t] != op.segment) multi_seg[t] = 1;
         };
         touch(op.out);
-        for (int i = 0; i < op.n_in; i++)
-            if (op.in[i] >= 0) {
-                last[op.in[i]] = std::max(last[op.in[i]], k);
-                touch(op.in[i]);
-            }
+        for (int i = 0; i < op.n_in; i++) {
+            if (op.in[i] < 0 || (g.block_head[k] && i == 0)) continue;  // fused: conv1's output is LDS-only
+            last[op.in[i]] = std::max(last[op.in[i]], k);
+            touch(op.in[i]);
+        }
     }
     g.local_seg.assign(nt, -1);
     for (int t = 0; t < nt; t++) {
@@ -143,6 +178,7 @@ void plan(Graph& g) {
         if (!multi_seg[t] && g.segs[sg].micro_batch > 0 && g.segs[sg].micro_batch < g.max_batch) g.local_seg[t] = sg;
     }
     for (int k = 0; k < no; k++) {
+        if (g.absorbed[k]) continue;
         const mvp_op_desc& op = g.ops[k];
         const Segment& sg = g.segs[op.segment];
         if (sg.micro_batch <= 0 || sg.micro_batch >= g.max_batch) continue;
@@ -152,7 +188,8 @@ void plan(Graph& g) {
             last[t] = std::max(last[t], sg.last_op);
         };
         widen(op.out);
-        for (int i = 0; i < op.n_in; i++) widen(op.in[i]);
+        for (int i = 0; i < op.n_in; i++)
+            if (!(g.block_head[k] && i == 0)) widen(op.in[i]);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
@@ -220,6 +257,8 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
             g->segs[i].micro_batch = seg_micro_batch[i];
         }
         mvp::validate(*g, w_elems, f_elems);
+        const char* nf = getenv("MVPOSE_NO_FUSE");  // diagnostics: run every conv on its own
+        mvp::fuse(*g, !(nf && nf[0] == '1'));
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
             hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
@@ -253,8 +292,16 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
                                       : g->arena + g->offset[t];
         return base + slice * mvp::tensor_bytes(d, 1);
     };
-    auto run_op = [&](const mvp_op_desc& op, int nb) {
+    auto run_op = [&](int k, int nb) {
+        const mvp_op_desc& op = g->ops[k];
         const mvp_tensor_desc& o = g->tensors[op.out];
+        if (g->absorbed[k]) return;
+        if (g->block_head[k]) {
+            const mvp_op_desc& c1 = g->ops[k - 1];
+            mvp::launch_basic_block_c32((const uint16_t*)ptr(op.in[1]), g->wb + c1.w_off, g->fb + c1.b_off,
+                                        g->wb + op.w_off, g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, o.h, o.w, s);
+            return;
+        }
         if (op.kind == MVP_OP_STEM) {
             const mvp_tensor_desc& x = g->tensors[op.in[0]];
             mvp::launch_stem((const uint16_t*)ptr(op.in[0]), g->fb + op.w_off, g->fb + op.b_off,
@@ -290,7 +337,7 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         for (int64_t b0 = 0; b0 < batch; b0 += mb) {
             slice = b0;
             const int nb = (int)std::min<int64_t>(mb, batch - b0);
-            for (int k = sg.first_op; k <= sg.last_op; k++) run_op(g->ops[k], nb);
+            for (int k = sg.first_op; k <= sg.last_op; k++) run_op(k, nb);
         }
         slice = 0;
     }

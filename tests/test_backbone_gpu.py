@@ -77,3 +77,23 @@ def test_arena_is_reused(models):
     per_crop = dev.arena_bytes / dev.max_batch
     # all ~330 intermediate tensors together would need > 60 MB per crop
     assert per_crop < 12e6, per_crop
+
+
+def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
+    """The fused 32-channel BasicBlock kernel (graph fusion pass) must reproduce the
+    two separate convs bit for bit, and it must free the intermediate tensors."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(11)
+    monkeypatch.setenv("MVPOSE_NO_FUSE", "1")
+    unfused = hrnet.HRNetBackbone(sd, max_batch=6)
+    monkeypatch.delenv("MVPOSE_NO_FUSE")
+    fused = hrnet.HRNetBackbone(sd, max_batch=6)
+    g = torch.Generator().manual_seed(5)
+    x = torch.zeros((5, 256, 192, 4))
+    x[..., :3] = torch.randn((5, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = unfused.forward(xb)
+    b = fused.forward(xb)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert fused.arena_bytes <= unfused.arena_bytes
