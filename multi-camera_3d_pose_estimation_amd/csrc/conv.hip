@@ -778,6 +778,10 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
     if (c.N == 0) return;
+    if (launch_conv1x1_direct(c, s)) {
+        MVP_HIP(hipGetLastError());
+        return;
+    }
     if (c.ks == 3 && c.stride == 1)
         launch_plane<3, 1>(p, s);
     else if (c.ks == 3 && c.stride == 2)

@@ -1,0 +1,194 @@
+// 1x1 convolutions (HRNet Bottleneck / downsample / fuse-layer projections) for gfx950.
+//
+// A 1x1 conv has no spatial reuse, so staging the input through LDS buys nothing:
+// each lane's B fragment (8 consecutive channels of one pixel, NHWC) is one 16-B
+// global load straight into registers.  The block's weight slice ([chunk][q][cout]
+// 16-B slots, BM couts x Cin) is DMA'd into LDS once; waves then run independently
+// over 16*PTW-pixel units with no barriers: loads of B (+ residual) -> MFMA
+// (v_mfma_f32_16x16x32_bf16, A fragments from LDS, each reused by PTW pixel tiles)
+// -> bias [+ residual] [+ ReLU] -> bf16 NHWC stores.  Same MFMA, same K order
+// (chunk 0..Cin/32-1) and same epilogue arithmetic as conv_mfma_kernel.
+#include <algorithm>
+#include <cstdlib>
+
+#include "conv.h"
+#include "mvp_common.h"
+
+namespace mvp {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+    __bf16 b = (__bf16)f;
+    return __builtin_bit_cast(uint16_t, b);
+}
+
+struct P1x1 {
+    const uint16_t* x;
+    const uint16_t* w;
+    const float* bias;
+    const uint16_t* res;
+    uint16_t* y;
+    const uint16_t* zero;
+    long n_pix;
+    int Cout, relu;
+};
+
+constexpr int kPTW = 2;  // 16-pixel tiles per wave per unit
+
+template <int BM, int KCH>
+__global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
+    constexpr int NCT = BM / 16, CIN = KCH * 32, SLOTS = KCH * 4 * BM;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    __shared__ float4 sbias[BM / 4];
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int co0 = blockIdx.y * BM;
+    for (int s0 = wave * 64; s0 < SLOTS; s0 += 256) {
+        const int sl = s0 + lane;
+        const void* src = p.zero;
+        if (sl < SLOTS) {
+            const int co = sl % BM, tq = sl / BM;  // tq = chunk * 4 + q
+            src = p.w + (size_t)(co0 + co) * CIN + tq * 8;
+        }
+        glds16(src, lds + s0 * 16);
+    }
+    if (tid < BM / 4) sbias[tid] = reinterpret_cast<const float4*>(p.bias + co0)[tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    const long n_units = (p.n_pix + 16 * kPTW - 1) / (16 * kPTW);
+    const int co_l = co0 + g * 4;
+    for (long u = (long)blockIdx.x * 4 + wave; u < n_units; u += (long)gridDim.x * 4) {
+        long pix[kPTW];
+        bool valid[kPTW];
+        bf16x8 b[kPTW][KCH];
+#pragma unroll
+        for (int i = 0; i < kPTW; i++) {
+            const long pp = u * 16 * kPTW + i * 16 + (lane & 15);
+            valid[i] = pp < p.n_pix;
+            pix[i] = valid[i] ? pp : p.n_pix - 1;
+            const uint16_t* src = p.x + pix[i] * CIN + g * 8;
+#pragma unroll
+            for (int ch = 0; ch < KCH; ch++) b[i][ch] = *reinterpret_cast<const bf16x8*>(src + ch * 32);
+        }
+        uint2 rv[kPTW][NCT];
+#pragma unroll
+        for (int i = 0; i < kPTW; i++)
+#pragma unroll
+            for (int c = 0; c < NCT; c++) {
+                const int co = co_l + c * 16;
+                const uint16_t* src =
+                    (p.res && co < p.Cout) ? p.res + pix[i] * p.Cout + co : p.zero + lane * 4;
+                rv[i][c] = *reinterpret_cast<const uint2*>(src);
+            }
+        f32x4 acc[kPTW][NCT];
+#pragma unroll
+        for (int i = 0; i < kPTW; i++)
+#pragma unroll
+            for (int c = 0; c < NCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ch = 0; ch < KCH; ch++)
+#pragma unroll
+            for (int c = 0; c < NCT; c++) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(lds + ((ch * 4 + g) * BM + c * 16 + (lane & 15)) * 16);
+#pragma unroll
+                for (int i = 0; i < kPTW; i++)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[i][ch], acc[i][c], 0, 0, 0);
+            }
+#pragma unroll
+        for (int i = 0; i < kPTW; i++) {
+            uint16_t* yrow = p.y + pix[i] * p.Cout;
+#pragma unroll
+            for (int c = 0; c < NCT; c++) {
+                const int co = co_l + c * 16;
+                const float4 bb = sbias[c * 4 + g];
+                float v0 = acc[i][c][0] + bb.x, v1 = acc[i][c][1] + bb.y;
+                float v2 = acc[i][c][2] + bb.z, v3 = acc[i][c][3] + bb.w;
+                const uint2 r = rv[i][c];
+                v0 += bf16_to_f32(r.x & 0xffff);
+                v1 += bf16_to_f32(r.x >> 16);
+                v2 += bf16_to_f32(r.y & 0xffff);
+                v3 += bf16_to_f32(r.y >> 16);
+                if (p.relu) {
+                    v0 = fmaxf(v0, 0.f);
+                    v1 = fmaxf(v1, 0.f);
+                    v2 = fmaxf(v2, 0.f);
+                    v3 = fmaxf(v3, 0.f);
+                }
+                uint2 o;
+                o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+                if (valid[i] && co < p.Cout) *reinterpret_cast<uint2*>(yrow + co) = o;
+            }
+        }
+    }
+}
+
+int g_cus1 = 0;
+
+template <int BM, int KCH>
+void launch_1x1(const P1x1& p, int cout_pad, hipStream_t s) {
+    constexpr int lds = KCH * 4 * BM * 16;
+    auto kern = conv1x1_kernel<BM, KCH>;
+    static int per_cu = 0;
+    if (per_cu == 0) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, lds));
+        if (per_cu < 1) per_cu = 1;
+    }
+    if (g_cus1 == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_cus1, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int y_blocks = cout_pad / BM;
+    const long units = (p.n_pix + 16 * kPTW - 1) / (16 * kPTW);
+    long gx = ((long)g_cus1 * per_cu + y_blocks - 1) / y_blocks;
+    gx = std::min(gx, (units + 3) / 4);
+    hipLaunchKernelGGL(kern, dim3((unsigned)gx, (unsigned)y_blocks), dim3(256), lds, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+template <int BM>
+bool dispatch_k(const P1x1& p, int kch, int cout_pad, hipStream_t s) {
+    switch (kch) {
+        case 1: launch_1x1<BM, 1>(p, cout_pad, s); return true;
+        case 2: launch_1x1<BM, 2>(p, cout_pad, s); return true;
+        case 4: launch_1x1<BM, 4>(p, cout_pad, s); return true;
+        case 8: launch_1x1<BM, 8>(p, cout_pad, s); return true;
+        default: return false;
+    }
+}
+
+}  // namespace
+
+bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
+    if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cin % 32 != 0) return false;
+    static const bool disabled = [] {
+        const char* e = getenv("MVPOSE_NO_1X1");  // diagnostics: use the generic conv kernel
+        return e && e[0] == '1';
+    }();
+    if (disabled) return false;
+    const int cout_pad = conv_cout_pad(c.Cout);
+    const int kch = c.Cin / 32;
+    P1x1 p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), (long)c.N * c.H * c.W, c.Cout, c.relu};
+    if (p.n_pix == 0) return true;
+    if (cout_pad % 128 == 0 && kch <= 2) {  // 128 couts: registers allow K <= 64
+        if (kch == 1) launch_1x1<128, 1>(p, cout_pad, s);
+        else launch_1x1<128, 2>(p, cout_pad, s);
+        return true;
+    }
+    if (cout_pad % 64 == 0) return dispatch_k<64>(p, kch, cout_pad, s);
+    return dispatch_k<32>(p, kch, cout_pad, s);
+}
+
+}  // namespace mvp
