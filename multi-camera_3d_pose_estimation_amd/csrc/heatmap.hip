@@ -213,6 +213,8 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
     float* shm = mom_lds;
     int* sad = reinterpret_cast<int*>(mom_lds + ((p.h * p.w + 3) & ~3));
     int* sbd = sad + p.img_w;
+    int* riy = sbd + p.img_w;  // separable path: per image row source row / weight index
+    int* rfq = riy + p.img_h;
     __shared__ double red[6][kBlock / 64];
     __shared__ int bbox[4];
     const long map = blockIdx.x;
@@ -265,61 +267,96 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
     double t[6] = {0, 0, 0, 0, 0, 0};
     if (c1 >= 0) {
         if (p.separable) {
-            // columns whose taps (ix, ix+1) touch [c0, c1]; rows whose (iy, iy+1) touch [r0, r1]
+            // Row table: source row iy and weight index fq of every image row (uniform per row).
+            for (int y = threadIdx.x; y < p.img_h; y += kBlock) {
+                const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
+                riy[y] = Yq >> 5;
+                rfq[y] = Yq & 31;
+            }
+            __syncthreads();
+            // Lanes own column pairs (packed f32 math); a run of rows sharing iy keeps its
+            // four taps in registers and accumulates S, S*yr, S*yr^2 (yr = row - run start)
+            // in f32, flushed to fp64 with the run's offset when iy changes.  The pixel
+            // value itself is OpenCV's float remap, op for op:
+            //   ((v00 w0 + v01 w1) + v10 w2) + v11 w3,  w = products of (1-f, f) pairs.
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            constexpr int NP = kMomCols / 2;
             const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
             for (int xb = threadIdx.x; xb < p.img_w; xb += kBlock * kMomCols) {
+#pragma clang fp contract(off)
                 int ix[kMomCols];
-                float fx[kMomCols], gx[kMomCols];
                 bool on[kMomCols];
-                double S[kMomCols], Sy[kMomCols], Syy[kMomCols];
-                float v00[kMomCols], v01[kMomCols], v10[kMomCols], v11[kMomCols];
+                f2 gx[NP], fx[NP];
                 bool any = false;
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
                     const int x = xb + j * kBlock;
                     const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
                     ix[j] = X >> 5;
-                    fx[j] = (float)(X & 31) * (1.f / 32.f);
-                    gx[j] = 1.f - fx[j];
+                    const float f = (float)(X & 31) * (1.f / 32.f);
+                    fx[j / 2][j & 1] = f;
+                    gx[j / 2][j & 1] = 1.f - f;
                     on[j] = x < p.img_w && ix[j] + 1 >= c0 && ix[j] <= c1;
                     any |= on[j];
-                    S[j] = Sy[j] = Syy[j] = 0.0;
-                    v00[j] = v01[j] = v10[j] = v11[j] = 0.f;
                 }
+                double S[kMomCols], Sy[kMomCols], Syy[kMomCols];
+#pragma unroll
+                for (int j = 0; j < kMomCols; j++) S[j] = Sy[j] = Syy[j] = 0.0;
                 if (__any(any)) {
-                    int cur_iy = -0x7fffffff;
-                    const int Y0b = sbd[0];
+                    f2 v00[NP], v01[NP], v10[NP], v11[NP], s32[NP], sy32[NP], syy32[NP];
+#pragma unroll
+                    for (int q = 0; q < NP; q++) {
+                        v00[q] = v01[q] = v10[q] = v11[q] = f2{0.f, 0.f};
+                        s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
+                    }
+                    int cur_iy = -0x7fffffff, y0 = 0;
+                    auto flush = [&]() {
+                        const double y0c = y0 - cy;
+#pragma unroll
+                        for (int j = 0; j < kMomCols; j++) {
+                            const double a = s32[j / 2][j & 1], b = sy32[j / 2][j & 1], c = syy32[j / 2][j & 1];
+                            S[j] += a;
+                            Sy[j] += y0c * a + b;
+                            Syy[j] += y0c * y0c * a + 2.0 * y0c * b + c;
+                        }
+#pragma unroll
+                        for (int q = 0; q < NP; q++) s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
+                    };
+                    const f2 thr2 = f2{p.thr, p.thr};
                     for (int y = 0; y < p.img_h; y++) {
-                        const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + Y0b) >> 5;
-                        const int iy = Yq >> 5;
+                        const int iy = riy[y];
                         if (iy + 1 < r0 || iy > r1) continue;  // whole row inactive (uniform)
-                        const float fy = (float)(Yq & 31) * (1.f / 32.f), gy = 1.f - fy;
                         if (iy != cur_iy) {
+                            flush();
                             cur_iy = iy;
+                            y0 = y;
                             const bool ry0 = iy >= 0 && iy < p.h, ry1 = iy + 1 >= 0 && iy + 1 < p.h;
 #pragma unroll
                             for (int j = 0; j < kMomCols; j++) {
                                 const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
-                                v00[j] = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
-                                v01[j] = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
-                                v10[j] = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
-                                v11[j] = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                                v00[j / 2][j & 1] = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
+                                v01[j / 2][j & 1] = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
+                                v10[j / 2][j & 1] = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
+                                v11[j / 2][j & 1] = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
                             }
                         }
-                        const double yc = y - cy, yc2 = yc * yc;
+                        const float fy = (float)rfq[y] * (1.f / 32.f), gy = 1.f - fy;
+                        const float yr = (float)(y - y0);
+                        const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
 #pragma unroll
-                        for (int j = 0; j < kMomCols; j++) {
-                            // OpenCV float remap: ((v0 w0 + v1 w1) + v2 w2) + v3 w3, w from the 32x32 table
-                            float v = __fmul_rn(v00[j], __fmul_rn(gy, gx[j]));
-                            v = __fadd_rn(v, __fmul_rn(v01[j], __fmul_rn(gy, fx[j])));
-                            v = __fadd_rn(v, __fmul_rn(v10[j], __fmul_rn(fy, gx[j])));
-                            v = __fadd_rn(v, __fmul_rn(v11[j], __fmul_rn(fy, fx[j])));
-                            const double dv = (v >= p.thr) ? (double)v : 0.0;  // heatmaps[heatmaps < thr] = 0
-                            S[j] += dv;
-                            Sy[j] = fma(yc, dv, Sy[j]);
-                            Syy[j] = fma(yc2, dv, Syy[j]);
+                        for (int q = 0; q < NP; q++) {
+                            const f2 w0 = gy * gx[q], w1 = gy * fx[q], w2 = fy * gx[q], w3 = fy * fx[q];
+                            f2 v = v00[q] * w0;
+                            v = v + v01[q] * w1;
+                            v = v + v10[q] * w2;
+                            v = v + v11[q] * w3;
+                            const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
+                            s32[q] = s32[q] + vs;
+                            sy32[q] = __builtin_elementwise_fma(vs, yr2, sy32[q]);
+                            syy32[q] = __builtin_elementwise_fma(vs, yrr2, syy32[q]);
                         }
                     }
+                    flush();
                 }
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
@@ -478,9 +515,9 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
                                    int img_w, float thr, int separable, double* out, void* stream) {
     MVP_ABI_BEGIN
     MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
-    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8;
-    MVP_REQUIRE(lds <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image width %d exceed the LDS budget", h, w,
-                img_w);
+    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8 + (size_t)img_h * 8;
+    MVP_REQUIRE(lds <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image %dx%d exceed the LDS budget", h, w,
+                img_h, img_w);
     if (N == 0) return MVP_OK;
     MVP_REQUIRE(hm && minv && out, "mvp_heatmap_moments: NULL device pointer");
     MomParams p{};
