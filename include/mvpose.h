@@ -72,6 +72,9 @@ int mvp_camera_pack(const double* K_host, const double* dist5_host, const double
  * ------------------------------------------------------------------------- */
 #define MVP_TRI_REFERENCE 0
 #define MVP_TRI_ALL_VIEWS 1
+/* OR-ed into mode: solve every point with the exact JacobiSVDImpl_ restatement
+ * (default: QR + inverse iteration, Jacobi only where that has not converged). */
+#define MVP_TRI_EXACT_JACOBI 0x10
 
 int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double* cams_dev,
                     int n_cams, const int* cam_idx_host, int n_cam_idx, int mode,

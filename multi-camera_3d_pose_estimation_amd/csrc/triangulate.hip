@@ -8,8 +8,12 @@
 //   1. undistort each view's (x, y) with its own K/dist: 5 fixed iterations,
 //      icdist<0 fallback, RR = K, rounded to f32 (cvUndistortPointsInternal);
 //   2. A (2V x 4): rows x·P[2]-P[0], y·P[2]-P[1] per view (icvTriangulatePoints);
-//   3. one-sided Hestenes Jacobi SVD on the rows of Aᵀ, eps = 10·DBL_EPSILON,
-//      descending selection sort, null vector = Vt row 3 (JacobiSVDImpl_);
+//   3. null vector = Vt row 3 of cv::SVD (JacobiSVDImpl_): by default computed by
+//      Householder QR + inverse iteration to the fp64 noise floor (qr_inverse_iteration,
+//      ~1/4 of the FP64 work), falling back per lane to the exact restatement —
+//      one-sided Hestenes Jacobi on the rows of Aᵀ, eps = 10·DBL_EPSILON,
+//      descending selection sort — when that iteration has not provably
+//      converged; MVP_TRI_EXACT_JACOBI forces the restatement for every lane;
 //   4. f32 homogeneous divide: s = w != 0 ? 1.f/w : 1.f (convertPointsFromHomogeneous).
 // The reference's camera selection (top-2 by confidence, ascending; parameters
 // keyed by selection position; pose_estimation.py:32-45) is reproduced in
@@ -166,6 +170,107 @@ __device__ __forceinline__ void jacobi_null_vector(double (&At)[4][M], double (&
     for (int q = 0; q < 4; q++) nv[q] = Vt[3][q];
 }
 
+// Fast null vector of A (M x 4): Householder QR (A = QR; R is 4x4 upper
+// triangular with A's right singular vectors), then inverse iteration on RᵀR
+// started from R⁻¹e₄.  Each step shrinks the component off the smallest right
+// singular vector by (σ₄/σ₃)² (~1e-6 on real rigs), so two or three steps reach
+// the fp64 noise floor, where the unit vector agrees with JacobiSVDImpl_'s Vt
+// row 3 to ~1e-13 (its own rounding error) at a fraction of the FP64 work.
+// Returns false unless the iteration has provably converged (ill-conditioned
+// geometry with σ₄ ≈ σ₃, NaN/Inf input): the caller then runs the exact Jacobi
+// restatement.  FMA contraction is allowed here: this is an approximation of the
+// Jacobi result, checked by its own convergence test, not a restatement of
+// OpenCV's rounding sequence.
+template <int M>
+__device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], double (&nv)[4]) {
+#pragma clang fp contract(fast)
+    double A[M][4];
+#pragma unroll
+    for (int r = 0; r < M; r++)
+#pragma unroll
+        for (int c = 0; c < 4; c++) A[r][c] = A0[r][c];
+    double R[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        double s = 0;
+#pragma unroll
+        for (int r = k; r < M; r++) s += A[r][k] * A[r][k];
+        const double nrm = sqrt(s);
+        if (k == 3) {
+            R[3][3] = nrm;
+            break;
+        }
+        const double akk = A[k][k];
+        const double alpha = akk >= 0 ? -nrm : nrm;
+        // reflector v = a - alpha·e_k; vᵀv / 2 = nrm (nrm + |akk|)
+        const double half_vtv = nrm * (nrm + fabs(akk));
+        const double inv = half_vtv > 0 ? 1.0 / half_vtv : 0.0;
+        A[k][k] = akk - alpha;
+        R[k][k] = alpha;
+#pragma unroll
+        for (int j = k + 1; j < 4; j++) {
+            double d = 0;
+#pragma unroll
+            for (int r = k; r < M; r++) d += A[r][k] * A[r][j];
+            const double t = d * inv;
+#pragma unroll
+            for (int r = k; r < M; r++) A[r][j] -= t * A[r][k];
+            R[k][j] = A[k][j];
+        }
+    }
+    // an exactly singular R (noise-free data): a perturbation far below the QR
+    // rounding error keeps R⁻¹ finite and changes nothing else
+    const double scale = fmax(fmax(fabs(R[0][0]), fabs(R[1][1])), fabs(R[2][2]));
+    if (fabs(R[3][3]) < 1e-18 * scale) R[3][3] = 1e-18 * scale;
+    double d[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = 1.0 / R[k][k];
+    auto back = [&](double (&x)[4]) {  // x <- R⁻¹ x
+        x[3] = x[3] * d[3];
+        x[2] = (x[2] - R[2][3] * x[3]) * d[2];
+        x[1] = (x[1] - R[1][2] * x[2] - R[1][3] * x[3]) * d[1];
+        x[0] = (x[0] - R[0][1] * x[1] - R[0][2] * x[2] - R[0][3] * x[3]) * d[0];
+    };
+    auto fwd = [&](double (&x)[4]) {  // x <- R⁻ᵀ x
+        x[0] = x[0] * d[0];
+        x[1] = (x[1] - R[0][1] * x[0]) * d[1];
+        x[2] = (x[2] - R[0][2] * x[0] - R[1][2] * x[1]) * d[2];
+        x[3] = (x[3] - R[0][3] * x[0] - R[1][3] * x[1] - R[2][3] * x[2]) * d[3];
+    };
+    auto normalize = [&](double (&x)[4]) {
+        const double is = 1.0 / sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) x[q] *= is;
+    };
+    double x[4] = {0.0, 0.0, 0.0, 1.0};
+    back(x);
+    normalize(x);
+    double prev = 1.0;  // step length of the previous iteration
+    for (int it = 0; it < 12; it++) {
+        double y[4] = {x[0], x[1], x[2], x[3]};
+        fwd(y);
+        back(y);
+        normalize(y);  // (RᵀR)⁻¹ is positive definite: no sign flip between iterates
+        double dd = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const double e = y[q] - x[q];
+            dd += e * e;
+            x[q] = y[q];
+        }
+        const double step = sqrt(dd);
+        // geometric convergence: remaining error ≈ step · (step / prev)
+        if (step <= 4e-16 || (step <= 1e-6 && step * step <= 1e-14 * prev)) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) nv[q] = x[q];
+            return true;
+        }
+        if (it >= 2 && !(step < 0.5 * prev)) return false;  // not contracting (or NaN)
+        prev = step;
+    }
+    return false;
+}
+
 __device__ __forceinline__ void write_result(const double (&nv)[4], int64_t p, float* __restrict__ out,
                                              double* __restrict__ out4) {
     // cvmSet into the f32 points4D, then convertPointsFromHomogeneous in f32.
@@ -203,7 +308,7 @@ __device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], const
 // by selection position (reference quirk, pose_estimation.py:36-45).
 __global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
-    CamIdx ci, int n_ci, float* __restrict__ out, double* __restrict__ out4) {
+    CamIdx ci, int n_ci, int exact, float* __restrict__ out, double* __restrict__ out4) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
     load_cams(scam, cams, n_cams);
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -242,13 +347,15 @@ __global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
     double A[4][4];
     add_view_rows(A, 0, u0x, u0y, scam[pos0] + 26);
     add_view_rows(A, 2, u1x, u1y, scam[pos1] + 26);
-    double At[4][4];
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) At[c][r] = A[r][c];
     double nv[4];
-    jacobi_null_vector<4>(At, nv);
+    if (exact || !qr_inverse_iteration<4>(A, nv)) {
+        double At[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) At[c][r] = A[r][c];
+        jacobi_null_vector<4>(At, nv);
+    }
     write_result(nv, p, out, out4);
 }
 
@@ -256,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
 template <int NV>
 __global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
-    CamIdx ci, float* __restrict__ out, double* __restrict__ out4) {
+    CamIdx ci, int exact, float* __restrict__ out, double* __restrict__ out4) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
     load_cams(scam, cams, n_cams);
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -270,13 +377,15 @@ __global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
         undistort_point(kp[col], kp[V + col], scam[col], ux, uy);
         add_view_rows(A, 2 * j, ux, uy, scam[col] + 26);
     }
-    double At[4][2 * NV];
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-#pragma unroll
-        for (int r = 0; r < 2 * NV; r++) At[c][r] = A[r][c];
     double nv[4];
-    jacobi_null_vector<2 * NV>(At, nv);
+    if (exact || !qr_inverse_iteration<2 * NV>(A, nv)) {
+        double At[4][2 * NV];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int r = 0; r < 2 * NV; r++) At[c][r] = A[r][c];
+        jacobi_null_vector<2 * NV>(At, nv);
+    }
     write_result(nv, p, out, out4);
 }
 
@@ -303,16 +412,18 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t blocks = (n_points + kBlock - 1) / kBlock;
     MVP_REQUIRE(blocks < (1LL << 31), "mvp_triangulate: too many points");
+    const int exact = (mode & MVP_TRI_EXACT_JACOBI) ? 1 : 0;
+    mode &= ~MVP_TRI_EXACT_JACOBI;
     if (mode == MVP_TRI_REFERENCE) {
         MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
                     "n_cam_idx <= n_cams");
         hipLaunchKernelGGL(triangulate_reference_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, n_points,
-                           V, cams, n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
+                           V, cams, n_cams, ci, n_cam_idx, exact, out_xyz, out_xyzw);
     } else if (mode == MVP_TRI_ALL_VIEWS) {
 #define MVP_TRI_CASE(NV)                                                                                    \
     case NV:                                                                                                \
         hipLaunchKernelGGL(triangulate_all_views_kernel<NV>, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, \
-                           n_points, V, cams, n_cams, ci, out_xyz, out_xyzw);                              \
+                           n_points, V, cams, n_cams, ci, exact, out_xyz, out_xyzw);                       \
         break;
         switch (n_cam_idx) {
             MVP_TRI_CASE(2)

@@ -18,6 +18,7 @@ from ._lib import call
 CAM_DOUBLES = 40
 TRI_REFERENCE = 0
 TRI_ALL_VIEWS = 1
+TRI_EXACT_JACOBI = 0x10  # mode flag: exact Jacobi SVD for every point (mvpose.h)
 
 
 def _stream(device=None) -> ctypes.c_void_p:
@@ -71,10 +72,13 @@ def pack_cameras(camera_params) -> np.ndarray:
 
 def triangulate(kpts: torch.Tensor, cams: torch.Tensor, cam_idx: Sequence[int] = (0, 1),
                 mode: int = TRI_REFERENCE, out: torch.Tensor | None = None,
-                return_xyzw: bool = False):
+                return_xyzw: bool = False, exact: bool = False):
     """kpts (..., 3, V) float32 on GPU (reference layout) -> (..., 3) float32.
 
-    cams: (n_cams, 40) float64 on GPU (pack_cameras)."""
+    cams: (n_cams, 40) float64 on GPU (pack_cameras).  exact=True solves every
+    point with the JacobiSVDImpl_ restatement instead of QR + inverse iteration."""
+    if exact:
+        mode = int(mode) | TRI_EXACT_JACOBI
     _require(kpts, torch.float32, "kpts")
     _require(cams, torch.float64, "cams")
     if kpts.dim() < 2 or kpts.shape[-2] != 3:

@@ -102,6 +102,52 @@ def test_all_views_vs_oracle(ops, V):
     _check(_run(ops, syn.reference_camera_params(cams), k, ci, mode=ops.TRI_ALL_VIEWS), ref)
 
 
+@pytest.mark.parametrize("V,mode,noise", [(2, 0, 1.0), (2, 0, 0.0), (2, 0, 40.0), (4, 1, 1.0), (8, 1, 3.0)])
+def test_fast_solver_matches_exact_jacobi(ops, V, mode, noise):
+    """QR + inverse-iteration null vector (default) vs the exact JacobiSVDImpl_
+    restatement on the same inputs: <= 1e-4 and >= 99 % bit-identical, including
+    noise-free (exactly singular A) and badly inconsistent (40 px) views."""
+    cams = syn.make_rig(V, seed=31 + V)
+    k = syn.make_kpts_2d(syn.make_poses(3000, seed=32), cams, seed=33, noise_px=noise)
+    cp = syn.reference_camera_params(cams)
+    ci = list(range(V)) if mode == ops.TRI_ALL_VIEWS else [0, 1]
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    kd = torch.tensor(k, device="cuda")
+    fast = ops.triangulate(kd, cams_d, ci, mode=mode).cpu().numpy()
+    exact = ops.triangulate(kd, cams_d, ci, mode=mode, exact=True).cpu().numpy()
+    np.testing.assert_allclose(fast, exact, rtol=0, atol=ATOL, equal_nan=True)
+    assert np.mean(fast == exact) >= 0.99
+
+
+def test_fast_solver_degenerate_inputs(ops):
+    """Random (geometrically inconsistent) 2D points and NaNs: the fallback must
+    reproduce the exact path."""
+    cams = syn.make_rig(2, seed=41)
+    rng = np.random.default_rng(42)
+    k = np.zeros((500, 17, 3, 2), np.float32)
+    k[:, :, 0] = rng.uniform(0, 1280, (500, 17, 2))
+    k[:, :, 1] = rng.uniform(0, 720, (500, 17, 2))
+    k[:, :, 2] = rng.uniform(0.3, 1, (500, 17, 2))
+    k[7, 3, 0, 1] = np.nan
+    k[9, 4, 1, 0] = np.inf
+    cp = syn.reference_camera_params(cams)
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    kd = torch.tensor(k, device="cuda")
+    fast, fw = (t.cpu().numpy() for t in ops.triangulate(kd, cams_d, [0, 1], return_xyzw=True))
+    exact, ew = (t.cpu().numpy() for t in ops.triangulate(kd, cams_d, [0, 1], exact=True, return_xyzw=True))
+    ref = cv_ref.get_pose_3D(cp, k, camera_indices=[0, 1])
+    np.testing.assert_allclose(exact, ref, rtol=1e-5, atol=ATOL, equal_nan=True)
+    # the null vectors agree up to sign; X = v/w is compared where w is not ~0 (points at infinity)
+    fw, ew = fw.reshape(-1, 4), ew.reshape(-1, 4)
+    ok = np.isfinite(ew).all(1)
+    assert np.array_equal(ok, np.isfinite(fw).all(1))
+    sgn = np.sign(np.sum(fw[ok] * ew[ok], axis=1, keepdims=True))
+    np.testing.assert_allclose(fw[ok] * sgn, ew[ok], rtol=0, atol=1e-9)
+    far = np.abs(ew[:, 3]) < 1e-6
+    sel = ok & ~far
+    np.testing.assert_allclose(fast.reshape(-1, 3)[sel], exact.reshape(-1, 3)[sel], rtol=1e-5, atol=ATOL)
+
+
 def test_full_size_roundtrip_property(ops):
     """BASELINE config 4 size (100k frames x 17 joints, V=2): noise-free
     projections must triangulate back to the poses; order of the two cameras

@@ -12,7 +12,8 @@ import json
 import sys
 from collections import defaultdict
 
-GROUPS = {"backbone": ("conv_mfma_kernel", "stem_kernel", "fuse_sum_kernel"), "moments": ("moments_kernel",),
+GROUPS = {"backbone": ("conv_mfma_kernel", "stem_kernel", "stem_mfma_kernel", "fuse_sum_kernel", "conv1x1_kernel",
+                       "basic_block", "wsconv"), "moments": ("moments_kernel",),
           "preprocess": ("preprocess_kernel",), "decode": ("decode_kernel",),
           "triangulate": ("triangulate_reference_kernel", "triangulate_all_views_kernel")}
 
@@ -27,7 +28,7 @@ def load(path, counter):
         for g, keys in GROUPS.items():
             if any(k in name for k in keys):
                 per[g][0] += float(r["Counter_Value"]) * 1024.0
-                if g != "backbone" or "stem_kernel" in name:
+                if g != "backbone" or "stem" in name:  # one stem dispatch per graph forward
                     launches[g] += 1
     return per, launches
 
