@@ -27,6 +27,11 @@ void launch_conv(const ConvLaunch& c, hipStream_t s);
 // Direct-load 1x1 conv (conv1x1.hip); false when the conv is not a bf16-output 1x1.
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s);
 
+// Weight-stationary 3x3/s1 conv for the Cin == Cout branch planes (wsconv.hip):
+// 64 ch at 32x24 and 128 ch at 16x12.  false when the conv is not one of those
+// (or MVPOSE_NO_WSCONV=1).
+bool launch_wsconv(const ConvLaunch& c, hipStream_t s);
+
 // 3x3/s2 stem conv on 4-channel (RGB + zero) bf16 crops, BN folded, ReLU.
 // w: [64][3][3][4] f32, bias [64] f32.  x [N][H][W][4] -> y [N][H/2][W/2][64].
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,

@@ -301,16 +301,33 @@ def build_hrnet_w32(sd, micro_batch=None) -> tuple[GraphSpec, int, int]:
     return g, x_in, out
 
 
-class HRNetBackbone:
-    """Device-resident HRNet-W32 + head on the libmvpose graph runtime.
+def basic_block_spec(c: int, h: int, w: int, seed: int = 0, n_blocks: int = 1):
+    """A chain of n_blocks HRNet BasicBlocks (conv3x3+BN+ReLU, conv3x3+BN, +x, ReLU)
+    on one c-channel h x w plane, for kernel tests and per-layer benchmarks.
+    Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    g = GraphSpec()
+    x = g.tensor(h, w, c)
+    y = x
+    for k in range(n_blocks):
+        for j in (1, 2):
+            sd[f"b{k}.conv{j}.weight"] = torch.randn((c, c, 3, 3), generator=gen) * (2.0 / (9 * c)) ** 0.5
+            sd[f"b{k}.bn{j}.weight"] = 1.0 + 0.1 * torch.randn((c,), generator=gen)
+            sd[f"b{k}.bn{j}.bias"] = 0.1 * torch.randn((c,), generator=gen)
+            sd[f"b{k}.bn{j}.running_mean"] = 0.1 * torch.randn((c,), generator=gen)
+            sd[f"b{k}.bn{j}.running_var"] = 1.0 + 0.2 * torch.rand((c,), generator=gen)
+        t = g.conv(sd, f"b{k}.conv1", f"b{k}.bn1", y, 1, True)
+        y = g.conv(sd, f"b{k}.conv2", f"b{k}.bn2", t, 1, True, res=y)
+    return g, x, y, sd
 
-    forward(crops (N,256,192,4) bf16 on GPU) -> heatmaps (N,17,64,48) f32."""
 
-    def __init__(self, state_dict=None, seed: int = 0, max_batch: int = 256, device="cuda", micro_batch=None):
-        if state_dict is None:
-            state_dict = random_state_dict(seed)
-        spec, self.input_id, self.output_id = build_hrnet_w32(state_dict, micro_batch)
-        self.spec = spec
+class ConvGraph:
+    """A GraphSpec instantiated on the device (mvp_graph_create): one bf16 NHWC
+    input tensor -> one output tensor, batch given per forward call."""
+
+    def __init__(self, spec: GraphSpec, input_id: int, output_id: int, max_batch: int, device="cuda"):
+        self.spec, self.input_id, self.output_id = spec, input_id, output_id
         w, f = spec.blobs()
         self.device = torch.device(device)
         self.w_dev = torch.from_numpy(w.view(np.int16).copy()).to(self.device)
@@ -336,6 +353,15 @@ class HRNetBackbone:
                  self.f_dev.numel(), self.max_batch, ctypes.byref(h))
         self._h = h
 
+    def run(self, x: torch.Tensor, out: torch.Tensor) -> torch.Tensor:
+        """x: [n][h][w][c] of the input tensor, out: the output tensor; stream-ordered on torch's stream."""
+        n = x.shape[0]
+        if n > self.max_batch:
+            raise ValueError(f"batch {n} > max_batch {self.max_batch}")
+        call("mvp_graph_forward", self._h, ctypes.c_void_p(x.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
+             ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        return out
+
     @property
     def arena_bytes(self) -> int:
         b = ctypes.c_int64()
@@ -351,20 +377,6 @@ class HRNetBackbone:
                 macs += h * w * op["cout"] * cin * op["ks"] ** 2
         return macs
 
-    def forward(self, crops: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        if crops.dtype != torch.bfloat16 or not crops.is_cuda or not crops.is_contiguous():
-            raise ValueError("crops must be a contiguous bf16 CUDA tensor (N,256,192,4)")
-        if tuple(crops.shape[1:]) != (INPUT_HW[0], INPUT_HW[1], 4):
-            raise ValueError(f"crops must be (N,{INPUT_HW[0]},{INPUT_HW[1]},4), got {tuple(crops.shape)}")
-        n = crops.shape[0]
-        if n > self.max_batch:
-            raise ValueError(f"batch {n} > max_batch {self.max_batch}")
-        if out is None:
-            out = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=crops.device)
-        call("mvp_graph_forward", self._h, ctypes.c_void_p(crops.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
-             ctypes.c_void_p(torch.cuda.current_stream(crops.device).cuda_stream))
-        return out
-
     def close(self):
         if getattr(self, "_h", None):
             call("mvp_graph_destroy", self._h)
@@ -375,3 +387,27 @@ class HRNetBackbone:
             self.close()
         except Exception:
             pass
+
+
+class HRNetBackbone(ConvGraph):
+    """Device-resident HRNet-W32 + head on the libmvpose graph runtime.
+
+    forward(crops (N,256,192,4) bf16 on GPU) -> heatmaps (N,17,64,48) f32."""
+
+    def __init__(self, state_dict=None, seed: int = 0, max_batch: int = 256, device="cuda", micro_batch=None):
+        if state_dict is None:
+            state_dict = random_state_dict(seed)
+        spec, input_id, output_id = build_hrnet_w32(state_dict, micro_batch)
+        super().__init__(spec, input_id, output_id, max_batch, device)
+
+    def forward(self, crops: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        if crops.dtype != torch.bfloat16 or not crops.is_cuda or not crops.is_contiguous():
+            raise ValueError("crops must be a contiguous bf16 CUDA tensor (N,256,192,4)")
+        if tuple(crops.shape[1:]) != (INPUT_HW[0], INPUT_HW[1], 4):
+            raise ValueError(f"crops must be (N,{INPUT_HW[0]},{INPUT_HW[1]},4), got {tuple(crops.shape)}")
+        n = crops.shape[0]
+        if n > self.max_batch:
+            raise ValueError(f"batch {n} > max_batch {self.max_batch}")
+        if out is None:
+            out = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=crops.device)
+        return self.run(crops, out)

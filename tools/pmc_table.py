@@ -26,3 +26,13 @@ for k in order:
     if "SQ_INSTS_VALU" in d and "SQ_INSTS_LDS" in d:
         out.append(f"valu={d['SQ_INSTS_VALU']:.3g} lds={d['SQ_INSTS_LDS']:.3g} vmem={d.get('SQ_INSTS_VMEM', 0):.3g}")
     print("  ".join(out))
+    extra = []
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
+        # per-SIMD MFMA busy over the kernel's active cycles, 256 CUs x 4 SIMDs
+        extra.append(f"mfma_busy={d['SQ_VALU_MFMA_BUSY_CYCLES'] / max(d['GRBM_GUI_ACTIVE'] * 1024, 1):5.3f}")
+    if "FETCH_SIZE" in d:
+        extra.append(f"fetchMB/launch={2 * d['FETCH_SIZE'] * 1024 / len(calls[k]) / 1e6:8.1f}")
+    if "WRITE_SIZE" in d:
+        extra.append(f"writeMB/launch={d['WRITE_SIZE'] * 1024 / len(calls[k]) / 1e6:8.1f}")
+    if extra:
+        print("    " + "  ".join(extra))
