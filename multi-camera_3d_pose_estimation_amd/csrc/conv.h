@@ -32,6 +32,11 @@ bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s);
 // (or MVPOSE_NO_WSCONV=1).
 bool launch_wsconv(const ConvLaunch& c, hipStream_t s);
 
+// Lean 3x3/s1 conv on 32x32x16 MFMAs for 384-pixel x 64-cout tiles (tconv.hip):
+// 64 ch @ 32x24 and 64x48, 128 ch @ 16x12, 256 ch @ 8x6 (ReLU epilogue).  false
+// when the conv is not one of those (or MVPOSE_NO_TCONV=1).
+bool launch_tconv(const ConvLaunch& c, hipStream_t s);
+
 // 3x3/s2 stem conv on 4-channel (RGB + zero) bf16 crops, BN folded, ReLU.
 // w: [64][3][3][4] f32, bias [64] f32.  x [N][H][W][4] -> y [N][H/2][W/2][64].
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,

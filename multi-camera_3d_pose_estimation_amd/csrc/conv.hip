@@ -778,7 +778,7 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
     if (c.N == 0) return;
-    if (launch_conv1x1_direct(c, s) || launch_wsconv(c, s)) {
+    if (launch_conv1x1_direct(c, s) || launch_tconv(c, s) || launch_wsconv(c, s)) {
         MVP_HIP(hipGetLastError());
         return;
     }

@@ -1,10 +1,10 @@
-"""GPU parity of the branch-plane BasicBlock convolutions (csrc/wsconv.hip for
-64 ch @ 32x24 and 128 ch @ 16x12; conv.hip / block.hip for the other planes)
-against a torch fp32 restatement that rounds to bf16 at the same tensor
-boundaries as the device graph (bf16 weights and activations, f32 bias and
-accumulation).  The weight-stationary kernel sums K in (tap, cin) order and the
-generic kernel in (cin chunk, tap) order, so both are compared against the
-reference with a tolerance, not bit for bit:
+"""GPU parity of the branch-plane BasicBlock convolutions against a torch fp32
+restatement that rounds to bf16 at the same tensor boundaries as the device
+graph (bf16 weights and activations, f32 bias and accumulation).  Every conv
+kernel family that serves a plane is checked: the generic conv_mfma_kernel
+(conv.hip; block.hip for the fused 32-channel block), the weight-stationary
+wsconv.hip and the 32x32x16 tconv.hip.  They sum K in different orders, so each
+is compared against the reference with a tolerance, not bit for bit:
   relative L2 error <= 4e-3, and |dev - ref| <= 3 bf16 ulps of max|ref|."""
 import numpy as np
 import pytest
@@ -12,7 +12,9 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)]
+PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]
+# (MVPOSE_NO_TCONV, MVPOSE_NO_WSCONV) per kernel family
+MODES = {"generic": ("1", "1"), "wsconv": ("1", "0"), "tconv": ("0", "1")}
 
 
 def _bf(t):
@@ -35,14 +37,18 @@ def _reference(sd, x, n_blocks):
     return y.permute(0, 2, 3, 1).contiguous()
 
 
-def _run(c, h, w, n, n_blocks, seed, monkeypatch, ws):
-    from mvpose import hrnet
+def _set_mode(monkeypatch, mode):
+    no_t, no_ws = MODES[mode]
+    monkeypatch.setenv("MVPOSE_NO_TCONV", no_t)
+    monkeypatch.setenv("MVPOSE_NO_WSCONV", no_ws)
     monkeypatch.setenv("MVPOSE_WSCONV64", "1")
+    monkeypatch.setenv("MVPOSE_TCONV128", "1")
+
+
+def _run(c, h, w, n, n_blocks, seed, monkeypatch, mode):
+    from mvpose import hrnet
+    _set_mode(monkeypatch, mode)
     spec, xi, yo, sd = hrnet.basic_block_spec(c, h, w, seed=seed, n_blocks=n_blocks)
-    if ws:
-        monkeypatch.delenv("MVPOSE_NO_WSCONV", raising=False)
-    else:
-        monkeypatch.setenv("MVPOSE_NO_WSCONV", "1")
     g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
     gen = torch.Generator().manual_seed(seed + 100)
     x = torch.randn((n, h, w, c), generator=gen).bfloat16()
@@ -58,26 +64,26 @@ def test_basic_block_vs_reference(c, h, w, monkeypatch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     n = 37  # ragged: not a multiple of any tile / grid size
-    for ws in (True, False):
-        got, ref = _run(c, h, w, n, 2, 3, monkeypatch, ws)
+    for mode in MODES:
+        got, ref = _run(c, h, w, n, 2, 3, monkeypatch, mode)
         assert torch.isfinite(got).all()
         rel = (torch.linalg.vector_norm(got - ref) / torch.linalg.vector_norm(ref)).item()
         mx = (got - ref).abs().max().item()
         scale = ref.abs().max().item()
-        print(f"C={c} {h}x{w} ws={ws}: rel L2 {rel:.2e}, max abs {mx:.3e} (max|ref| {scale:.2f})")
+        print(f"C={c} {h}x{w} {mode}: rel L2 {rel:.2e}, max abs {mx:.3e} (max|ref| {scale:.2f})")
         assert rel <= 4e-3
         assert mx <= 3 * scale * 2.0 ** -8
 
 
-@pytest.mark.parametrize("c,h,w", [(64, 32, 24), (128, 16, 12)])
-def test_wsconv_batch_positions(c, h, w, monkeypatch):
+@pytest.mark.parametrize("mode", ["wsconv", "tconv"])
+@pytest.mark.parametrize("c,h,w", [(64, 32, 24), (128, 16, 12), (256, 8, 6)])
+def test_batch_positions(c, h, w, mode, monkeypatch):
     """A crop's output must not depend on its batch position or the batch size
-    (tile scheduling over a persistent grid)."""
+    (tile scheduling over a persistent grid, multi-crop tiles)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet
-    monkeypatch.delenv("MVPOSE_NO_WSCONV", raising=False)
-    monkeypatch.setenv("MVPOSE_WSCONV64", "1")
+    _set_mode(monkeypatch, mode)
     spec, xi, yo, _ = hrnet.basic_block_spec(c, h, w, seed=5)
     g = hrnet.ConvGraph(spec, xi, yo, max_batch=600)
     gen = torch.Generator().manual_seed(9)

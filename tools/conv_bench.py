@@ -1,5 +1,6 @@
-"""Per-plane BasicBlock timing (two 3x3 convs + residual) at the bench batch, with
-the weight-stationary kernel on and off.  HIP events on torch's stream.
+"""Per-plane BasicBlock timing (two 3x3 convs + residual) at the bench batch, per
+conv kernel family (generic conv_mfma_kernel, wsconv, tconv).  HIP events on
+torch's stream.
   python tools/conv_bench.py [batch] [reps]"""
 import os
 import sys
@@ -12,9 +13,12 @@ from mvpose import hrnet  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-for c, h, w in [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)]:
-    for ws in ("0", "1"):
-        os.environ["MVPOSE_NO_WSCONV"] = ws
+MODES = {"generic": ("1", "1"), "wsconv": ("1", "0"), "tconv": ("0", "1")}
+os.environ["MVPOSE_WSCONV64"] = "1"
+os.environ["MVPOSE_TCONV128"] = "1"
+for c, h, w in [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]:
+    for mode, (no_t, no_ws) in MODES.items():
+        os.environ["MVPOSE_NO_TCONV"], os.environ["MVPOSE_NO_WSCONV"] = no_t, no_ws
         spec, xi, yo, _ = hrnet.basic_block_spec(c, h, w, seed=1)
         g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
         x = torch.randn((n, h, w, c), device="cuda").bfloat16()
@@ -29,6 +33,6 @@ for c, h, w in [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)]:
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps / 2  # per conv
         flop = 2.0 * n * h * w * c * c * 9
-        print(f"C={c:3d} {h}x{w} ws={'off' if ws == '1' else 'on '}: {us:7.1f} us/conv  "
+        print(f"C={c:3d} {h}x{w} {mode:8s}: {us:7.1f} us/conv  "
               f"{flop / us / 1e6:6.1f} TFLOP/s ({flop / us / 1e6 / 2500 * 100:4.1f}% of 2.5 PF)", flush=True)
         g.close()
