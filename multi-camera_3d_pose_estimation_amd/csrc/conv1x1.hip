@@ -7,7 +7,11 @@
 // over 16*PTW-pixel units with no barriers: loads of B (+ residual) -> MFMA
 // (v_mfma_f32_16x16x32_bf16, A fragments from LDS, each reused by PTW pixel tiles)
 // -> bias [+ residual] [+ ReLU] -> bf16 NHWC stores.  Same MFMA, same K order
-// (chunk 0..Cin/32-1) and same epilogue arithmetic as conv_mfma_kernel.
+// (chunk 0..Cin/32-1) and same epilogue arithmetic as conv_mfma_kernel.  The A
+// rows are a permutation of the block's couts, so that each lane group owns BM/4
+// consecutive couts of its pixel: residual loads and stores are 16 B per lane
+// (the layer1 64->256 projections are memory-bound; 8-B accesses made them
+// issue-bound).
 #include <algorithm>
 #include <cstdlib>
 
@@ -57,7 +61,10 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
         const void* src = p.zero;
         if (sl < SLOTS) {
             const int co = sl % BM, tq = sl / BM;  // tq = chunk * 4 + q
-            src = p.w + (size_t)(co0 + co) * CIN + tq * 8;
+            // A row r of cout tile c holds cout (r>>2)*(BM/4) + 4c + (r&3): output lane
+            // group g then owns the BM/4 consecutive couts g*(BM/4) .. of its pixel
+            const int c = co >> 4, r = co & 15;
+            src = p.w + (size_t)(co0 + (r >> 2) * (BM / 4) + c * 4 + (r & 3)) * CIN + tq * 8;
         }
         glds16(src, lds + s0 * 16);
     }
@@ -66,7 +73,6 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
     __syncthreads();
 
     const long n_units = (p.n_pix + 16 * kPTW - 1) / (16 * kPTW);
-    const int co_l = co0 + g * 4;
     for (long u = (long)blockIdx.x * 4 + wave; u < n_units; u += (long)gridDim.x * 4) {
         long pix[kPTW];
         bool valid[kPTW];
@@ -80,16 +86,17 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
 #pragma unroll
             for (int ch = 0; ch < KCH; ch++) b[i][ch] = *reinterpret_cast<const bf16x8*>(src + ch * 32);
         }
-        uint2 rv[kPTW][NCT];
+        // residual: the lane's BM/4 consecutive couts, 16 B per load
+        constexpr int RQ = BM / 32;  // uint4 per lane per pixel tile
+        uint4 rv[kPTW][RQ];
+        const int cog = co0 + g * (BM / 4);
+        const bool co_ok = cog < p.Cout;
 #pragma unroll
-        for (int i = 0; i < kPTW; i++)
+        for (int i = 0; i < kPTW; i++) {
+            const uint16_t* src = (p.res && co_ok) ? p.res + pix[i] * p.Cout + cog : p.zero + lane * (BM / 4);
 #pragma unroll
-            for (int c = 0; c < NCT; c++) {
-                const int co = co_l + c * 16;
-                const uint16_t* src =
-                    (p.res && co < p.Cout) ? p.res + pix[i] * p.Cout + co : p.zero + lane * 4;
-                rv[i][c] = *reinterpret_cast<const uint2*>(src);
-            }
+            for (int q = 0; q < RQ; q++) rv[i][q] = *reinterpret_cast<const uint4*>(src + q * 8);
+        }
         f32x4 acc[kPTW][NCT];
 #pragma unroll
         for (int i = 0; i < kPTW; i++)
@@ -106,28 +113,29 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
             }
 #pragma unroll
         for (int i = 0; i < kPTW; i++) {
-            uint16_t* yrow = p.y + pix[i] * p.Cout;
+            uint32_t o[2 * NCT];
 #pragma unroll
             for (int c = 0; c < NCT; c++) {
-                const int co = co_l + c * 16;
-                const float4 bb = sbias[c * 4 + g];
-                float v0 = acc[i][c][0] + bb.x, v1 = acc[i][c][1] + bb.y;
-                float v2 = acc[i][c][2] + bb.z, v3 = acc[i][c][3] + bb.w;
-                const uint2 r = rv[i][c];
-                v0 += bf16_to_f32(r.x & 0xffff);
-                v1 += bf16_to_f32(r.x >> 16);
-                v2 += bf16_to_f32(r.y & 0xffff);
-                v3 += bf16_to_f32(r.y >> 16);
+                const float4 bb = sbias[g * (BM / 16) + c];
+                float v[4] = {acc[i][c][0] + bb.x, acc[i][c][1] + bb.y, acc[i][c][2] + bb.z, acc[i][c][3] + bb.w};
+                const uint4 r4 = rv[i][c >> 1];
+                const uint32_t r0 = (c & 1) ? r4.z : r4.x, r1 = (c & 1) ? r4.w : r4.y;
+                v[0] += bf16_to_f32(r0 & 0xffff);
+                v[1] += bf16_to_f32(r0 >> 16);
+                v[2] += bf16_to_f32(r1 & 0xffff);
+                v[3] += bf16_to_f32(r1 >> 16);
                 if (p.relu) {
-                    v0 = fmaxf(v0, 0.f);
-                    v1 = fmaxf(v1, 0.f);
-                    v2 = fmaxf(v2, 0.f);
-                    v3 = fmaxf(v3, 0.f);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
                 }
-                uint2 o;
-                o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-                o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-                if (valid[i] && co < p.Cout) *reinterpret_cast<uint2*>(yrow + co) = o;
+                o[2 * c] = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+                o[2 * c + 1] = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+            }
+            if (valid[i] && co_ok) {
+                uint16_t* yrow = p.y + pix[i] * p.Cout + cog;
+#pragma unroll
+                for (int q = 0; q < RQ; q++)
+                    *reinterpret_cast<uint4*>(yrow + q * 8) = uint4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
             }
         }
     }
@@ -173,6 +181,8 @@ bool dispatch_k(const P1x1& p, int kch, int cout_pad, hipStream_t s) {
 
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
     if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cin % 32 != 0) return false;
+    const int bm = conv_cout_pad(c.Cout) % 128 == 0 && c.Cin <= 64 ? 128 : conv_cout_pad(c.Cout) % 64 == 0 ? 64 : 32;
+    if (c.Cout % (bm / 4) != 0) return false;  // lane groups own bm/4 consecutive couts
     static const bool disabled = [] {
         const char* e = getenv("MVPOSE_NO_1X1");  // diagnostics: use the generic conv kernel
         return e && e[0] == '1';

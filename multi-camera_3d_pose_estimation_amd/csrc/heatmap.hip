@@ -197,7 +197,8 @@ struct MomParams {
 };
 
 constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
-constexpr int kMomCols = 8;            // image columns per lane (separable path)
+constexpr int kMomBlock = 320;         // 5 waves x 4 columns per lane = 1280: every lane busy on 1280-wide frames
+constexpr int kMomCols = 4;            // image columns per lane (separable path)
 
 // One workgroup per (crop, joint) map.  The fixed-point warp of an image pixel
 // (OpenCV WarpAffineInvoker) is X = (X0(y) + adelta(x)) >> 5, Y = (Y0(y) + bdelta(x)) >> 5.
@@ -208,14 +209,13 @@ constexpr int kMomCols = 8;            // image columns per lane (separable path
 // x-moments are applied per column at the end.  Rows / columns whose taps are
 // all below thr·(1-1e-6) contribute exact zeros and are skipped (bounding box
 // of active heatmap cells).
-__global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
+__global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     extern __shared__ __attribute__((aligned(16))) float mom_lds[];
     float* shm = mom_lds;
     int* sad = reinterpret_cast<int*>(mom_lds + ((p.h * p.w + 3) & ~3));
     int* sbd = sad + p.img_w;
     int* riy = sbd + p.img_w;  // separable path: per image row source row / weight index
-    int* rfq = riy + p.img_h;
-    __shared__ double red[6][kBlock / 64];
+    __shared__ double red[6][kMomBlock / 64];
     __shared__ int bbox[4];
     const long map = blockIdx.x;
     const int n = map / p.K;
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
     __syncthreads();
     const float thr_lo = p.thr * (1.f - 1e-6f);
     int c0 = p.w, c1 = -1, r0 = p.h, r1 = -1;
-    for (int i = threadIdx.x; i < p.h * p.w; i += kBlock) {
+    for (int i = threadIdx.x; i < p.h * p.w; i += kMomBlock) {
         const float v = src[i];
         shm[i] = v;
         if (!(v < thr_lo)) {  // active (or NaN)
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
             r1 = max(r1, r);
         }
     }
-    for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
+    for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
         sad[x] = (int)rint(M[0] * x * 1024.0);
         sbd[x] = (int)rint(M[3] * x * 1024.0);
     }
@@ -268,10 +268,10 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
     if (c1 >= 0) {
         if (p.separable) {
             // Row table: source row iy and weight index fq of every image row (uniform per row).
-            for (int y = threadIdx.x; y < p.img_h; y += kBlock) {
+            // packed (iy + 4096) << 5 | fq, one word per row (+1 pad entry for the prefetch)
+            for (int y = threadIdx.x; y <= p.img_h; y += kMomBlock) {
                 const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
-                riy[y] = Yq >> 5;
-                rfq[y] = Yq & 31;
+                riy[y] = (((Yq >> 5) + 4096) << 5) | (Yq & 31);
             }
             __syncthreads();
             // Lanes own column pairs (packed f32 math); a run of rows sharing iy keeps its
@@ -282,7 +282,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
             typedef float f2 __attribute__((ext_vector_type(2)));
             constexpr int NP = kMomCols / 2;
             const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
-            for (int xb = threadIdx.x; xb < p.img_w; xb += kBlock * kMomCols) {
+            for (int xb = threadIdx.x; xb < p.img_w; xb += kMomBlock * kMomCols) {
 #pragma clang fp contract(off)
                 int ix[kMomCols];
                 bool on[kMomCols];
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
                 bool any = false;
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
-                    const int x = xb + j * kBlock;
+                    const int x = xb + j * kMomBlock;
                     const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
                     ix[j] = X >> 5;
                     const float f = (float)(X & 31) * (1.f / 32.f);
@@ -323,8 +323,13 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
                         for (int q = 0; q < NP; q++) s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
                     };
                     const f2 thr2 = f2{p.thr, p.thr};
+                    // the next row's table word is read one iteration ahead, so its LDS
+                    // latency hides under this row's arithmetic
+                    int tnext = riy[0];
                     for (int y = 0; y < p.img_h; y++) {
-                        const int iy = riy[y];
+                        const int tw = __builtin_amdgcn_readfirstlane(tnext);
+                        tnext = riy[y + 1];
+                        const int iy = (tw >> 5) - 4096, fq = tw & 31;
                         if (iy + 1 < r0 || iy > r1) continue;  // whole row inactive (uniform)
                         if (iy != cur_iy) {
                             flush();
@@ -340,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
                                 v11[j / 2][j & 1] = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
                             }
                         }
-                        const float fy = (float)rfq[y] * (1.f / 32.f), gy = 1.f - fy;
+                        const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
                         const float yr = (float)(y - y0);
                         const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
 #pragma unroll
@@ -360,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
                 }
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
-                    const double xc = (double)(xb + j * kBlock) - cx;
+                    const double xc = (double)(xb + j * kMomBlock) - cx;
                     t[0] += S[j];
                     t[1] = fma(xc, S[j], t[1]);
                     t[2] += Sy[j];
@@ -374,7 +379,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
                 const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
                 const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
                 const double yc = y - cy;
-                for (int x = threadIdx.x; x < p.img_w; x += kBlock) {
+                for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
                     const int X = (X0 + sad[x]) >> 5;
                     const int Y = (Y0 + sbd[x]) >> 5;
                     const int ix = X >> 5, iy = Y >> 5;
@@ -421,7 +426,7 @@ __global__ __launch_bounds__(kBlock) void moments_kernel(MomParams p) {
 #pragma unroll
     for (int q = 0; q < 6; q++) {
         a[q] = 0;
-        for (int k = 0; k < kBlock / 64; k++) a[q] += red[q][k];
+        for (int k = 0; k < kMomBlock / 64; k++) a[q] += red[q][k];
     }
     double* o = p.out + 6 * map;
     if (a[0] == 0.0) {
@@ -532,7 +537,7 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     p.img_w = img_w;
     p.thr = thr;
     p.separable = separable;
-    hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * K)), dim3(kBlock), lds,
+    hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * K)), dim3(kMomBlock), lds,
                        reinterpret_cast<hipStream_t>(stream), p);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END

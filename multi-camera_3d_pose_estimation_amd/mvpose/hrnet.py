@@ -322,6 +322,25 @@ def basic_block_spec(c: int, h: int, w: int, seed: int = 0, n_blocks: int = 1):
     return g, x, y, sd
 
 
+def projection_spec(cin: int, cout: int, h: int, w: int, k: int = 1, seed: int = 0):
+    """Two k x k convs cin -> cout on one h x w plane: t = conv_a(x) (BN, no ReLU) and
+    y = relu(conv_b(x) + t) (the Bottleneck conv3 + downsample pattern), for kernel
+    tests.  Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    g = GraphSpec()
+    x = g.tensor(h, w, cin)
+    for j in ("a", "b"):
+        sd[f"{j}.weight"] = torch.randn((cout, cin, k, k), generator=gen) * (2.0 / (k * k * cin)) ** 0.5
+        sd[f"{j}bn.weight"] = 1.0 + 0.1 * torch.randn((cout,), generator=gen)
+        sd[f"{j}bn.bias"] = 0.1 * torch.randn((cout,), generator=gen)
+        sd[f"{j}bn.running_mean"] = 0.1 * torch.randn((cout,), generator=gen)
+        sd[f"{j}bn.running_var"] = 1.0 + 0.2 * torch.rand((cout,), generator=gen)
+    t = g.conv(sd, "a", "abn", x, 1, False)
+    y = g.conv(sd, "b", "bbn", x, 1, True, res=t)
+    return g, x, y, sd
+
+
 class ConvGraph:
     """A GraphSpec instantiated on the device (mvp_graph_create): one bf16 NHWC
     input tensor -> one output tensor, batch given per forward call."""
