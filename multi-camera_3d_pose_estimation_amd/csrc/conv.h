@@ -57,6 +57,10 @@ const uint16_t* conv_zero_region();
 //   y = relu(conv3x3(relu(conv3x3(x, w1) + b1), w2) + b2 + x), all bf16 NHWC [N][H][W][32],
 // w1/w2 [32][3][3][32] bf16, b1/b2 [32] f32.  Bit-identical to the two convs run separately.
 bool basic_block_c32_supported(int H, int W);
+// 32x32x16 version of the fused block (tblock.hip) for W = 48, H % 16 == 0; false when
+// not applicable (or MVPOSE_NO_TBLOCK=1).  Not bit-identical to the separate convs.
+bool launch_tblock32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                     uint16_t* y, int N, int H, int W, hipStream_t s);
 void launch_basic_block_c32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                             const float* b2, uint16_t* y, int N, int H, int W, hipStream_t s);
 

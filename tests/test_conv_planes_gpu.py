@@ -13,8 +13,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]
-# (MVPOSE_NO_TCONV, MVPOSE_NO_WSCONV) per kernel family
-MODES = {"generic": ("1", "1"), "wsconv": ("1", "0"), "tconv": ("0", "1")}
+# (MVPOSE_NO_TCONV, MVPOSE_NO_WSCONV, MVPOSE_NO_TBLOCK) per kernel family; the 32-channel
+# plane runs the fused block: basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv")
+MODES = {"generic": ("1", "1", "1"), "wsconv": ("1", "0", "1"), "tconv": ("0", "1", "0")}
 
 
 def _bf(t):
@@ -38,9 +39,10 @@ def _reference(sd, x, n_blocks):
 
 
 def _set_mode(monkeypatch, mode):
-    no_t, no_ws = MODES[mode]
+    no_t, no_ws, no_tb = MODES[mode]
     monkeypatch.setenv("MVPOSE_NO_TCONV", no_t)
     monkeypatch.setenv("MVPOSE_NO_WSCONV", no_ws)
+    monkeypatch.setenv("MVPOSE_NO_TBLOCK", no_tb)
     monkeypatch.setenv("MVPOSE_WSCONV64", "1")
     monkeypatch.setenv("MVPOSE_TCONV128", "1")
 
@@ -76,7 +78,7 @@ def test_basic_block_vs_reference(c, h, w, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["wsconv", "tconv"])
-@pytest.mark.parametrize("c,h,w", [(64, 32, 24), (128, 16, 12), (256, 8, 6)])
+@pytest.mark.parametrize("c,h,w", [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)])
 def test_batch_positions(c, h, w, mode, monkeypatch):
     """A crop's output must not depend on its batch position or the batch size
     (tile scheduling over a persistent grid, multi-crop tiles)."""
