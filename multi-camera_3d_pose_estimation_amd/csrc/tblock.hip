@@ -58,6 +58,38 @@ __host__ __device__ constexpr int row_cout(int r) { return 16 * ((r >> 2) & 1) +
 
 constexpr int kZeroSlots = 4096;
 
+// ds_read_b128 serves a wave in 4 lane groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31}
+// and the same +32); a group is conflict-free when its 16 slots are distinct mod 16.  A
+// 32-pixel fragment that wraps an image row shifts the pixels after the wrap by the pad
+// slot (2-way conflicts: 43 % extra LDS cycles measured on the 64-ch plane), so lanes
+// are mapped to pixels group by group: each lane group reads a row-contiguous 16-pixel
+// run.  Returns the tile pixel (row-major [crop][row][col]) of fragment f, column r32.
+__device__ __forceinline__ int lane_rank(int r32, int& g2) {
+    if (r32 < 4) { g2 = 0; return r32; }
+    if (r32 < 12) { g2 = 1; return r32 - 4; }
+    if (r32 < 16) { g2 = 0; return r32 - 8; }
+    if (r32 < 20) { g2 = 1; return r32 - 8; }
+    if (r32 < 28) { g2 = 0; return r32 - 12; }
+    g2 = 1;
+    return r32 - 16;
+}
+template <int W, int TH, int NB>
+__device__ __forceinline__ int frag_pixel(int f, int r32) {
+    int g2;
+    const int rank = lane_rank(r32, g2), g = 2 * f + g2;
+    if constexpr (W % 16 == 0) {
+        return g * 16 + rank;  // 16-pixel runs never straddle a row
+    } else if constexpr (W == 24 && TH == 16 && NB == 1) {
+        // 16 head runs (row r, x 0..15), then 8 tail pairs (rows k and k+8, x 16..23):
+        // 8 rows of pitch 25 slots = 200 = 8 mod 16, so the two halves use disjoint banks
+        if (g < 16) return g * 24 + rank;
+        const int k = g - 16;
+        return rank < 8 ? k * 24 + 16 + rank : (k + 8) * 24 + 8 + rank;
+    } else {
+        return f * 32 + r32;
+    }
+}
+
 template <int W, int TH_, bool DB_>
 struct TBCfg {
     static constexpr int NW = 8, NTH = NW * 64, TH = TH_;
@@ -153,7 +185,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
     int b1v[G::MF1], m1w[G::MF1], b2v[G::MF2], r2v[G::MF2], e2[G::MF2];
 #pragma unroll
     for (int i = 0; i < G::MF1; i++) {
-        int pp = (wave + 8 * i) * 32 + r32;
+        int pp = frag_pixel<W, TH, 1>(wave + 8 * i, r32);
         if (pp >= (TH + 2) * W) pp = 0;  // unused slot
         const int r = pp / W, x = pp - (pp / W) * W;
         b1v[i] = (h * G::HSI + r * RS + x) * 16;                     // input halo, tap (0,0)
@@ -161,7 +193,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
     }
 #pragma unroll
     for (int i = 0; i < G::MF2; i++) {
-        int pp = (wave + 8 * i) * 32 + r32;
+        int pp = frag_pixel<W, TH, 1>(wave + 8 * i, r32);
         if (pp >= TH * W) pp = 0;
         const int r = pp / W, x = pp - (pp / W) * W;
         b2v[i] = G::MOFF + (h * G::HSM + r * RS + x) * 16;              // intermediate, tap (0,0)
@@ -248,7 +280,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
 #pragma unroll
             for (int i = 0; i < G::MF1; i++) {
                 if (i < nf1) {
-                    const int pp = (wave + 8 * i) * 32 + r32;
+                    const int pp = frag_pixel<W, TH, 1>(wave + 8 * i, r32);
                     const int iy = ho0 - 1 + pp / W;
                     const bool live = (unsigned)iy < (unsigned)H;
                     uint32_t o[8];

@@ -67,6 +67,38 @@ __host__ __device__ constexpr int row_cout(int r) { return 16 * ((r >> 2) & 1) +
 
 constexpr int kZeroSlots = 4096;  // 16-B slots of the shared zero region
 
+// ds_read_b128 serves a wave in 4 lane groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31}
+// and the same +32); a group is conflict-free when its 16 slots are distinct mod 16.  A
+// 32-pixel fragment that wraps an image row shifts the pixels after the wrap by the pad
+// slot (2-way conflicts: 43 % extra LDS cycles measured on the 64-ch plane), so lanes
+// are mapped to pixels group by group: each lane group reads a row-contiguous 16-pixel
+// run.  Returns the tile pixel (row-major [crop][row][col]) of fragment f, column r32.
+__device__ __forceinline__ int lane_rank(int r32, int& g2) {
+    if (r32 < 4) { g2 = 0; return r32; }
+    if (r32 < 12) { g2 = 1; return r32 - 4; }
+    if (r32 < 16) { g2 = 0; return r32 - 8; }
+    if (r32 < 20) { g2 = 1; return r32 - 8; }
+    if (r32 < 28) { g2 = 0; return r32 - 12; }
+    g2 = 1;
+    return r32 - 16;
+}
+template <int W, int TH, int NB>
+__device__ __forceinline__ int frag_pixel(int f, int r32) {
+    int g2;
+    const int rank = lane_rank(r32, g2), g = 2 * f + g2;
+    if constexpr (W % 16 == 0) {
+        return g * 16 + rank;  // 16-pixel runs never straddle a row
+    } else if constexpr (W == 24 && TH == 16 && NB == 1) {
+        // 16 head runs (row r, x 0..15), then 8 tail pairs (rows k and k+8, x 16..23):
+        // 8 rows of pitch 25 slots = 200 = 8 mod 16, so the two halves use disjoint banks
+        if (g < 16) return g * 24 + rank;
+        const int k = g - 16;
+        return rank < 8 ? k * 24 + 16 + rank : (k + 8) * 24 + 8 + rank;
+    } else {
+        return f * 32 + r32;
+    }
+}
+
 template <int CIN, int H, int W, int TH, int NB, bool WRES>
 struct TCfg {
     static constexpr int NW = 8, NT_THREADS = NW * 64;
@@ -177,7 +209,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     int bv[G::NT], eoff[G::NT], enb[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; t++) {
-        const int pp = (pg * G::NT + t) * 32 + r32;
+        const int pp = frag_pixel<W, TH, NB>(pg * G::NT + t, r32);
         const int nb = pp / (TH * W), rem = pp - nb * (TH * W);
         const int ty = rem / W, x = rem - (rem / W) * W;
         bv[t] = (h * G::HS + nb * G::HR * G::RS + ty * G::RS + x) * 16;

@@ -5,7 +5,7 @@ N=${1:-pc}; ROOT=$(pwd); OUT=$ROOT/gpurun_out/$N
 mkdir -p "$OUT"; export TMPDIR=/tmp; cd /tmp || exit 1
 P1="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_MFMA SQ_WAVES"
 P2="SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE"
-for cfg in "64 32 24 1" "64 32 24 0" "32 64 48 0" "128 16 12 1"; do
+for cfg in ${CFGS:-"64 32 24 1" "32 64 48 1"}; do
   tag=$(echo $cfg | tr ' ' '_')
   i=0; mkdir -p "$OUT/$tag"
   for P in "$P1" "$P2" "FETCH_SIZE" "WRITE_SIZE"; do
