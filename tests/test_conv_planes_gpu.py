@@ -13,9 +13,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]
-# (MVPOSE_NO_TCONV, MVPOSE_NO_WSCONV, MVPOSE_NO_TBLOCK) per kernel family; the 32-channel
-# plane runs the fused block: basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv")
-MODES = {"generic": ("1", "1", "1"), "wsconv": ("1", "0", "1"), "tconv": ("0", "1", "0")}
+# environment per kernel family: the 32-channel plane runs the fused block,
+# basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv")
+_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_WSCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
+MODES = {
+    "generic": dict(_OFF),
+    "wsconv": dict(_OFF, MVPOSE_NO_WSCONV="0"),
+    "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0"),
+}
 
 
 def _bf(t):
@@ -39,10 +44,8 @@ def _reference(sd, x, n_blocks):
 
 
 def _set_mode(monkeypatch, mode):
-    no_t, no_ws, no_tb = MODES[mode]
-    monkeypatch.setenv("MVPOSE_NO_TCONV", no_t)
-    monkeypatch.setenv("MVPOSE_NO_WSCONV", no_ws)
-    monkeypatch.setenv("MVPOSE_NO_TBLOCK", no_tb)
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     monkeypatch.setenv("MVPOSE_WSCONV64", "1")
     monkeypatch.setenv("MVPOSE_TCONV128", "1")
 

@@ -13,13 +13,14 @@ from mvpose import hrnet  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-MODES = {"generic": ("1", "1", "1"), "wsconv": ("1", "0", "1"), "tconv": ("0", "1", "0")}
+_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_WSCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
+MODES = {"generic": dict(_OFF), "wsconv": dict(_OFF, MVPOSE_NO_WSCONV="0"),
+         "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0")}
 os.environ["MVPOSE_WSCONV64"] = "1"
 os.environ["MVPOSE_TCONV128"] = "1"
 for c, h, w in [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]:
-    for mode, (no_t, no_ws, no_tb) in MODES.items():
-        os.environ["MVPOSE_NO_TCONV"], os.environ["MVPOSE_NO_WSCONV"] = no_t, no_ws
-        os.environ["MVPOSE_NO_TBLOCK"] = no_tb
+    for mode, env in MODES.items():
+        os.environ.update(env)
         spec, xi, yo, _ = hrnet.basic_block_spec(c, h, w, seed=1)
         g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
         x = torch.randn((n, h, w, c), device="cuda").bfloat16()
