@@ -47,10 +47,10 @@ using namespace mfma_tile;
 constexpr int kZeroSlots = 4096;  // 16-B slots of the shared zero region
 
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM_ = 64>
 struct TCfg {
     static constexpr int NW = 8, NT_THREADS = NW * 64;
-    static constexpr int BM = 64, MG = BM / 32, PG = NW / MG;   // cout groups x pixel groups
+    static constexpr int BM = BM_, MG = BM / 32, PG = NW / MG;  // cout groups x pixel groups
     static constexpr int NT = 3;                                 // 32-pixel fragments per wave
     static constexpr int P = NB * TH * W;                        // output pixels per tile
     static constexpr int NCH = CIN / 32;                         // items per tile
@@ -80,13 +80,13 @@ struct TParams {
     uint16_t* y;
     const uint16_t* zero;
     uint16_t* sink;
-    int N, Cout, n_tiles, ncb;  // ncb = Cout / 64 column blocks (1 when weights are resident)
+    int N, Cout, n_tiles, ncb;  // ncb = Cout / BM column blocks (1 when weights are resident)
     int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 1 = no DMA, 2 = no stores, 3 = both
 };
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
 __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
-    using G = TCfg<CIN, H, W, TH, NB, WRES>;
+    using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -287,10 +287,10 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
 int g_t_cus = 0;
 uint16_t* g_t_sink = nullptr;
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
 void launch_t_kernel(const TParams& p, hipStream_t s) {
-    using G = TCfg<CIN, H, W, TH, NB, WRES>;
-    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES>;
+    using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
+    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -300,7 +300,7 @@ void launch_t_kernel(const TParams& p, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
 }
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM = 64>
 void launch_t(const ConvLaunch& c, hipStream_t s) {
     if (g_t_cus == 0) {
         int dev = 0;
@@ -308,24 +308,31 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
         MVP_HIP(hipDeviceGetAttribute(&g_t_cus, hipDeviceAttributeMultiprocessorCount, dev));
         MVP_HIP(hipMalloc(&g_t_sink, 64 * 32));
     }
-    MVP_REQUIRE(!WRES || c.Cout == 64, "tconv: resident weights need Cout == 64");
-    const long tiles = (long)((c.N + NB - 1) / NB) * (H / TH) * (c.Cout / 64);
+    MVP_REQUIRE(!WRES || c.Cout == BM, "tconv: resident weights need Cout == BM");
+    MVP_REQUIRE(c.Cout % BM == 0, "tconv: Cout %d not a multiple of %d", c.Cout, BM);
+    const long tiles = (long)((c.N + NB - 1) / NB) * (H / TH) * (c.Cout / BM);
     MVP_REQUIRE(tiles < (1L << 30), "tconv: too many tiles");
     const char* dg = getenv("MVPOSE_TCONV_DIAG");
-    TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / 64,
+    TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM,
               dg ? atoi(dg) : 0};
     if (c.res)
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, true>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM>(p, s);
     else
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, false>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM>(p, s);
 }
 
 }  // namespace
 
 bool launch_tconv(const ConvLaunch& c, hipStream_t s) {
-    if (c.ks != 3 || c.stride != 1 || c.out_f32_nchw || !c.relu || c.Cout % 64 != 0) return false;
+    if (c.ks != 3 || c.stride != 1 || c.out_f32_nchw || !c.relu || c.Cout % 32 != 0) return false;
     const char* e = getenv("MVPOSE_NO_TCONV");  // diagnostics/tests: fall back to the other kernels
     if (e && e[0] == '1') return false;
+    // transition1.0: 256 -> 32 @ 64x48, 32-cout tiles of 768 pixels (8 pixel groups), streamed weights
+    if (c.Cin == 256 && c.Cout == 32 && c.H == 64 && c.W == 48) {
+        launch_t<256, 64, 48, 16, 1, false, 32>(c, s);
+        return true;
+    }
+    if (c.Cout % 64 != 0) return false;
     if (c.Cin == 64 && c.Cout == 64 && c.H == 32 && c.W == 24) {
         launch_t<64, 32, 24, 16, 1, true>(c, s);
         return true;

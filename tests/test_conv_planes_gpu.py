@@ -102,14 +102,16 @@ def test_batch_positions(c, h, w, mode, monkeypatch):
     assert torch.equal(full[411:414], part)
 
 
-@pytest.mark.parametrize("cin,cout,h,w", [(64, 256, 64, 48), (256, 64, 64, 48), (64, 64, 64, 48), (64, 32, 32, 24),
-                                          (128, 64, 16, 12), (256, 128, 8, 6)])
-def test_projection_1x1_vs_reference(cin, cout, h, w):
-    """1x1 convs (conv1x1.hip, permuted-cout epilogue): y = relu(conv_b(x) + conv_a(x))."""
+@pytest.mark.parametrize("cin,cout,h,w,k", [(64, 256, 64, 48, 1), (256, 64, 64, 48, 1), (64, 64, 64, 48, 1),
+                                            (64, 32, 32, 24, 1), (128, 64, 16, 12, 1), (256, 128, 8, 6, 1),
+                                            (256, 32, 64, 48, 3)])
+def test_projection_vs_reference(cin, cout, h, w, k):
+    """y = relu(conv_b(x) + conv_a(x)): 1x1 convs (conv1x1.hip, permuted-cout epilogue) and
+    transition1's 256->32 3x3 (tconv.hip with 32-cout tiles for conv_b)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet
-    spec, xi, yo, sd = hrnet.projection_spec(cin, cout, h, w, seed=4)
+    spec, xi, yo, sd = hrnet.projection_spec(cin, cout, h, w, k=k, seed=4)
     n = 23
     g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
     gen = torch.Generator().manual_seed(8)
@@ -123,11 +125,11 @@ def test_projection_1x1_vs_reference(cin, cout, h, w):
     for j in ("a", "b"):
         wt, b = hrnet.fold_bn(sd, j, f"{j}bn")
         wt = _bf(torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 3, 1, 2))).float())
-        zs.append(torch.nn.functional.conv2d(xf, wt) + torch.from_numpy(b).float()[None, :, None, None])
+        zs.append(torch.nn.functional.conv2d(xf, wt, padding=k // 2) + torch.from_numpy(b).float()[None, :, None, None])
     t = _bf(zs[0])
     ref = _bf(torch.relu(zs[1] + t)).permute(0, 2, 3, 1)
     got = out.float().cpu()
     rel = (torch.linalg.vector_norm(got - ref) / torch.linalg.vector_norm(ref)).item()
     mx = (got - ref).abs().max().item()
-    print(f"1x1 {cin}->{cout} {h}x{w}: rel L2 {rel:.2e}, max abs {mx:.3e}")
+    print(f"{k}x{k} {cin}->{cout} {h}x{w}: rel L2 {rel:.2e}, max abs {mx:.3e}")
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
