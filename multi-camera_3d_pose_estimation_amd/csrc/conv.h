@@ -20,6 +20,10 @@ struct ConvLaunch {
     float* yf;            // f32 NCHW (when out_f32_nchw)
     int N, H, W, Cin, Cout;
     int ks, stride, relu, out_f32_nchw;
+    // 1x1 only: second input (graph cat-fusion) — channels [c1, Cin) of the conv come
+    // from x2 [N][H][W][Cin - c1], the first c1 from x
+    const uint16_t* x2 = nullptr;
+    int c1 = 0;
 };
 
 void launch_conv(const ConvLaunch& c, hipStream_t s);

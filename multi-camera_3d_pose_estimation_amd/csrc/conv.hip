@@ -778,6 +778,11 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
     if (c.N == 0) return;
+    if (c.x2) {  // graph cat-fusion: only the direct 1x1 kernel reads two inputs
+        MVP_REQUIRE(c.ks == 1 && launch_conv1x1_direct(c, s), "conv: dual-input conv needs the 1x1 kernel");
+        MVP_HIP(hipGetLastError());
+        return;
+    }
     if (launch_conv1x1_direct(c, s) || launch_tconv(c, s) || launch_wsconv(c, s)) {
         MVP_HIP(hipGetLastError());
         return;

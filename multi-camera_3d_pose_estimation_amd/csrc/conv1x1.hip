@@ -44,6 +44,10 @@ struct P1x1 {
     const uint16_t* zero;
     long n_pix;
     int Cout, relu;
+    // dual input (graph cat-fusion): K chunks [0, kch1) read x (c1 channels per pixel),
+    // the rest x2 (c2 channels); single input: x2 = nullptr, c1 = Cin, kch1 = Cin / 32
+    const uint16_t* x2;
+    int c1, c2, kch1;
 };
 
 constexpr int kPTW = 2;  // 16-pixel tiles per wave per unit
@@ -82,9 +86,11 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
             const long pp = u * 16 * kPTW + i * 16 + (lane & 15);
             valid[i] = pp < p.n_pix;
             pix[i] = valid[i] ? pp : p.n_pix - 1;
-            const uint16_t* src = p.x + pix[i] * CIN + g * 8;
+            const uint16_t* src = p.x + pix[i] * p.c1 + g * 8;
+            const uint16_t* src2 = p.x2 ? p.x2 + pix[i] * p.c2 + g * 8 - p.kch1 * 32 : src;
 #pragma unroll
-            for (int ch = 0; ch < KCH; ch++) b[i][ch] = *reinterpret_cast<const bf16x8*>(src + ch * 32);
+            for (int ch = 0; ch < KCH; ch++)
+                b[i][ch] = *reinterpret_cast<const bf16x8*>((ch < p.kch1 ? src : src2) + ch * 32);
         }
         // residual: the lane's BM/4 consecutive couts, 16 B per load
         constexpr int RQ = BM / 32;  // uint4 per lane per pixel tile
@@ -187,10 +193,18 @@ bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
         const char* e = getenv("MVPOSE_NO_1X1");  // diagnostics: use the generic conv kernel
         return e && e[0] == '1';
     }();
-    if (disabled) return false;
+    if (disabled && !c.x2) return false;
     const int cout_pad = conv_cout_pad(c.Cout);
     const int kch = c.Cin / 32;
-    P1x1 p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), (long)c.N * c.H * c.W, c.Cout, c.relu};
+    P1x1 p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), (long)c.N * c.H * c.W, c.Cout, c.relu,
+           nullptr, c.Cin, 0, c.Cin / 32};
+    if (c.x2) {  // dual input: c.Cin = c1 + c2
+        MVP_REQUIRE(c.c1 % 32 == 0 && c.c1 > 0 && c.c1 < c.Cin, "conv1x1: dual input split %d of %d", c.c1, c.Cin);
+        p.x2 = c.x2;
+        p.c1 = c.c1;
+        p.c2 = c.Cin - c.c1;
+        p.kch1 = c.c1 / 32;
+    }
     if (p.n_pix == 0) return true;
     if (cout_pad % 128 == 0 && kch <= 2) {  // 128 couts: registers allow K <= 64
         if (kch == 1) launch_1x1<128, 1>(p, cout_pad, s);

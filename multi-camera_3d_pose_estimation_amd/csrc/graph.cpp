@@ -24,8 +24,11 @@ struct Graph {
     const uint16_t* wb = nullptr;
     const float* fb = nullptr;
     int max_batch = 0;
-    std::vector<int> absorbed;    // op folded into the next op (fused BasicBlock), not run on its own
+    std::vector<int> absorbed;    // op folded into another op (fused BasicBlock / cat-fusion), not run on its own
     std::vector<int> block_head;  // op runs the fused BasicBlock of (op - 1, op)
+    std::vector<int> cat_src;     // 1x1 op that also computes the absorbed 1x1 op cat_src[k] (-1: none)
+    std::vector<uint16_t*> cat_w; // its concatenated weights [cout_pad][cin_k + cin_src] (owned)
+    std::vector<float*> cat_b;    // and summed biases [cout_pad] (owned)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -141,6 +144,74 @@ void fuse(Graph& g, bool enable) {
     }
 }
 
+// Cat-fusion pass: y = act(conv1x1_B(h) + bias_B + t) whose residual t = conv1x1_A(x) + bias_A
+// (no activation, consumed only here: the Bottleneck downsample) becomes ONE 1x1 conv over
+// the channel concatenation [h, x] with weights [W_B | W_A] and bias bias_B + bias_A.  The
+// t tensor (256 channels at 64x48 in HRNet-W32: 1.6 GB per 1024 crops, written then read
+// back as the residual) disappears, and t is no longer rounded to bf16 before the add.
+void cat_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.cat_src.assign(no, -1);
+    g.cat_w.assign(no, nullptr);
+    g.cat_b.assign(no, nullptr);
+    if (!enable) return;
+    std::vector<int> uses(nt, 0), producer(nt, -1);
+    for (int k = 0; k < no; k++) {
+        const mvp_op_desc& op = g.ops[k];
+        producer[op.out] = k;
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0 && !(g.block_head[k] && i == 0)) uses[op.in[i]]++;
+    }
+    auto plain_1x1 = [&](const mvp_op_desc& op) {
+        return op.kind == MVP_OP_CONV && op.ks == 1 && op.stride == 1 && op.cin % 32 == 0 &&
+               g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    for (int b = 0; b < no; b++) {
+        const mvp_op_desc& B = g.ops[b];
+        if (g.absorbed[b] || g.block_head[b] || !plain_1x1(B) || B.n_in < 2 || B.in[1] < 0) continue;
+        const int t = B.in[1], a = producer[t];
+        if (a < 0 || a >= b || g.absorbed[a] || g.block_head[a] || g.cat_src[a] >= 0) continue;
+        const mvp_op_desc& A = g.ops[a];
+        if (!plain_1x1(A) || (A.n_in > 1 && A.in[1] >= 0) || A.relu || A.cout != B.cout) continue;
+        if (uses[t] != 1 || t == g.output || A.segment != B.segment) continue;
+        const int kch = (A.cin + B.cin) / 32;  // conv1x1_kernel instantiations: K = 32, 64, 128, 256
+        if (kch != 2 && kch != 4 && kch != 8) continue;
+        g.absorbed[a] = 1;
+        g.cat_src[b] = a;
+    }
+}
+
+// Device-side concatenated weights / summed biases of the cat-fused ops (graph create time).
+void cat_build(Graph& g) {
+    for (int b = 0; b < (int)g.ops.size(); b++) {
+        const int a = g.cat_src[b];
+        if (a < 0) continue;
+        const mvp_op_desc& B = g.ops[b];
+        const mvp_op_desc& A = g.ops[a];
+        const int cp = conv_cout_pad(B.cout), cin = B.cin + A.cin;
+        MVP_HIP(hipMalloc(&g.cat_w[b], (size_t)cp * cin * sizeof(uint16_t)));
+        MVP_HIP(hipMalloc(&g.cat_b[b], (size_t)cp * sizeof(float)));
+        MVP_HIP(hipMemcpy2D(g.cat_w[b], (size_t)cin * 2, g.wb + B.w_off, (size_t)B.cin * 2, (size_t)B.cin * 2, cp,
+                            hipMemcpyDeviceToDevice));
+        MVP_HIP(hipMemcpy2D(g.cat_w[b] + B.cin, (size_t)cin * 2, g.wb + A.w_off, (size_t)A.cin * 2,
+                            (size_t)A.cin * 2, cp, hipMemcpyDeviceToDevice));
+        std::vector<float> hb(cp), ha(cp);
+        MVP_HIP(hipMemcpy(hb.data(), g.fb + B.b_off, cp * sizeof(float), hipMemcpyDeviceToHost));
+        MVP_HIP(hipMemcpy(ha.data(), g.fb + A.b_off, cp * sizeof(float), hipMemcpyDeviceToHost));
+        for (int i = 0; i < cp; i++) hb[i] += ha[i];
+        MVP_HIP(hipMemcpy(g.cat_b[b], hb.data(), cp * sizeof(float), hipMemcpyHostToDevice));
+    }
+}
+
+void cat_free(Graph& g) {
+    for (uint16_t* p : g.cat_w)
+        if (p) (void)hipFree(p);
+    for (float* p : g.cat_b)
+        if (p) (void)hipFree(p);
+    g.cat_w.clear();
+    g.cat_b.clear();
+}
+
 // Greedy first-fit placement of tensors in one arena by lifetime [def, last use].
 // A tensor produced and consumed only inside one micro-batched segment is
 // "local": it is sized for one micro-batch and re-used by every micro-batch.
@@ -167,8 +238,14 @@ void plan(Graph& g) {
         touch(op.out);
         for (int i = 0; i < op.n_in; i++) {
             if (op.in[i] < 0 || (g.block_head[k] && i == 0)) continue;  // fused: conv1's output is LDS-only
+            if (g.cat_src[k] >= 0 && i == 1) continue;                  // cat-fused: never materialised
             last[op.in[i]] = std::max(last[op.in[i]], k);
             touch(op.in[i]);
+        }
+        if (g.cat_src[k] >= 0) {  // the absorbed op's input is read here
+            const int x = g.ops[g.cat_src[k]].in[0];
+            last[x] = std::max(last[x], k);
+            touch(x);
         }
     }
     g.local_seg.assign(nt, -1);
@@ -189,7 +266,8 @@ void plan(Graph& g) {
         };
         widen(op.out);
         for (int i = 0; i < op.n_in; i++)
-            if (!(g.block_head[k] && i == 0)) widen(op.in[i]);
+            if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1)) widen(op.in[i]);
+        if (g.cat_src[k] >= 0) widen(g.ops[g.cat_src[k]].in[0]);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
@@ -259,6 +337,9 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::validate(*g, w_elems, f_elems);
         const char* nf = getenv("MVPOSE_NO_FUSE");  // diagnostics: run every conv on its own
         mvp::fuse(*g, !(nf && nf[0] == '1'));
+        const char* nc = getenv("MVPOSE_NO_CATFUSE");  // diagnostics: keep the downsample conv separate
+        mvp::cat_fuse(*g, !(nc && nc[0] == '1') && !(nf && nf[0] == '1'));
+        mvp::cat_build(*g);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
             hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
@@ -267,6 +348,7 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
                           hipGetErrorString(e));
         }
     } catch (...) {
+        mvp::cat_free(*g);
         delete g;
         throw;
     }
@@ -324,6 +406,15 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             c.ks = op.ks;
             c.stride = op.stride;
             c.relu = op.relu;
+            if (g->cat_src[k] >= 0) {  // cat-fused: [in[0], absorbed op's input] x [W | W_absorbed]
+                const mvp_op_desc& a = g->ops[g->cat_src[k]];
+                c.x2 = (const uint16_t*)ptr(a.in[0]);
+                c.c1 = op.cin;
+                c.Cin = op.cin + a.cin;
+                c.w = g->cat_w[k];
+                c.bias = g->cat_b[k];
+                c.res = nullptr;
+            }
             mvp::launch_conv(c, s);
         } else {
             const uint16_t* ins[4];
@@ -356,6 +447,7 @@ extern "C" int mvp_graph_destroy(void* handle) {
     Graph* g = static_cast<Graph*>(handle);
     if (g) {
         if (g->arena) (void)hipFree(g->arena);
+        mvp::cat_free(*g);
         delete g;
     }
     MVP_ABI_END

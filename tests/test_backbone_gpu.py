@@ -84,7 +84,10 @@ def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
     two separate convs bit for bit, and it must free the intermediate tensors."""
     from mvpose import hrnet
     sd = hrnet.random_state_dict(11)
-    monkeypatch.setenv("MVPOSE_NO_TBLOCK", "1")  # tblock (32x32x16) is checked by tolerance: test_conv_planes_gpu
+    # tblock (32x32x16) and the downsample cat-fusion change rounding; they are checked by
+    # tolerance in test_conv_planes_gpu.py
+    monkeypatch.setenv("MVPOSE_NO_TBLOCK", "1")
+    monkeypatch.setenv("MVPOSE_NO_CATFUSE", "1")
     monkeypatch.setenv("MVPOSE_NO_FUSE", "1")
     unfused = hrnet.HRNetBackbone(sd, max_batch=6)
     monkeypatch.delenv("MVPOSE_NO_FUSE")
@@ -98,3 +101,23 @@ def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
     torch.cuda.synchronize()
     assert torch.equal(a, b)
     assert fused.arena_bytes <= unfused.arena_bytes
+
+
+def test_cat_fusion_matches_unfused(models, monkeypatch):
+    """The layer1 downsample 1x1 is folded into conv3 (graph cat-fusion, no bf16 rounding of
+    the downsample output): heatmaps stay within bf16 rounding of the unfused graph."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(13)
+    monkeypatch.setenv("MVPOSE_NO_CATFUSE", "1")
+    plain = hrnet.HRNetBackbone(sd, max_batch=4)
+    monkeypatch.delenv("MVPOSE_NO_CATFUSE")
+    fused = hrnet.HRNetBackbone(sd, max_batch=4)
+    g = torch.Generator().manual_seed(6)
+    x = torch.zeros((4, 256, 192, 4))
+    x[..., :3] = torch.randn((4, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = fused.forward(xb)
+    torch.cuda.synchronize()
+    rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    assert rel < 1e-2, rel
