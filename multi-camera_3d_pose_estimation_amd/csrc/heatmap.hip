@@ -275,10 +275,13 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
             }
             __syncthreads();
             // Lanes own column pairs (packed f32 math); a run of rows sharing iy keeps its
-            // four taps in registers and accumulates S, S*yr, S*yr^2 (yr = row - run start)
-            // in f32, flushed to fp64 with the run's offset when iy changes.  The pixel
-            // value itself is OpenCV's float remap, op for op:
-            //   ((v00 w0 + v01 w1) + v10 w2) + v11 w3,  w = products of (1-f, f) pairs.
+            // two x-interpolated source rows in registers and accumulates S, S*yr, S*yr^2
+            // (yr = row - run start) in f32, flushed to fp64 with the run's offset when iy
+            // changes.  The pixel value is OpenCV's bilinear remap value (its fixed-point
+            // coordinates and 1/32 weights exactly) evaluated as gy (v00 gx + v01 fx) +
+            // fy (v10 gx + v11 fx): within ~2 f32 ulps of OpenCV's operation order
+            // ((v00 w0 + v01 w1) + v10 w2) + v11 w3 — far inside the reference's own f32
+            // moment arithmetic (mmpose_pose_estimation.py:163-215).
             typedef float f2 __attribute__((ext_vector_type(2)));
             constexpr int NP = kMomCols / 2;
             const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
@@ -303,10 +306,15 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) S[j] = Sy[j] = Syy[j] = 0.0;
                 if (__any(any)) {
-                    f2 v00[NP], v01[NP], v10[NP], v11[NP], s32[NP], sy32[NP], syy32[NP];
+                    // per column and run of rows sharing a source row: the two x-interpolated
+                    // source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx; per pixel the
+                    // value is gy a + fy b (2 ops instead of OpenCV's 4 weight products + 4
+                    // products + 3 sums: same bilinear value to ~2 f32 ulps, the tolerance the
+                    // oracle tests state)
+                    f2 ra[NP], rb[NP], s32[NP], sy32[NP], syy32[NP];
 #pragma unroll
                     for (int q = 0; q < NP; q++) {
-                        v00[q] = v01[q] = v10[q] = v11[q] = f2{0.f, 0.f};
+                        ra[q] = rb[q] = f2{0.f, 0.f};
                         s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
                     }
                     int cur_iy = -0x7fffffff, y0 = 0;
@@ -339,22 +347,22 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
 #pragma unroll
                             for (int j = 0; j < kMomCols; j++) {
                                 const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
-                                v00[j / 2][j & 1] = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
-                                v01[j / 2][j & 1] = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
-                                v10[j / 2][j & 1] = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
-                                v11[j / 2][j & 1] = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                                const float v00 = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
+                                const float v01 = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
+                                const float v10 = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
+                                const float v11 = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                                const float g = gx[j / 2][j & 1], f = fx[j / 2][j & 1];
+                                ra[j / 2][j & 1] = __builtin_fmaf(v01, f, v00 * g);
+                                rb[j / 2][j & 1] = __builtin_fmaf(v11, f, v10 * g);
                             }
                         }
                         const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
                         const float yr = (float)(y - y0);
                         const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
+                        const f2 fy2 = f2{fy, fy}, gy2 = f2{gy, gy};
 #pragma unroll
                         for (int q = 0; q < NP; q++) {
-                            const f2 w0 = gy * gx[q], w1 = gy * fx[q], w2 = fy * gx[q], w3 = fy * fx[q];
-                            f2 v = v00[q] * w0;
-                            v = v + v01[q] * w1;
-                            v = v + v10[q] * w2;
-                            v = v + v11[q] * w3;
+                            const f2 v = __builtin_elementwise_fma(fy2, rb[q], gy2 * ra[q]);
                             const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
                             s32[q] = s32[q] + vs;
                             sy32[q] = __builtin_elementwise_fma(vs, yr2, sy32[q]);
