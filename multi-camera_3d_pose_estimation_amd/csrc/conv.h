@@ -41,6 +41,11 @@ bool launch_wsconv(const ConvLaunch& c, hipStream_t s);
 // when the conv is not one of those (or MVPOSE_NO_TCONV=1).
 bool launch_tconv(const ConvLaunch& c, hipStream_t s);
 
+// 3x3/s2 conv on a polyphase halo, 16-channel items (s2conv.hip): transitions 2/3
+// and the downsampling fuse-layer convs of HRNet-W32 with >= 64 couts (no residual).
+// false when the conv is not one of those planes (or MVPOSE_NO_S2CONV=1).
+bool launch_s2conv(const ConvLaunch& c, hipStream_t s);
+
 // 3x3/s2 stem conv on 4-channel (RGB + zero) bf16 crops, BN folded, ReLU.
 // w: [64][3][3][4] f32, bias [64] f32.  x [N][H][W][4] -> y [N][H/2][W/2][64].
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,

@@ -783,7 +783,7 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
         MVP_HIP(hipGetLastError());
         return;
     }
-    if (launch_conv1x1_direct(c, s) || launch_tconv(c, s) || launch_wsconv(c, s)) {
+    if (launch_conv1x1_direct(c, s) || launch_tconv(c, s) || launch_wsconv(c, s) || launch_s2conv(c, s)) {
         MVP_HIP(hipGetLastError());
         return;
     }

@@ -341,6 +341,21 @@ def projection_spec(cin: int, cout: int, h: int, w: int, k: int = 1, seed: int =
     return g, x, y, sd
 
 
+def conv_spec(cin: int, cout: int, h: int, w: int, k: int = 3, stride: int = 1, relu: bool = True, seed: int = 0):
+    """One k x k conv (+ folded BN, optional ReLU) cin -> cout on an h x w plane, for
+    kernel tests and per-conv benchmarks.  Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {"c.weight": torch.randn((cout, cin, k, k), generator=gen) * (2.0 / (k * k * cin)) ** 0.5,
+          "bn.weight": 1.0 + 0.1 * torch.randn((cout,), generator=gen),
+          "bn.bias": 0.1 * torch.randn((cout,), generator=gen),
+          "bn.running_mean": 0.1 * torch.randn((cout,), generator=gen),
+          "bn.running_var": 1.0 + 0.2 * torch.rand((cout,), generator=gen)}
+    g = GraphSpec()
+    x = g.tensor(h, w, cin)
+    y = g.conv(sd, "c", "bn", x, stride, relu)
+    return g, x, y, sd
+
+
 class ConvGraph:
     """A GraphSpec instantiated on the device (mvp_graph_create): one bf16 NHWC
     input tensor -> one output tensor, batch given per forward call."""
