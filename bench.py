@@ -97,6 +97,20 @@ def cpu_baseline(n_frames, views, seed=0):
                       f"+ OpenCV-4.9-semantics triangulation in C)"}
 
 
+def tri_valu_issue(tri_ms):
+    """The triangulation kernel's real bound: FP64 VALU issue (OpenCV-order fp64
+    undistortion + QR).  From the committed PMC pass (profiles/r01_tri_pmc.json):
+    VALU instructions per launch x 4 cycles (wave64 on a 16-lane SIMD) over 1024
+    SIMDs at 2.4 GHz = the issue floor; frac = floor / measured launch time."""
+    path = os.path.join(ROOT, "profiles", "r01_tri_pmc.json")
+    if not os.path.exists(path):
+        return None
+    pmc = json.load(open(path))
+    floor = pmc["valu_issue_floor_ms"]
+    return {"valu_instr_per_launch": pmc["valu_instr_per_launch"], "issue_floor_ms": floor,
+            "frac": floor / tri_ms, "source": "profiles/r01_tri_pmc.json"}
+
+
 def main():
     args = parse()
     world, rank, dev = setup_dist(args)
@@ -157,13 +171,14 @@ def main():
     tri_out = torch.empty((TRI_T, 17, 3), dtype=torch.float32, device=dev)
     for _ in range(2):
         ops.triangulate(kst, pipe.cams, [0, 1], out=tri_out)
+    tri_reps = 200  # ~13 ms: shorter windows swing +-15 % with the clock state
     e[2].record(s)
-    for _ in range(reps):
+    for _ in range(tri_reps):
         ops.triangulate(kst, pipe.cams, [0, 1], out=tri_out)
     e[3].record(s)
     torch.cuda.synchronize()
     bb_ms = e[0].elapsed_time(e[1]) / reps
-    tri_ms = e[2].elapsed_time(e[3]) / reps
+    tri_ms = e[2].elapsed_time(e[3]) / tri_reps
     flops = 2.0 * est.backbone.macs_per_crop() * crops.shape[0]
     bb_tflops = flops / (bb_ms * 1e-3) / 1e12
     tri_bytes = 12.0 * 17 * (V + 1) * TRI_T  # read x,y,conf per view + write xyz per joint
@@ -199,7 +214,8 @@ def main():
                                                  f"(BASELINE config 4 stream)",
                                      "achieved": tri_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": tri_gbs / HBM_PEAK_GBS, "bytes_per_launch": tri_bytes,
-                                     "frames_per_s": TRI_T / (tri_ms * 1e-3), "avg_launch_ms": tri_ms},
+                                     "frames_per_s": TRI_T / (tri_ms * 1e-3), "avg_launch_ms": tri_ms,
+                                     "valu_issue": tri_valu_issue(tri_ms)},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(args.cpu_sample_frames, V)

@@ -70,6 +70,88 @@ __device__ __forceinline__ void undistort_point(float uf, float vf, const double
     oy = (float)(yy * ww);
 }
 
+// 1/b with the arithmetic of the compiler's IEEE fp64 division (v_div_scale,
+// v_rcp_f64, two Newton steps, one quotient correction, v_div_fmas, v_div_fixup)
+// minus the scale / fixup instructions, which are identities for finite, normal
+// b away from the exponent limits: bit-identical there, 7 instructions not 11.
+// Used for every reciprocal of the fast path; every b here is O(1) to O(1e6).
+__device__ __forceinline__ double recip_rn(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(e, r, r);
+}
+
+// sqrt(s) for s > 0 by v_rsq_f64 + two Goldschmidt steps + one residual
+// correction (~1 ulp); the fast solver's norms only.
+__device__ __forceinline__ double sqrt_fast(double s) {
+    const double y = __builtin_amdgcn_rsq(s);
+    double g = s * y, h = 0.5 * y;
+    double r = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    r = __builtin_fma(-g, h, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    const double d = __builtin_fma(-g, g, s);
+    return s > 0 ? __builtin_fma(d, h, g) : 0.0;
+}
+
+// 1/sqrt(s), s > 0, to ~1 ulp: v_rsq_f64 + two Newton steps.
+__device__ __forceinline__ double rsqrt_fast(double s) {
+    double y = __builtin_amdgcn_rsq(s);
+    double t = s * y;
+    double e = __builtin_fma(-t, y, 1.0);
+    y = __builtin_fma(0.5 * y, e, y);
+    t = s * y;
+    e = __builtin_fma(-t, y, 1.0);
+    return __builtin_fma(0.5 * y, e, y);
+}
+
+// Per-camera constants of the fast undistortion, computed once per block with
+// the same IEEE operations the per-point code would do (1./fx, 1./fy).
+struct CamFast {
+    double ifx, ify;
+};
+
+// undistort_point with the loop-invariant reciprocals from CamFast and every
+// division as recip_rn; branch-free, so the two views of a point interleave.
+// Same operation sequence and rounding as undistort_point for finite input.
+__device__ __forceinline__ void undistort_point_fast(float uf, float vf, const double* __restrict__ c,
+                                                     const CamFast& cf, float& ox, float& oy) {
+    const double cx = c[2], cy = c[5];
+    const double k0 = c[9], k1 = c[10], k2 = c[11], k3 = c[12], k4 = c[13];
+    const double u = uf, v = vf;
+    double x = (u - cx) * cf.ifx;
+    double y = (v - cy) * cf.ify;
+    const double x0 = x, y0 = y;
+    bool neg = false;
+#pragma unroll
+    for (int j = 0; j < 5; j++) {
+        double r2 = x * x + y * y;
+        double icdist = recip_rn(1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+        neg = neg || (icdist < 0);
+        double deltaX = 2 * k2 * x * y + k3 * (r2 + 2 * x * x);
+        double deltaY = k2 * (r2 + 2 * y * y) + 2 * k3 * x * y;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    // OpenCV breaks out with the initial guess on icdist < 0: the iterates after
+    // such a step are discarded here instead — selects, not a branch, so both
+    // views' chains stay in one basic block for the scheduler to interleave
+    // (the branch form measured 0.081 vs 0.058 ms per 1.7 M points)
+    x = neg ? x0 : x;
+    y = neg ? y0 : y;
+    double xx = c[0] * x + c[1] * y + c[2];
+    double yy = c[3] * x + c[4] * y + c[5];
+    const double ww = recip_rn(c[6] * x + c[7] * y + c[8]);
+    ox = (float)(xx * ww);
+    oy = (float)(yy * ww);
+}
+
 // JacobiSVDImpl_<double> on At (4 rows of length M); returns Vt row of the
 // smallest singular value after OpenCV's descending selection sort.
 template <int M>
@@ -195,7 +277,7 @@ __device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], d
         double s = 0;
 #pragma unroll
         for (int r = k; r < M; r++) s += A[r][k] * A[r][k];
-        const double nrm = sqrt(s);
+        const double nrm = sqrt_fast(s);
         if (k == 3) {
             R[3][3] = nrm;
             break;
@@ -204,7 +286,7 @@ __device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], d
         const double alpha = akk >= 0 ? -nrm : nrm;
         // reflector v = a - alpha·e_k; vᵀv / 2 = nrm (nrm + |akk|)
         const double half_vtv = nrm * (nrm + fabs(akk));
-        const double inv = half_vtv > 0 ? 1.0 / half_vtv : 0.0;
+        const double inv = half_vtv > 0 ? recip_rn(half_vtv) : 0.0;
         A[k][k] = akk - alpha;
         R[k][k] = alpha;
 #pragma unroll
@@ -224,7 +306,7 @@ __device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], d
     if (fabs(R[3][3]) < 1e-18 * scale) R[3][3] = 1e-18 * scale;
     double d[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) d[k] = 1.0 / R[k][k];
+    for (int k = 0; k < 4; k++) d[k] = recip_rn(R[k][k]);
     auto back = [&](double (&x)[4]) {  // x <- R⁻¹ x
         x[3] = x[3] * d[3];
         x[2] = (x[2] - R[2][3] * x[3]) * d[2];
@@ -238,14 +320,14 @@ __device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], d
         x[3] = (x[3] - R[0][3] * x[0] - R[1][3] * x[1] - R[2][3] * x[2]) * d[3];
     };
     auto normalize = [&](double (&x)[4]) {
-        const double is = 1.0 / sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
+        const double is = rsqrt_fast(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
 #pragma unroll
         for (int q = 0; q < 4; q++) x[q] *= is;
     };
     double x[4] = {0.0, 0.0, 0.0, 1.0};
     back(x);
     normalize(x);
-    double prev = 1.0;  // step length of the previous iteration
+    double prev = 1.0;  // squared step length of the previous iteration
     for (int it = 0; it < 12; it++) {
         double y[4] = {x[0], x[1], x[2], x[3]};
         fwd(y);
@@ -258,15 +340,15 @@ __device__ __forceinline__ bool qr_inverse_iteration(const double (&A0)[M][4], d
             dd += e * e;
             x[q] = y[q];
         }
-        const double step = sqrt(dd);
-        // geometric convergence: remaining error ≈ step · (step / prev)
-        if (step <= 4e-16 || (step <= 1e-6 && step * step <= 1e-14 * prev)) {
+        // squared step dd; geometric convergence: remaining error ≈ step · (step / prev),
+        // i.e. step <= 4e-16, or step <= 1e-6 and step² <= 1e-14 · prev
+        if (dd <= 1.6e-31 || (dd <= 1e-12 && dd * dd <= 1e-28 * prev)) {
 #pragma unroll
             for (int q = 0; q < 4; q++) nv[q] = x[q];
             return true;
         }
-        if (it >= 2 && !(step < 0.5 * prev)) return false;  // not contracting (or NaN)
-        prev = step;
+        if (it >= 2 && !(dd < 0.25 * prev)) return false;  // not contracting (or NaN)
+        prev = dd;
     }
     return false;
 }
@@ -297,20 +379,62 @@ __device__ __forceinline__ void add_view_rows(double (*A)[4], int r, float ux, f
     }
 }
 
-__device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], const double* __restrict__ cams,
-                                          int n_cams) {
+__device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], CamFast* sfast,
+                                          const double* __restrict__ cams, int n_cams) {
     const int total = n_cams * MVP_CAM_DOUBLES;
     for (int i = threadIdx.x; i < total; i += blockDim.x) scam[i / MVP_CAM_DOUBLES][i % MVP_CAM_DOUBLES] = cams[i];
+    if (threadIdx.x < n_cams) {
+        const double* c = cams + threadIdx.x * MVP_CAM_DOUBLES;
+        sfast[threadIdx.x].ifx = 1. / c[0];
+        sfast[threadIdx.x].ify = 1. / c[4];
+    }
     __syncthreads();
+}
+
+// Solver stages.  kExact: the restatement for every lane (OpenCV undistortion
+// with IEEE divisions, Jacobi SVD).  kFast: fast undistortion + QR / inverse
+// iteration, with the Jacobi restatement (on the same A) for the lanes whose
+// iteration has not provably converged.
+//
+// Measured and dropped (tools/pmc_tri.sh, V=2, 1.7 M points): moving the Jacobi
+// fallback to a second launch over marked lanes cuts the fast kernel from 110 to
+// 66 VGPRs (4 -> 7 waves per SIMD) but made it slower (69 vs 58 us; VALU busy
+// 59 % vs 73 %), and the marker sweep cost another 23 us.
+enum Stage { kExact = 0, kFast = 1 };
+
+template <int S>
+__device__ __forceinline__ void undistort_view(float u, float v, const double* __restrict__ c, const CamFast& cf,
+                                               float& ox, float& oy) {
+    if constexpr (S == kExact)
+        undistort_point(u, v, c, ox, oy);
+    else
+        undistort_point_fast(u, v, c, cf, ox, oy);
+}
+
+template <int S, int M>
+__device__ __forceinline__ void solve_and_write(const double (&A)[M][4], int64_t p, float* __restrict__ out,
+                                                double* __restrict__ out4) {
+    double nv[4];
+    if (S == kExact || !qr_inverse_iteration<M>(A, nv)) {
+        double At[4][M];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int r = 0; r < M; r++) At[c][r] = A[r][c];
+        jacobi_null_vector<M>(At, nv);
+    }
+    write_result(nv, p, out, out4);
 }
 
 // MVP_TRI_REFERENCE: top-2 listed cameras by confidence (ascending), params keyed
 // by selection position (reference quirk, pose_estimation.py:36-45).
-__global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
+template <int S>
+__device__ __forceinline__ void triangulate_reference_body(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
-    CamIdx ci, int n_ci, int exact, float* __restrict__ out, double* __restrict__ out4) {
+    CamIdx ci, int n_ci, float* __restrict__ out, double* __restrict__ out4) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
-    load_cams(scam, cams, n_cams);
+    __shared__ CamFast sfast[kMaxCams];
+    load_cams(scam, sfast, cams, n_cams);
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const float* __restrict__ kp = kpts + p * 3 * V;
@@ -342,30 +466,22 @@ __global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
     const int col0 = ci.v[pos0], col1 = ci.v[pos1];
     float u0x, u0y, u1x, u1y;
     // points come from the selected columns; parameters from camera key = position
-    undistort_point(kp[col0], kp[V + col0], scam[pos0], u0x, u0y);
-    undistort_point(kp[col1], kp[V + col1], scam[pos1], u1x, u1y);
+    undistort_view<S>(kp[col0], kp[V + col0], scam[pos0], sfast[pos0], u0x, u0y);
+    undistort_view<S>(kp[col1], kp[V + col1], scam[pos1], sfast[pos1], u1x, u1y);
     double A[4][4];
     add_view_rows(A, 0, u0x, u0y, scam[pos0] + 26);
     add_view_rows(A, 2, u1x, u1y, scam[pos1] + 26);
-    double nv[4];
-    if (exact || !qr_inverse_iteration<4>(A, nv)) {
-        double At[4][4];
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) At[c][r] = A[r][c];
-        jacobi_null_vector<4>(At, nv);
-    }
-    write_result(nv, p, out, out4);
+    solve_and_write<S, 4>(A, p, out, out4);
 }
 
 // MVP_TRI_ALL_VIEWS: one 2·NV x 4 DLT over the NV listed views.
-template <int NV>
-__global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
+template <int S, int NV>
+__device__ __forceinline__ void triangulate_all_views_body(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams,
-    CamIdx ci, int exact, float* __restrict__ out, double* __restrict__ out4) {
+    CamIdx ci, float* __restrict__ out, double* __restrict__ out4) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
-    load_cams(scam, cams, n_cams);
+    __shared__ CamFast sfast[kMaxCams];
+    load_cams(scam, sfast, cams, n_cams);
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const float* __restrict__ kp = kpts + p * 3 * V;
@@ -374,19 +490,24 @@ __global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
     for (int j = 0; j < NV; j++) {
         const int col = ci.v[j];
         float ux, uy;
-        undistort_point(kp[col], kp[V + col], scam[col], ux, uy);
+        undistort_view<S>(kp[col], kp[V + col], scam[col], sfast[col], ux, uy);
         add_view_rows(A, 2 * j, ux, uy, scam[col] + 26);
     }
-    double nv[4];
-    if (exact || !qr_inverse_iteration<2 * NV>(A, nv)) {
-        double At[4][2 * NV];
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-            for (int r = 0; r < 2 * NV; r++) At[c][r] = A[r][c];
-        jacobi_null_vector<2 * NV>(At, nv);
-    }
-    write_result(nv, p, out, out4);
+    solve_and_write<S, 2 * NV>(A, p, out, out4);
+}
+
+template <int S>
+__global__ __launch_bounds__(kBlock) void triangulate_reference_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
+    int n_ci, float* __restrict__ out, double* __restrict__ out4) {
+    triangulate_reference_body<S>(kpts, n, V, cams, n_cams, ci, n_ci, out, out4);
+}
+
+template <int S, int NV>
+__global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
+    float* __restrict__ out, double* __restrict__ out4) {
+    triangulate_all_views_body<S, NV>(kpts, n, V, cams, n_cams, ci, out, out4);
 }
 
 }  // namespace
@@ -412,18 +533,27 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t blocks = (n_points + kBlock - 1) / kBlock;
     MVP_REQUIRE(blocks < (1LL << 31), "mvp_triangulate: too many points");
-    const int exact = (mode & MVP_TRI_EXACT_JACOBI) ? 1 : 0;
+    const bool exact = (mode & MVP_TRI_EXACT_JACOBI) != 0;
     mode &= ~MVP_TRI_EXACT_JACOBI;
+    const dim3 grid((unsigned)blocks), block(kBlock);
     if (mode == MVP_TRI_REFERENCE) {
         MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
                     "n_cam_idx <= n_cams");
-        hipLaunchKernelGGL(triangulate_reference_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, n_points,
-                           V, cams, n_cams, ci, n_cam_idx, exact, out_xyz, out_xyzw);
+        if (exact)
+            hipLaunchKernelGGL(triangulate_reference_kernel<kExact>, grid, block, 0, s, kpts, n_points, V, cams,
+                               n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
+        else
+            hipLaunchKernelGGL(triangulate_reference_kernel<kFast>, grid, block, 0, s, kpts, n_points, V, cams,
+                               n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
     } else if (mode == MVP_TRI_ALL_VIEWS) {
-#define MVP_TRI_CASE(NV)                                                                                    \
-    case NV:                                                                                                \
-        hipLaunchKernelGGL(triangulate_all_views_kernel<NV>, dim3((unsigned)blocks), dim3(kBlock), 0, s, kpts, \
-                           n_points, V, cams, n_cams, ci, exact, out_xyz, out_xyzw);                       \
+#define MVP_TRI_CASE(NV)                                                                                      \
+    case NV:                                                                                                  \
+        if (exact)                                                                                            \
+            hipLaunchKernelGGL((triangulate_all_views_kernel<kExact, NV>), grid, block, 0, s, kpts, n_points, V, \
+                               cams, n_cams, ci, out_xyz, out_xyzw);                                          \
+        else                                                                                                  \
+            hipLaunchKernelGGL((triangulate_all_views_kernel<kFast, NV>), grid, block, 0, s, kpts, n_points, V,  \
+                               cams, n_cams, ci, out_xyz, out_xyzw);                                          \
         break;
         switch (n_cam_idx) {
             MVP_TRI_CASE(2)

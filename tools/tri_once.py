@@ -1,0 +1,27 @@
+"""One triangulation workload for counter collection: V=2 reference mode,
+T frames (default 100k, BASELINE config 4 stream), fast solver, `reps` launches.
+
+    python tools/tri_once.py [T] [reps]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd"))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from mvpose import ops, synthetic as syn  # noqa: E402
+
+T = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+cams = syn.make_rig(2, seed=1)
+k = syn.make_kpts_2d(syn.make_poses(min(T, 2000), seed=2), cams, seed=3)
+k = np.ascontiguousarray(np.tile(k, (T // k.shape[0] + 1, 1, 1, 1))[:T])
+kd = torch.tensor(k, device="cuda")
+cd = torch.tensor(ops.pack_cameras(syn.reference_camera_params(cams)), device="cuda")
+out = torch.empty((T, 17, 3), device="cuda")
+for _ in range(reps):
+    ops.triangulate(kd, cd, [0, 1], mode=ops.TRI_REFERENCE, out=out)
+torch.cuda.synchronize()
+print("tri_once done", T, reps)

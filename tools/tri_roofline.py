@@ -28,7 +28,7 @@ for V, mode, ci in ((2, ops.TRI_REFERENCE, [0, 1]), (4, ops.TRI_ALL_VIEWS, [0, 1
             ops.triangulate(kd, cd, ci, mode=mode, out=out, exact=exact)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        n = 20
+        n = 300
         e0.record()
         for _ in range(n):
             ops.triangulate(kd, cd, ci, mode=mode, out=out, exact=exact)
