@@ -31,6 +31,26 @@ void launch_conv(const ConvLaunch& c, hipStream_t s);
 // Direct-load 1x1 conv (conv1x1.hip); false when the conv is not a bf16-output 1x1.
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s);
 
+// Bottleneck join (conv1x1.hip): y = relu(W1·[x | x2] + b1 [+ res]) with 256 couts,
+// then y2 = relu(W2·y + b2) with 64 couts from the bf16 y still in registers (the
+// next Bottleneck's conv1), so y is written once and never re-read for it.
+// W1 [256][cin1 (+ cin2)] bf16, W2 [64][256] bf16.  cin1 + cin2 must be 64 or 128.
+struct PairLaunch {
+    const uint16_t* x = nullptr;
+    const uint16_t* x2 = nullptr;  // dual input (cat-fused downsample) or nullptr
+    int c1 = 0, c2 = 0;            // channels of x, x2
+    const uint16_t* w1 = nullptr;
+    const float* b1 = nullptr;
+    const uint16_t* res = nullptr;  // 256-ch residual or nullptr
+    uint16_t* y = nullptr;
+    const uint16_t* w2 = nullptr;
+    const float* b2 = nullptr;
+    uint16_t* y2 = nullptr;
+    long n_pix = 0;
+};
+bool conv1x1_pair_supported(int cin_total, int cmid, int cout2);
+void launch_conv1x1_pair(const PairLaunch& p, hipStream_t s);
+
 // Weight-stationary 3x3/s1 conv for the Cin == Cout branch planes (wsconv.hip):
 // 64 ch at 32x24 and 128 ch at 16x12.  false when the conv is not one of those
 // (or MVPOSE_NO_WSCONV=1).

@@ -635,27 +635,24 @@ __global__ __launch_bounds__(256) void stem_kernel(const uint16_t* __restrict__ 
 template <int WO>
 __global__ __launch_bounds__(256) void stem_mfma_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, uint16_t* __restrict__ y,
-                                                        int H, int Ho) {
+                                                        int H, int Ho, long n_tiles) {
     constexpr int W = 2 * WO;   // input width
     constexpr int LW = W + 2;   // staged row (pixels) with the zero border
-    constexpr int P = 2 * WO;   // output pixels per workgroup
+    constexpr int P = 2 * WO;   // output pixels per tile
     static_assert(P % 64 == 0, "two output rows must split into 16-pixel tiles per wave");
     constexpr int PTW = P / 64;
     __shared__ uint2 sx[5 * LW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
     const int tiles = Ho / 2;
-    const int n = blockIdx.x / tiles, ho0 = (blockIdx.x - n * tiles) * 2;
-    const uint2* xin = reinterpret_cast<const uint2*>(x) + (size_t)n * H * W;
-    for (int i = tid; i < 5 * LW; i += 256) {
-        const int r = i / LW, c = i - r * LW;
-        const int hi = 2 * ho0 - 1 + r, wi = c - 1;
-        sx[i] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? xin[(size_t)hi * W + wi] : uint2{0u, 0u};
-    }
+    // A row r of cout tile c holds cout (r >> 2) * 16 + 4c + (r & 3), so lane group g
+    // ends up owning the 16 consecutive couts 16g .. 16g+15 of its pixel: 2 x 16-B
+    // stores per pixel instead of 4 x 8 B.  Fragments are built once per
+    // (persistent) workgroup.
     bf16x8 afr[4][2];
     float4 b4[4];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-        const int co = c * 16 + (lane & 15);
+        const int r = lane & 15, co = (r >> 2) * 16 + 4 * c + (r & 3);
 #pragma unroll
         for (int kc = 0; kc < 2; kc++) {
 #pragma unroll
@@ -664,42 +661,48 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(const uint16_t* __restri
                 afr[c][kc][j] = (__bf16)(tap < 9 ? w[(co * 9 + tap) * 4 + ch] : 0.f);
             }
         }
-        b4[c] = *reinterpret_cast<const float4*>(bias + c * 16 + g * 4);
+        b4[c] = *reinterpret_cast<const float4*>(bias + g * 16 + 4 * c);
     }
-    __syncthreads();
-    f32x4 acc[PTW][4];
-#pragma unroll
-    for (int i = 0; i < PTW; i++) {
-        const int pix = (wave * PTW + i) * 16 + (lane & 15);
-        const int orow = pix / WO, ocol = pix - (pix / WO) * WO;
-        auto tap_px = [&](int tap) { return sx[(2 * orow + tap / 3) * LW + 2 * ocol + tap % 3]; };
-        const uint2 t0 = tap_px(2 * g), t1 = tap_px(2 * g + 1);
-        const uint2 t8 = g == 0 ? tap_px(8) : uint2{0u, 0u};
-        union {
-            uint4 u;
-            bf16x8 v;
-        } b0, b1;
-        b0.u = uint4{t0.x, t0.y, t1.x, t1.y};
-        b1.u = uint4{t8.x, t8.y, 0u, 0u};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][0], b0.v, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][1], b1.v, acc[i][c], 0, 0, 0);
+    for (long t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const int n = (int)(t / tiles), ho0 = (int)(t - (long)n * tiles) * 2;
+        const uint2* xin = reinterpret_cast<const uint2*>(x) + (size_t)n * H * W;
+        __syncthreads();  // the previous tile's reads of sx are done
+        for (int i = tid; i < 5 * LW; i += 256) {
+            const int r = i / LW, c = i - r * LW;
+            const int hi = 2 * ho0 - 1 + r, wi = c - 1;
+            sx[i] = (hi >= 0 && hi < H && wi >= 0 && wi < W) ? xin[(size_t)hi * W + wi] : uint2{0u, 0u};
         }
-    }
+        __syncthreads();
 #pragma unroll
-    for (int i = 0; i < PTW; i++) {
-        const int pix = (wave * PTW + i) * 16 + (lane & 15);
-        const int orow = pix / WO, ocol = pix - (pix / WO) * WO;
-        uint16_t* out = y + (((size_t)n * Ho + ho0 + orow) * WO + ocol) * 64;
+        for (int i = 0; i < PTW; i++) {
+            const int pix = (wave * PTW + i) * 16 + (lane & 15);
+            const int orow = pix / WO, ocol = pix - (pix / WO) * WO;
+            auto tap_px = [&](int tap) { return sx[(2 * orow + tap / 3) * LW + 2 * ocol + tap % 3]; };
+            const uint2 t0 = tap_px(2 * g), t1 = tap_px(2 * g + 1);
+            const uint2 t8 = g == 0 ? tap_px(8) : uint2{0u, 0u};
+            union {
+                uint4 u;
+                bf16x8 v;
+            } b0, b1;
+            b0.u = uint4{t0.x, t0.y, t1.x, t1.y};
+            b1.u = uint4{t8.x, t8.y, 0u, 0u};
+            f32x4 acc[4];
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const float v0 = fmaxf(acc[i][c][0] + b4[c].x, 0.f), v1 = fmaxf(acc[i][c][1] + b4[c].y, 0.f);
-            const float v2 = fmaxf(acc[i][c][2] + b4[c].z, 0.f), v3 = fmaxf(acc[i][c][3] + b4[c].w, 0.f);
-            uint2 o;
-            o.x = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-            o.y = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
-            *reinterpret_cast<uint2*>(out + c * 16 + g * 4) = o;
+            for (int c = 0; c < 4; c++) {
+                acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][0], b0.v, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][1], b1.v, acc[c], 0, 0, 0);
+            }
+            uint32_t o[8];
+#pragma unroll
+            for (int c = 0; c < 4; c++) {
+                const float v0 = fmaxf(acc[c][0] + b4[c].x, 0.f), v1 = fmaxf(acc[c][1] + b4[c].y, 0.f);
+                const float v2 = fmaxf(acc[c][2] + b4[c].z, 0.f), v3 = fmaxf(acc[c][3] + b4[c].w, 0.f);
+                o[2 * c] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+                o[2 * c + 1] = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+            }
+            uint16_t* out = y + (((size_t)n * Ho + ho0 + orow) * WO + ocol) * 64 + g * 16;
+            *reinterpret_cast<uint4*>(out) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(out + 8) = uint4{o[4], o[5], o[6], o[7]};
         }
     }
 }
@@ -804,8 +807,16 @@ void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t*
     const long total = (long)N * Ho * Wo * 4;
     if (total == 0) return;
     if (Wo == 96 && H % 2 == 0 && Ho % 2 == 0) {  // the 256x192 crop: MFMA path
-        hipLaunchKernelGGL(stem_mfma_kernel<96>, dim3((unsigned)((long)N * Ho / 2)), dim3(256), 0, s, x, w, bias, y,
-                           H, Ho);
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0;
+            MVP_HIP(hipGetDevice(&dev));
+            MVP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        const long n_tiles = (long)N * Ho / 2;
+        const long grid = std::min<long>(n_tiles, (long)cus * 8);
+        hipLaunchKernelGGL(stem_mfma_kernel<96>, dim3((unsigned)grid), dim3(256), 0, s, x, w, bias, y, H, Ho,
+                           n_tiles);
         MVP_HIP(hipGetLastError());
         return;
     }

@@ -147,6 +147,181 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
     }
 }
 
+// ------------------------------------------------------------ bottleneck join
+// Layer1 of HRNet-W32 alternates conv3 (64 -> 256, + residual, ReLU) and the next
+// block's conv1 (256 -> 64, ReLU) at 64x48: the 256-ch tensor (1.6 GB per 1024
+// crops) was written by one launch and read straight back by the next.  Here one
+// wave computes all 256 couts of 16 pixels (A rows permuted as in conv1x1_kernel
+// with BM = 256, so lane group g holds couts 64g .. 64g+63 of its pixel), writes
+// them, and feeds the same bf16 values to the second GEMM as B fragments without
+// any lane exchange: the second GEMM's K order is permuted to match — K chunk j,
+// lane group g covers channels 64g + 8j .. 64g + 8j + 7 — by the order the W2
+// slots are DMA'd into LDS.  y is rounded to bf16 before the second GEMM, as in
+// the unfused graph; only the f32 summation order of the second GEMM differs.
+struct PPair {
+    const uint16_t* x;
+    const uint16_t* x2;
+    int c1, c2, kch1;
+    const uint16_t* w1;
+    const float* b1;
+    const uint16_t* res;
+    uint16_t* y;
+    const uint16_t* w2;
+    const float* b2;
+    uint16_t* y2;
+    const uint16_t* zero;
+    long n_pix;
+};
+
+constexpr int kPairThreads = 512;  // 8 waves per workgroup; <= 128 VGPRs so two workgroups fit a CU
+
+template <int KCH>
+__global__ __launch_bounds__(kPairThreads, 2) void conv1x1_pair_kernel(PPair p) {
+    constexpr int BM = 256, NCT = BM / 16, CIN = KCH * 32;
+    constexpr int S1 = KCH * 4 * BM;  // expand weight slots [chunk][q][row]
+    constexpr int S2 = 8 * 4 * 64;    // reduce weight slots [chunk][q][row]
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    __shared__ float4 sb1[BM / 4];
+    __shared__ float4 sb2[16];
+    const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    constexpr int NWAVES = kPairThreads / 64;
+    for (int s0 = wave * 64; s0 < S1 + S2; s0 += kPairThreads) {
+        const int sl = s0 + lane;
+        const void* src = p.zero;
+        if (sl < S1) {
+            const int co = sl % BM, tq = sl / BM;
+            const int c = co >> 4, r = co & 15;
+            src = p.w1 + (size_t)((r >> 2) * (BM / 4) + c * 4 + (r & 3)) * CIN + tq * 8;
+        } else if (sl < S1 + S2) {
+            const int s2 = sl - S1, co = s2 % 64, tq = s2 / 64;  // tq = chunk j * 4 + q
+            const int c = co >> 4, r = co & 15, j = tq >> 2, q = tq & 3;
+            src = p.w2 + (size_t)((r >> 2) * 16 + c * 4 + (r & 3)) * 256 + q * 64 + j * 8;
+        }
+        glds16(src, lds + s0 * 16);
+    }
+    if (tid < BM / 4) sb1[tid] = reinterpret_cast<const float4*>(p.b1)[tid];
+    if (tid < 16) sb2[tid] = reinterpret_cast<const float4*>(p.b2)[tid];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint8_t* lds2 = lds + S1 * 16;
+
+    const long n_units = (p.n_pix + 15) / 16;
+    const long ustep = (long)gridDim.x * NWAVES;
+    // software pipeline: the next unit's input and residual loads are issued before
+    // this unit's MFMAs (both halves' residuals: 2 x 4 x 16 B per lane)
+    bf16x8 bn[KCH];
+    uint4 rn0[4], rn1[4];
+    auto load_unit = [&](long u) {
+        const long pp = u * 16 + (lane & 15);
+        const long pix = pp < p.n_pix ? pp : p.n_pix - 1;
+        const uint16_t* src = p.x + pix * p.c1 + g * 8;
+        const uint16_t* src2 = p.x2 ? p.x2 + pix * p.c2 + g * 8 - p.kch1 * 32 : src;
+#pragma unroll
+        for (int ch = 0; ch < KCH; ch++)
+            bn[ch] = *reinterpret_cast<const bf16x8*>((ch < p.kch1 ? src : src2) + ch * 32);
+        const uint16_t* rsrc = p.res ? p.res + pix * BM + g * 64 : p.zero + lane * 64;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            rn0[q] = *reinterpret_cast<const uint4*>(rsrc + q * 8);
+            rn1[q] = *reinterpret_cast<const uint4*>(rsrc + 32 + q * 8);
+        }
+    };
+    long u = (long)blockIdx.x * NWAVES + wave;
+    if (u < n_units) load_unit(u);
+    for (; u < n_units; u += ustep) {
+        const long pp = u * 16 + (lane & 15);
+        const bool valid = pp < p.n_pix;
+        const long pix = valid ? pp : p.n_pix - 1;
+        bf16x8 b[KCH];
+#pragma unroll
+        for (int ch = 0; ch < KCH; ch++) b[ch] = bn[ch];
+        uint4 rv[4], rv_next[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            rv[q] = rn0[q];
+            rv_next[q] = rn1[q];
+        }
+        if (u + ustep < n_units) load_unit(u + ustep);
+        uint16_t* yrow = p.y + pix * BM + g * 64;
+        f32x4 acc2[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) acc2[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // two halves of 8 cout tiles: lane group g's couts 64g + 32h .. 64g + 32h + 31,
+        // i.e. the second GEMM's K chunks j = 4h .. 4h + 3 (register pressure: one half
+        // of the accumulators and packed outputs live at a time)
+#pragma unroll 1
+        for (int h = 0; h < 2; h++) {
+            f32x4 acc[NCT / 2];
+#pragma unroll
+            for (int c = 0; c < NCT / 2; c++) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ch = 0; ch < KCH; ch++)
+#pragma unroll
+                for (int c = 0; c < NCT / 2; c++) {
+                    const int ct = h * (NCT / 2) + c;
+                    const bf16x8 a =
+                        *reinterpret_cast<const bf16x8*>(lds + ((ch * 4 + g) * BM + ct * 16 + (lane & 15)) * 16);
+                    acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[ch], acc[c], 0, 0, 0);
+                }
+            uint32_t o[NCT];
+#pragma unroll
+            for (int c = 0; c < NCT / 2; c++) {
+                const float4 bb = sb1[g * (BM / 16) + h * (NCT / 2) + c];
+                float v[4] = {acc[c][0] + bb.x, acc[c][1] + bb.y, acc[c][2] + bb.z, acc[c][3] + bb.w};
+                const uint4 r4 = rv[c >> 1];
+                const uint32_t r0 = (c & 1) ? r4.z : r4.x, r1 = (c & 1) ? r4.w : r4.y;
+                v[0] += bf16_to_f32(r0 & 0xffff);
+                v[1] += bf16_to_f32(r0 >> 16);
+                v[2] += bf16_to_f32(r1 & 0xffff);
+                v[3] += bf16_to_f32(r1 >> 16);
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+                o[2 * c] = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+                o[2 * c + 1] = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+            }
+            if (valid) {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    *reinterpret_cast<uint4*>(yrow + h * 32 + q * 8) =
+                        uint4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+            }
+            // second GEMM, K chunks j = 4h + jj: this lane group's channels 64g + 8j .. +7
+#pragma unroll
+            for (int jj = 0; jj < 4; jj++) {
+                const int j = h * 4 + jj;
+                union {
+                    uint4 u;
+                    bf16x8 v;
+                } bj;
+                bj.u = uint4{o[4 * jj], o[4 * jj + 1], o[4 * jj + 2], o[4 * jj + 3]};
+#pragma unroll
+                for (int c = 0; c < 4; c++) {
+                    const bf16x8 a =
+                        *reinterpret_cast<const bf16x8*>(lds2 + ((j * 4 + g) * 64 + c * 16 + (lane & 15)) * 16);
+                    acc2[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bj.v, acc2[c], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) rv[q] = rv_next[q];
+        }
+        uint32_t o2[8];
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float4 bb = sb2[g * 4 + c];
+            const float v0 = fmaxf(acc2[c][0] + bb.x, 0.f), v1 = fmaxf(acc2[c][1] + bb.y, 0.f);
+            const float v2 = fmaxf(acc2[c][2] + bb.z, 0.f), v3 = fmaxf(acc2[c][3] + bb.w, 0.f);
+            o2[2 * c] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+            o2[2 * c + 1] = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
+        }
+        if (valid) {
+            uint16_t* y2row = p.y2 + pix * 64 + g * 16;
+            *reinterpret_cast<uint4*>(y2row) = uint4{o2[0], o2[1], o2[2], o2[3]};
+            *reinterpret_cast<uint4*>(y2row + 8) = uint4{o2[4], o2[5], o2[6], o2[7]};
+        }
+    }
+}
+
 int g_cus1 = 0;
 
 template <int BM, int KCH>
@@ -184,6 +359,43 @@ bool dispatch_k(const P1x1& p, int kch, int cout_pad, hipStream_t s) {
 }
 
 }  // namespace
+
+bool conv1x1_pair_supported(int cin_total, int cmid, int cout2) {
+    const char* e = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics/tests: keep the two launches
+    if (e && e[0] == '1') return false;
+    return (cin_total == 64 || cin_total == 128) && cmid == 256 && cout2 == 64;
+}
+
+void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
+    const int cin = c.c1 + (c.x2 ? c.c2 : 0);
+    MVP_REQUIRE(conv1x1_pair_supported(cin, 256, 64), "conv1x1_pair: unsupported cin %d", cin);
+    MVP_REQUIRE(c.c1 % 32 == 0 && c.c1 > 0 && (!c.x2 || c.c2 % 32 == 0), "conv1x1_pair: channel split %d/%d", c.c1,
+                c.c2);
+    if (c.n_pix == 0) return;
+    PPair p{c.x, c.x2, c.c1, c.x2 ? c.c2 : 0, c.c1 / 32, c.w1, c.b1, c.res, c.y, c.w2, c.b2, c.y2,
+            conv_zero_region(), c.n_pix};
+    if (g_cus1 == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_cus1, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const long units = (c.n_pix + 15) / 16;
+    auto go = [&](auto kern, int kch) {
+        const int lds = (kch * 4 * 256 + 8 * 4 * 64) * 16;
+        static int per_cu[2] = {0, 0};
+        int& pc = per_cu[kch == 4];
+        if (pc == 0) {
+            MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+            MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, kPairThreads, lds));
+            if (pc < 1) pc = 1;
+        }
+        const long grid = std::min<long>((long)g_cus1 * pc, (units + 7) / 8);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kPairThreads), lds, s, p);
+    };
+    if (cin == 64) go(conv1x1_pair_kernel<2>, 2);
+    else go(conv1x1_pair_kernel<4>, 4);
+    MVP_HIP(hipGetLastError());
+}
 
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
     if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cin % 32 != 0) return false;

@@ -29,6 +29,7 @@ struct Graph {
     std::vector<int> cat_src;     // 1x1 op that also computes the absorbed 1x1 op cat_src[k] (-1: none)
     std::vector<uint16_t*> cat_w; // its concatenated weights [cout_pad][cin_k + cin_src] (owned)
     std::vector<float*> cat_b;    // and summed biases [cout_pad] (owned)
+    std::vector<int> pair_tail;   // 1x1 op whose 256->64 successor (absorbed) runs in the same launch (-1: none)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -181,6 +182,36 @@ void cat_fuse(Graph& g, bool enable) {
     }
 }
 
+// Pair-fusion pass (Bottleneck join): a 1x1 conv A producing 256 channels with ReLU (the
+// Bottleneck's conv3, single input + residual or cat-fused with the downsample) whose
+// output T is read by a 1x1 conv B (256 -> 64, ReLU, no residual: the next Bottleneck's
+// conv1) runs as one conv1x1_pair launch that writes T (still needed as the next
+// residual) and B's output; T is no longer re-read for B.
+void pair_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.pair_tail.assign(no, -1);
+    if (!enable) return;
+    std::vector<int> producer(nt, -1);
+    for (int k = 0; k < no; k++) producer[g.ops[k].out] = k;
+    auto plain_1x1 = [&](int k) {
+        const mvp_op_desc& op = g.ops[k];
+        return !g.absorbed[k] && !g.block_head[k] && op.kind == MVP_OP_CONV && op.ks == 1 && op.stride == 1 &&
+               op.relu && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    for (int b = 0; b < no; b++) {
+        const mvp_op_desc& B = g.ops[b];
+        if (!plain_1x1(b) || (B.n_in > 1 && B.in[1] >= 0) || B.cin != 256 || B.cout != 64) continue;
+        const int a = producer[B.in[0]];
+        if (a < 0 || a >= b || !plain_1x1(a) || g.pair_tail[a] >= 0) continue;
+        const mvp_op_desc& A = g.ops[a];
+        const int cin = A.cin + (g.cat_src[a] >= 0 ? g.ops[g.cat_src[a]].cin : 0);
+        if (A.cout != 256 || A.segment != B.segment) continue;
+        if (!conv1x1_pair_supported(cin, A.cout, B.cout)) continue;
+        g.pair_tail[a] = b;
+        g.absorbed[b] = 1;
+    }
+}
+
 // Device-side concatenated weights / summed biases of the cat-fused ops (graph create time).
 void cat_build(Graph& g) {
     for (int b = 0; b < (int)g.ops.size(); b++) {
@@ -247,6 +278,13 @@ void plan(Graph& g) {
             last[x] = std::max(last[x], k);
             touch(x);
         }
+        if (g.pair_tail[k] >= 0) {  // the absorbed successor's output is written here
+            const int y2 = g.ops[g.pair_tail[k]].out;
+            first[y2] = k;
+            if (last[y2] < k) last[y2] = k;
+            seg_of_def[y2] = op.segment;
+            touch(y2);
+        }
     }
     g.local_seg.assign(nt, -1);
     for (int t = 0; t < nt; t++) {
@@ -268,6 +306,7 @@ void plan(Graph& g) {
         for (int i = 0; i < op.n_in; i++)
             if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1)) widen(op.in[i]);
         if (g.cat_src[k] >= 0) widen(g.ops[g.cat_src[k]].in[0]);
+        if (g.pair_tail[k] >= 0) widen(g.ops[g.pair_tail[k]].out);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
@@ -339,6 +378,8 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::fuse(*g, !(nf && nf[0] == '1'));
         const char* nc = getenv("MVPOSE_NO_CATFUSE");  // diagnostics: keep the downsample conv separate
         mvp::cat_fuse(*g, !(nc && nc[0] == '1') && !(nf && nf[0] == '1'));
+        const char* np = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics: keep conv3 / next conv1 apart
+        mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
         mvp::cat_build(*g);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
@@ -414,6 +455,24 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
                 c.w = g->cat_w[k];
                 c.bias = g->cat_b[k];
                 c.res = nullptr;
+            }
+            if (g->pair_tail[k] >= 0) {  // Bottleneck join: this conv + the next block's conv1
+                const mvp_op_desc& b = g->ops[g->pair_tail[k]];
+                mvp::PairLaunch pl;
+                pl.x = c.x;
+                pl.x2 = c.x2;
+                pl.c1 = c.x2 ? c.c1 : c.Cin;
+                pl.c2 = c.x2 ? c.Cin - c.c1 : 0;
+                pl.w1 = c.w;
+                pl.b1 = c.bias;
+                pl.res = c.res;
+                pl.y = c.y;
+                pl.w2 = g->wb + b.w_off;
+                pl.b2 = g->fb + b.b_off;
+                pl.y2 = (uint16_t*)ptr(b.out);
+                pl.n_pix = (long)nb * x.h * x.w;
+                mvp::launch_conv1x1_pair(pl, s);
+                return;
             }
             mvp::launch_conv(c, s);
         } else {

@@ -341,6 +341,28 @@ def projection_spec(cin: int, cout: int, h: int, w: int, k: int = 1, seed: int =
     return g, x, y, sd
 
 
+def join_spec(h: int, w: int, seed: int = 0, cat: bool = False):
+    """Layer1 Bottleneck join on an h x w plane: r = conv_r(x) (64 -> 256; ReLU unless
+    `cat`, when it is the downsample that cat-fusion folds into conv_a), y = relu(conv_a(x)
+    + r) (64 -> 256, the Bottleneck conv3) and out = relu(conv_b(y)) (256 -> 64, the next
+    Bottleneck's conv1) — the pattern the graph's pair-fusion pass runs as one launch.
+    Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    g = GraphSpec()
+    x = g.tensor(h, w, 64)
+    for j, (co, ci) in (("r", (256, 64)), ("a", (256, 64)), ("b", (64, 256))):
+        sd[f"{j}.weight"] = torch.randn((co, ci, 1, 1), generator=gen) * (2.0 / ci) ** 0.5
+        sd[f"{j}bn.weight"] = 1.0 + 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.bias"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_mean"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_var"] = 1.0 + 0.2 * torch.rand((co,), generator=gen)
+    r = g.conv(sd, "r", "rbn", x, 1, not cat)
+    y = g.conv(sd, "a", "abn", x, 1, True, res=r)
+    out = g.conv(sd, "b", "bbn", y, 1, True)
+    return g, x, out, sd
+
+
 def conv_spec(cin: int, cout: int, h: int, w: int, k: int = 3, stride: int = 1, relu: bool = True, seed: int = 0):
     """One k x k conv (+ folded BN, optional ReLU) cin -> cout on an h x w plane, for
     kernel tests and per-conv benchmarks.  Returns (spec, input id, output id, state dict)."""

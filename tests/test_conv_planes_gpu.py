@@ -133,3 +133,38 @@ def test_projection_vs_reference(cin, cout, h, w, k):
     mx = (got - ref).abs().max().item()
     print(f"{k}x{k} {cin}->{cout} {h}x{w}: rel L2 {rel:.2e}, max abs {mx:.3e}")
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
+
+
+@pytest.mark.parametrize("cat", [False, True])
+@pytest.mark.parametrize("pair", [False, True])
+def test_bottleneck_join(cat, pair, monkeypatch):
+    """Layer1 conv3 (+ residual, or + the cat-fused downsample) followed by the next
+    block's 256 -> 64 conv1, with the pair-fusion pass on (one conv1x1_pair launch,
+    the second GEMM's K order permuted) and off (two conv1x1 launches), against a
+    torch fp32 restatement with bf16 rounding at the graph's tensor boundaries."""
+    from mvpose import hrnet
+    monkeypatch.setenv("MVPOSE_NO_PAIRFUSE", "0" if pair else "1")
+    h, w, n = 64, 48, 3
+    spec, xi, yo, sd = hrnet.join_spec(h, w, seed=21, cat=cat)
+    g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+    gen = torch.Generator().manual_seed(22)
+    x = torch.randn((n, h, w, 64), generator=gen).bfloat16()
+    out = torch.empty((n, h, w, 64), dtype=torch.bfloat16, device="cuda")
+    g.run(x.cuda(), out)
+    torch.cuda.synchronize()
+
+    def conv(name, t):
+        wt, b = hrnet.fold_bn(sd, name, name + "bn")
+        wt = _bf(torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 3, 1, 2))).float())
+        return torch.nn.functional.conv2d(t, wt) + torch.from_numpy(b).float()[None, :, None, None]
+
+    xf = x.float().permute(0, 3, 1, 2)
+    r = conv("r", xf)
+    r = r if cat else _bf(torch.relu(r))
+    y = _bf(torch.relu(conv("a", xf) + r))
+    ref = _bf(torch.relu(conv("b", y))).permute(0, 2, 3, 1)
+    dev = out.float().cpu()
+    rel = (torch.linalg.vector_norm(dev - ref) / torch.linalg.vector_norm(ref)).item()
+    assert rel <= 4e-3, rel
+    ulp = 2.0 ** (torch.floor(torch.log2(ref.abs().max())) - 7)
+    assert (dev - ref).abs().max().item() <= 3 * ulp, ((dev - ref).abs().max().item(), ulp)
