@@ -103,7 +103,10 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
  *   (mx, my, vxx, vxy, vxy, vyy); minv_dev [N][6] = image -> heatmap map;
  *   separable != 0 asserts (host-checked with mvp_warp_is_separable) that every
  *   map's fixed-point source column depends on x only and source row on y only,
- *   enabling the column-resident fast path.
+ *   enabling the column-resident fast path (per run of rows sharing a source
+ *   row, columns whose taps are all clearly above / below thr are summed in
+ *   closed form); separable == 2 runs that path walking every row of every
+ *   column (diagnostics, tests).
  * ------------------------------------------------------------------------- */
 int mvp_preprocess(const uint8_t* frames_dev, int n, int H, int W, const double* minv_dev, int out_h, int out_w,
                    const float* mean3_host, const float* std3_host, int swap_rb, int with_flip, uint16_t* out_dev,

@@ -194,6 +194,7 @@ struct MomParams {
     int N, K, h, w, img_h, img_w;
     float thr;
     int separable;  // host-verified: source column depends on x only, source row on y only
+                    // (2: the separable path without the per-run closed forms)
 };
 
 constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
@@ -215,6 +216,11 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     int* sad = reinterpret_cast<int*>(mom_lds + ((p.h * p.w + 3) & ~3));
     int* sbd = sad + p.img_w;
     int* riy = sbd + p.img_w;  // separable path: per image row source row / weight index
+    // separable path, per run of image rows sharing source row iy = r - 1 (r = 0 .. h):
+    // first / one-past-last image row and the run's weight sums (mom_run_layout)
+    int* rstart = riy + ((p.img_h + 2) & ~1);
+    int* rend = rstart + ((p.h + 2) & ~1);  // even int counts keep rsum 8-B aligned
+    double* rsum = reinterpret_cast<double*>(rend + ((p.h + 2) & ~1));
     __shared__ double red[6][kMomBlock / 64];
     __shared__ int bbox[4];
     const long map = blockIdx.x;
@@ -268,28 +274,67 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     if (c1 >= 0) {
         if (p.separable) {
             // Row table: source row iy and weight index fq of every image row (uniform per row).
-            // packed (iy + 4096) << 5 | fq, one word per row (+1 pad entry for the prefetch)
-            for (int y = threadIdx.x; y <= p.img_h; y += kMomBlock) {
-                const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
-                riy[y] = (((Yq >> 5) + 4096) << 5) | (Yq & 31);
+            // packed (iy + 4096) << 5 | fq, one word per row
+            for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
+                rstart[r] = p.img_h;
+                rend[r] = 0;
             }
             __syncthreads();
-            // Lanes own column pairs (packed f32 math); a run of rows sharing iy keeps its
-            // two x-interpolated source rows in registers and accumulates S, S*yr, S*yr^2
-            // (yr = row - run start) in f32, flushed to fp64 with the run's offset when iy
-            // changes.  The pixel value is OpenCV's bilinear remap value (its fixed-point
-            // coordinates and 1/32 weights exactly) evaluated as gy (v00 gx + v01 fx) +
-            // fy (v10 gx + v11 fx): within ~2 f32 ulps of OpenCV's operation order
-            // ((v00 w0 + v01 w1) + v10 w2) + v11 w3 — far inside the reference's own f32
-            // moment arithmetic (mmpose_pose_estimation.py:163-215).
+            for (int y = threadIdx.x; y < p.img_h; y += kMomBlock) {
+                const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
+                const int iy = Yq >> 5;
+                riy[y] = ((iy + 4096) << 5) | (Yq & 31);
+                if (iy >= -1 && iy < p.h) {  // rows of other runs read no map row: zero
+                    atomicMin(&rstart[iy + 1], y);
+                    atomicMax(&rend[iy + 1], y + 1);
+                }
+            }
+            __syncthreads();
+            // Per run (the affine row map is monotone, so a run is contiguous): sums over its
+            // rows of gy, fy, gy·yr, fy·yr, gy·yr², fy·yr² (yr = row - run start), exact in fp64.
+            // A column whose 4 taps are all >= thr·(1+2e-6) has every pixel of the run above
+            // the threshold (a bilinear value is a convex combination of its taps): its run
+            // sums are a·G + b·F in closed form.  Taps all < thr·(1-2e-6): all zero.  Only
+            // the remaining ("mixed") columns walk the run's rows.
+            for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
+                double g0 = 0, f0 = 0, g1 = 0, f1 = 0, g2 = 0, f2 = 0;
+                for (int y = rstart[r]; y < rend[r]; y++) {
+                    const double fy = (double)(riy[y] & 31) * (1.0 / 32.0), gy = 1.0 - fy;
+                    const double yr = y - rstart[r];
+                    g0 += gy;
+                    f0 += fy;
+                    g1 += gy * yr;
+                    f1 += fy * yr;
+                    g2 += gy * yr * yr;
+                    f2 += fy * yr * yr;
+                }
+                double* q = rsum + 6 * r;
+                q[0] = g0;
+                q[1] = f0;
+                q[2] = g1;
+                q[3] = f1;
+                q[4] = g2;
+                q[5] = f2;
+            }
+            __syncthreads();
+            // Lanes own column pairs (packed f32 math).  Per run, a column's two
+            // x-interpolated source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx are
+            // formed once; the pixel value is OpenCV's bilinear remap value (its fixed-point
+            // coordinates and 1/32 weights exactly) evaluated as gy a + fy b: within ~2 f32
+            // ulps of OpenCV's operation order ((v00 w0 + v01 w1) + v10 w2) + v11 w3 — far
+            // inside the reference's own f32 moment arithmetic (mmpose_pose_estimation.py:163-215).
+            // Mixed columns accumulate S, S*yr, S*yr^2 over the run's rows in f32, flushed
+            // to fp64 with the run's offset.
             typedef float f2 __attribute__((ext_vector_type(2)));
             constexpr int NP = kMomCols / 2;
             const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
+            const float thr_hi = p.thr * (1.f + 2e-6f), thr_lo2 = p.thr * (1.f - 2e-6f);
+            const bool closed = p.separable != 2;  // 2: walk every column (diagnostics / tests)
             for (int xb = threadIdx.x; xb < p.img_w; xb += kMomBlock * kMomCols) {
 #pragma clang fp contract(off)
                 int ix[kMomCols];
                 bool on[kMomCols];
-                f2 gx[NP], fx[NP];
+                float gx[kMomCols], fx[kMomCols];
                 bool any = false;
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
@@ -297,8 +342,8 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                     const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
                     ix[j] = X >> 5;
                     const float f = (float)(X & 31) * (1.f / 32.f);
-                    fx[j / 2][j & 1] = f;
-                    gx[j / 2][j & 1] = 1.f - f;
+                    fx[j] = f;
+                    gx[j] = 1.f - f;
                     on[j] = x < p.img_w && ix[j] + 1 >= c0 && ix[j] <= c1;
                     any |= on[j];
                 }
@@ -306,20 +351,60 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) S[j] = Sy[j] = Syy[j] = 0.0;
                 if (__any(any)) {
-                    // per column and run of rows sharing a source row: the two x-interpolated
-                    // source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx; per pixel the
-                    // value is gy a + fy b (2 ops instead of OpenCV's 4 weight products + 4
-                    // products + 3 sums: same bilinear value to ~2 f32 ulps, the tolerance the
-                    // oracle tests state)
-                    f2 ra[NP], rb[NP], s32[NP], sy32[NP], syy32[NP];
+                    const f2 thr2 = f2{p.thr, p.thr};
+                    for (int r = max(r0, 0); r <= min(r1 + 1, p.h); r++) {  // iy = r - 1 in [r0 - 1, r1]
+                        const int ys = rstart[r], ye = rend[r];
+                        if (ys >= ye) continue;
+                        const int iy = r - 1;
+                        const bool ry0 = iy >= 0, ry1 = iy + 1 < p.h;
+                        const double* q = rsum + 6 * r;
+                        const double y0c = ys - cy;
+                        f2 ra[NP], rb[NP];
+                        bool mixed = false;
 #pragma unroll
-                    for (int q = 0; q < NP; q++) {
-                        ra[q] = rb[q] = f2{0.f, 0.f};
-                        s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
-                    }
-                    int cur_iy = -0x7fffffff, y0 = 0;
-                    auto flush = [&]() {
-                        const double y0c = y0 - cy;
+                        for (int j = 0; j < kMomCols; j++) {
+                            const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
+                            const float v00 = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
+                            const float v01 = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
+                            const float v10 = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
+                            const float v11 = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                            const float a = __builtin_fmaf(v01, fx[j], v00 * gx[j]);
+                            const float b = __builtin_fmaf(v11, fx[j], v10 * gx[j]);
+                            const bool full = closed && v00 >= thr_hi && v01 >= thr_hi && v10 >= thr_hi && v11 >= thr_hi;
+                            const bool empty = closed && v00 < thr_lo2 && v01 < thr_lo2 && v10 < thr_lo2 && v11 < thr_lo2;
+                            if (full) {
+                                const double da = a, db = b;
+                                const double s0 = da * q[0] + db * q[1];
+                                const double s1 = da * q[2] + db * q[3];
+                                const double s2 = da * q[4] + db * q[5];
+                                S[j] += s0;
+                                Sy[j] += y0c * s0 + s1;
+                                Syy[j] += y0c * y0c * s0 + 2.0 * y0c * s1 + s2;
+                            }
+                            const bool walk = !full && !empty;
+                            mixed |= walk;
+                            ra[j / 2][j & 1] = walk ? a : 0.f;
+                            rb[j / 2][j & 1] = walk ? b : 0.f;
+                        }
+                        if (!__any(mixed)) continue;  // every column of the wave done in closed form
+                        f2 s32[NP], sy32[NP], syy32[NP];
+#pragma unroll
+                        for (int k = 0; k < NP; k++) s32[k] = sy32[k] = syy32[k] = f2{0.f, 0.f};
+                        for (int y = ys; y < ye; y++) {
+                            const int fq = riy[y] & 31;
+                            const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
+                            const float yr = (float)(y - ys);
+                            const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
+                            const f2 fy2 = f2{fy, fy}, gy2 = f2{gy, gy};
+#pragma unroll
+                            for (int k = 0; k < NP; k++) {
+                                const f2 v = __builtin_elementwise_fma(fy2, rb[k], gy2 * ra[k]);
+                                const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
+                                s32[k] = s32[k] + vs;
+                                sy32[k] = __builtin_elementwise_fma(vs, yr2, sy32[k]);
+                                syy32[k] = __builtin_elementwise_fma(vs, yrr2, syy32[k]);
+                            }
+                        }
 #pragma unroll
                         for (int j = 0; j < kMomCols; j++) {
                             const double a = s32[j / 2][j & 1], b = sy32[j / 2][j & 1], c = syy32[j / 2][j & 1];
@@ -327,49 +412,7 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                             Sy[j] += y0c * a + b;
                             Syy[j] += y0c * y0c * a + 2.0 * y0c * b + c;
                         }
-#pragma unroll
-                        for (int q = 0; q < NP; q++) s32[q] = sy32[q] = syy32[q] = f2{0.f, 0.f};
-                    };
-                    const f2 thr2 = f2{p.thr, p.thr};
-                    // the next row's table word is read one iteration ahead, so its LDS
-                    // latency hides under this row's arithmetic
-                    int tnext = riy[0];
-                    for (int y = 0; y < p.img_h; y++) {
-                        const int tw = __builtin_amdgcn_readfirstlane(tnext);
-                        tnext = riy[y + 1];
-                        const int iy = (tw >> 5) - 4096, fq = tw & 31;
-                        if (iy + 1 < r0 || iy > r1) continue;  // whole row inactive (uniform)
-                        if (iy != cur_iy) {
-                            flush();
-                            cur_iy = iy;
-                            y0 = y;
-                            const bool ry0 = iy >= 0 && iy < p.h, ry1 = iy + 1 >= 0 && iy + 1 < p.h;
-#pragma unroll
-                            for (int j = 0; j < kMomCols; j++) {
-                                const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
-                                const float v00 = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
-                                const float v01 = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
-                                const float v10 = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
-                                const float v11 = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
-                                const float g = gx[j / 2][j & 1], f = fx[j / 2][j & 1];
-                                ra[j / 2][j & 1] = __builtin_fmaf(v01, f, v00 * g);
-                                rb[j / 2][j & 1] = __builtin_fmaf(v11, f, v10 * g);
-                            }
-                        }
-                        const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
-                        const float yr = (float)(y - y0);
-                        const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
-                        const f2 fy2 = f2{fy, fy}, gy2 = f2{gy, gy};
-#pragma unroll
-                        for (int q = 0; q < NP; q++) {
-                            const f2 v = __builtin_elementwise_fma(fy2, rb[q], gy2 * ra[q]);
-                            const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
-                            s32[q] = s32[q] + vs;
-                            sy32[q] = __builtin_elementwise_fma(vs, yr2, sy32[q]);
-                            syy32[q] = __builtin_elementwise_fma(vs, yrr2, syy32[q]);
-                        }
                     }
-                    flush();
                 }
 #pragma unroll
                 for (int j = 0; j < kMomCols; j++) {
@@ -528,7 +571,9 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
                                    int img_w, float thr, int separable, double* out, void* stream) {
     MVP_ABI_BEGIN
     MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
-    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8 + (size_t)img_h * 8;
+    // map, 2 column tables, row table, run starts / ends, run sums (fp64): moments_kernel's layout
+    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8 + (size_t)((img_h + 2) & ~1) * 4 +
+                       (size_t)((h + 2) & ~1) * 8 + (size_t)(h + 1) * 48;
     MVP_REQUIRE(lds <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image %dx%d exceed the LDS budget", h, w,
                 img_h, img_w);
     if (N == 0) return MVP_OK;

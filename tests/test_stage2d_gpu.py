@@ -136,18 +136,29 @@ def test_moments_golden_revert(lib):
     _check_moments(out[0], d["out_rev"])
 
 
-@pytest.mark.parametrize("kind", ["dense", "peaked"])
+@pytest.mark.parametrize("kind", ["dense", "peaked", "threshold"])
 @pytest.mark.parametrize("separable", [True, False])
 def test_moments_full_frame_vs_oracle(lib, kind, separable):
     """1280x720 revert of a 64x48 map against oracle warp + fp64 moments, on both
-    kernel paths (the separable column-resident path with bbox culling, and the
-    general per-pixel path); dense maps (every pixel above threshold) and peaked
-    maps (small active region, culling exercised)."""
+    kernel paths (the separable column-resident path with bbox culling and per-run
+    closed forms, and the general per-pixel path); dense maps (every pixel above
+    threshold: closed forms), peaked maps (small active region, culling exercised)
+    and maps whose taps sit at and around the threshold (thr, thr·(1 ± 1e-6),
+    thr·(1 ± 3e-6): the classification margins and the per-row walk)."""
     _lib, geometry = lib
     rng = np.random.default_rng(3)
     hm = _planted_heatmaps(rng, 1)
     if kind == "dense":
         hm = np.abs(hm) + 0.02
+    elif kind == "threshold":
+        # the separable path evaluates a pixel as gy·a + fy·b, within ~2 f32 ulps of
+        # OpenCV's four-product order: a map whose every cell straddles the threshold by a
+        # few ulps flips thousands of pixels there, by design (documented tolerance)
+        if separable:
+            pytest.skip("near-threshold maps: exact-order path here, separable path in "
+                        "test_moments_closed_form_matches_walk")
+        near = np.float32(0.01) * (1 + np.array([0, 1e-6, -1e-6, 3e-6, -3e-6, 1e-3, -1e-3], np.float32))
+        hm = rng.choice(near, size=hm.shape).astype(np.float32)
     else:
         yy, xx = np.mgrid[0:64, 0:48]
         for k in range(17):
@@ -168,3 +179,27 @@ def test_moments_full_frame_vs_oracle(lib, kind, separable):
     np.testing.assert_allclose(out[0][:, :2], ref[:, :2], rtol=2e-6, atol=1e-6)
     scale = (ref[:, 0] ** 2 + ref[:, 1] ** 2)[:, None]
     assert np.all(np.abs(out[0][:, 2:] - ref[:, 2:]) <= 2e-6 * np.abs(ref[:, 2:]) + 1e-9 * scale + 1e-9)
+
+
+@pytest.mark.parametrize("kind", ["dense", "peaked", "threshold", "random"])
+def test_moments_closed_form_matches_walk(lib, kind):
+    """Separable path: the per-run closed forms (columns whose 4 taps are all >= thr·(1+2e-6)
+    summed as a·G + b·F, all < thr·(1-2e-6) skipped) against walking every row of every
+    column with the same pixel formula (separable=2): identical threshold decisions, so
+    only the f32/fp64 summation differs."""
+    _lib, geometry = lib
+    rng = np.random.default_rng(9)
+    hm = _planted_heatmaps(rng, 2)
+    if kind == "dense":
+        hm = np.abs(hm) + 0.02
+    elif kind == "threshold":
+        near = np.float32(0.01) * (1 + np.array([0, 1e-6, -1e-6, 2e-6, -2e-6, 3e-6, -3e-6, 1e-3], np.float32))
+        hm = rng.choice(near, size=hm.shape).astype(np.float32)
+    elif kind == "random":
+        hm = (rng.standard_normal(hm.shape) * 0.05).astype(np.float32)
+    g = geometry.CropGeometry.whole_image(1280, 720)
+    fast = _moments(_lib, hm, g.revert_minv, 720, 1280, separable=1)
+    walk = _moments(_lib, hm, g.revert_minv, 720, 1280, separable=2)
+    np.testing.assert_allclose(fast[..., :2], walk[..., :2], rtol=1e-6, atol=1e-6)
+    scale = (walk[..., 0] ** 2 + walk[..., 1] ** 2)[..., None]
+    assert np.all(np.abs(fast[..., 2:] - walk[..., 2:]) <= 1e-6 * np.abs(walk[..., 2:]) + 1e-9 * scale + 1e-9)
