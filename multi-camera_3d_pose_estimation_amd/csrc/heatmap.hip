@@ -308,13 +308,16 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                     g2 += gy * yr * yr;
                     f2 += fy * yr * yr;
                 }
+                // folded with the run's centred offset y0c = start - cy: a closed-form column
+                // adds a·q[0] + b·q[1] to S, a·q[2] + b·q[3] to Sy and a·q[4] + b·q[5] to Syy
+                const double y0c = rstart[r] - cy;
                 double* q = rsum + 6 * r;
                 q[0] = g0;
                 q[1] = f0;
-                q[2] = g1;
-                q[3] = f1;
-                q[4] = g2;
-                q[5] = f2;
+                q[2] = y0c * g0 + g1;
+                q[3] = y0c * f0 + f1;
+                q[4] = y0c * y0c * g0 + 2.0 * y0c * g1 + g2;
+                q[5] = y0c * y0c * f0 + 2.0 * y0c * f1 + f2;
             }
             __syncthreads();
             // Lanes own column pairs (packed f32 math).  Per run, a column's two
@@ -374,12 +377,9 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                             const bool empty = closed && v00 < thr_lo2 && v01 < thr_lo2 && v10 < thr_lo2 && v11 < thr_lo2;
                             if (full) {
                                 const double da = a, db = b;
-                                const double s0 = da * q[0] + db * q[1];
-                                const double s1 = da * q[2] + db * q[3];
-                                const double s2 = da * q[4] + db * q[5];
-                                S[j] += s0;
-                                Sy[j] += y0c * s0 + s1;
-                                Syy[j] += y0c * y0c * s0 + 2.0 * y0c * s1 + s2;
+                                S[j] = fma(da, q[0], fma(db, q[1], S[j]));
+                                Sy[j] = fma(da, q[2], fma(db, q[3], Sy[j]));
+                                Syy[j] = fma(da, q[4], fma(db, q[5], Syy[j]));
                             }
                             const bool walk = !full && !empty;
                             mixed |= walk;
