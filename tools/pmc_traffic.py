@@ -13,7 +13,8 @@ import sys
 from collections import defaultdict
 
 GROUPS = {"backbone": ("conv_mfma_kernel", "stem_kernel", "stem_mfma_kernel", "fuse_sum_kernel", "conv1x1_kernel",
-                       "basic_block", "wsconv", "tconv_kernel"), "moments": ("moments_kernel",),
+                       "conv1x1_pair_kernel", "basic_block", "wsconv", "tconv_kernel", "tblock32_kernel",
+                       "s2conv_kernel"), "moments": ("moments_kernel",),
           "preprocess": ("preprocess_kernel",), "decode": ("decode_kernel",),
           "triangulate": ("triangulate_reference_kernel",
                           "triangulate_all_views_kernel")}
