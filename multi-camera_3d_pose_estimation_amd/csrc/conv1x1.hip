@@ -173,10 +173,14 @@ struct PPair {
     long n_pix;
 };
 
-constexpr int kPairThreads = 512;  // 8 waves per workgroup; <= 128 VGPRs so two workgroups fit a CU
+// threads per workgroup (one workgroup per CU, 2 waves per SIMD): 12-wave workgroups
+// (3 per SIMD) measured slower, 1067 vs 1018 us per join
+template <int KCH>
+constexpr int pair_threads() { return 512; }
 
 template <int KCH>
-__global__ __launch_bounds__(kPairThreads, 2) void conv1x1_pair_kernel(PPair p) {
+__global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PPair p) {
+    constexpr int kPairThreads = pair_threads<KCH>();
     constexpr int BM = 256, NCT = BM / 16, CIN = KCH * 32;
     constexpr int S1 = KCH * 4 * BM;  // expand weight slots [chunk][q][row]
     constexpr int S2 = 8 * 4 * 64;    // reduce weight slots [chunk][q][row]
@@ -381,6 +385,7 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
     }
     const long units = (c.n_pix + 15) / 16;
     auto go = [&](auto kern, int kch) {
+        const int kPairThreads = kch == 2 ? pair_threads<2>() : pair_threads<4>();
         const int lds = (kch * 4 * 256 + 8 * 4 * 64) * 16;
         static int per_cu[2] = {0, 0};
         int& pc = per_cu[kch == 4];
@@ -389,7 +394,7 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
             MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, kPairThreads, lds));
             if (pc < 1) pc = 1;
         }
-        const long grid = std::min<long>((long)g_cus1 * pc, (units + 7) / 8);
+        const long grid = std::min<long>((long)g_cus1 * pc, (units + kPairThreads / 64 - 1) / (kPairThreads / 64));
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kPairThreads), lds, s, p);
     };
     if (cin == 64) go(conv1x1_pair_kernel<2>, 2);
