@@ -28,6 +28,10 @@ struct ConvLaunch {
 
 void launch_conv(const ConvLaunch& c, hipStream_t s);
 
+// Heatmap head (conv1x1.hip): 1x1 32 -> 17 + bias, f32 NCHW output; false otherwise
+// (or MVPOSE_NO_HEAD1X1=1).
+bool launch_head1x1(const ConvLaunch& c, hipStream_t s);
+
 // Direct-load 1x1 conv (conv1x1.hip); false when the conv is not a bf16-output 1x1.
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s);
 

@@ -326,6 +326,47 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
     }
 }
 
+// ------------------------------------------------------------ heatmap head
+// HeatmapHead.final_layer: 1x1 conv 32 -> K (17) + bias, f32 NCHW heatmaps out (the
+// decode / moments input layout).  One lane per pixel: its 32 bf16 inputs (4 x 16 B),
+// K x 32 f32 FMAs against weights that are uniform across the wave (scalar loads),
+// K coalesced f32 plane stores.  Memory-bound (64 B in, 68 B out per pixel); the
+// generic MFMA kernel spent 197 us per 1024 crops on it (masked 4x48 tiles, f32
+// NCHW scatter).  Sums in f32 in channel order.
+template <int KOUT>
+__global__ __launch_bounds__(256) void head1x1_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, float* __restrict__ y,
+                                                      long n_pix, int hw) {
+    const long pix = (long)blockIdx.x * 256 + threadIdx.x;
+    if (pix >= n_pix) return;
+    float xv[32];
+    const uint4* src = reinterpret_cast<const uint4*>(x + pix * 32);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint4 u = src[q];
+        const uint32_t e[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            xv[q * 8 + 2 * j] = bf16_to_f32(e[j] & 0xffff);
+            xv[q * 8 + 2 * j + 1] = bf16_to_f32(e[j] >> 16);
+        }
+    }
+    const long n = pix / hw, pp = pix - n * hw;
+    float* out = y + n * KOUT * hw + pp;
+#pragma unroll
+    for (int k = 0; k < KOUT; k++) {
+        float acc = bias[k];
+        const uint32_t* wk = reinterpret_cast<const uint32_t*>(w + k * 32);
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const uint32_t wp = wk[c];
+            acc = __builtin_fmaf(bf16_to_f32(wp & 0xffff), xv[2 * c], acc);
+            acc = __builtin_fmaf(bf16_to_f32(wp >> 16), xv[2 * c + 1], acc);
+        }
+        out[(long)k * hw] = acc;
+    }
+}
+
 int g_cus1 = 0;
 
 template <int BM, int KCH>
@@ -400,6 +441,19 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
     if (cin == 64) go(conv1x1_pair_kernel<2>, 2);
     else go(conv1x1_pair_kernel<4>, 4);
     MVP_HIP(hipGetLastError());
+}
+
+bool launch_head1x1(const ConvLaunch& c, hipStream_t s) {
+    if (c.ks != 1 || c.stride != 1 || !c.out_f32_nchw || c.Cin != 32 || c.Cout != 17 || c.res || c.relu || c.x2)
+        return false;
+    const char* e = getenv("MVPOSE_NO_HEAD1X1");  // diagnostics/tests: generic conv kernel
+    if (e && e[0] == '1') return false;
+    const long n_pix = (long)c.N * c.H * c.W;
+    if (n_pix == 0) return true;
+    hipLaunchKernelGGL(head1x1_kernel<17>, dim3((unsigned)((n_pix + 255) / 256)), dim3(256), 0, s, c.x, c.w, c.bias,
+                       c.yf, n_pix, c.H * c.W);
+    MVP_HIP(hipGetLastError());
+    return true;
 }
 
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {

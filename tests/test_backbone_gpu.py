@@ -150,3 +150,24 @@ def test_pair_fusion_matches_unfused(models, monkeypatch):
     assert rel < 2e-2, rel
     assert not torch.equal(a, b)  # the fused path ran (its summation order shows somewhere)
     assert fused.arena_bytes <= plain.arena_bytes
+
+
+def test_head_kernel_matches_generic(models, monkeypatch):
+    """The dedicated heatmap-head kernel (1x1 32 -> 17, f32 NCHW, VALU FMAs in channel
+    order) against the generic MFMA conv on the same bf16 features: f32 summation
+    order only."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(19)
+    monkeypatch.setenv("MVPOSE_NO_HEAD1X1", "1")
+    plain = hrnet.HRNetBackbone(sd, max_batch=3)
+    monkeypatch.delenv("MVPOSE_NO_HEAD1X1")
+    head = hrnet.HRNetBackbone(sd, max_batch=3)
+    g = torch.Generator().manual_seed(8)
+    x = torch.zeros((3, 256, 192, 4))
+    x[..., :3] = torch.randn((3, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = head.forward(xb)
+    torch.cuda.synchronize()
+    scale = a.abs().max().item()
+    assert (a - b).abs().max().item() <= 1e-5 * scale
