@@ -130,7 +130,7 @@ def main():
     out = {}
 
     def step():
-        o = pipe.process(frames, out)
+        o = pipe.process(frames, out, overlap_moments=True)  # moments beside the next backbone
         mdist.gather_frames(o["kpts_3d"], world * B)   # per-step 3D joints to rank 0 (204 B/frame)
         return o
 

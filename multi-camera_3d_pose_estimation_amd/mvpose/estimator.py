@@ -6,7 +6,12 @@ Per batch of N camera-frames (uint8, device-resident):
     mvp_graph_forward   HRNet-W32 + HeatmapHead on 2N crops (bf16 MFMA)
     mvp_heatmap_decode  flip-test average + MSRAHeatmap decode + restore
     mvp_heatmap_moments revert_heatmap + get_heatmap_means_cov
-All on one stream; no host synchronisation inside `run`.
+No host synchronisation inside `run`.  By default everything runs on the current
+stream; with overlap_moments=True the moments kernel (whose output nothing else
+on the path reads: triangulation uses the decoded keypoints) is issued on a side
+stream so that it runs beside the next batch's backbone.  The flip-averaged
+heatmaps it reads are double-buffered for that, and the returned
+"moments_done" event orders any consumer of "gaussians" (wait_moments()).
 """
 from __future__ import annotations
 
@@ -69,16 +74,29 @@ class BatchPoseEstimator:
         nc = n * (2 if flip_test else 1)
         self.crops = torch.empty((nc, INPUT_HW[0], INPUT_HW[1], 4), dtype=torch.bfloat16, device=self.device)
         self.heatmaps = torch.empty((nc, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=self.device)
-        self.avg = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=self.device)
+        # two flip-averaged heatmap buffers: decode of batch i+1 may start while the
+        # side-stream moments of batch i still reads the other one
+        self._avg = [torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=self.device)
+                     for _ in range(2)]
+        self._avg_busy = [None, None]   # side-stream event after the last moments read of each buffer
+        self._avg_k = 1                 # buffer the last run wrote
+        self._side = None
         self._mean = (ctypes.c_float * 3)(*MEAN)
         self._std = (ctypes.c_float * 3)(*STD)
         self._flip = (ctypes.c_int * N_JOINTS)(*COCO_FLIP_INDICES)
 
+    @property
+    def avg(self) -> torch.Tensor:
+        """Flip-averaged heatmaps of the last run (valid until the run after next)."""
+        return self._avg[self._avg_k]
+
     def run(self, frames: torch.Tensor, n_views: int = 1, kpts_tkv: torch.Tensor | None = None,
-            argmax: bool = False):
+            argmax: bool = False, overlap_moments: bool = False):
         """frames: (N, H, W, 3) uint8 on the GPU, ordered (t, v) when n_views > 1.
         Returns dict: keypoints (N,17,2) f32 image px, scores (N,17) f32,
-        gaussians (N,17,6) f64 [mx,my,vxx,vxy,vxy,vyy], and optionally argmax."""
+        gaussians (N,17,6) f64 [mx,my,vxx,vxy,vxy,vyy], and optionally argmax.
+        overlap_moments: gaussians are produced on a side stream; read them only after
+        wait_moments(out) (or a device synchronisation)."""
         if frames.dtype != torch.uint8 or not frames.is_cuda or not frames.is_contiguous():
             raise ValueError("frames must be a contiguous uint8 CUDA tensor (N, H, W, 3)")
         n, h, w, c = frames.shape
@@ -95,17 +113,44 @@ class BatchPoseEstimator:
         kp = torch.empty((n, N_JOINTS, 2), dtype=torch.float32, device=dev)
         sc = torch.empty((n, N_JOINTS), dtype=torch.float32, device=dev)
         am = torch.empty((n, N_JOINTS), dtype=torch.int32, device=dev) if argmax else None
-        avg = self.avg[:n]
+        k = self._avg_k ^ 1
+        main = torch.cuda.current_stream(dev)
+        if self._avg_busy[k] is not None:       # moments of two runs ago still reading buffer k
+            main.wait_event(self._avg_busy[k])
+            self._avg_busy[k] = None
+        self._avg_k = k
+        avg = self._avg[k][:n]
         call("mvp_heatmap_decode", _ptr(hm[:n]), _ptr(hm[n:]) if self.flip_test else None, n, N_JOINTS,
              HEATMAP_HW[0], HEATMAP_HW[1], self._flip, 1, _ptr(self.center_scale), INPUT_HW[1], INPUT_HW[0],
              _ptr(avg), _ptr(kp), _ptr(sc), _ptr(am), _ptr(kpts_tkv), int(n_views), s)
         gauss = torch.empty((n, N_JOINTS, 6), dtype=torch.float64, device=dev)
+        done = None
+        if overlap_moments:
+            if self._side is None:
+                self._side = torch.cuda.Stream(dev)
+            decoded = torch.cuda.Event()
+            decoded.record(main)
+            self._side.wait_event(decoded)
+            ms = ctypes.c_void_p(self._side.cuda_stream)
+            gauss.record_stream(self._side)
+        else:
+            ms = s
         call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(self.revert_minv),
-             h, w, ctypes.c_float(HEATMAP_THR), int(self.separable), _ptr(gauss), s)
-        out = {"keypoints": kp, "scores": sc, "gaussians": gauss, "heatmaps": avg}
+             h, w, ctypes.c_float(HEATMAP_THR), int(self.separable), _ptr(gauss), ms)
+        if overlap_moments:
+            done = torch.cuda.Event()
+            done.record(self._side)
+            self._avg_busy[k] = done
+        out = {"keypoints": kp, "scores": sc, "gaussians": gauss, "heatmaps": avg, "moments_done": done}
         if argmax:
             out["argmax"] = am
         return out
+
+    @staticmethod
+    def wait_moments(out: dict) -> None:
+        """Order the current stream after an overlapped run's moments (no-op otherwise)."""
+        if out.get("moments_done") is not None:
+            torch.cuda.current_stream().wait_event(out["moments_done"])
 
     # ---- the reference's per-frame callable contract (pose_estimation.py:88, :104-110)
     def predict(self, frame, return_full_heatmaps=False):

@@ -6,6 +6,10 @@ process(frames (T, V, H, W, 3) uint8 on GPU) returns, device-resident:
     kpts_2d     (T, 17, 3, V) float32   [x, y, score] per camera   (pose_estimation.py:135)
     heatmaps_2d (T, V, 17, 6) float64   [mx, my, vxx, vxy, vxy, vyy] (mmpose_pose_estimation.py:208-210)
     kpts_3d     (T, 17, 3)    float32   triangulated                 (pose_estimation.py:319-322)
+
+process(..., overlap_moments=True) computes heatmaps_2d on a side stream beside the
+next batch's backbone (triangulation reads only kpts_2d); call wait(out) before reading
+heatmaps_2d on the current stream.
 """
 from __future__ import annotations
 
@@ -33,7 +37,7 @@ class MultiViewPipeline:
     def max_frames(self) -> int:
         return self.estimator.max_frames // self.n_views
 
-    def process(self, frames: torch.Tensor, out: dict | None = None) -> dict:
+    def process(self, frames: torch.Tensor, out: dict | None = None, overlap_moments: bool = False) -> dict:
         T, V = frames.shape[:2]
         if V != self.n_views:
             raise ValueError(f"frames carry {V} views, pipeline has {self.n_views} cameras")
@@ -43,11 +47,20 @@ class MultiViewPipeline:
         if "kpts_2d" not in out or tuple(out["kpts_2d"].shape) != (T, N_JOINTS, 3, V):
             out["kpts_2d"] = torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)
             out.pop("kpts_3d", None)
-        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"])
+        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments)
         out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
+        if r["moments_done"] is not None:
+            out["moments_done"] = r["moments_done"]
+        else:
+            out.pop("moments_done", None)
         out["kpts_3d"] = ops.triangulate(out["kpts_2d"], self.cams, self.camera_indices, mode=self.mode,
                                          out=out.get("kpts_3d"))
         return out
+
+    @staticmethod
+    def wait(out: dict) -> None:
+        """Order the current stream after an overlapped process()'s heatmaps_2d."""
+        BatchPoseEstimator.wait_moments(out)
 
     def process_stream(self, frames: torch.Tensor) -> dict:
         """Arbitrary-length sequence (T, V, H, W, 3): chunked to the estimator's batch."""

@@ -49,3 +49,23 @@ def test_predict_contract(pipe):
     assert inst["keypoints"].shape == (1, 17, 2) and inst["keypoints"].dtype == np.float32
     assert inst["keypoint_scores"].shape == (1, 17)
     assert hm.shape == (17, 6) and hm.dtype == np.float64
+
+
+def test_overlapped_moments_match_serial(pipe):
+    """overlap_moments=True (moments on a side stream beside the next batch, double-buffered
+    heatmaps) gives bit-identical outputs to the serial path, across buffer reuse."""
+    p, _, syn = pipe
+    T = 4
+    fa = torch.tensor(syn.make_frames(T * 2, seed=11).reshape(T, 2, 720, 1280, 3), device="cuda")
+    fb = torch.tensor(syn.make_frames(T * 2, seed=12).reshape(T, 2, 720, 1280, 3), device="cuda")
+    serial = [{k: v.clone() for k, v in p.process(f).items()} for f in (fa, fb)]
+    outs = [p.process(f, {}, overlap_moments=True) for f in (fa, fb, fa, fb)]
+    for o in outs:
+        assert o["moments_done"] is not None
+        p.wait(o)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        ref = serial[i % 2]
+        for k in ("kpts_2d", "heatmaps_2d", "kpts_3d"):
+            assert torch.equal(torch.nan_to_num(o[k]), torch.nan_to_num(ref[k])), (i, k)
+    assert "moments_done" not in p.process(fa, outs[0])
