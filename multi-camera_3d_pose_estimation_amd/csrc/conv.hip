@@ -560,7 +560,21 @@ void launch_plane(const ConvParams& p, hipStream_t s) {
         else
             launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
     } else {
-        if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
+        const char* e = getenv("MVPOSE_S2_TILE");  // tuning experiments only
+        const int v = e ? atoi(e) : 0;  // 7: the pre-sweep 4-wave default
+        if (v == 1 && p.Wo % 8 == 0 && p.Ho % 16 == 0) return launch_tile<KS, S, 16, 8, 1, 4>(p, s);
+        if (v == 2 && p.Wo % 8 == 0 && p.Ho % 8 == 0) return launch_tile<KS, S, 8, 8, 2, 4>(p, s);
+        if (v == 3 && p.Wo % 16 == 0 && p.Ho % 8 == 0) return launch_tile<KS, S, 8, 16, 1, 4>(p, s);
+        if (v == 4 && p.Wo % 16 == 0 && p.Ho % 4 == 0) return launch_tile<KS, S, 4, 16, 2, 4>(p, s);
+        if (v == 5 && p.Wo % 8 == 0 && p.Ho % 16 == 0) return launch_tile<KS, S, 16, 8, 1, 8>(p, s);
+        if (v == 6 && p.Wo % 16 == 0 && p.Ho % 8 == 0) return launch_tile<KS, S, 8, 16, 1, 8>(p, s);
+        // Cin >= 64 (stem conv2 64@128x96, transition1.1 256@64x48): 16x8-pixel tiles on
+        // 8 waves (2 per SIMD) sharing one weight slice — 800 -> 650-710 us and
+        // 1052 -> 771 us per 1024 crops (tools/s2_tile_sweep.py); the 32-ch planes keep
+        // the 4-wave tiles (55 vs 62 us)
+        if (v == 0 && p.Cin >= 64 && p.Wo % 8 == 0 && p.Ho % 16 == 0)
+            launch_tile<KS, S, 16, 8, 1, 8>(p, s);
+        else if (p.Wo % 16 == 0 && p.Ho % 4 == 0)
             launch_tile<KS, S, 4, 16, 1, 4>(p, s);
         else if (p.Wo % 8 == 0 && p.Ho % 8 == 0)
             launch_tile<KS, S, 8, 8, 1, 4>(p, s);
