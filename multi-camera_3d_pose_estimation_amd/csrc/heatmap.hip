@@ -17,6 +17,9 @@
 //    covariance.  The 17 x H x W reverted heatmap is never written: each lane
 //    evaluates the warp for its image pixels from the LDS-resident map and
 //    accumulates fp64 raw moments.
+#include <algorithm>
+#include <cstdlib>
+
 #include "mvp_common.h"
 
 namespace {
@@ -195,13 +198,18 @@ struct MomParams {
     float thr;
     int separable;  // host-verified: source column depends on x only, source row on y only
                     // (2: the separable path without the per-run closed forms)
+    int jpb;        // joints per workgroup: the warp tables depend on the crop only, so a
+                    // workgroup builds them once and reuses them for jpb maps of its crop
 };
 
 constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
 constexpr int kMomBlock = 320;         // 5 waves x 4 columns per lane = 1280: every lane busy on 1280-wide frames
 constexpr int kMomCols = 4;            // image columns per lane (separable path)
+constexpr int kMomJointsPerBlock = 17;  // maps per workgroup sharing one set of warp tables (all of a
+                                        // COCO crop: 8680-8717 -> 8823-8832 frames/s in the bench vs 1)
 
-// One workgroup per (crop, joint) map.  The fixed-point warp of an image pixel
+// One workgroup per (crop, group of jpb joints); the column / row / run tables are
+// built once per workgroup, then the maps of its joints are processed in turn.  The fixed-point warp of an image pixel
 // (OpenCV WarpAffineInvoker) is X = (X0(y) + adelta(x)) >> 5, Y = (Y0(y) + bdelta(x)) >> 5.
 // Separable path (axis-aligned crops, the only ones the pipeline makes): each
 // lane owns image columns (source column ix and weight fx fixed), walks the rows,
@@ -223,277 +231,285 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     double* rsum = reinterpret_cast<double*>(rend + ((p.h + 2) & ~1));
     __shared__ double red[6][kMomBlock / 64];
     __shared__ int bbox[4];
-    const long map = blockIdx.x;
-    const int n = map / p.K;
+    const int groups = (p.K + p.jpb - 1) / p.jpb;
+    const int n = blockIdx.x / groups;
+    const int k0 = (blockIdx.x - n * groups) * p.jpb, k1 = min(p.K, k0 + p.jpb);
     const double* M = p.minv + 6 * n;
-    const float* src = p.hm + map * p.h * p.w;
-    if (threadIdx.x == 0) {
-        bbox[0] = p.w;
-        bbox[1] = -1;
-        bbox[2] = p.h;
-        bbox[3] = -1;
-    }
-    __syncthreads();
-    const float thr_lo = p.thr * (1.f - 1e-6f);
-    int c0 = p.w, c1 = -1, r0 = p.h, r1 = -1;
-    for (int i = threadIdx.x; i < p.h * p.w; i += kMomBlock) {
-        const float v = src[i];
-        shm[i] = v;
-        if (!(v < thr_lo)) {  // active (or NaN)
-            const int r = i / p.w, c = i - (i / p.w) * p.w;
-            c0 = min(c0, c);
-            c1 = max(c1, c);
-            r0 = min(r0, r);
-            r1 = max(r1, r);
-        }
-    }
     for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
         sad[x] = (int)rint(M[0] * x * 1024.0);
         sbd[x] = (int)rint(M[3] * x * 1024.0);
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        c0 = min(c0, __shfl_xor(c0, off));
-        c1 = max(c1, __shfl_xor(c1, off));
-        r0 = min(r0, __shfl_xor(r0, off));
-        r1 = max(r1, __shfl_xor(r1, off));
-    }
-    if ((threadIdx.x & 63) == 0) {
-        atomicMin(&bbox[0], c0);
-        atomicMax(&bbox[1], c1);
-        atomicMin(&bbox[2], r0);
-        atomicMax(&bbox[3], r1);
-    }
     __syncthreads();
-    c0 = bbox[0];
-    c1 = bbox[1];
-    r0 = bbox[2];
-    r1 = bbox[3];
     const double cx = 0.5 * p.img_w, cy = 0.5 * p.img_h;  // centred coordinates (cancellation)
-    double t[6] = {0, 0, 0, 0, 0, 0};
-    if (c1 >= 0) {
-        if (p.separable) {
-            // Row table: source row iy and weight index fq of every image row (uniform per row).
-            // packed (iy + 4096) << 5 | fq, one word per row
-            for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
-                rstart[r] = p.img_h;
-                rend[r] = 0;
+    if (p.separable) {
+        // Row table: source row iy and weight index fq of every image row (uniform per row).
+        // packed (iy + 4096) << 5 | fq, one word per row
+        for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
+            rstart[r] = p.img_h;
+            rend[r] = 0;
+        }
+        __syncthreads();
+        for (int y = threadIdx.x; y < p.img_h; y += kMomBlock) {
+            const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
+            const int iy = Yq >> 5;
+            riy[y] = ((iy + 4096) << 5) | (Yq & 31);
+            if (iy >= -1 && iy < p.h) {  // rows of other runs read no map row: zero
+                atomicMin(&rstart[iy + 1], y);
+                atomicMax(&rend[iy + 1], y + 1);
             }
-            __syncthreads();
-            for (int y = threadIdx.x; y < p.img_h; y += kMomBlock) {
-                const int Yq = ((int)rint((M[4] * y + M[5]) * 1024.0) + 16 + sbd[0]) >> 5;
-                const int iy = Yq >> 5;
-                riy[y] = ((iy + 4096) << 5) | (Yq & 31);
-                if (iy >= -1 && iy < p.h) {  // rows of other runs read no map row: zero
-                    atomicMin(&rstart[iy + 1], y);
-                    atomicMax(&rend[iy + 1], y + 1);
-                }
+        }
+        __syncthreads();
+        // Per run (the affine row map is monotone, so a run is contiguous): sums over its
+        // rows of gy, fy, gy·yr, fy·yr, gy·yr², fy·yr² (yr = row - run start), exact in fp64.
+        // A column whose 4 taps are all >= thr·(1+2e-6) has every pixel of the run above
+        // the threshold (a bilinear value is a convex combination of its taps): its run
+        // sums are a·G + b·F in closed form.  Taps all < thr·(1-2e-6): all zero.  Only
+        // the remaining ("mixed") columns walk the run's rows.
+        for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
+            double g0 = 0, f0 = 0, g1 = 0, f1 = 0, g2 = 0, f2 = 0;
+            for (int y = rstart[r]; y < rend[r]; y++) {
+                const double fy = (double)(riy[y] & 31) * (1.0 / 32.0), gy = 1.0 - fy;
+                const double yr = y - rstart[r];
+                g0 += gy;
+                f0 += fy;
+                g1 += gy * yr;
+                f1 += fy * yr;
+                g2 += gy * yr * yr;
+                f2 += fy * yr * yr;
             }
-            __syncthreads();
-            // Per run (the affine row map is monotone, so a run is contiguous): sums over its
-            // rows of gy, fy, gy·yr, fy·yr, gy·yr², fy·yr² (yr = row - run start), exact in fp64.
-            // A column whose 4 taps are all >= thr·(1+2e-6) has every pixel of the run above
-            // the threshold (a bilinear value is a convex combination of its taps): its run
-            // sums are a·G + b·F in closed form.  Taps all < thr·(1-2e-6): all zero.  Only
-            // the remaining ("mixed") columns walk the run's rows.
-            for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
-                double g0 = 0, f0 = 0, g1 = 0, f1 = 0, g2 = 0, f2 = 0;
-                for (int y = rstart[r]; y < rend[r]; y++) {
-                    const double fy = (double)(riy[y] & 31) * (1.0 / 32.0), gy = 1.0 - fy;
-                    const double yr = y - rstart[r];
-                    g0 += gy;
-                    f0 += fy;
-                    g1 += gy * yr;
-                    f1 += fy * yr;
-                    g2 += gy * yr * yr;
-                    f2 += fy * yr * yr;
-                }
-                // folded with the run's centred offset y0c = start - cy: a closed-form column
-                // adds a·q[0] + b·q[1] to S, a·q[2] + b·q[3] to Sy and a·q[4] + b·q[5] to Syy
-                const double y0c = rstart[r] - cy;
-                double* q = rsum + 6 * r;
-                q[0] = g0;
-                q[1] = f0;
-                q[2] = y0c * g0 + g1;
-                q[3] = y0c * f0 + f1;
-                q[4] = y0c * y0c * g0 + 2.0 * y0c * g1 + g2;
-                q[5] = y0c * y0c * f0 + 2.0 * y0c * f1 + f2;
+            // folded with the run's centred offset y0c = start - cy: a closed-form column
+            // adds a·q[0] + b·q[1] to S, a·q[2] + b·q[3] to Sy and a·q[4] + b·q[5] to Syy
+            const double y0c = rstart[r] - cy;
+            double* q = rsum + 6 * r;
+            q[0] = g0;
+            q[1] = f0;
+            q[2] = y0c * g0 + g1;
+            q[3] = y0c * f0 + f1;
+            q[4] = y0c * y0c * g0 + 2.0 * y0c * g1 + g2;
+            q[5] = y0c * y0c * f0 + 2.0 * y0c * f1 + f2;
+        }
+        __syncthreads();
+    }
+    const float thr_lo = p.thr * (1.f - 1e-6f);
+    for (int kj = k0; kj < k1; kj++) {
+        const long map = (long)n * p.K + kj;
+        const float* src = p.hm + map * p.h * p.w;
+        if (threadIdx.x == 0) {  // every thread read the previous map's bbox before its reduction barrier
+            bbox[0] = p.w;
+            bbox[1] = -1;
+            bbox[2] = p.h;
+            bbox[3] = -1;
+        }
+        __syncthreads();
+        int c0 = p.w, c1 = -1, r0 = p.h, r1 = -1;
+        for (int i = threadIdx.x; i < p.h * p.w; i += kMomBlock) {
+            const float v = src[i];
+            shm[i] = v;
+            if (!(v < thr_lo)) {  // active (or NaN)
+                const int r = i / p.w, c = i - (i / p.w) * p.w;
+                c0 = min(c0, c);
+                c1 = max(c1, c);
+                r0 = min(r0, r);
+                r1 = max(r1, r);
             }
-            __syncthreads();
-            // Lanes own column pairs (packed f32 math).  Per run, a column's two
-            // x-interpolated source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx are
-            // formed once; the pixel value is OpenCV's bilinear remap value (its fixed-point
-            // coordinates and 1/32 weights exactly) evaluated as gy a + fy b: within ~2 f32
-            // ulps of OpenCV's operation order ((v00 w0 + v01 w1) + v10 w2) + v11 w3 — far
-            // inside the reference's own f32 moment arithmetic (mmpose_pose_estimation.py:163-215).
-            // Mixed columns accumulate S, S*yr, S*yr^2 over the run's rows in f32, flushed
-            // to fp64 with the run's offset.
-            typedef float f2 __attribute__((ext_vector_type(2)));
-            constexpr int NP = kMomCols / 2;
-            const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
-            const float thr_hi = p.thr * (1.f + 2e-6f), thr_lo2 = p.thr * (1.f - 2e-6f);
-            const bool closed = p.separable != 2;  // 2: walk every column (diagnostics / tests)
-            for (int xb = threadIdx.x; xb < p.img_w; xb += kMomBlock * kMomCols) {
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            c0 = min(c0, __shfl_xor(c0, off));
+            c1 = max(c1, __shfl_xor(c1, off));
+            r0 = min(r0, __shfl_xor(r0, off));
+            r1 = max(r1, __shfl_xor(r1, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&bbox[0], c0);
+            atomicMax(&bbox[1], c1);
+            atomicMin(&bbox[2], r0);
+            atomicMax(&bbox[3], r1);
+        }
+        __syncthreads();
+        c0 = bbox[0];
+        c1 = bbox[1];
+        r0 = bbox[2];
+        r1 = bbox[3];
+        double t[6] = {0, 0, 0, 0, 0, 0};
+        if (c1 >= 0) {
+            if (p.separable) {
+                // Lanes own column pairs (packed f32 math).  Per run, a column's two
+                // x-interpolated source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx are
+                // formed once; the pixel value is OpenCV's bilinear remap value (its fixed-point
+                // coordinates and 1/32 weights exactly) evaluated as gy a + fy b: within ~2 f32
+                // ulps of OpenCV's operation order ((v00 w0 + v01 w1) + v10 w2) + v11 w3 — far
+                // inside the reference's own f32 moment arithmetic (mmpose_pose_estimation.py:163-215).
+                // Mixed columns accumulate S, S*yr, S*yr^2 over the run's rows in f32, flushed
+                // to fp64 with the run's offset.
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                constexpr int NP = kMomCols / 2;
+                const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
+                const float thr_hi = p.thr * (1.f + 2e-6f), thr_lo2 = p.thr * (1.f - 2e-6f);
+                const bool closed = p.separable != 2;  // 2: walk every column (diagnostics / tests)
+                for (int xb = threadIdx.x; xb < p.img_w; xb += kMomBlock * kMomCols) {
 #pragma clang fp contract(off)
-                int ix[kMomCols];
-                bool on[kMomCols];
-                float gx[kMomCols], fx[kMomCols];
-                bool any = false;
+                    int ix[kMomCols];
+                    bool on[kMomCols];
+                    float gx[kMomCols], fx[kMomCols];
+                    bool any = false;
 #pragma unroll
-                for (int j = 0; j < kMomCols; j++) {
-                    const int x = xb + j * kMomBlock;
-                    const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
-                    ix[j] = X >> 5;
-                    const float f = (float)(X & 31) * (1.f / 32.f);
-                    fx[j] = f;
-                    gx[j] = 1.f - f;
-                    on[j] = x < p.img_w && ix[j] + 1 >= c0 && ix[j] <= c1;
-                    any |= on[j];
-                }
-                double S[kMomCols], Sy[kMomCols], Syy[kMomCols];
+                    for (int j = 0; j < kMomCols; j++) {
+                        const int x = xb + j * kMomBlock;
+                        const int X = (x < p.img_w) ? ((X0 + sad[x]) >> 5) : 0;
+                        ix[j] = X >> 5;
+                        const float f = (float)(X & 31) * (1.f / 32.f);
+                        fx[j] = f;
+                        gx[j] = 1.f - f;
+                        on[j] = x < p.img_w && ix[j] + 1 >= c0 && ix[j] <= c1;
+                        any |= on[j];
+                    }
+                    double S[kMomCols], Sy[kMomCols], Syy[kMomCols];
 #pragma unroll
-                for (int j = 0; j < kMomCols; j++) S[j] = Sy[j] = Syy[j] = 0.0;
-                if (__any(any)) {
-                    const f2 thr2 = f2{p.thr, p.thr};
-                    for (int r = max(r0, 0); r <= min(r1 + 1, p.h); r++) {  // iy = r - 1 in [r0 - 1, r1]
-                        const int ys = rstart[r], ye = rend[r];
-                        if (ys >= ye) continue;
-                        const int iy = r - 1;
-                        const bool ry0 = iy >= 0, ry1 = iy + 1 < p.h;
-                        const double* q = rsum + 6 * r;
-                        const double y0c = ys - cy;
-                        f2 ra[NP], rb[NP];
-                        bool mixed = false;
+                    for (int j = 0; j < kMomCols; j++) S[j] = Sy[j] = Syy[j] = 0.0;
+                    if (__any(any)) {
+                        const f2 thr2 = f2{p.thr, p.thr};
+                        for (int r = max(r0, 0); r <= min(r1 + 1, p.h); r++) {  // iy = r - 1 in [r0 - 1, r1]
+                            const int ys = rstart[r], ye = rend[r];
+                            if (ys >= ye) continue;
+                            const int iy = r - 1;
+                            const bool ry0 = iy >= 0, ry1 = iy + 1 < p.h;
+                            const double* q = rsum + 6 * r;
+                            const double y0c = ys - cy;
+                            f2 ra[NP], rb[NP];
+                            bool mixed = false;
 #pragma unroll
-                        for (int j = 0; j < kMomCols; j++) {
-                            const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
-                            const float v00 = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
-                            const float v01 = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
-                            const float v10 = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
-                            const float v11 = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
-                            const float a = __builtin_fmaf(v01, fx[j], v00 * gx[j]);
-                            const float b = __builtin_fmaf(v11, fx[j], v10 * gx[j]);
-                            const bool full = closed && v00 >= thr_hi && v01 >= thr_hi && v10 >= thr_hi && v11 >= thr_hi;
-                            const bool empty = closed && v00 < thr_lo2 && v01 < thr_lo2 && v10 < thr_lo2 && v11 < thr_lo2;
-                            if (full) {
-                                const double da = a, db = b;
-                                S[j] = fma(da, q[0], fma(db, q[1], S[j]));
-                                Sy[j] = fma(da, q[2], fma(db, q[3], Sy[j]));
-                                Syy[j] = fma(da, q[4], fma(db, q[5], Syy[j]));
+                            for (int j = 0; j < kMomCols; j++) {
+                                const bool cx0 = ix[j] >= 0 && ix[j] < p.w, cx1 = ix[j] + 1 >= 0 && ix[j] + 1 < p.w;
+                                const float v00 = (on[j] && ry0 && cx0) ? shm[iy * p.w + ix[j]] : 0.f;
+                                const float v01 = (on[j] && ry0 && cx1) ? shm[iy * p.w + ix[j] + 1] : 0.f;
+                                const float v10 = (on[j] && ry1 && cx0) ? shm[(iy + 1) * p.w + ix[j]] : 0.f;
+                                const float v11 = (on[j] && ry1 && cx1) ? shm[(iy + 1) * p.w + ix[j] + 1] : 0.f;
+                                const float a = __builtin_fmaf(v01, fx[j], v00 * gx[j]);
+                                const float b = __builtin_fmaf(v11, fx[j], v10 * gx[j]);
+                                const bool full = closed && v00 >= thr_hi && v01 >= thr_hi && v10 >= thr_hi && v11 >= thr_hi;
+                                const bool empty = closed && v00 < thr_lo2 && v01 < thr_lo2 && v10 < thr_lo2 && v11 < thr_lo2;
+                                if (full) {
+                                    const double da = a, db = b;
+                                    S[j] = fma(da, q[0], fma(db, q[1], S[j]));
+                                    Sy[j] = fma(da, q[2], fma(db, q[3], Sy[j]));
+                                    Syy[j] = fma(da, q[4], fma(db, q[5], Syy[j]));
+                                }
+                                const bool walk = !full && !empty;
+                                mixed |= walk;
+                                ra[j / 2][j & 1] = walk ? a : 0.f;
+                                rb[j / 2][j & 1] = walk ? b : 0.f;
                             }
-                            const bool walk = !full && !empty;
-                            mixed |= walk;
-                            ra[j / 2][j & 1] = walk ? a : 0.f;
-                            rb[j / 2][j & 1] = walk ? b : 0.f;
-                        }
-                        if (!__any(mixed)) continue;  // every column of the wave done in closed form
-                        f2 s32[NP], sy32[NP], syy32[NP];
+                            if (!__any(mixed)) continue;  // every column of the wave done in closed form
+                            f2 s32[NP], sy32[NP], syy32[NP];
 #pragma unroll
-                        for (int k = 0; k < NP; k++) s32[k] = sy32[k] = syy32[k] = f2{0.f, 0.f};
-                        for (int y = ys; y < ye; y++) {
-                            const int fq = riy[y] & 31;
-                            const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
-                            const float yr = (float)(y - ys);
-                            const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
-                            const f2 fy2 = f2{fy, fy}, gy2 = f2{gy, gy};
+                            for (int k = 0; k < NP; k++) s32[k] = sy32[k] = syy32[k] = f2{0.f, 0.f};
+                            for (int y = ys; y < ye; y++) {
+                                const int fq = riy[y] & 31;
+                                const float fy = (float)fq * (1.f / 32.f), gy = 1.f - fy;
+                                const float yr = (float)(y - ys);
+                                const f2 yr2 = f2{yr, yr}, yrr2 = f2{yr * yr, yr * yr};
+                                const f2 fy2 = f2{fy, fy}, gy2 = f2{gy, gy};
 #pragma unroll
-                            for (int k = 0; k < NP; k++) {
-                                const f2 v = __builtin_elementwise_fma(fy2, rb[k], gy2 * ra[k]);
-                                const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
-                                s32[k] = s32[k] + vs;
-                                sy32[k] = __builtin_elementwise_fma(vs, yr2, sy32[k]);
-                                syy32[k] = __builtin_elementwise_fma(vs, yrr2, syy32[k]);
+                                for (int k = 0; k < NP; k++) {
+                                    const f2 v = __builtin_elementwise_fma(fy2, rb[k], gy2 * ra[k]);
+                                    const f2 vs = f2{v.x >= thr2.x ? v.x : 0.f, v.y >= thr2.y ? v.y : 0.f};  // h[h < thr] = 0
+                                    s32[k] = s32[k] + vs;
+                                    sy32[k] = __builtin_elementwise_fma(vs, yr2, sy32[k]);
+                                    syy32[k] = __builtin_elementwise_fma(vs, yrr2, syy32[k]);
+                                }
                             }
-                        }
 #pragma unroll
-                        for (int j = 0; j < kMomCols; j++) {
-                            const double a = s32[j / 2][j & 1], b = sy32[j / 2][j & 1], c = syy32[j / 2][j & 1];
-                            S[j] += a;
-                            Sy[j] += y0c * a + b;
-                            Syy[j] += y0c * y0c * a + 2.0 * y0c * b + c;
+                            for (int j = 0; j < kMomCols; j++) {
+                                const double a = s32[j / 2][j & 1], b = sy32[j / 2][j & 1], c = syy32[j / 2][j & 1];
+                                S[j] += a;
+                                Sy[j] += y0c * a + b;
+                                Syy[j] += y0c * y0c * a + 2.0 * y0c * b + c;
+                            }
                         }
                     }
-                }
 #pragma unroll
-                for (int j = 0; j < kMomCols; j++) {
-                    const double xc = (double)(xb + j * kMomBlock) - cx;
-                    t[0] += S[j];
-                    t[1] = fma(xc, S[j], t[1]);
-                    t[2] += Sy[j];
-                    t[3] = fma(xc * xc, S[j], t[3]);
-                    t[4] = fma(xc, Sy[j], t[4]);
-                    t[5] += Syy[j];
+                    for (int j = 0; j < kMomCols; j++) {
+                        const double xc = (double)(xb + j * kMomBlock) - cx;
+                        t[0] += S[j];
+                        t[1] = fma(xc, S[j], t[1]);
+                        t[2] += Sy[j];
+                        t[3] = fma(xc * xc, S[j], t[3]);
+                        t[4] = fma(xc, Sy[j], t[4]);
+                        t[5] += Syy[j];
+                    }
                 }
-            }
-        } else {
-            for (int y = 0; y < p.img_h; y++) {
-                const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
-                const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
-                const double yc = y - cy;
-                for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
-                    const int X = (X0 + sad[x]) >> 5;
-                    const int Y = (Y0 + sbd[x]) >> 5;
-                    const int ix = X >> 5, iy = Y >> 5;
-                    if (ix >= p.w || ix + 1 < 0 || iy >= p.h || iy + 1 < 0) continue;  // border value 0
-                    const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
-                    const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
-                    const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
-                    const bool x0 = ix >= 0, x1 = ix + 1 < p.w, y0 = iy >= 0, y1 = iy + 1 < p.h;
-                    const float v0 = (x0 && y0) ? shm[iy * p.w + ix] : 0.f;
-                    const float v1 = (x1 && y0) ? shm[iy * p.w + ix + 1] : 0.f;
-                    const float v2 = (x0 && y1) ? shm[(iy + 1) * p.w + ix] : 0.f;
-                    const float v3 = (x1 && y1) ? shm[(iy + 1) * p.w + ix + 1] : 0.f;
-                    float v = __fmul_rn(v0, w0);
-                    v = __fadd_rn(v, __fmul_rn(v1, w1));
-                    v = __fadd_rn(v, __fmul_rn(v2, w2));
-                    v = __fadd_rn(v, __fmul_rn(v3, w3));
-                    if (!(v >= p.thr)) continue;
-                    const double dv = v, xc = x - cx;
-                    t[0] += dv;
-                    t[1] += xc * dv;
-                    t[2] += yc * dv;
-                    t[3] += xc * xc * dv;
-                    t[4] += xc * yc * dv;
-                    t[5] += yc * yc * dv;
+            } else {
+                for (int y = 0; y < p.img_h; y++) {
+                    const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
+                    const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
+                    const double yc = y - cy;
+                    for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
+                        const int X = (X0 + sad[x]) >> 5;
+                        const int Y = (Y0 + sbd[x]) >> 5;
+                        const int ix = X >> 5, iy = Y >> 5;
+                        if (ix >= p.w || ix + 1 < 0 || iy >= p.h || iy + 1 < 0) continue;  // border value 0
+                        const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+                        const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
+                        const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
+                        const bool x0 = ix >= 0, x1 = ix + 1 < p.w, y0 = iy >= 0, y1 = iy + 1 < p.h;
+                        const float v0 = (x0 && y0) ? shm[iy * p.w + ix] : 0.f;
+                        const float v1 = (x1 && y0) ? shm[iy * p.w + ix + 1] : 0.f;
+                        const float v2 = (x0 && y1) ? shm[(iy + 1) * p.w + ix] : 0.f;
+                        const float v3 = (x1 && y1) ? shm[(iy + 1) * p.w + ix + 1] : 0.f;
+                        float v = __fmul_rn(v0, w0);
+                        v = __fadd_rn(v, __fmul_rn(v1, w1));
+                        v = __fadd_rn(v, __fmul_rn(v2, w2));
+                        v = __fadd_rn(v, __fmul_rn(v3, w3));
+                        if (!(v >= p.thr)) continue;
+                        const double dv = v, xc = x - cx;
+                        t[0] += dv;
+                        t[1] += xc * dv;
+                        t[2] += yc * dv;
+                        t[3] += xc * xc * dv;
+                        t[4] += xc * yc * dv;
+                        t[5] += yc * yc * dv;
+                    }
                 }
             }
         }
-    }
-    // t = {S, Sx, Sy, Sxx, Sxy, Syy}
+        // t = {S, Sx, Sy, Sxx, Sxy, Syy}
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-        double v = t[q];
+        for (int q = 0; q < 6; q++) {
+            double v = t[q];
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
-        t[q] = v;
-    }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0)
+            for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+            t[q] = v;
+        }
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (lane == 0)
 #pragma unroll
-        for (int q = 0; q < 6; q++) red[q][wv] = t[q];
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    double a[6];
+            for (int q = 0; q < 6; q++) red[q][wv] = t[q];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double a[6];
 #pragma unroll
-    for (int q = 0; q < 6; q++) {
-        a[q] = 0;
-        for (int k = 0; k < kMomBlock / 64; k++) a[q] += red[q][k];
-    }
-    double* o = p.out + 6 * map;
-    if (a[0] == 0.0) {
-        for (int q = 0; q < 6; q++) o[q] = 0.0;
-        return;
-    }
-    const double mxc = a[1] / a[0], myc = a[2] / a[0];
-    const double vxx = a[3] / a[0] - mxc * mxc;
-    const double vxy = a[4] / a[0] - mxc * myc;
-    const double vyy = a[5] / a[0] - myc * myc;
-    o[0] = mxc + cx;
-    o[1] = myc + cy;
-    o[2] = vxx;
-    o[3] = vxy;
-    o[4] = vxy;
-    o[5] = vyy;
+            for (int q = 0; q < 6; q++) {
+                a[q] = 0;
+                for (int k = 0; k < kMomBlock / 64; k++) a[q] += red[q][k];
+            }
+            double* o = p.out + 6 * map;
+            if (a[0] == 0.0) {
+                for (int q = 0; q < 6; q++) o[q] = 0.0;
+            } else {
+                const double mxc = a[1] / a[0], myc = a[2] / a[0];
+                const double vxx = a[3] / a[0] - mxc * mxc;
+                const double vxy = a[4] / a[0] - mxc * myc;
+                const double vyy = a[5] / a[0] - myc * myc;
+                o[0] = mxc + cx;
+                o[1] = myc + cy;
+                o[2] = vxx;
+                o[3] = vxy;
+                o[4] = vxy;
+                o[5] = vyy;
+            }
+        }
+    }  // joints of this workgroup
 }
 
 }  // namespace
@@ -590,7 +606,11 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     p.img_w = img_w;
     p.thr = thr;
     p.separable = separable;
-    hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * K)), dim3(kMomBlock), lds,
+    const char* je = getenv("MVPOSE_MOM_JPB");  // tuning experiments / tests only
+    const int jpb_env = je ? atoi(je) : 0;
+    p.jpb = jpb_env > 0 ? std::min(jpb_env, K) : std::min(kMomJointsPerBlock, K);
+    const long groups = (K + p.jpb - 1) / p.jpb;
+    hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * groups)), dim3(kMomBlock), lds,
                        reinterpret_cast<hipStream_t>(stream), p);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END

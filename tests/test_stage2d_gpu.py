@@ -203,3 +203,33 @@ def test_moments_closed_form_matches_walk(lib, kind):
     np.testing.assert_allclose(fast[..., :2], walk[..., :2], rtol=1e-6, atol=1e-6)
     scale = (walk[..., 0] ** 2 + walk[..., 1] ** 2)[..., None]
     assert np.all(np.abs(fast[..., 2:] - walk[..., 2:]) <= 1e-6 * np.abs(walk[..., 2:]) + 1e-9 * scale + 1e-9)
+
+
+@pytest.mark.parametrize("jpb", [1, 4, 5, 17])
+@pytest.mark.parametrize("separable", [1, 0])
+def test_moments_joints_per_block_bit_identical(lib, jpb, separable, monkeypatch):
+    """Workgroups that build the crop's warp tables once and reuse them for jpb joints
+    (ragged last group for 4 and 5) give bit-identical moments to one map per workgroup;
+    frames carry different warps, so tables must not leak across crops."""
+    _lib, geometry = lib
+    rng = np.random.default_rng(21)
+    hm = _planted_heatmaps(rng, 3)
+    g = geometry.CropGeometry.whole_image(1280, 720)
+    minv = np.tile(g.revert_minv, (3, 1))
+    minv[1, 2] += 3.7
+    minv[1, 5] -= 2.1
+    minv[2, 0] *= 1.01
+    hd = torch.tensor(hm, device="cuda")
+    md = torch.tensor(minv, device="cuda")
+
+    def run(j):
+        monkeypatch.setenv("MVPOSE_MOM_JPB", str(j))
+        out = torch.full((3, 17, 6), float("nan"), dtype=torch.float64, device="cuda")
+        _lib.call("mvp_heatmap_moments", _p(hd), 3, 17, 64, 48, _p(md), 720, 1280, ctypes.c_float(0.01),
+                  separable, _p(out), _s())
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
+    ref = run(1)
+    assert not np.isnan(ref).any()
+    np.testing.assert_array_equal(run(jpb), ref)
