@@ -207,6 +207,7 @@ constexpr int kMomBlock = 320;         // 5 waves x 4 columns per lane = 1280: e
 constexpr int kMomCols = 4;            // image columns per lane (separable path)
 constexpr int kMomJointsPerBlock = 17;  // maps per workgroup sharing one set of warp tables (all of a
                                         // COCO crop: 8680-8717 -> 8823-8832 frames/s in the bench vs 1)
+static_assert(kMomBlock % 64 == 0 && kMomCols % 2 == 0, "whole waves (per-wave reduction slots), packed column pairs");
 
 // One workgroup per (crop, group of jpb joints); the column / row / run tables are
 // built once per workgroup, then the maps of its joints are processed in turn.  The fixed-point warp of an image pixel
