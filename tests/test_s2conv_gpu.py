@@ -47,3 +47,30 @@ def test_stride2_vs_reference(cin, cout, h, w, relu, mode, monkeypatch):
     mx = (got - ref).abs().max().item()
     print(f"{mode} {cin}->{cout} {h}x{w}/2 relu={relu}: rel L2 {rel:.2e}, max abs {mx:.3e}")
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(64, 64, 128, 96), (256, 64, 64, 48)])
+def test_generic_stride2_tile_shapes_bit_identical(cin, cout, h, w, monkeypatch):
+    """The generic kernel's tile shapes differ only in which workgroup computes a pixel
+    (same K order and epilogue): the 8-wave 16x8 tiles deployed for the Cin >= 64 planes
+    equal the 4-wave tiles (MVPOSE_S2_TILE=7) bit for bit, at a batch (7) whose last
+    tile rows are partial in no dimension but whose crop count is odd."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    monkeypatch.setenv("MVPOSE_NO_S2CONV", "1")
+    spec, xi, yo, _ = hrnet.conv_spec(cin, cout, h, w, k=3, stride=2, relu=True, seed=3)
+    n = 7
+    g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+    x = torch.randn((n, h, w, cin), generator=torch.Generator().manual_seed(5)).bfloat16().cuda()
+    outs = []
+    for v in ("0", "7", "1", "2"):
+        monkeypatch.setenv("MVPOSE_S2_TILE", v)
+        out = torch.full((n, h // 2, w // 2, cout), float("nan"), dtype=torch.bfloat16, device="cuda")
+        g.run(x, out)
+        torch.cuda.synchronize()
+        outs.append(out.cpu())
+    g.close()
+    assert not torch.isnan(outs[0].float()).any()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
