@@ -27,7 +27,16 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0   # dense bf16 MFMA spec
 METRIC = "multi-view frames/sec end-to-end (2-cam HRNet-W32, 17 kpts) at 1/2/4/8 GPUs"
-TRI_T = 100_000             # frames per triangulation-roofline launch
+TRI_T = 1_000_000           # frames per triangulation-roofline launch: 612 MB (V=2) / 1.02 GB (V=4)
+                            # per launch, well past the 256 MiB Infinity Cache -> an HBM measurement
+SGD_V, SGD_T, SGD_M = 8, 400, 256   # BASELINE config 5 (V=8, T=400); M trajectories per launch
+SGD_ITERS = 40
+# FP32 FLOP per (frame, camera, joint) projection + likelihood forward + adjoint in sgd_kernel
+# (csrc/sgd.hip project / quad_cost / project_adjoint, distortion on, counted by hand: DESIGN.md
+# §4) and per trajectory coordinate (stencil + segment adjoints + Adam)
+SGD_FLOP_PER_PROJ = 175
+SGD_FLOP_PER_COORD = 25
+FP32_PEAK_TFLOPS = 157.3    # vector FP32 (MI355X_MICROARCH.md)
 
 
 def parse():
@@ -38,8 +47,25 @@ def parse():
     ap.add_argument("--frames", type=int, default=256, help="synchronised frames per step per GPU")
     ap.add_argument("--views", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-frames", type=int, default=12)
+    ap.add_argument("--cpu-sample-frames", type=int, default=12,
+                    help="frames of the all-threads CPU baseline sample (config 1 is 50 frames)")
+    ap.add_argument("--cpu-sample-frames-1t", type=int, default=2, help="frames of the 1-thread sample")
+    ap.add_argument("--no-extra", action="store_true", help="skip the config 3 / config 5 side lines")
     return ap.parse_args()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a torchrun environment: start N ranks (one process per GPU)
+    through torch.distributed.run as a CHILD process, before this process touches the GPU,
+    and exit with its status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
 
 def committed_traffic():
@@ -56,6 +82,8 @@ def committed_traffic():
 
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -66,10 +94,21 @@ def setup_dist(args):
     return world, rank, torch.device("cuda", local if world > 1 else 0)
 
 
-def cpu_baseline(n_frames, views, seed=0):
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _cpu_path(n_frames, views, seed=0):
     """The reference-equivalent CPU path (oracle restatement):
     torch-CPU fp32 HRNet-W32 at batch 1 per camera with flip test, numpy decode,
-    revert + moments, OpenCV-semantics triangulation — timed on this host."""
+    revert + moments, OpenCV-semantics triangulation.  Returns seconds."""
     sys.path.insert(0, ROOT)
     from oracle import cv_ref, heatmap_ref, hrnet_ref
     from mvpose import hrnet, synthetic as syn
@@ -85,19 +124,36 @@ def cpu_baseline(n_frames, views, seed=0):
         for v in range(views):
             x = torch.from_numpy(heatmap_ref.preprocess(frames[t, v], M))[None]
             avg, _, _ = hrnet_ref.flip_test_forward(model, x)
-            k, s, _ = heatmap_ref.msra_decode(avg[0].numpy())
+            k, sc, _ = heatmap_ref.msra_decode(avg[0].numpy())
             kpts[t, :, :2, v] = heatmap_ref.keypoints_to_image(k, center, scale)
-            kpts[t, :, 2, v] = s
+            kpts[t, :, 2, v] = sc
             heatmap_ref.heatmap_means_cov_f64(heatmap_ref.warp_affine_linear_f32(avg[0].numpy(), Mh, 720, 1280))
     cv_ref.get_pose_3D(cp, kpts, camera_indices=[0, 1])
-    dt = time.perf_counter() - t0
-    return {"value": n_frames / dt, "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n_frames} synthetic {views}-cam 1280x720 frames, batch 1 per camera, flip test, "
-                      f"{dt:.1f} s (oracle/ restatement: torch-CPU fp32 HRNet-W32 + numpy decode/revert/moments "
-                      f"+ OpenCV-4.9-semantics triangulation in C)"}
+    return time.perf_counter() - t0
 
 
-def tri_valu_issue(tri_ms):
+def cpu_baseline(n_frames, n_frames_1t, views):
+    """Config 1 on this host's cores: all threads, then 1 thread, each on a
+    bounded sample of the 50-frame config so the default bench stays within minutes."""
+    n_threads = torch.get_num_threads()
+    dt = _cpu_path(n_frames, views)
+    torch.set_num_threads(1)
+    try:
+        dt1 = _cpu_path(n_frames_1t, views) if n_frames_1t > 0 else None
+    finally:
+        torch.set_num_threads(n_threads)
+    out = {"value": n_frames / dt, "unit": "frames/s", "cores": n_threads, "kind": "port",
+           "host_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+           "sample": f"{n_frames} of config 1's 50 synthetic {views}-cam 1280x720 frames, batch 1 per camera, "
+                     f"flip test, {dt:.1f} s on {n_threads} threads (oracle/ restatement: torch-CPU fp32 "
+                     f"HRNet-W32 + numpy decode/revert/moments + OpenCV-4.9-semantics triangulation in C)"}
+    if dt1 is not None:
+        out["value_1thread"] = n_frames_1t / dt1
+        out["sample_1thread"] = f"{n_frames_1t} frames, {dt1:.1f} s on 1 thread"
+    return out
+
+
+def tri_valu_issue(tri_ms, n_points):
     """The triangulation kernel's real bound: FP64 VALU issue (OpenCV-order fp64
     undistortion + QR).  From the committed PMC pass (profiles/r01_tri_pmc.json):
     VALU instructions per launch x 4 cycles (wave64 on a 16-lane SIMD) over 1024
@@ -106,23 +162,99 @@ def tri_valu_issue(tri_ms):
     if not os.path.exists(path):
         return None
     pmc = json.load(open(path))
-    floor = pmc["valu_issue_floor_ms"]
-    return {"valu_instr_per_launch": pmc["valu_instr_per_launch"], "issue_floor_ms": floor,
+    scale = n_points / pmc["points_per_launch"]   # VALU instructions scale with the points
+    floor = pmc["valu_issue_floor_ms"] * scale
+    return {"valu_instr_per_launch": pmc["valu_instr_per_launch"] * scale, "issue_floor_ms": floor,
             "frac": floor / tri_ms, "source": "profiles/r01_tri_pmc.json"}
+
+
+def tri_line(ops, syn, dev, s, views, mode, reps=10):
+    """One triangulation launch over a resident TRI_T-frame stream (the per-step 256-frame
+    launch is latency-bound and says nothing about the kernel).  HIP events on the launch
+    stream; the stream is ~2.4-4x the Infinity Cache, so every launch streams from HBM."""
+    cams = syn.make_rig(views, seed=1)
+    cd = torch.tensor(ops.pack_cameras(syn.reference_camera_params(cams)), device=dev)
+    k = torch.tensor(syn.make_kpts_2d(syn.make_poses(2000, seed=2), cams, seed=3), device=dev)
+    k = k.repeat((TRI_T + k.shape[0] - 1) // k.shape[0], 1, 1, 1)[:TRI_T].contiguous()
+    ci = list(range(views)) if mode == ops.TRI_ALL_VIEWS else [0, 1]
+    out = torch.empty((TRI_T, 17, 3), dtype=torch.float32, device=dev)
+    for _ in range(2):
+        ops.triangulate(k, cd, ci, mode=mode, out=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        ops.triangulate(k, cd, ci, mode=mode, out=out)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    v_used = views if mode == ops.TRI_ALL_VIEWS else 2
+    nbytes = 12.0 * 17 * (v_used + 1) * TRI_T   # read x,y,conf per used view + write xyz, per joint
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    del k, out
+    return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+            "bytes_per_frame": 12 * 17 * (v_used + 1), "bytes_per_launch": nbytes,
+            "frames_per_s": TRI_T / (ms * 1e-3), "avg_launch_ms": ms, "launches": reps,
+            "workload": f"{TRI_T} resident synchronised {views}-cam frames per launch"}
+
+
+def sgd_line(dev):
+    """BASELINE config 5: V=8, T=400 reprojection + smoothness + body-length refinement
+    (pose_refinement.py:894-1096), SGD_M trajectories per launch (one workgroup each), a fixed
+    SGD_ITERS iterations (early stop disabled).  Outside the timed region of the headline."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from mvpose import refine, synthetic as syn
+    rng = np.random.default_rng(5)
+    cams = syn.make_rig(SGD_V, seed=5)
+    poses = syn.make_poses(SGD_T, seed=6)
+    g = np.zeros((SGD_T, SGD_V, 17, 6))
+    for v, c in enumerate(cams):
+        g[:, v, :, 0:2] = syn.project(poses, c) + rng.normal(0, 2.0, (SGD_T, 17, 2))
+        g[:, v, :, 2] = g[:, v, :, 5] = 9.0
+    x0 = (poses + rng.normal(0, 3.0, poses.shape)).astype(np.float32)
+    with open(os.path.join(ROOT, "tests", "golden", "body_part_lengths.json")) as f:
+        lengths = json.load(f)["my_lengths"]
+    camlist = [[c["K"], c["R"], c["T"], c["dist"]] for c in cams]
+    kw = dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=10 ** 9, tolerance=1e-5,
+              max_iter=SGD_ITERS - 1, body_lengths=dict(lengths), device=dev)
+    res = {}
+    for M in (1, SGD_M):
+        G = torch.tensor(np.broadcast_to(g, (M,) + g.shape).copy(), device=dev)
+        X = torch.tensor(np.broadcast_to(x0, (M,) + x0.shape).copy(), device=dev)
+        refine.refine_trajectories(G, X, camlist, **kw)
+        s = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        r = refine.refine_trajectories(G, X, camlist, **kw)
+        e1.record(s)
+        torch.cuda.synchronize()
+        assert int(r["iters"].min()) == SGD_ITERS, r["iters"]
+        res[M] = e0.elapsed_time(e1) / SGD_ITERS
+    flop_iter = SGD_T * 17 * (SGD_V * SGD_FLOP_PER_PROJ + 3 * SGD_FLOP_PER_COORD)
+    tf = flop_iter * SGD_M / (res[SGD_M] * 1e-3) / 1e12
+    return {"workload": f"BASELINE config 5: V={SGD_V}, T={SGD_T}, one window, {SGD_ITERS} Adam iterations, "
+                        f"lr 0.01, lambda_s 1e-6, lambda_b 1 (early stop off)",
+            "ms_per_iter_1traj": res[1], "ms_per_iter_M": res[SGD_M], "M": SGD_M,
+            "trajectory_iterations_per_s": SGD_M / (res[SGD_M] * 1e-3),
+            "roofline": {"bound": "fp32 valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": tf / FP32_PEAK_TFLOPS, "flop_per_iter_per_traj": flop_iter,
+                         "flop_model": f"{SGD_FLOP_PER_PROJ} FLOP per (t, v, j) projection + likelihood + "
+                                       f"adjoint, {SGD_FLOP_PER_COORD} per coordinate (stencil, segments, Adam)"}}
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world, rank, dev = setup_dist(args)
     from mvpose import dist as mdist, hrnet, ops, synthetic as syn
     from mvpose.estimator import BatchPoseEstimator
     from mvpose.pipeline import MultiViewPipeline
 
     B, V = args.frames, args.views
-    sd = hrnet.random_state_dict(0) if rank == 0 or world == 1 else hrnet.random_state_dict(0)
-    est = BatchPoseEstimator(sd, max_frames=B * V, device=dev)
-    # weights live once on rank 0; ship them over RCCL (xGMI) — the only start-up collective
-    mdist.broadcast_([est.backbone.w_dev, est.backbone.f_dev], src=0)
+    est = BatchPoseEstimator(hrnet.random_state_dict(0), max_frames=B * V, device=dev)
+    # the weights live once on rank 0; ship them over RCCL (xGMI) and re-derive each rank's
+    # graph copies (the only start-up collective)
+    est.backbone.sync_weights(src=0)
     cams = syn.make_rig(V, seed=1)
     pipe = MultiViewPipeline(syn.reference_camera_params(cams), estimator=est, device=dev)
     g = torch.Generator(device=dev).manual_seed(1234 + rank)
@@ -156,33 +288,30 @@ def main():
     # ---- per-kernel timing with HIP events on the launch stream (not part of the timed region)
     s = torch.cuda.current_stream(dev)
     crops = est.crops[: 2 * B * V]
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     reps = max(3, args.steps // 2)
     e[0].record(s)
     for _ in range(reps):
         est.backbone.forward(crops, out=est.heatmaps[: 2 * B * V])
     e[1].record(s)
-    # triangulation roofline on a resident stream of TRI_T synchronised frames (BASELINE config 4's
-    # 100k-frame stream; one launch = TRI_T*17 problems) — the per-step launch (B frames) is
-    # latency-bound and says nothing about the kernel
-    kst = syn.make_kpts_2d(syn.make_poses(2000, seed=2), cams, seed=3)
-    kst = np.ascontiguousarray(np.tile(kst, (TRI_T // kst.shape[0] + 1, 1, 1, 1))[:TRI_T])
-    kst = torch.tensor(kst, device=dev)
-    tri_out = torch.empty((TRI_T, 17, 3), dtype=torch.float32, device=dev)
-    for _ in range(2):
-        ops.triangulate(kst, pipe.cams, [0, 1], out=tri_out)
-    tri_reps = 200  # ~13 ms: shorter windows swing +-15 % with the clock state
-    e[2].record(s)
-    for _ in range(tri_reps):
-        ops.triangulate(kst, pipe.cams, [0, 1], out=tri_out)
-    e[3].record(s)
     torch.cuda.synchronize()
     bb_ms = e[0].elapsed_time(e[1]) / reps
-    tri_ms = e[2].elapsed_time(e[3]) / tri_reps
     flops = 2.0 * est.backbone.macs_per_crop() * crops.shape[0]
     bb_tflops = flops / (bb_ms * 1e-3) / 1e12
-    tri_bytes = 12.0 * 17 * (V + 1) * TRI_T  # read x,y,conf per view + write xyz per joint
-    tri_gbs = tri_bytes / (tri_ms * 1e-3) / 1e9
+    extra = {}
+    if rank == 0:
+        del frames
+        torch.cuda.empty_cache()
+        tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
+        tri["kernel"] = "triangulate_reference_kernel"
+        tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17)
+        extra["roofline_triangulate"] = tri
+        if not args.no_extra:
+            t4 = tri_line(ops, syn, dev, s, 4, ops.TRI_ALL_VIEWS)
+            t4["kernel"] = "triangulate_all_views_kernel"
+            t4["config"] = "BASELINE config 3: 4-cam overdetermined 8x4 DLT, all views"
+            extra["roofline_triangulate_v4"] = t4
+            extra["sgd"] = sgd_line(dev)
 
     if rank == 0:
         traffic, traffic_src = committed_traffic()
@@ -203,22 +332,15 @@ def main():
             "config": {"workload": f"BASELINE config 2: {V}-cam HRNet-W32 256x192 bf16 (flip test) + batched "
                                    f"4x4 DLT-SVD triangulation", "frames_per_step_per_gpu": B, "views": V,
                        "crops_per_step_per_gpu": 2 * B * V, "parallelism": f"dp{world} (frame-sharded)"},
-            "roofline": {"bound": "mfma", "kernel": "HRNet-W32 conv graph (tconv/wsconv/basic_block/conv_mfma "
-                                                    "kernels, one graph forward = one launch)",
+            "roofline": {"bound": "mfma", "kernel": "HRNet-W32 conv graph (one graph forward = one launch)",
                          "achieved": bb_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": bb_tflops / BF16_PEAK_TFLOPS,
                          "traffic": traffic.get("backbone", {}).get("hbm_bytes_per_launch"),
                          "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": bb_ms},
-            "roofline_triangulate": {"bound": "hbm", "kernel": "triangulate_reference_kernel",
-                                     "workload": f"{TRI_T} resident synchronised {V}-cam frames per launch "
-                                                 f"(BASELINE config 4 stream)",
-                                     "achieved": tri_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                     "frac": tri_gbs / HBM_PEAK_GBS, "bytes_per_launch": tri_bytes,
-                                     "frames_per_s": TRI_T / (tri_ms * 1e-3), "avg_launch_ms": tri_ms,
-                                     "valu_issue": tri_valu_issue(tri_ms)},
         }
+        res.update(extra)
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(args.cpu_sample_frames, V)
+            res["cpu_baseline"] = cpu_baseline(args.cpu_sample_frames, args.cpu_sample_frames_1t, V)
         print(json.dumps(res))
     if world > 1:
         torch.distributed.destroy_process_group()

@@ -178,6 +178,11 @@ int mvp_graph_create(const mvp_tensor_desc* tensors_host, int n_tensors, const m
 /* input_dev: [batch][h][w][c] of the input tensor; output_dev: the output tensor. */
 int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* output_dev, void* stream);
 int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);
+/* The weight blobs passed to mvp_graph_create were rewritten in place (e.g. an RCCL
+ * broadcast from rank 0 after every rank built its graph): re-derive every weight
+ * the graph copied out of them at create time (cat-fused 1x1 weights / biases).
+ * Blocking (device-synchronising). */
+int mvp_graph_refresh_weights(void* handle);
 int mvp_graph_destroy(void* handle);
 
 /* ---------------------------------------------------------------------------

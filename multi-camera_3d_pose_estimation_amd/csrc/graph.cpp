@@ -212,16 +212,26 @@ void pair_fuse(Graph& g, bool enable) {
     }
 }
 
-// Device-side concatenated weights / summed biases of the cat-fused ops (graph create time).
-void cat_build(Graph& g) {
+// Device-side concatenated weights / summed biases of the cat-fused ops: allocated at graph
+// create time, filled from the blobs by cat_fill (create and mvp_graph_refresh_weights).
+void cat_alloc(Graph& g) {
+    for (int b = 0; b < (int)g.ops.size(); b++) {
+        const int a = g.cat_src[b];
+        if (a < 0) continue;
+        const mvp_op_desc& B = g.ops[b];
+        const int cp = conv_cout_pad(B.cout), cin = B.cin + g.ops[a].cin;
+        MVP_HIP(hipMalloc(&g.cat_w[b], (size_t)cp * cin * sizeof(uint16_t)));
+        MVP_HIP(hipMalloc(&g.cat_b[b], (size_t)cp * sizeof(float)));
+    }
+}
+
+void cat_fill(Graph& g) {
     for (int b = 0; b < (int)g.ops.size(); b++) {
         const int a = g.cat_src[b];
         if (a < 0) continue;
         const mvp_op_desc& B = g.ops[b];
         const mvp_op_desc& A = g.ops[a];
         const int cp = conv_cout_pad(B.cout), cin = B.cin + A.cin;
-        MVP_HIP(hipMalloc(&g.cat_w[b], (size_t)cp * cin * sizeof(uint16_t)));
-        MVP_HIP(hipMalloc(&g.cat_b[b], (size_t)cp * sizeof(float)));
         MVP_HIP(hipMemcpy2D(g.cat_w[b], (size_t)cin * 2, g.wb + B.w_off, (size_t)B.cin * 2, (size_t)B.cin * 2, cp,
                             hipMemcpyDeviceToDevice));
         MVP_HIP(hipMemcpy2D(g.cat_w[b] + B.cin, (size_t)cin * 2, g.wb + A.w_off, (size_t)A.cin * 2,
@@ -380,7 +390,8 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::cat_fuse(*g, !(nc && nc[0] == '1') && !(nf && nf[0] == '1'));
         const char* np = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics: keep conv3 / next conv1 apart
         mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
-        mvp::cat_build(*g);
+        mvp::cat_alloc(*g);
+        mvp::cat_fill(*g);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
             hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
@@ -491,6 +502,18 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         }
         slice = 0;
     }
+    MVP_ABI_END
+}
+
+// The blobs were rewritten in place (e.g. a weight broadcast from rank 0 after the graph was
+// built): re-derive every weight the graph copied out of them at create time.  Blocking.
+extern "C" int mvp_graph_refresh_weights(void* handle) {
+    MVP_ABI_BEGIN
+    Graph* g = static_cast<Graph*>(handle);
+    MVP_REQUIRE(g != nullptr, "mvp_graph_refresh_weights: NULL handle");
+    MVP_HIP(hipDeviceSynchronize());
+    mvp::cat_fill(*g);
+    MVP_HIP(hipDeviceSynchronize());
     MVP_ABI_END
 }
 

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mvp_graph_create": (c_int, None),
     "mvp_graph_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     "mvp_graph_arena_bytes": (c_int, None),
+    "mvp_graph_refresh_weights": (c_int, [c_void_p]),
     "mvp_graph_destroy": (c_int, [c_void_p]),
     "mvp_sgd_workspace_floats": (c_int, [c_int, c_int, c_int, c_int, P(c_int64)]),
     # mvp_sgd_params struct pointer declared in mvpose/refine.py

@@ -114,19 +114,41 @@ def _conv_shapes():
     return out
 
 
-def random_state_dict(seed: int = 0):
+RES_GAMMA = 0.25    # last BN of every residual branch (BasicBlock bn2, Bottleneck bn3)
+FUSE_GAMMA = 0.5    # BNs of the HRModule fuse layers
+HEAD_STD = 0.005    # head weight std relative to He-normal; bias ~ HEAD_BIAS + N(0, 0.01)
+HEAD_BIAS = -0.15
+
+
+def random_state_dict(seed: int = 0, stable: bool = True):
     """Seeded weights in mmpose naming: He-normal convs, BN with randomised affine
-    and running statistics (so folding is exercised), head bias ~ N(0, 0.1)."""
+    and running statistics (so folding is exercised).
+
+    stable=True (default) keeps the activations O(1) through the ~90 layers the way a
+    trained network does: the residual branches' last BN and the fuse-layer BNs get
+    scaled-down gammas (RES_GAMMA, FUSE_GAMMA; otherwise every residual add and every
+    multi-branch fuse sum doubles the variance and the heatmaps reach ~1e8), and the head
+    is scaled and biased (HEAD_STD, HEAD_BIAS) so the heatmaps are trained-model-like: O(0.1)
+    values, a few per cent of cells above get_heatmap_means_cov's 0.01 threshold.
+    stable=False: the round-1 weights (plain He-normal, gamma ~ 1, head bias ~ N(0, 0.1))."""
     g = torch.Generator().manual_seed(seed)
     sd = {}
     for conv, bn, cout, cin, k in _conv_shapes():
         std = (2.0 / (cin * k * k)) ** 0.5
+        if bn is None and stable:
+            std *= HEAD_STD
         sd[conv + ".weight"] = torch.randn((cout, cin, k, k), generator=g) * std
         if bn is None:
-            sd[conv + ".bias"] = torch.randn((cout,), generator=g) * 0.1
+            b = torch.randn((cout,), generator=g)
+            sd[conv + ".bias"] = HEAD_BIAS + 0.01 * b if stable else 0.1 * b
         else:
-            sd[bn + ".weight"] = 1.0 + 0.1 * torch.randn((cout,), generator=g)
-            sd[bn + ".bias"] = 0.1 * torch.randn((cout,), generator=g)
+            gain = 1.0
+            if stable and (bn.endswith(".bn3") or (".branches." in bn and bn.endswith(".bn2"))):
+                gain = RES_GAMMA
+            elif stable and ".fuse_layers." in bn:
+                gain = FUSE_GAMMA
+            sd[bn + ".weight"] = gain * (1.0 + 0.1 * torch.randn((cout,), generator=g))
+            sd[bn + ".bias"] = gain * 0.1 * torch.randn((cout,), generator=g)
             sd[bn + ".running_mean"] = 0.1 * torch.randn((cout,), generator=g)
             sd[bn + ".running_var"] = 1.0 + 0.2 * torch.rand((cout,), generator=g)
             sd[bn + ".num_batches_tracked"] = torch.tensor(0)
@@ -417,6 +439,20 @@ class ConvGraph:
         call("mvp_graph_forward", self._h, ctypes.c_void_p(x.data_ptr()), n, ctypes.c_void_p(out.data_ptr()),
              ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
         return out
+
+    def refresh_weights(self) -> None:
+        """w_dev / f_dev were rewritten in place: re-derive the graph's own weight copies."""
+        call("mvp_graph_refresh_weights", self._h)
+
+    def sync_weights(self, src: int = 0) -> None:
+        """Frame-sharded data parallelism: every rank takes rank `src`'s folded weights (one
+        RCCL broadcast of the two blobs over xGMI), then re-derives its graph copies."""
+        from . import dist as mdist
+        world, _ = mdist.world_rank()
+        if world > 1:
+            mdist.broadcast_([self.w_dev, self.f_dev], src=src)
+            torch.cuda.synchronize(self.device)
+            self.refresh_weights()
 
     @property
     def arena_bytes(self) -> int:

@@ -171,3 +171,27 @@ def test_head_kernel_matches_generic(models, monkeypatch):
     torch.cuda.synchronize()
     scale = a.abs().max().item()
     assert (a - b).abs().max().item() <= 1e-5 * scale
+
+
+def test_refresh_weights_after_inplace_overwrite(models):
+    """Multi-GPU start-up: every rank builds its graph, then rank 0's weights arrive by
+    broadcast INTO the blobs (bench.py / HRNetBackbone.sync_weights).  The graph's own
+    create-time copies (cat-fused layer1 weights and biases) must be re-derived:
+    graph A + B's blobs + refresh == graph B, and without the refresh it is not."""
+    from mvpose import hrnet
+    a = hrnet.HRNetBackbone(hrnet.random_state_dict(23), max_batch=2)
+    b = hrnet.HRNetBackbone(hrnet.random_state_dict(29), max_batch=2)
+    g = torch.Generator().manual_seed(9)
+    x = torch.zeros((2, 256, 192, 4))
+    x[..., :3] = torch.randn((2, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    want = b.forward(xb).clone()
+    a.w_dev.copy_(b.w_dev)
+    a.f_dev.copy_(b.f_dev)
+    torch.cuda.synchronize()
+    stale = a.forward(xb).clone()
+    a.refresh_weights()
+    fresh = a.forward(xb)
+    torch.cuda.synchronize()
+    assert not torch.equal(stale, want)
+    assert torch.equal(fresh, want)

@@ -5,9 +5,10 @@ bit-exactly to those vectors by test_oracle_sgd.py).
 Tolerances (written here, float32 path):
 * projection: |Δuv| <= 2e-3 px on ~1e3 px values (a few f32 ulp; the
   reference's [R|T] product goes through BLAS in an order we do not reproduce);
-* refinement: trajectories within 2e-2 cm after the golden runs' 5-60 Adam
-  steps (lr 0.01-0.05 cm per step; Adam normalises the gradient, so f32
-  rounding differences in the gradient move a step by far less than lr);
+* refinement: trajectories within SGD_ATOL = 1e-4 cm after the golden runs' 5-60
+  Adam steps (measured <= 6.1e-5 cm, profiles/r01_sgd_bench.log: f32 rounding of the
+  gradient in a different summation order than torch's autograd; Adam normalises the
+  gradient, so such differences move a step by far less than lr);
   running-mean cost histories within rtol 1e-4; identical iteration counts
   (early stop) and identical history lengths.
 """
@@ -23,6 +24,7 @@ from oracle import sgd_ref
 from test_oracle_sgd import SGD_CASES, sgd_cams, sgd_kwargs
 
 pytestmark = pytest.mark.gpu
+SGD_ATOL = 1e-4
 
 with open(os.path.join(GOLDEN, "body_part_lengths.json")) as _f:
     MY_LENGTHS = json.load(_f)["my_lengths"]
@@ -60,8 +62,8 @@ def test_sgd_matches_reference_golden(refine, case):
                                               body_lengths=dict(MY_LENGTHS))
     opt.sgd_optimize(print_frequency=10 ** 9, **sgd_kwargs(d))
     assert opt.best_trajectory.shape == d["best"].shape
-    np.testing.assert_allclose(opt.best_trajectory.numpy(), d["best"], rtol=0, atol=2e-2)
-    np.testing.assert_allclose(opt.trajectory.numpy(), d["final"], rtol=0, atol=2e-2)
+    np.testing.assert_allclose(opt.best_trajectory.numpy(), d["best"], rtol=0, atol=SGD_ATOL)
+    np.testing.assert_allclose(opt.trajectory.numpy(), d["final"], rtol=0, atol=SGD_ATOL)
     for k, v in opt.all_costs_total.items():
         ref = d["hist_" + k]
         assert len(v) == len(ref), k
@@ -98,8 +100,8 @@ def test_sgd_matches_oracle(refine, V, T, kw):
     opt = refine.Optimized_3d_Pose_Estimation(gauss, init, decomposed_cam_params_initial=dict(enumerate(cams)),
                                               body_lengths=dict(MY_LENGTHS))
     opt.sgd_optimize(print_frequency=10 ** 9, **kw)
-    np.testing.assert_allclose(opt.best_trajectory.numpy(), ref.best_trajectory.numpy(), rtol=0, atol=2e-2)
-    np.testing.assert_allclose(opt.trajectory.numpy(), ref.trajectory.numpy(), rtol=0, atol=2e-2)
+    np.testing.assert_allclose(opt.best_trajectory.numpy(), ref.best_trajectory.numpy(), rtol=0, atol=SGD_ATOL)
+    np.testing.assert_allclose(opt.trajectory.numpy(), ref.trajectory.numpy(), rtol=0, atol=SGD_ATOL)
     assert list(opt.all_costs_total) == list(ref.all_costs_total)
     for k in ref.all_costs_total:
         np.testing.assert_allclose(np.array(opt.all_costs_total[k], np.float64),
