@@ -75,6 +75,14 @@ bool launch_s2conv(const ConvLaunch& c, hipStream_t s);
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,
                  hipStream_t s);
 
+// Fused stem (stem2.hip): conv1 (3x3/s2 4 -> 64, w1 f32 [64][3][3][4]) and conv2 (3x3/s2
+// 64 -> 64, w2 bf16 [64][3][3][64]), both BN-folded with ReLU, in one launch; conv1's
+// output never leaves LDS.  x [N][256][192][4] -> y [N][64][48][64].  stem2_supported is
+// false for other shapes (or MVPOSE_NO_STEMFUSE=1).
+bool stem2_supported(int H, int W, int cin2, int cout2);
+void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uint16_t* w2, const float* b2,
+                  uint16_t* y, int N, int H, int W, hipStream_t s);
+
 // HRModule fuse: out = relu( sum_i up_i(in_i) ), nearest upsample factor up_i
 // (1, 2, 4, 8); all tensors bf16 NHWC with C channels, out at resolution H x W.
 void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_t* out, int N, int H, int W,

@@ -30,6 +30,7 @@ struct Graph {
     std::vector<uint16_t*> cat_w; // its concatenated weights [cout_pad][cin_k + cin_src] (owned)
     std::vector<float*> cat_b;    // and summed biases [cout_pad] (owned)
     std::vector<int> pair_tail;   // 1x1 op whose 256->64 successor (absorbed) runs in the same launch (-1: none)
+    std::vector<int> stem_head;   // 3x3/s2 conv that also runs the (absorbed) stem op stem_head[k] (-1: none)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -212,6 +213,36 @@ void pair_fuse(Graph& g, bool enable) {
     }
 }
 
+// Stem-fusion pass: the stem conv (OP_STEM, 4 -> 64, s2) whose output feeds only a
+// 3x3/s2 64 -> 64 conv (HRNet's conv2) runs inside that conv's launch (stem2.hip); the
+// 128x96x64 intermediate (1.6 GB per 1024 crops) is never allocated.
+void stem_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.stem_head.assign(no, -1);
+    if (!enable) return;
+    std::vector<int> uses(nt, 0);
+    for (const mvp_op_desc& op : g.ops)
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0) uses[op.in[i]]++;
+    for (int a = 0; a < no; a++) {
+        const mvp_op_desc& A = g.ops[a];
+        if (A.kind != MVP_OP_STEM || g.absorbed[a] || uses[A.out] != 1 || A.out == g.output) continue;
+        for (int b = a + 1; b < no; b++) {
+            const mvp_op_desc& B = g.ops[b];
+            if (B.in[0] != A.out) continue;
+            const mvp_tensor_desc& x = g.tensors[A.in[0]];
+            if (B.kind == MVP_OP_CONV && !g.absorbed[b] && !g.block_head[b] && g.cat_src[b] < 0 &&
+                g.pair_tail[b] < 0 && B.ks == 3 && B.stride == 2 && B.relu && (B.n_in < 2 || B.in[1] < 0) &&
+                B.segment == A.segment && g.tensors[B.out].dtype == MVP_DT_BF16_NHWC &&
+                stem2_supported(x.h, x.w, B.cin, B.cout)) {
+                g.absorbed[a] = 1;
+                g.stem_head[b] = a;
+            }
+            break;
+        }
+    }
+}
+
 // Device-side concatenated weights / summed biases of the cat-fused ops: allocated at graph
 // create time, filled from the blobs by cat_fill (create and mvp_graph_refresh_weights).
 void cat_alloc(Graph& g) {
@@ -279,12 +310,18 @@ void plan(Graph& g) {
         touch(op.out);
         for (int i = 0; i < op.n_in; i++) {
             if (op.in[i] < 0 || (g.block_head[k] && i == 0)) continue;  // fused: conv1's output is LDS-only
+            if (g.stem_head[k] >= 0 && i == 0) continue;                 // fused stem: LDS-only
             if (g.cat_src[k] >= 0 && i == 1) continue;                  // cat-fused: never materialised
             last[op.in[i]] = std::max(last[op.in[i]], k);
             touch(op.in[i]);
         }
         if (g.cat_src[k] >= 0) {  // the absorbed op's input is read here
             const int x = g.ops[g.cat_src[k]].in[0];
+            last[x] = std::max(last[x], k);
+            touch(x);
+        }
+        if (g.stem_head[k] >= 0) {  // the absorbed stem's input is read here
+            const int x = g.ops[g.stem_head[k]].in[0];
             last[x] = std::max(last[x], k);
             touch(x);
         }
@@ -314,7 +351,9 @@ void plan(Graph& g) {
         };
         widen(op.out);
         for (int i = 0; i < op.n_in; i++)
-            if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1)) widen(op.in[i]);
+            if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1) && !(g.stem_head[k] >= 0 && i == 0))
+                widen(op.in[i]);
+        if (g.stem_head[k] >= 0) widen(g.ops[g.stem_head[k]].in[0]);
         if (g.cat_src[k] >= 0) widen(g.ops[g.cat_src[k]].in[0]);
         if (g.pair_tail[k] >= 0) widen(g.ops[g.pair_tail[k]].out);
     }
@@ -390,6 +429,7 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::cat_fuse(*g, !(nc && nc[0] == '1') && !(nf && nf[0] == '1'));
         const char* np = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics: keep conv3 / next conv1 apart
         mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
+        mvp::stem_fuse(*g, !(nf && nf[0] == '1'));
         mvp::cat_alloc(*g);
         mvp::cat_fill(*g);
         mvp::plan(*g);
@@ -434,6 +474,13 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             const mvp_op_desc& c1 = g->ops[k - 1];
             mvp::launch_basic_block_c32((const uint16_t*)ptr(op.in[1]), g->wb + c1.w_off, g->fb + c1.b_off,
                                         g->wb + op.w_off, g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, o.h, o.w, s);
+            return;
+        }
+        if (g->stem_head[k] >= 0) {  // stem conv1 + this conv2 in one launch
+            const mvp_op_desc& st = g->ops[g->stem_head[k]];
+            const mvp_tensor_desc& x = g->tensors[st.in[0]];
+            mvp::launch_stem2((const uint16_t*)ptr(st.in[0]), g->fb + st.w_off, g->fb + st.b_off, g->wb + op.w_off,
+                              g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, x.h, x.w, s);
             return;
         }
         if (op.kind == MVP_OP_STEM) {

@@ -19,11 +19,16 @@ typedef const __attribute__((address_space(1))) void gbl_void;
 __device__ __forceinline__ void glds16(const void* src, void* lds_base) {
     __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)lds_base, 16, 0, 0);
 }
-__device__ __forceinline__ float relu1(float v) {  // one v_max_f32 (fmaxf adds a canonicalize)
+__device__ __forceinline__ float relu1_asm(float v) {  // one v_max_f32 (fmaxf adds a canonicalize)
     float r;
     asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(v));
     return r;
 }
+// ReLU the compiler can see: the inline-asm form above hides its operand from the hazard
+// recognizer, so applied straight to an MFMA result it read the accumulator before the
+// MFMA had written it (stem2: couts 16h+0/1 wrong).  __builtin_amdgcn_fmed3f(v, 0, +inf)
+// is one v_med3_f32 with the required wait states.
+__device__ __forceinline__ float relu1(float v) { return __builtin_amdgcn_fmed3f(v, 0.f, __builtin_inff()); }
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {  // RNE, v_cvt_pk_bf16_f32
     return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
 }

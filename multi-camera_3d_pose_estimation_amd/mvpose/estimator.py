@@ -2,7 +2,7 @@
 mmpose_pose_estimation.py:222-272, for all cameras x frames of a batch at once).
 
 Per batch of N camera-frames (uint8, device-resident):
-    mvp_preprocess      crop (whole-image bbox) + normalise, original + flipped
+    mvp_preprocess      crop (per-crop bbox, default the whole image) + normalise, original + flipped
     mvp_graph_forward   HRNet-W32 + HeatmapHead on 2N crops (bf16 MFMA)
     mvp_heatmap_decode  flip-test average + MSRAHeatmap decode + restore
     mvp_heatmap_moments revert_heatmap + get_heatmap_means_cov
@@ -48,9 +48,10 @@ def _stream(dev):
 
 
 class BatchPoseEstimator:
-    """GPU equivalent of PoseEstimator (mmpose_pose_estimation.py:81-272) without
-    the detector: every frame uses the whole-image bbox, which is what the
-    reference falls back to when RTMDet finds no person (:246-250)."""
+    """GPU equivalent of PoseEstimator (mmpose_pose_estimation.py:81-272) from the
+    person bbox on: each crop takes its bbox from `run(..., bboxes=)` (the detector's
+    first person box, :242-250) or, without one, the whole image — what the reference
+    falls back to when RTMDet finds no person (:246-250)."""
 
     def __init__(self, state_dict=None, seed: int = 0, max_frames: int = 256, frame_hw=(720, 1280),
                  flip_test: bool = True, swap_rb: bool = True, device="cuda"):
@@ -80,6 +81,13 @@ class BatchPoseEstimator:
                      for _ in range(2)]
         self._avg_busy = [None, None]   # side-stream event after the last moments read of each buffer
         self._avg_k = 1                 # buffer the last run wrote
+        # per-crop bbox geometry (run(bboxes=...)), double-buffered like the heatmaps: the side-stream
+        # moments of run i read revert_minv while run i+1 uploads its own; pinned host staging
+        self._geo_dev = [(torch.empty((n, 6), dtype=torch.float64, device=self.device),
+                          torch.empty((n, 6), dtype=torch.float64, device=self.device),
+                          torch.empty((n, 4), dtype=torch.float32, device=self.device)) for _ in range(2)]
+        self._geo_host = [None, None]
+        self._geo_copied = [None, None]  # event after the last H2D copy out of each host buffer
         self._side = None
         self._mean = (ctypes.c_float * 3)(*MEAN)
         self._std = (ctypes.c_float * 3)(*STD)
@@ -90,9 +98,39 @@ class BatchPoseEstimator:
         """Flip-averaged heatmaps of the last run (valid until the run after next)."""
         return self._avg[self._avg_k]
 
+    def _bbox_geometry(self, k: int, n: int, bboxes):
+        """Upload the crop geometry of n bboxes (xyxy; a row with a non-finite value = no
+        detection = the whole image) into geometry buffer k; returns (crop_minv,
+        revert_minv, center_scale, separable) device views."""
+        bb = np.array(bboxes, dtype=np.float64).reshape(-1, 4)
+        if bb.shape[0] != n:
+            raise ValueError(f"bboxes: {bb.shape[0]} boxes for {n} frames")
+        miss = ~np.isfinite(bb).all(axis=1)
+        bb[miss] = (0.0, 0.0, float(self.frame_w), float(self.frame_h))
+        cm, rm, cs = geometry.crop_geometry_batch(bb)
+        sep = all(warp_is_separable(m, self.frame_h, self.frame_w) for m in np.unique(rm, axis=0))
+        if self._geo_host[k] is None:
+            m = self.max_frames
+            self._geo_host[k] = (torch.empty((m, 6), dtype=torch.float64).pin_memory(),
+                                 torch.empty((m, 6), dtype=torch.float64).pin_memory(),
+                                 torch.empty((m, 4), dtype=torch.float32).pin_memory())
+        if self._geo_copied[k] is not None:     # the previous upload out of host buffer k is done
+            self._geo_copied[k].synchronize()
+        dev = self._geo_dev[k]
+        for host, d, a in zip(self._geo_host[k], dev, (cm, rm, cs)):
+            host[:n].copy_(torch.from_numpy(a))
+            d[:n].copy_(host[:n], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._geo_copied[k] = ev
+        return dev[0][:n], dev[1][:n], dev[2][:n], sep
+
     def run(self, frames: torch.Tensor, n_views: int = 1, kpts_tkv: torch.Tensor | None = None,
-            argmax: bool = False, overlap_moments: bool = False):
+            argmax: bool = False, overlap_moments: bool = False, bboxes=None):
         """frames: (N, H, W, 3) uint8 on the GPU, ordered (t, v) when n_views > 1.
+        bboxes: None (every crop = the whole image) or (N, 4) xyxy image boxes, one per
+        frame (a row of NaNs = no detection = the whole image), as the reference's
+        detector stage hands them to inference_topdown (mmpose_pose_estimation.py:242-253).
         Returns dict: keypoints (N,17,2) f32 image px, scores (N,17) f32,
         gaussians (N,17,6) f64 [mx,my,vxx,vxy,vxy,vyy], and optionally argmax.
         overlap_moments: gaussians are produced on a side stream; read them only after
@@ -107,21 +145,29 @@ class BatchPoseEstimator:
         dev, s = self.device, _stream(self.device)
         nc = n * (2 if self.flip_test else 1)
         crops = self.crops[:nc]
-        call("mvp_preprocess", _ptr(frames), n, h, w, _ptr(self.crop_minv), INPUT_HW[0], INPUT_HW[1], self._mean,
+        k = self._avg_k ^ 1
+        main = torch.cuda.current_stream(dev)
+        if bboxes is None:
+            crop_minv, revert_minv, center_scale = self.crop_minv, self.revert_minv, self.center_scale
+            separable = self.separable
+        else:
+            if self._avg_busy[k] is not None:   # moments of two runs ago still reading geometry buffer k
+                main.wait_event(self._avg_busy[k])
+                self._avg_busy[k] = None
+            crop_minv, revert_minv, center_scale, separable = self._bbox_geometry(k, n, bboxes)
+        call("mvp_preprocess", _ptr(frames), n, h, w, _ptr(crop_minv), INPUT_HW[0], INPUT_HW[1], self._mean,
              self._std, int(self.swap_rb), int(self.flip_test), _ptr(crops), s)
         hm = self.backbone.forward(crops, out=self.heatmaps[:nc])
         kp = torch.empty((n, N_JOINTS, 2), dtype=torch.float32, device=dev)
         sc = torch.empty((n, N_JOINTS), dtype=torch.float32, device=dev)
         am = torch.empty((n, N_JOINTS), dtype=torch.int32, device=dev) if argmax else None
-        k = self._avg_k ^ 1
-        main = torch.cuda.current_stream(dev)
         if self._avg_busy[k] is not None:       # moments of two runs ago still reading buffer k
             main.wait_event(self._avg_busy[k])
             self._avg_busy[k] = None
         self._avg_k = k
         avg = self._avg[k][:n]
         call("mvp_heatmap_decode", _ptr(hm[:n]), _ptr(hm[n:]) if self.flip_test else None, n, N_JOINTS,
-             HEATMAP_HW[0], HEATMAP_HW[1], self._flip, 1, _ptr(self.center_scale), INPUT_HW[1], INPUT_HW[0],
+             HEATMAP_HW[0], HEATMAP_HW[1], self._flip, 1, _ptr(center_scale), INPUT_HW[1], INPUT_HW[0],
              _ptr(avg), _ptr(kp), _ptr(sc), _ptr(am), _ptr(kpts_tkv), int(n_views), s)
         gauss = torch.empty((n, N_JOINTS, 6), dtype=torch.float64, device=dev)
         done = None
@@ -135,8 +181,8 @@ class BatchPoseEstimator:
             gauss.record_stream(self._side)
         else:
             ms = s
-        call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(self.revert_minv),
-             h, w, ctypes.c_float(HEATMAP_THR), int(self.separable), _ptr(gauss), ms)
+        call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(revert_minv),
+             h, w, ctypes.c_float(HEATMAP_THR), int(separable), _ptr(gauss), ms)
         if overlap_moments:
             done = torch.cuda.Event()
             done.record(self._side)
@@ -153,11 +199,12 @@ class BatchPoseEstimator:
             torch.cuda.current_stream().wait_event(out["moments_done"])
 
     # ---- the reference's per-frame callable contract (pose_estimation.py:88, :104-110)
-    def predict(self, frame, return_full_heatmaps=False):
+    def predict(self, frame, return_full_heatmaps=False, bbox=None):
         """Single frame (H, W, 3) uint8 numpy/tensor -> (pred_instances, heatmaps (17,6) f64)
-        with pred_instances['keypoints'] (1,17,2) f32 and ['keypoint_scores'] (1,17) f32."""
+        with pred_instances['keypoints'] (1,17,2) f32 and ['keypoint_scores'] (1,17) f32.
+        bbox: optional xyxy person box (None = the whole image)."""
         f = torch.as_tensor(np.ascontiguousarray(frame), device=self.device).reshape(1, *np.shape(frame))
-        r = self.run(f.contiguous())
+        r = self.run(f.contiguous(), bboxes=None if bbox is None else [bbox])
         inst = {"keypoints": r["keypoints"].cpu().numpy(), "keypoint_scores": r["scores"].cpu().numpy()}
         if return_full_heatmaps:
             return inst, r["heatmaps"][0].cpu().numpy()

@@ -165,6 +165,76 @@ def inverse_map(M):
     return np.array(m)
 
 
+def _warp_points(center, scale_w, out_w, out_h):
+    """mmpose get_warp_matrix's three point pairs for N boxes (rot 0, shift 0): src (N,3,2)
+    and dst (N,3,2) float32, with warp_matrix's f32 rounding points."""
+    n = center.shape[0]
+    src = np.zeros((n, 3, 2), np.float32)
+    dst = np.zeros((n, 3, 2), np.float32)
+    src[:, 0] = center
+    src[:, 1, 0] = (center[:, 0].astype(np.float64) + scale_w.astype(np.float64) * -0.5).astype(np.float32)
+    src[:, 1, 1] = center[:, 1]
+    d = src[:, 0] - src[:, 1]
+    src[:, 2, 0] = src[:, 1, 0] + -d[:, 1]
+    src[:, 2, 1] = src[:, 1, 1] + d[:, 0]
+    dst[:, 0] = (out_w * 0.5, out_h * 0.5)
+    dst[:, 1] = (out_w * 0.5 + out_w * -0.5, out_h * 0.5)
+    dd = dst[:, 0] - dst[:, 1]
+    dst[:, 2, 0] = dst[:, 1, 0] + -dd[:, 1]
+    dst[:, 2, 1] = dst[:, 1, 1] + dd[:, 0]
+    return src, dst
+
+
+def _affine_batch(src, dst):
+    """affine_from_points for N point triples (the same 6x6 systems, solved batched)."""
+    s = src.astype(np.float64)
+    d = dst.astype(np.float64)
+    n = s.shape[0]
+    A = np.zeros((n, 6, 6))
+    b = np.zeros((n, 6))
+    for i in range(3):
+        A[:, 2 * i, 0], A[:, 2 * i, 1], A[:, 2 * i, 2] = s[:, i, 0], s[:, i, 1], 1.0
+        A[:, 2 * i + 1, 3], A[:, 2 * i + 1, 4], A[:, 2 * i + 1, 5] = s[:, i, 0], s[:, i, 1], 1.0
+        b[:, 2 * i], b[:, 2 * i + 1] = d[:, i, 0], d[:, i, 1]
+    return np.linalg.solve(A, b[..., None])[..., 0]
+
+
+def _inverse_map_batch(M):
+    """inverse_map for (N,6) maps (fp64, OpenCV's op order)."""
+    m = np.array(M, np.float64, copy=True)
+    D = m[:, 0] * m[:, 4] - m[:, 1] * m[:, 3]
+    with np.errstate(divide="ignore"):
+        D = np.where(D != 0, 1.0 / np.where(D != 0, D, 1.0), 0.0)
+    a11, a22 = m[:, 4] * D, m[:, 0] * D
+    m[:, 0], m[:, 4] = a11, a22
+    m[:, 1] *= -D
+    m[:, 3] *= -D
+    b1 = -m[:, 0] * m[:, 2] - m[:, 1] * m[:, 5]
+    b2 = -m[:, 3] * m[:, 2] - m[:, 4] * m[:, 5]
+    m[:, 2], m[:, 5] = b1, b2
+    return m
+
+
+def crop_geometry_batch(bboxes_xyxy, padding=BBOX_PADDING):
+    """Vectorised CropGeometry for N boxes: (crop_minv (N,6) f64, revert_minv (N,6) f64,
+    center_scale (N,4) f32) — the same numbers CropGeometry(box) gives one box at a time
+    (mmpose bbox_xyxy2cs -> TopdownAffine -> get_warp_matrix, mmpose_pose_estimation.py:253)."""
+    bb = np.asarray(bboxes_xyxy, np.float64).reshape(-1, 4)
+    x1, y1, x2, y2 = (bb[:, i] for i in range(4))   # sums in fp64, then f32 (bbox_center_scale)
+    center = (np.stack([x1 + x2, y1 + y2], 1).astype(np.float32) * np.float32(0.5)).astype(np.float32)
+    scale = (np.stack([x2 - x1, y2 - y1], 1).astype(np.float32) * np.float32(padding)).astype(np.float32)
+    ar = INPUT_SIZE[0] / INPUT_SIZE[1]
+    w, h = scale[:, 0].astype(np.float64), scale[:, 1].astype(np.float64)
+    wide = w > h * ar
+    scale = np.where(wide[:, None], np.stack([w, w / ar], 1), np.stack([h * ar, h], 1)).astype(np.float32)
+    s_in, d_in = _warp_points(center, scale[:, 0], *INPUT_SIZE)
+    crop_minv = _inverse_map_batch(_affine_batch(s_in, d_in))
+    s_hm, d_hm = _warp_points(center, scale[:, 0], *HEATMAP_SIZE)
+    revert_minv = _inverse_map_batch(_affine_batch(d_hm, s_hm))
+    cs = np.concatenate([center, scale], 1).astype(np.float32)
+    return crop_minv, revert_minv, cs
+
+
 class CropGeometry:
     """Everything the GPU stages need for one bbox: crop map (crop -> image),
     revert map (image -> heatmap), center/scale for the keypoint restore."""

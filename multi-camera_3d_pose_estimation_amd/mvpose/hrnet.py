@@ -385,6 +385,18 @@ def join_spec(h: int, w: int, seed: int = 0, cat: bool = False):
     return g, x, out, sd
 
 
+def stem_spec(seed: int = 0):
+    """HRNet's stem on a 256x192 crop: conv1 (3x3/s2 4 -> 64) and conv2 (3x3/s2 64 -> 64),
+    BN + ReLU each (the pattern the graph's stem-fusion pass runs as one launch), for
+    kernel tests.  Returns (spec, input id, output id, state dict)."""
+    sd = {k: v for k, v in random_state_dict(seed).items() if k.startswith(("backbone.conv", "backbone.bn"))}
+    g = GraphSpec()
+    x = g.tensor(INPUT_HW[0], INPUT_HW[1], 4)
+    y = g.stem(sd, "backbone.conv1", "backbone.bn1", x)
+    y = g.conv(sd, "backbone.conv2", "backbone.bn2", y, 2, True)
+    return g, x, y, sd
+
+
 def conv_spec(cin: int, cout: int, h: int, w: int, k: int = 3, stride: int = 1, relu: bool = True, seed: int = 0):
     """One k x k conv (+ folded BN, optional ReLU) cin -> cout on an h x w plane, for
     kernel tests and per-conv benchmarks.  Returns (spec, input id, output id, state dict)."""

@@ -37,7 +37,9 @@ class MultiViewPipeline:
     def max_frames(self) -> int:
         return self.estimator.max_frames // self.n_views
 
-    def process(self, frames: torch.Tensor, out: dict | None = None, overlap_moments: bool = False) -> dict:
+    def process(self, frames: torch.Tensor, out: dict | None = None, overlap_moments: bool = False,
+                bboxes=None) -> dict:
+        """bboxes: None (whole-image crops) or (T, V, 4) xyxy person boxes (NaN row = none)."""
         T, V = frames.shape[:2]
         if V != self.n_views:
             raise ValueError(f"frames carry {V} views, pipeline has {self.n_views} cameras")
@@ -47,7 +49,8 @@ class MultiViewPipeline:
         if "kpts_2d" not in out or tuple(out["kpts_2d"].shape) != (T, N_JOINTS, 3, V):
             out["kpts_2d"] = torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)
             out.pop("kpts_3d", None)
-        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments)
+        bb = None if bboxes is None else np.asarray(bboxes, np.float64).reshape(T * V, 4)
+        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments, bboxes=bb)
         out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
         if r["moments_done"] is not None:
             out["moments_done"] = r["moments_done"]
@@ -62,9 +65,10 @@ class MultiViewPipeline:
         """Order the current stream after an overlapped process()'s heatmaps_2d."""
         BatchPoseEstimator.wait_moments(out)
 
-    def process_stream(self, frames: torch.Tensor) -> dict:
+    def process_stream(self, frames: torch.Tensor, bboxes=None) -> dict:
         """Arbitrary-length sequence (T, V, H, W, 3): chunked to the estimator's batch."""
         T = frames.shape[0]
         step = self.max_frames
-        parts = [self.process(frames[t:t + step]) for t in range(0, T, step)]
+        parts = [self.process(frames[t:t + step], bboxes=None if bboxes is None else bboxes[t:t + step])
+                 for t in range(0, T, step)]
         return {k: torch.cat([p[k] for p in parts]) for k in parts[0]}

@@ -89,6 +89,7 @@ def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
     monkeypatch.setenv("MVPOSE_NO_TBLOCK", "1")
     monkeypatch.setenv("MVPOSE_NO_CATFUSE", "1")
     monkeypatch.setenv("MVPOSE_NO_PAIRFUSE", "1")
+    monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "1")  # stem2.hip sums K in its own order (tolerance test)
     monkeypatch.setenv("MVPOSE_NO_FUSE", "1")
     unfused = hrnet.HRNetBackbone(sd, max_batch=6)
     monkeypatch.delenv("MVPOSE_NO_FUSE")
@@ -149,6 +150,29 @@ def test_pair_fusion_matches_unfused(models, monkeypatch):
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
     assert rel < 2e-2, rel
     assert not torch.equal(a, b)  # the fused path ran (its summation order shows somewhere)
+    assert fused.arena_bytes <= plain.arena_bytes
+
+
+def test_stem_fusion_matches_unfused(models, monkeypatch):
+    """Stem conv1 + conv2 in one launch (stem2.hip, the 128x96x64 intermediate only in LDS):
+    same bf16 rounding points as the two-launch graph, K summed in another order; through
+    the rest of the network that is a rounding-level difference (<= 2e-2 relative, as for
+    the Bottleneck join) and the arena shrinks."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(37)
+    monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "1")
+    plain = hrnet.HRNetBackbone(sd, max_batch=4)
+    monkeypatch.delenv("MVPOSE_NO_STEMFUSE")
+    fused = hrnet.HRNetBackbone(sd, max_batch=4)
+    g = torch.Generator().manual_seed(38)
+    x = torch.zeros((4, 256, 192, 4))
+    x[..., :3] = torch.randn((4, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = fused.forward(xb)
+    torch.cuda.synchronize()
+    rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    assert rel < 2e-2, rel
     assert fused.arena_bytes <= plain.arena_bytes
 
 

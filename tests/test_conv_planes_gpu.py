@@ -168,3 +168,43 @@ def test_bottleneck_join(cat, pair, monkeypatch):
     assert rel <= 4e-3, rel
     ulp = 2.0 ** (torch.floor(torch.log2(ref.abs().max())) - 7)
     assert (dev - ref).abs().max().item() <= 3 * ulp, ((dev - ref).abs().max().item(), ulp)
+
+
+@pytest.mark.parametrize("fused", [False, True])
+def test_stem_vs_reference(fused, monkeypatch):
+    """HRNet stem conv1 (3x3/s2, 4 -> 64) + conv2 (3x3/s2, 64 -> 64): the fused stem2.hip
+    launch (conv1's 128x96x64 output only in LDS) and the two-launch path, against a
+    torch fp32 restatement with bf16 weights and a bf16 conv1 output (the graph's
+    rounding points); ragged batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "0" if fused else "1")
+    spec, xi, yo, sd = hrnet.stem_spec(seed=31)
+    n = 13
+    g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+    gen = torch.Generator().manual_seed(32)
+    x = torch.zeros((n, 256, 192, 4))
+    x[..., :3] = torch.randn((n, 256, 192, 3), generator=gen)
+    xb = x.bfloat16()
+    out = torch.empty((n, 64, 48, 64), dtype=torch.bfloat16, device="cuda")
+    g.run(xb.cuda(), out)
+    torch.cuda.synchronize()
+    arena = g.arena_bytes
+    g.close()
+
+    def conv(name, bn, t):
+        wt, b = hrnet.fold_bn(sd, name, bn)
+        wt = _bf(torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 3, 1, 2))).float())
+        return torch.nn.functional.conv2d(t, wt, stride=2, padding=1) + torch.from_numpy(b).float()[None, :, None, None]
+
+    xf = xb.float()[..., :3].permute(0, 3, 1, 2)
+    h = _bf(torch.relu(conv("backbone.conv1", "backbone.bn1", xf)))
+    ref = _bf(torch.relu(conv("backbone.conv2", "backbone.bn2", h))).permute(0, 2, 3, 1)
+    dev = out.float().cpu()
+    rel = (torch.linalg.vector_norm(dev - ref) / torch.linalg.vector_norm(ref)).item()
+    mx = (dev - ref).abs().max().item()
+    print(f"stem fused={fused}: rel L2 {rel:.2e}, max abs {mx:.3e}, arena {arena}")
+    assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
+    if fused:
+        assert arena == 0  # the 128x96x64 intermediate is never allocated
