@@ -83,6 +83,14 @@ bool stem2_supported(int H, int W, int cin2, int cout2);
 void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uint16_t* w2, const float* b2,
                   uint16_t* y, int N, int H, int W, hipStream_t s);
 
+// Transition1 (trans1.hip): t0 = relu(conv3x3/s1(x, w0) + b0) (256 -> 32) and t1 =
+// relu(conv3x3/s2(x, w1) + b1) (256 -> 64) from ONE pass over x [N][64][48][256];
+// w0 [32][3][3][256] and w1 [64][3][3][256] bf16 at element offsets w0_off / w1_off of wb.  trans1_supported is false for other
+// shapes (or MVPOSE_NO_TRANSFUSE=1).
+bool trans1_supported(int H, int W, int C, int cout0, int cout1);
+void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
+                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s);
+
 // HRModule fuse: out = relu( sum_i up_i(in_i) ), nearest upsample factor up_i
 // (1, 2, 4, 8); all tensors bf16 NHWC with C channels, out at resolution H x W.
 void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_t* out, int N, int H, int W,

@@ -31,6 +31,7 @@ struct Graph {
     std::vector<float*> cat_b;    // and summed biases [cout_pad] (owned)
     std::vector<int> pair_tail;   // 1x1 op whose 256->64 successor (absorbed) runs in the same launch (-1: none)
     std::vector<int> stem_head;   // 3x3/s2 conv that also runs the (absorbed) stem op stem_head[k] (-1: none)
+    std::vector<int> twin;        // 3x3/s1 conv whose (absorbed) 3x3/s2 sibling on the same input runs in its launch
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -243,6 +244,33 @@ void stem_fuse(Graph& g, bool enable) {
     }
 }
 
+// Transition-fusion pass: HRNet's transition1 reads the layer1 output (256 ch @ 64x48) with
+// two 3x3 convs (s1 -> 32 ch, s2 -> 64 ch); trans1.hip runs both from one pass over it.
+void twin_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size();
+    g.twin.assign(no, -1);
+    if (!enable) return;
+    auto plain3 = [&](int k, int stride) {
+        const mvp_op_desc& op = g.ops[k];
+        return op.kind == MVP_OP_CONV && !g.absorbed[k] && !g.block_head[k] && g.cat_src[k] < 0 &&
+               g.pair_tail[k] < 0 && g.stem_head[k] < 0 && op.ks == 3 && op.stride == stride && op.relu &&
+               (op.n_in < 2 || op.in[1] < 0) && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    for (int a = 0; a < no; a++) {
+        if (!plain3(a, 1)) continue;
+        const mvp_op_desc& A = g.ops[a];
+        const mvp_tensor_desc& x = g.tensors[A.in[0]];
+        for (int b = a + 1; b < no; b++) {
+            const mvp_op_desc& B = g.ops[b];
+            if (B.in[0] != A.in[0] || !plain3(b, 2) || B.segment != A.segment) continue;
+            if (!trans1_supported(x.h, x.w, x.c, A.cout, B.cout)) continue;
+            g.twin[a] = b;
+            g.absorbed[b] = 1;
+            break;
+        }
+    }
+}
+
 // Device-side concatenated weights / summed biases of the cat-fused ops: allocated at graph
 // create time, filled from the blobs by cat_fill (create and mvp_graph_refresh_weights).
 void cat_alloc(Graph& g) {
@@ -320,6 +348,13 @@ void plan(Graph& g) {
             last[x] = std::max(last[x], k);
             touch(x);
         }
+        if (g.twin[k] >= 0) {  // the absorbed sibling's output is written here
+            const int y2 = g.ops[g.twin[k]].out;
+            first[y2] = k;
+            if (last[y2] < k) last[y2] = k;
+            seg_of_def[y2] = op.segment;
+            touch(y2);
+        }
         if (g.stem_head[k] >= 0) {  // the absorbed stem's input is read here
             const int x = g.ops[g.stem_head[k]].in[0];
             last[x] = std::max(last[x], k);
@@ -354,6 +389,7 @@ void plan(Graph& g) {
             if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1) && !(g.stem_head[k] >= 0 && i == 0))
                 widen(op.in[i]);
         if (g.stem_head[k] >= 0) widen(g.ops[g.stem_head[k]].in[0]);
+        if (g.twin[k] >= 0) widen(g.ops[g.twin[k]].out);
         if (g.cat_src[k] >= 0) widen(g.ops[g.cat_src[k]].in[0]);
         if (g.pair_tail[k] >= 0) widen(g.ops[g.pair_tail[k]].out);
     }
@@ -430,6 +466,7 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         const char* np = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics: keep conv3 / next conv1 apart
         mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
         mvp::stem_fuse(*g, !(nf && nf[0] == '1'));
+        mvp::twin_fuse(*g, !(nf && nf[0] == '1'));
         mvp::cat_alloc(*g);
         mvp::cat_fill(*g);
         mvp::plan(*g);
@@ -474,6 +511,12 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             const mvp_op_desc& c1 = g->ops[k - 1];
             mvp::launch_basic_block_c32((const uint16_t*)ptr(op.in[1]), g->wb + c1.w_off, g->fb + c1.b_off,
                                         g->wb + op.w_off, g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, o.h, o.w, s);
+            return;
+        }
+        if (g->twin[k] >= 0) {  // transition1: this 3x3/s1 conv and its 3x3/s2 sibling, one pass
+            const mvp_op_desc& b = g->ops[g->twin[k]];
+            mvp::launch_trans1((const uint16_t*)ptr(op.in[0]), g->wb, op.w_off, g->fb + op.b_off, b.w_off,
+                               g->fb + b.b_off, (uint16_t*)ptr(op.out), (uint16_t*)ptr(b.out), nb, s);
             return;
         }
         if (g->stem_head[k] >= 0) {  // stem conv1 + this conv2 in one launch

@@ -397,6 +397,26 @@ def stem_spec(seed: int = 0):
     return g, x, y, sd
 
 
+def transition_spec(seed: int = 0, output: int = 0):
+    """HRNet-W32 transition1 on the layer1 output (256 ch @ 64x48): t0 = 3x3/s1 -> 32 ch and
+    t1 = 3x3/s2 -> 64 ch, both BN + ReLU (the pair the graph's transition-fusion pass runs
+    as one launch); the graph output is t0 (output=0) or t1 (output=1).  For kernel tests.
+    Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    for j, co in (("t0", 32), ("t1", 64)):
+        sd[f"{j}.weight"] = torch.randn((co, 256, 3, 3), generator=gen) * (2.0 / (9 * 256)) ** 0.5
+        sd[f"{j}bn.weight"] = 1.0 + 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.bias"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_mean"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_var"] = 1.0 + 0.2 * torch.rand((co,), generator=gen)
+    g = GraphSpec()
+    x = g.tensor(64, 48, 256)
+    t0 = g.conv(sd, "t0", "t0bn", x, 1, True)
+    t1 = g.conv(sd, "t1", "t1bn", x, 2, True)
+    return g, x, (t0, t1)[output], sd
+
+
 def conv_spec(cin: int, cout: int, h: int, w: int, k: int = 3, stride: int = 1, relu: bool = True, seed: int = 0):
     """One k x k conv (+ folded BN, optional ReLU) cin -> cout on an h x w plane, for
     kernel tests and per-conv benchmarks.  Returns (spec, input id, output id, state dict)."""

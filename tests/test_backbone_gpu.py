@@ -89,7 +89,8 @@ def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
     monkeypatch.setenv("MVPOSE_NO_TBLOCK", "1")
     monkeypatch.setenv("MVPOSE_NO_CATFUSE", "1")
     monkeypatch.setenv("MVPOSE_NO_PAIRFUSE", "1")
-    monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "1")  # stem2.hip sums K in its own order (tolerance test)
+    monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "1")  # stem2.hip / trans1.hip sum K in their own order
+    monkeypatch.setenv("MVPOSE_NO_TRANSFUSE", "1")  # (tolerance tests)
     monkeypatch.setenv("MVPOSE_NO_FUSE", "1")
     unfused = hrnet.HRNetBackbone(sd, max_batch=6)
     monkeypatch.delenv("MVPOSE_NO_FUSE")

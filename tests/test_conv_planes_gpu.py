@@ -208,3 +208,35 @@ def test_stem_vs_reference(fused, monkeypatch):
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
     if fused:
         assert arena == 0  # the 128x96x64 intermediate is never allocated
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("output", [0, 1])
+def test_transition1_vs_reference(fused, output, monkeypatch):
+    """HRNet transition1 on the layer1 output: t0 (3x3/s1 256 -> 32) and t1 (3x3/s2 256 -> 64)
+    from one pass over the 256-ch tensor (trans1.hip) and as two launches, against a torch
+    fp32 restatement with bf16 weights; ragged batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    monkeypatch.setenv("MVPOSE_NO_TRANSFUSE", "0" if fused else "1")
+    spec, xi, yo, sd = hrnet.transition_spec(seed=51, output=output)
+    n = 11
+    g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+    gen = torch.Generator().manual_seed(52)
+    x = torch.relu(torch.randn((n, 64, 48, 256), generator=gen)).bfloat16()
+    ho, wo, co = spec.tensors[yo][:3]
+    out = torch.empty((n, ho, wo, co), dtype=torch.bfloat16, device="cuda")
+    g.run(x.cuda(), out)
+    torch.cuda.synchronize()
+    g.close()
+    name = ("t0", "t1")[output]
+    wt, b = hrnet.fold_bn(sd, name, name + "bn")
+    wt = _bf(torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 3, 1, 2))).float())
+    z = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt, stride=1 + output, padding=1)
+    ref = _bf(torch.relu(z + torch.from_numpy(b).float()[None, :, None, None])).permute(0, 2, 3, 1)
+    dev = out.float().cpu()
+    rel = (torch.linalg.vector_norm(dev - ref) / torch.linalg.vector_norm(ref)).item()
+    mx = (dev - ref).abs().max().item()
+    print(f"transition1 t{output} fused={fused}: rel L2 {rel:.2e}, max abs {mx:.3e}")
+    assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
