@@ -241,6 +241,28 @@ def sgd_line(dev):
                                        f"adjoint, {SGD_FLOP_PER_COORD} per coordinate (stencil, segments, Adam)"}}
 
 
+def ingest_line(est, V, n_frames=512, batch=128):
+    """SURVEY §7 "host frame supply": the same 2D stage fed from HOST memory (decoded
+    frames in RAM, as the reference holds whole videos, utils.py:849-909) through the
+    overlapped pinned-staging / copy-stream pipeline (FrameStreamer).  PCIe-inclusive;
+    never the headline value (frames resident in HBM)."""
+    from mvpose.pose_estimation import FrameStreamer
+    rng = np.random.default_rng(7)
+    base = rng.integers(0, 256, (16, 720, 1280, 3), dtype=np.uint8)
+    stacks = [np.ascontiguousarray(np.tile(base, (n_frames // 16, 1, 1, 1))) for _ in range(V)]
+    fs = FrameStreamer(est, V, (720, 1280), batch)
+    fs.run([s[:batch] for s in stacks])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kp, _ = fs.run(stacks)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    gb = n_frames * V * 720 * 1280 * 3 / 1e9
+    return {"frames_per_s": n_frames / dt, "frames": n_frames, "batch_frames": batch, "host_to_device_GBps": gb / dt,
+            "path": "host RAM -> pinned staging (gather thread) -> H2D on a copy stream -> crop/HRNet/decode/"
+                    "moments on the compute stream (2D stage only, serial moments)"}
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -312,6 +334,7 @@ def main():
             t4["config"] = "BASELINE config 3: 4-cam overdetermined 8x4 DLT, all views"
             extra["roofline_triangulate_v4"] = t4
             extra["sgd"] = sgd_line(dev)
+            extra["host_ingest"] = ingest_line(est, V)
 
     if rank == 0:
         traffic, traffic_src = committed_traffic()

@@ -84,7 +84,7 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
  * 2D stage around the backbone (replaces, per camera frame, what
  * PoseEstimator.predict gets from mmpose at mmpose_pose_estimation.py:253-267).
  *
- * mvp_preprocess: TopdownAffine for a whole-image bbox + PoseDataPreprocessor.
+ * mvp_preprocess: TopdownAffine for each crop's bbox + PoseDataPreprocessor.
  *   frames_dev [n][H][W][3] uint8 (as the reference hands them to the model);
  *   minv_dev [n][6] float64 = the crop -> image map cv2.warpAffine uses
  *   internally (inverse of mmpose get_warp_matrix); mean3/std3 host f32;
@@ -116,6 +116,11 @@ int mvp_heatmap_decode(const float* hm_dev, const float* hm_flip_dev, int N, int
                        float* avg_dev, float* kpts_dev, float* scores_dev, int32_t* argmax_dev, float* kpts_tkv_dev,
                        int V, void* stream);
 int mvp_warp_is_separable(const double* minv_host, int img_h, int img_w, int* separable_out);
+/* revert_heatmap only (not on the hot path, which fuses it into the moments): each crop's
+ * K maps [N][K][h][w] f32 warped to the image, out [N][K][img_h][img_w] f32 — cv2.warpAffine
+ * INTER_LINEAR / BORDER_CONSTANT with minv = the image -> heatmap map (as for moments). */
+int mvp_heatmap_revert(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
+                       int img_w, float* out_dev, void* stream);
 int mvp_heatmap_moments(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
                         int img_w, float thr, int separable, double* out_dev, void* stream);
 

@@ -513,6 +513,47 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     }  // joints of this workgroup
 }
 
+// ---------------------------------------------------------------- revert only
+// mmpose merge_data_samples' revert_heatmap (cv2.warpAffine INTER_LINEAR, BORDER_CONSTANT
+// 0) of each crop's K flip-averaged maps to the full image: the values moments_kernel's
+// general path thresholds, in OpenCV's fixed-point coordinates and operation order.
+// Not on the hot path (moments fuse the revert); PoseEstimator.predict(return_full_heatmaps).
+// Grid (ceil(img_w / 256), img_h, N); a thread computes one pixel's taps once for all K maps.
+__global__ __launch_bounds__(kBlock) void revert_kernel(const float* __restrict__ hm, const double* __restrict__ minv,
+                                                        float* __restrict__ out, int K, int h, int w, int img_h,
+                                                        int img_w) {
+    const int x = blockIdx.x * kBlock + threadIdx.x, y = blockIdx.y, n = blockIdx.z;
+    if (x >= img_w) return;
+    const double* M = minv + 6 * n;
+    const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
+    const int Y0 = (int)rint((M[4] * y + M[5]) * 1024.0) + 16;
+    const int X = (X0 + (int)rint(M[0] * x * 1024.0)) >> 5;
+    const int Y = (Y0 + (int)rint(M[3] * x * 1024.0)) >> 5;
+    const int ix = X >> 5, iy = Y >> 5;
+    const long plane = (long)img_h * img_w, pix = (long)y * img_w + x;
+    float* o = out + (long)n * K * plane + pix;
+    if (ix >= w || ix + 1 < 0 || iy >= h || iy + 1 < 0) {
+        for (int k = 0; k < K; k++) o[k * plane] = 0.f;
+        return;
+    }
+    const float fx = (float)(X & 31) * (1.f / 32.f), fy = (float)(Y & 31) * (1.f / 32.f);
+    const float w0 = __fmul_rn(1.f - fy, 1.f - fx), w1 = __fmul_rn(1.f - fy, fx);
+    const float w2 = __fmul_rn(fy, 1.f - fx), w3 = __fmul_rn(fy, fx);
+    const bool x0 = ix >= 0, x1 = ix + 1 < w, y0 = iy >= 0, y1 = iy + 1 < h;
+    const float* src = hm + (long)n * K * h * w;
+    for (int k = 0; k < K; k++, src += h * w) {
+        const float v0 = (x0 && y0) ? src[iy * w + ix] : 0.f;
+        const float v1 = (x1 && y0) ? src[iy * w + ix + 1] : 0.f;
+        const float v2 = (x0 && y1) ? src[(iy + 1) * w + ix] : 0.f;
+        const float v3 = (x1 && y1) ? src[(iy + 1) * w + ix + 1] : 0.f;
+        float v = __fmul_rn(v0, w0);
+        v = __fadd_rn(v, __fmul_rn(v1, w1));
+        v = __fadd_rn(v, __fmul_rn(v2, w2));
+        v = __fadd_rn(v, __fmul_rn(v3, w3));
+        o[k * plane] = v;
+    }
+}
+
 }  // namespace
 
 extern "C" int mvp_preprocess(const uint8_t* frames, int n, int H, int W, const double* minv, int out_h, int out_w,
@@ -613,6 +654,19 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     const long groups = (K + p.jpb - 1) / p.jpb;
     hipLaunchKernelGGL(moments_kernel, dim3((unsigned)((long)N * groups)), dim3(kMomBlock), lds,
                        reinterpret_cast<hipStream_t>(stream), p);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_heatmap_revert(const float* hm, int N, int K, int h, int w, const double* minv, int img_h,
+                                  int img_w, float* out, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0 && img_h < 65536,
+                "mvp_heatmap_revert: bad sizes");
+    if (N == 0) return MVP_OK;
+    MVP_REQUIRE(hm && minv && out, "mvp_heatmap_revert: NULL device pointer");
+    hipLaunchKernelGGL(revert_kernel, dim3((unsigned)((img_w + kBlock - 1) / kBlock), (unsigned)img_h, (unsigned)N),
+                       dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), hm, minv, out, K, h, w, img_h, img_w);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END
 }

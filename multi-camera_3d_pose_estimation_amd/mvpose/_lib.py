@@ -46,6 +46,8 @@ SIGNATURES = {
                                    c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                    c_void_p]),
     "mvp_warp_is_separable": (c_int, [P(c_double), c_int, c_int, P(c_int)]),
+    "mvp_heatmap_revert": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                                   c_void_p]),
     "mvp_heatmap_moments": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float,
                                     c_int, c_void_p, c_void_p]),
     # graph argtypes with struct pointers are (re)declared in mvpose/hrnet.py

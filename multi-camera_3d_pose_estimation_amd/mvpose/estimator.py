@@ -192,6 +192,20 @@ class BatchPoseEstimator:
             out["argmax"] = am
         return out
 
+    def revert_heatmaps(self, bbox=None, index: int = 0) -> np.ndarray:
+        """The last run's flip-averaged maps of frame `index`, reverted to the image
+        (mvp_heatmap_revert): (17, H, W) f32 numpy — mmpose's _pred_heatmaps for that crop."""
+        if bbox is None:
+            minv = self.revert_minv[:1]
+        else:
+            _, rm, _ = geometry.crop_geometry_batch([bbox])
+            minv = torch.tensor(rm, device=self.device)
+        src = self.avg[index:index + 1].contiguous()
+        out = torch.empty((1, N_JOINTS, self.frame_h, self.frame_w), dtype=torch.float32, device=self.device)
+        call("mvp_heatmap_revert", _ptr(src), 1, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(minv), self.frame_h,
+             self.frame_w, _ptr(out), _stream(self.device))
+        return out[0].cpu().numpy()
+
     @staticmethod
     def wait_moments(out: dict) -> None:
         """Order the current stream after an overlapped run's moments (no-op otherwise)."""

@@ -4,6 +4,9 @@
   ignore_nonlinear_distortions=False)`` (pose_estimation.py:11-65): one batched
   ``mvp_triangulate`` launch instead of T·J ``utils.triangulate_points`` calls;
   same selection quirks, float32 output, optional inv(R_W0) rotation.
+* ``get_pose_2D(frames, model, confidence=0.5, pose_keypoints=range(17))`` (:71-151):
+  the V cameras' frames of one time step -> ((17, 3, V) f32 [x, y, score], list of V
+  (17, 6) heatmap Gaussians); with a GPU estimator the V frames are one batched run.
 * ``load_frames(recording_paths, start_end_frames)`` (utils.py:849-909): decoded
   frame stacks, one per camera, sliced ``[start:end]`` (the default ``[0, -1]``
   drops the last frame, quirk F4).  Video decoding itself is outside this
@@ -49,6 +52,44 @@ def get_pose_3D(camera_params, all_kpts_2d, world_trans_rot=None, camera_indices
     return out
 
 
+def get_pose_2D(frames, model, confidence=0.5, pose_keypoints=range(17)):
+    """pose_estimation.py:71-151.  frames: V frames (H, W, 3) uint8 of one time step.
+
+    model: a BatchPoseEstimator / mvpose PoseEstimator (the V frames go through the GPU
+    in ONE batched run), or any per-frame callable with the reference's contract
+    (model(frame) -> (pred_instances, heatmaps); an onepose-style model's dict output
+    with 'points' / 'confidence' is parsed as the reference does, :99-101).
+    Returns (results_stacked (17, 3, V) float32, heatmaps list of V arrays).
+    confidence and pose_keypoints select only the keypoints the reference DRAWS on the
+    frames (:117-131, then discarded with the GUI window), so they do not change the
+    output — as in the reference."""
+    from .mmpose_pose_estimation import PoseEstimator
+    if isinstance(model, (BatchPoseEstimator, PoseEstimator)):
+        est = model if isinstance(model, BatchPoseEstimator) else None
+        batch = np.ascontiguousarray(np.stack([np.asarray(f) for f in frames]))
+        if est is None:
+            r = model.predict_batch(batch)
+        else:
+            r = est.run(torch.from_numpy(batch).to(est.device).contiguous())
+        pts = r["keypoints"].cpu().numpy()
+        conf = r["scores"].cpu().numpy()
+        heat = list(r["gaussians"].cpu().numpy())
+    else:
+        results = [model(frame) for frame in frames]
+        if getattr(model, "__module__", "").startswith("onepose"):
+            pts = [np.asarray(res["points"]) for res in results]
+            conf = [np.asarray(res["confidence"]).squeeze() for res in results]
+        else:
+            pts = [np.asarray(res[0]["keypoints"]).squeeze() for res in results]
+            conf = [np.asarray(res[0]["keypoint_scores"]).squeeze() for res in results]
+        try:
+            heat = [res[1] for res in results]
+        except (IndexError, KeyError, TypeError):
+            heat = []
+    stacked = np.stack([np.concatenate((p, np.expand_dims(c, 1)), axis=1) for p, c in zip(pts, conf)], axis=2)
+    return stacked, heat
+
+
 def load_frames(recording_paths, start_end_frames=(0, -1)):
     """{camera: (T', H, W, 3) uint8} memory-mapped, sliced [start:end]."""
     if isinstance(recording_paths, (list, tuple)):
@@ -58,6 +99,9 @@ def load_frames(recording_paths, start_end_frames=(0, -1)):
     a, b = (0, -1) if start_end_frames is None else start_end_frames
     out = {}
     for k, path in recording_paths.items():
+        if isinstance(path, np.ndarray):                 # already-decoded frames in memory
+            out[k] = path[a:b]
+            continue
         if not str(path).endswith(".npy"):
             raise NotImplementedError(
                 f"{path}: video decoding is not part of the GPU hot path; pass decoded frames as a "
@@ -93,29 +137,84 @@ def build_estimator(model, detector_model="coco_base", model_yaml="", frame_hw=(
     return BatchPoseEstimator(sd, max_frames=max_frames, frame_hw=tuple(frame_hw), swap_rb=False, device=dev)
 
 
+class FrameStreamer:
+    """Overlapped host -> GPU frame supply for recorded videos (the reference decodes and
+    holds whole videos on the host, utils.py:849-909, then loops frame by frame).
+
+    Per chunk of `batch_frames` synchronised frames: a host thread gathers the V cameras'
+    frames into a PINNED staging buffer (numpy copies release the GIL), the H2D copy runs
+    on a dedicated copy stream, and the estimator consumes the device buffer on the
+    compute stream — so chunk i+1's gather and copy overlap chunk i's kernels.  Two pinned
+    and two device buffers; every hand-off is an event (no host synchronisation inside the
+    loop).  Outputs accumulate on the device and come back with one copy at the end."""
+
+    def __init__(self, est: BatchPoseEstimator, n_views: int, frame_hw, batch_frames: int = 128):
+        self.est = est
+        self.V = int(n_views)
+        self.H, self.W = (int(v) for v in frame_hw)
+        self.step = max(1, min(int(batch_frames), est.max_frames // self.V))
+        shape = (self.step, self.V, self.H, self.W, 3)
+        self.host = [torch.empty(shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.dev = [torch.empty(shape, dtype=torch.uint8, device=est.device) for _ in range(2)]
+        self.copy_stream = torch.cuda.Stream(est.device)
+        self.copied = [None, None]     # copy-stream event: H2D of buffer k done (host buffer reusable)
+        self.consumed = [None, None]   # compute-stream event: kernels done reading device buffer k
+
+    def _gather(self, stacks, t0, t1, k):
+        h = self.host[k].numpy()
+        for v, s in enumerate(stacks):
+            np.copyto(h[: t1 - t0, v], s[t0:t1])
+
+    def run(self, stacks, n_frames=None):
+        """stacks: V arrays (T, H, W, 3) uint8 (memory-mapped .npy or in memory).  Returns
+        device tensors kpts_2d (T, 17, 3, V) f32 and heatmaps (T, V, 17, 6) f64."""
+        from concurrent.futures import ThreadPoolExecutor
+        T = min(len(s) for s in stacks) if n_frames is None else int(n_frames)
+        dev = self.est.device
+        kp = torch.empty((T, N_JOINTS, 3, self.V), dtype=torch.float32, device=dev)
+        hm = torch.empty((T, self.V, N_JOINTS, 6), dtype=torch.float64, device=dev)
+        chunks = [(t, min(T, t + self.step)) for t in range(0, T, self.step)]
+        main = torch.cuda.current_stream(dev)
+        with ThreadPoolExecutor(max_workers=1) as pool:
+            fut = pool.submit(self._gather, stacks, *chunks[0], 0) if chunks else None
+            for i, (t0, t1) in enumerate(chunks):
+                k = i & 1
+                fut.result()                                   # chunk i is in pinned buffer k
+                if i + 1 < len(chunks):                        # gather chunk i+1 meanwhile
+                    kn = k ^ 1
+                    if self.copied[kn] is not None:
+                        self.copied[kn].synchronize()          # its previous H2D has left buffer kn
+                    fut = pool.submit(self._gather, stacks, *chunks[i + 1], kn)
+                n = t1 - t0
+                with torch.cuda.stream(self.copy_stream):
+                    if self.consumed[k] is not None:
+                        self.copy_stream.wait_event(self.consumed[k])
+                    self.dev[k][:n].copy_(self.host[k][:n], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.copy_stream)
+                    self.copied[k] = ev
+                main.wait_event(ev)
+                fr = self.dev[k][:n].reshape(n * self.V, self.H, self.W, 3)
+                r = self.est.run(fr, n_views=self.V, kpts_tkv=kp[t0:t1])
+                hm[t0:t1] = r["gaussians"].reshape(n, self.V, N_JOINTS, 6)
+                ce = torch.cuda.Event()
+                ce.record(main)
+                self.consumed[k] = ce
+        return kp, hm
+
+
 def run_pose_est(model, confidence=0.5, camera_indices=None, recording_paths=None, start_end_frames=(0, -1),
                  frame_shape=(1080, 1920), batch_frames=128):
-    """-> kpts_2d (T, 17, 3, V) float32, heatmaps (T, V, 17, 6) float64 (numpy)."""
+    """-> kpts_2d (T, 17, 3, V) float32, heatmaps (T, V, 17, 6) float64 (numpy).
+    recording_paths values may also be in-memory (T, H, W, 3) uint8 arrays."""
     frames = load_frames(recording_paths, start_end_frames)
     cams = list(frames.keys()) if camera_indices is None else list(camera_indices)
     stacks = [frames[c] for c in cams]
-    T = min(len(s) for s in stacks)
     V = len(stacks)
     H, W = stacks[0].shape[1:3]
     est = model if isinstance(model, BatchPoseEstimator) else build_estimator(model, frame_hw=(H, W))
-    dev = est.device
-    step = max(1, min(batch_frames, est.max_frames // V))
-    kpts_2d = np.zeros((T, N_JOINTS, 3, V), np.float32)
-    heat = np.zeros((T, V, N_JOINTS, 6), np.float64)
-    for t0 in range(0, T, step):
-        t1 = min(T, t0 + step)
-        host = np.stack([np.stack([s[t] for s in stacks]) for t in range(t0, t1)])   # (t, v, H, W, 3)
-        fr = torch.from_numpy(host).to(dev).reshape((t1 - t0) * V, H, W, 3).contiguous()
-        kt = torch.empty((t1 - t0, N_JOINTS, 3, V), dtype=torch.float32, device=dev)
-        r = est.run(fr, n_views=V, kpts_tkv=kt)
-        kpts_2d[t0:t1] = kt.cpu().numpy()
-        heat[t0:t1] = r["gaussians"].reshape(t1 - t0, V, N_JOINTS, 6).cpu().numpy()
-    return kpts_2d, heat
+    kp, hm = FrameStreamer(est, V, (H, W), batch_frames).run(stacks)
+    return kp.cpu().numpy(), hm.cpu().numpy()
 
 
 def estimate_pose_from_video(camera_names, recording_paths, model, detector_model="coco_base", model_yaml="",
