@@ -84,7 +84,7 @@ struct TParams {
     int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 1 = no DMA, 2 = no stores, 3 = both
 };
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM, int LD = 1>
 __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
@@ -232,7 +232,9 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
 #pragma unroll
         for (int t = 0; t < G::NT; t++) bva[t] = bv[t] + boff;
         const int ava = WRES ? av + chunk * G::WT * 16 : av + boff;
-        bf16x8 fa[2], fb[2][G::NT];
+        // fragments of step s+LD are read before step s's MFMAs (LD = LDS read look-ahead)
+        constexpr int NBF = LD + 1;
+        bf16x8 fa[NBF], fb[NBF][G::NT];
         auto load = [&](int step, bf16x8& a, bf16x8 (&b)[G::NT]) {
             const int tap = step >> 1, ks = step & 1;
             const int dy = tap / 3, dx = tap % 3;
@@ -241,11 +243,12 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
             for (int t = 0; t < G::NT; t++)
                 b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] + (ks * 2 * G::HS + dy * G::RS + dx) * 16);
         };
-        load(0, fa[0], fb[0]);
+#pragma unroll
+        for (int s0 = 0; s0 < LD; s0++) load(s0, fa[s0], fb[s0]);
 #pragma unroll
         for (int step = 0; step < 18; step++) {
-            const int cur = step & 1;
-            if (step + 1 < 18) load(step + 1, fa[cur ^ 1], fb[cur ^ 1]);
+            const int cur = step % NBF;
+            if (step + LD < 18) load(step + LD, fa[(step + LD) % NBF], fb[(step + LD) % NBF]);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int t = 0; t < G::NT; t++)
@@ -290,7 +293,11 @@ uint16_t* g_t_sink = nullptr;
 template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
 void launch_t_kernel(const TParams& p, hipStream_t s) {
     using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
-    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM>;
+    static const int ld = [] {  // experiment: MVPOSE_TCONV_LD=2 reads fragments two steps ahead
+        const char* e = getenv("MVPOSE_TCONV_LD");
+        return e && e[0] == '2' ? 2 : 1;
+    }();
+    auto kern = ld == 2 ? tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM, 2> : tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM, 1>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
