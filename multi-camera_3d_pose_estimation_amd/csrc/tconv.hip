@@ -81,10 +81,10 @@ struct TParams {
     const uint16_t* zero;
     uint16_t* sink;
     int N, Cout, n_tiles, ncb;  // ncb = Cout / BM column blocks (1 when weights are resident)
-    int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 1 = no DMA, 2 = no stores, 3 = both
+    int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 2 = no stores
 };
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM, int LD = 1>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
 __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     const int mg = wave % G::MG, pg = wave / G::MG;
     if ((int)blockIdx.x >= p.n_tiles) return;
     constexpr int tiles_h = H / TH;
-    const bool do_dma = !(p.diag & 1), do_st = !(p.diag & 2);
+    const bool do_st = !(p.diag & 2);
 
     // weight slot (within one chunk's [tap][q][cout] image) -> element offset in w[cout][3][3][Cin]
     auto wsrc_off = [&](int ws) {
@@ -168,7 +168,25 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     const int av = WRES ? G::WOFF + (h * G::BM + mg * 32 + r32) * 16 : (G::HT + h * G::BM + mg * 32 + r32) * 16;
 
     const int n_items = ((p.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1) * G::NCH;
-    if (WRES && do_dma) {  // all weight chunks, once (column block 0: host guarantees ncb == 1)
+    // The lane's 16 folded-BN biases, loaded ONCE: a workgroup's tiles all have the same
+    // column block (tile = blockIdx.x + k * gridDim.x and gridDim.x % ncb == 0, checked by
+    // the launcher).  Initialising the accumulators from a per-tile global load made the
+    // compiler wait for ALL outstanding VMEM (vmcnt(0): the next item's DMA, issued after
+    // it) before the tile's first MFMA; from LDS, it waited for the previous tile's stores
+    // (a conservative LDS-DMA alias wait before the read).
+    f32x16 bias_init;
+    {
+        const float* bp = p.bias + (blockIdx.x % p.ncb) * G::BM + mg * 32 + 16 * h;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * j);
+            bias_init[4 * j] = b4.x;
+            bias_init[4 * j + 1] = b4.y;
+            bias_init[4 * j + 2] = b4.z;
+            bias_init[4 * j + 3] = b4.w;
+        }
+    }
+    if (WRES) {  // all weight chunks, once (column block 0: host guarantees ncb == 1)
 #pragma unroll
         for (int j = 0; j < G::WPPW; j++) {
             const int s = (j * G::NW + wave) * 64 + lane;
@@ -177,7 +195,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
             glds16(src, lds + G::WOFF + (j * G::NW + wave) * 1024);
         }
     }
-    if (do_dma) issue(0, 0);
+    issue(0, 0);
     f32x16 acc[G::NT];
     for (int k = 0; k < n_items; k++) {
         const int buf = k & 1, chunk = k % G::NCH;
@@ -196,17 +214,8 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
         tile_of(tile, n0, ho0, cb);
         const int cob = cb * G::BM + mg * 32 + 16 * h;  // this lane's 16 couts
         if (first) {
-            f32x16 b;
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float4 b4 = *reinterpret_cast<const float4*>(p.bias + cob + 4 * j);
-                b[4 * j] = b4.x;
-                b[4 * j + 1] = b4.y;
-                b[4 * j + 2] = b4.z;
-                b[4 * j + 3] = b4.w;
-            }
-#pragma unroll
-            for (int t = 0; t < G::NT; t++) acc[t] = b;
+            for (int t = 0; t < G::NT; t++) acc[t] = bias_init;
         }
         // residual of this tile (last item), issued before the next DMA so that the
         // epilogue's wait never waits for it
@@ -223,7 +232,10 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
         }
         asm volatile("" ::: "memory");
         const bool more = k + 1 < n_items;
-        if (more && do_dma) issue(k + 1, buf ^ 1);
+        // unconditional (the last item re-fetches itself into the idle slot): a branch around
+        // the DMA made the compiler fall back to vmcnt(0) — waiting for this DMA — before the
+        // residual's first use in the epilogue
+        issue(more ? k + 1 : k, buf ^ 1);
         asm volatile("" ::: "memory");
 
         // ---- 9 taps x 2 k-steps x NT MFMAs; fragments of step s+1 read before step s's MFMAs
@@ -232,8 +244,9 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
 #pragma unroll
         for (int t = 0; t < G::NT; t++) bva[t] = bv[t] + boff;
         const int ava = WRES ? av + chunk * G::WT * 16 : av + boff;
-        // fragments of step s+LD are read before step s's MFMAs (LD = LDS read look-ahead)
-        constexpr int NBF = LD + 1;
+        // fragments of step s+LD are read before step s's MFMAs (LD = LDS read look-ahead; 2
+        // measured level with 1: the loop is not LDS-latency bound)
+        constexpr int LD = 1, NBF = LD + 1;
         bf16x8 fa[NBF], fb[NBF][G::NT];
         auto load = [&](int step, bf16x8& a, bf16x8 (&b)[G::NT]) {
             const int tap = step >> 1, ks = step & 1;
@@ -257,12 +270,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
         }
 
         if (last && do_st) {
-            if (RES) {
-                if (more && do_dma)
-                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
-                else
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
 #pragma unroll
             for (int t = 0; t < G::NT; t++) {
                 const bool ok = n0 + enb[t] < p.N;
@@ -293,17 +301,14 @@ uint16_t* g_t_sink = nullptr;
 template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
 void launch_t_kernel(const TParams& p, hipStream_t s) {
     using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
-    static const int ld = [] {  // experiment: MVPOSE_TCONV_LD=2 reads fragments two steps ahead
-        const char* e = getenv("MVPOSE_TCONV_LD");
-        return e && e[0] == '2' ? 2 : 1;
-    }();
-    auto kern = ld == 2 ? tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM, 2> : tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM, 1>;
+    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr = true;
     }
     const int grid = std::min(p.n_tiles, g_t_cus);
+    MVP_REQUIRE(grid % p.ncb == 0, "tconv: grid %d not a multiple of the %d column blocks", grid, p.ncb);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
 }
 

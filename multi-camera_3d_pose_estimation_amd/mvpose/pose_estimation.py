@@ -148,8 +148,11 @@ class FrameStreamer:
     and two device buffers; every hand-off is an event (no host synchronisation inside the
     loop).  Outputs accumulate on the device and come back with one copy at the end."""
 
-    def __init__(self, est: BatchPoseEstimator, n_views: int, frame_hw, batch_frames: int = 128):
+    def __init__(self, est: BatchPoseEstimator, n_views: int, frame_hw, batch_frames: int = 128,
+                 gather_threads: int = 8):
+        from concurrent.futures import ThreadPoolExecutor
         self.est = est
+        self.pool = ThreadPoolExecutor(max_workers=max(1, min(int(gather_threads), os.cpu_count() or 1)))
         self.V = int(n_views)
         self.H, self.W = (int(v) for v in frame_hw)
         self.step = max(1, min(int(batch_frames), est.max_frames // self.V))
@@ -161,9 +164,16 @@ class FrameStreamer:
         self.consumed = [None, None]   # compute-stream event: kernels done reading device buffer k
 
     def _gather(self, stacks, t0, t1, k):
+        """Chunk [t0, t1) of every camera into pinned buffer k, in pieces of 4 frames over the
+        gather threads (numpy releases the GIL for the copies)."""
         h = self.host[k].numpy()
-        for v, s in enumerate(stacks):
-            np.copyto(h[: t1 - t0, v], s[t0:t1])
+        jobs = [(v, a, min(t1, a + 4)) for v in range(self.V) for a in range(t0, t1, 4)]
+
+        def cp(job):
+            v, a, b = job
+            np.copyto(h[a - t0:b - t0, v], stacks[v][a:b])
+        for _ in self.pool.map(cp, jobs):
+            pass
 
     def run(self, stacks, n_frames=None):
         """stacks: V arrays (T, H, W, 3) uint8 (memory-mapped .npy or in memory).  Returns
