@@ -233,6 +233,17 @@ int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, in
 
 /* project_points_torch (pose_refinement.py:94-179): pts [n][3] f32 -> uv [n][2] f32 for one camera
  * record (R as a 3x3 matrix). */
+/* Extrinsic-from-samples refinement (sgd_optimize(extrinsic_optimization_IDs=[id],
+ * optimize_trajectory=False), reference pose_refinement.py:684-706, :800-831, :915-943):
+ * one pass over the triangulated Gaussian samples samples_dev [n_points][3] f32, ordered
+ * (t, joint, sample) with n_samples per (t, joint); targets_dev [n_points / n_samples][6] f32
+ * = (mean x, mean y, Σ⁻¹ 00, 01, 10, 11) per (t, joint); cam_dev = the learnable camera's
+ * MVP_SGD_CAM_FLOATS record (R as a matrix).  Writes per-block fp64 partial sums
+ * partial_dev [n_blocks][14] = [Σ 0.5 dᵀΣ⁻¹d over finite terms, finite count, Σ dq/dR (9,
+ * row-major), Σ dq/dT (3)]; the caller reduces them (cost = sum / count, gradients / count). */
+int mvp_extrinsic_sample_grad(const float* samples_dev, const float* targets_dev, int n_samples, int64_t n_points,
+                              const float* cam_dev, int ignore_distortions, int n_blocks, double* partial_dev,
+                              void* stream);
 int mvp_project_points(const float* pts, int64_t n, const float* cam, int ignore_distortions, float* uv,
                        void* stream);
 

@@ -473,6 +473,80 @@ __global__ void project_kernel(const float* __restrict__ pts, long n, const floa
     uv[2 * i + 1] = o.v;
 }
 
+// ---- extrinsic-from-samples cost (pose_refinement.py:800-831): the learnable camera's
+// reprojection of the triangulated Gaussian samples against the target Gaussians,
+// cost = -nan_mean(-0.5 dᵀΣ⁻¹d) over (t, joint, sample), and its gradient with respect to
+// the camera's R (3x3 matrix entries, the reference's default learnable form) and T.
+// dcost/dP (camera-frame point) comes from the projection adjoint; dP/dR_ij = X_j,
+// dP/dT_i = 1.  One grid-stride pass; per-block fp64 partial sums
+// [quad sum, finite count, dR (9, row-major), dT (3)] — the host reduces and steps Adam.
+constexpr int kExtBlock = 256;
+constexpr int kExtSums = 14;
+
+__global__ __launch_bounds__(kExtBlock) void extrinsic_grad_kernel(const float* __restrict__ samples,
+                                                                   const float* __restrict__ tgt, int n_samples,
+                                                                   long n_points, const float* __restrict__ cam,
+                                                                   int ign, double* __restrict__ partial) {
+    __shared__ double red[kExtBlock / 64][8];
+    float c[MVP_SGD_CAM_FLOATS];
+#pragma unroll
+    for (int k = 0; k < MVP_SGD_CAM_FLOATS; k++) c[k] = cam[k];
+    const float* K = c;
+    double acc[kExtSums];
+#pragma unroll
+    for (int k = 0; k < kExtSums; k++) acc[k] = 0.0;
+    for (long i = (long)blockIdx.x * kExtBlock + threadIdx.x; i < n_points; i += (long)gridDim.x * kExtBlock) {
+        const float X0 = samples[3 * i], X1 = samples[3 * i + 1], X2 = samples[3 * i + 2];
+        const Target g = load_target(tgt + (i / n_samples) * 6);
+        const Proj o = project(c, X0, X1, X2, ign != 0);
+        const float d0 = o.u - g.m0, d1 = o.v - g.m1;
+        const float val = quad_cost(g, d0, d1);
+        if (!finite(val)) continue;
+        const float s01 = g.a01 + g.a10;
+        const float gu = 0.5f * (2.f * g.a00 * d0 + s01 * d1);
+        const float gv = 0.5f * (s01 * d0 + 2.f * g.a11 * d1);
+        // project_adjoint up to the camera-frame point P = R X + T
+        const float ih2 = 1.f / o.h2;
+        const float gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
+        const float gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
+        float gx = gxd, gy = gyd;
+        if (!ign) {
+            const float* d = c + 21;
+            const float x = o.x, y = o.y, r2 = o.r2, rad = o.rad;
+            const float k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3], k3 = d[4];
+            const float drad = k1 + 2.f * k2 * r2 + 3.f * k3 * r2 * r2;
+            const float dxx = rad + 2.f * x * x * drad + 2.f * p1 * y + 6.f * p2 * x;
+            const float dxy = 2.f * x * y * drad + 2.f * p1 * x + 2.f * p2 * y;
+            const float dyy = rad + 2.f * y * y * drad + 6.f * p1 * y + 2.f * p2 * x;
+            gx = dxx * gxd + dxy * gyd;
+            gy = dxy * gxd + dyy * gyd;
+        }
+        const float iP2 = 1.f / o.P2;
+        const float gp[3] = {gx * iP2, gy * iP2, -(gx * o.x + gy * o.y) * iP2};
+        const float xs[3] = {X0, X1, X2};
+        acc[0] += val;
+        acc[1] += 1.0;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+#pragma unroll
+            for (int q = 0; q < 3; q++) acc[2 + 3 * r + q] += (double)gp[r] * xs[q];
+            acc[11 + r] += gp[r];
+        }
+    }
+    // block reduction in two halves of 7 (red holds 8 per wave)
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        double v[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) v[k] = acc[7 * half + k];
+        block_sum<kExtBlock, 7>(v, red);
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int k = 0; k < 7; k++) partial[(long)blockIdx.x * kExtSums + 7 * half + k] = v[k];
+        __syncthreads();
+    }
+}
+
 }  // namespace
 
 extern "C" int mvp_sgd_workspace_floats(int M, int T, int V, int J, int64_t* out) {
@@ -549,6 +623,19 @@ extern "C" int mvp_project_points(const float* pts, int64_t n, const float* cam,
     constexpr int kBlock = 256;
     hipLaunchKernelGGL(project_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        (hipStream_t)stream, pts, (long)n, cam, ignore_distortions, uv);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_extrinsic_sample_grad(const float* samples, const float* targets, int n_samples,
+                                         int64_t n_points, const float* cam, int ignore_distortions, int n_blocks,
+                                         double* partial, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n_samples > 0 && n_points >= 0 && n_points % n_samples == 0 && n_blocks > 0,
+                "mvp_extrinsic_sample_grad: bad sizes");
+    MVP_REQUIRE(samples && targets && cam && partial, "mvp_extrinsic_sample_grad: NULL device pointer");
+    hipLaunchKernelGGL(extrinsic_grad_kernel, dim3((unsigned)n_blocks), dim3(kExtBlock), 0, (hipStream_t)stream,
+                       samples, targets, n_samples, (long)n_points, cam, ignore_distortions, partial);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END
 }

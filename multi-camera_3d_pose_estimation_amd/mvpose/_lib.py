@@ -59,6 +59,8 @@ SIGNATURES = {
     "mvp_sgd_workspace_floats": (c_int, [c_int, c_int, c_int, c_int, P(c_int64)]),
     # mvp_sgd_params struct pointer declared in mvpose/refine.py
     "mvp_sgd_refine": (c_int, None),
+    "mvp_extrinsic_sample_grad": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_void_p,
+                                          c_void_p]),
     "mvp_project_points": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
     "mvp_linear_interpolation": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int,
                                          c_void_p, c_void_p]),

@@ -12,20 +12,26 @@ Host mirror of the reference's refinement API (pose_refinement.py):
   launch, one workgroup each — the throughput form (SGD shards as replicas).
 * ``project_points_torch`` (:94-179) and ``linear_interpolation`` (:15-84) on the GPU.
 
-Scope: the trajectory-only path the CLI runs (:1210-1214).  Extrinsic learning
-from samples (:684-706, :800-831), the NN trajectory parameterisation
-(``use_NN``) and ``randomize_params`` are outside the hot path and raise
-NotImplementedError.
+* Extrinsic learning from samples (``sgd_optimize(extrinsic_optimization_IDs=[id],
+  optimize_trajectory=False, GT_camera_IDs=[a, b])``, :684-706, :800-831, :915-943):
+  the per-step cost and R/T gradient over every triangulated Gaussian sample is one
+  HIP launch (mvp_extrinsic_sample_grad); the 12 learnable numbers, Adam and
+  clip_grad_norm_ stay torch CPU tensors exactly as in the reference.
+
+Scope: the NN trajectory parameterisation (``use_NN``), ``randomize_params`` and
+joint trajectory + extrinsic optimisation raise NotImplementedError.
 """
 from __future__ import annotations
 
 import ctypes
 import math
+import random
 
 import numpy as np
 import torch
 
 from . import _lib
+from . import ops
 from ._lib import call
 
 CAM_FLOATS = 26
@@ -159,6 +165,29 @@ def linear_interpolation(points, k=5, k_std=2, median_std=2, use_rolling_average
     return out.to(home) if was_tensor else out.cpu().numpy()
 
 
+EXT_SUMS = 14
+
+
+def extrinsic_sample_grad(samples, targets, cam, n_samples, ignore_distortions=False, n_blocks=None):
+    """One mvp_extrinsic_sample_grad pass.  samples (T, J, N, 3) f32 and targets (T, J, 6) f32
+    [mean x, mean y, Σ⁻¹ 00, 01, 10, 11] on the GPU, cam = one MVP_SGD_CAM_FLOATS f32 record on
+    the GPU.  Returns the reduced fp64 sums (14,) on the device:
+    [Σ 0.5 dᵀΣ⁻¹d, finite count, Σ dq/dR (9), Σ dq/dT (3)]."""
+    n_pts = samples.numel() // 3
+    if samples.dtype != torch.float32 or targets.dtype != torch.float32 or cam.dtype != torch.float32:
+        raise TypeError("samples, targets and cam must be float32")
+    if not (samples.is_contiguous() and targets.is_contiguous() and cam.numel() == CAM_FLOATS):
+        raise ValueError("samples/targets must be contiguous, cam one 26-float record")
+    if targets.numel() * n_samples != 6 * n_pts:
+        raise ValueError(f"targets {tuple(targets.shape)} do not match {n_pts} samples of {n_samples} per target")
+    if n_blocks is None:
+        n_blocks = max(1, min(1024, (n_pts + 255) // 256))
+    part = torch.empty((n_blocks, EXT_SUMS), dtype=torch.float64, device=samples.device)
+    call("mvp_extrinsic_sample_grad", _ptr(samples), _ptr(targets), int(n_samples), int(n_pts), _ptr(cam),
+         int(bool(ignore_distortions)), int(n_blocks), _ptr(part), _stream(samples.device))
+    return part.sum(0)
+
+
 def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=None, lr=0.001, betas=(0.9, 0.999),
                         lambda_smooth=1.0, lambda_body_length=1.0, patience=100, tolerance=1e-5, max_iter=1000,
                         batch_size=None, ignore_distortions=False, own_camera_gaussians=False, max_grad_norm=1.0,
@@ -254,8 +283,15 @@ class Optimized_3d_Pose_Estimation:
                      print_frequency=100, batch_size=None, N_sample_points=100, GT_camera_IDs=None,
                      ignore_distortions=False, reset_camera_params=False, print_compute_times=False,
                      time_interval=[0, -1], randomize_params=False, use_NN=False, own_camera_gaussians=False):
-        if extrinsic_optimization_IDs or not optimize_trajectory or use_NN or randomize_params:
-            raise NotImplementedError("only the trajectory-only refinement (the CLI's path) runs on the GPU")
+        if use_NN or randomize_params:
+            raise NotImplementedError("use_NN / randomize_params are not part of the GPU path")
+        if extrinsic_optimization_IDs is not None and optimize_trajectory is False:
+            return self._sgd_extrinsic(list(extrinsic_optimization_IDs), GT_camera_IDs, lr, betas, lambda_smooth,
+                                       lambda_body_length, patience, tolerance, max_iter, print_frequency,
+                                       batch_size, N_sample_points, ignore_distortions, reset_camera_params,
+                                       time_interval)
+        if extrinsic_optimization_IDs:
+            raise NotImplementedError("joint trajectory + extrinsic optimisation is not part of the GPU path")
         if self.n_dims != 3:
             raise NotImplementedError("3D trajectories only")
         a, b = time_interval
@@ -295,4 +331,156 @@ class Optimized_3d_Pose_Estimation:
         if print_frequency and print_frequency < 10 ** 8:
             for it in range(0, iters, print_frequency):
                 print(f"Iteration {it}: " + ", ".join(f"{n}: {im[it, COST_NAMES.index(n)]:.2e}" for n in names))
+        return self
+
+    # ---- extrinsic learning from samples (pose_refinement.py:894-1096 with
+    # optimize_trajectory=False): sample_gaussians (:684-706), construct_sample_cost
+    # (:800-831), the Adam loop (:1000-1089).
+    def sample_gaussians(self, G, GT, N):
+        """:684-706 — np.random.multivariate_normal per (t, GT camera, joint) in the reference's
+        loop order on the global numpy RNG (so seeded runs draw the same samples); returns
+        (T, J, N, 2 cams, 2) float64."""
+        T, J = G.shape[0], G.shape[2]
+        means = G[:, GT, :, :2]
+        covs = G[:, GT, :, 2:].reshape(T, 2, J, 2, 2)
+        samples = np.empty((T, 2, J, N, 2))
+        for t in range(T):
+            for c in range(2):
+                for j in range(J):
+                    samples[t, c, j] = np.random.multivariate_normal(means[t, c, j].numpy(), covs[t, c, j].numpy(), N)
+        return np.transpose(samples, (0, 2, 3, 1, 4))
+
+    def _window_costs(self, G, X, B, lambda_smooth, lambda_body_length):
+        """The smoothness / body-length costs of each window (:836-860) for the fixed trajectory
+        X (T, J, 3): one mvp_sgd_refine launch with max_iter=0 and lr=0 (the trajectory does not
+        move), its per-window cost rows.  Returns {name: [f32 per window]}."""
+        cam0 = [c.detach() for c in self.decomposed_cam_params[self.camera_IDs[0]]]
+        r = refine_trajectories(G[:, :1][None], X[None], [cam0], body_lengths=self.body_lengths,
+                                lr=0.0, lambda_smooth=lambda_smooth, lambda_body_length=lambda_body_length,
+                                patience=1, max_iter=0, batch_size=B, device=self.device)
+        bc = r["batch_costs"][0, 0].cpu().numpy()
+        out = {}
+        if lambda_smooth > 0:
+            out["smoothness_cost"] = [np.float32(v) for v in bc[:, COST_NAMES.index("smoothness_cost")]]
+        if lambda_body_length > 0:
+            out["body_length_cost"] = [np.float32(v) for v in bc[:, COST_NAMES.index("body_length_cost")]]
+        return out
+
+    def _sgd_extrinsic(self, ext_ids, GT, lr, betas, lambda_smooth, lambda_body_length, patience, tolerance,
+                       max_iter, print_frequency, batch_size, N_sample_points, ignore_distortions,
+                       reset_camera_params, time_interval):
+        if self.n_dims != 3:
+            raise NotImplementedError("3D trajectories only")
+        a, b = time_interval
+        G_sub = self.gaussians[a:b]
+        n_sub = len(G_sub)
+        B = n_sub if batch_size is None else int(batch_size)
+        T = int(np.floor(n_sub / B) * B)
+        if T != n_sub:
+            # the reference's cov_invs_subset keeps all n_sub rows (:898) and its einsum fails
+            raise ValueError(f"batch_size {B} must divide the {n_sub} frames of time_interval {time_interval} "
+                             "when learning extrinsics from samples (the reference fails here too)")
+        G = G_sub[:T]
+        if reset_camera_params:
+            self.decomposed_cam_params = {k: [c.clone().detach() for c in v]
+                                          for k, v in self.decomposed_cam_params_initial.items()}
+        if GT is None:          # the reference's branch for this iterates over None (:918-919)
+            raise TypeError("GT_camera_IDs is required when learning extrinsics from samples")
+        assert len(ext_ids) == 1
+        assert len(GT) == 2
+        assert min(i in self.decomposed_cam_params for i in GT)
+        assert ext_ids[0] in self.decomposed_cam_params
+        if self.n_cams <= 2:
+            raise ValueError("construct_sample_cost reads camera index 2's Gaussians (:802-805): need >= 3 cameras")
+        if not self.body_lengths:
+            raise ValueError("body_lengths is required (create_body_length_vect, :767-779)")
+        ID = ext_ids[0]
+        # :935-945 — axis-angle of the initial R (not the learnable one), non-zero R / T entries
+        self.decomposed_cam_params_initial[ID][1] = rotation_conversion(self.decomposed_cam_params_initial[ID][1],
+                                                                        to_vector=True)
+        Rp, Tp = self.decomposed_cam_params[ID][1], self.decomposed_cam_params[ID][2]
+        Rp[Rp == 0] = random.random() / 10 ** 6
+        Tp[Tp == 0] = random.random() / 10 ** 6
+        Rp.requires_grad_(True)
+        Tp.requires_grad_(True)
+        learnable = [Rp, Tp]
+        trajectory = self.initial_trajectory[a:b].clone().detach()
+        self.trajectory = trajectory
+        self.best_trajectory = None
+        self.best_decomposed_cam_params = None
+        n_win = (T - B) // (B // 2) + 1
+        optimizer = torch.optim.Adam(learnable, lr=lr, betas=betas)
+
+        dev = self.device
+        N = int(self.N_sample_points)
+        samples = self.sample_gaussians(G, GT, N)                    # (T, J, N, 2, 2) f64
+        self.samples = samples
+        J = G.shape[2]
+        # construct_sample_cost: triangulate every sample with the GT pair (utils.triangulate_points)
+        kt = np.empty((T * J * N, 3, 2), np.float32)
+        flat = samples.reshape(-1, 2, 2)
+        kt[:, 0, :] = flat[:, :, 0]
+        kt[:, 1, :] = flat[:, :, 1]
+        kt[:, 2, :] = 1.0
+        p1, p2 = self.decomposed_cam_params[GT[0]], self.decomposed_cam_params[GT[1]]
+        pair = ops.pack_cameras([[p.detach().numpy() for p in (p1[0], p1[1], p1[2], p1[3])],
+                                 [p.detach().numpy() for p in (p2[0], p2[1], p2[2], p2[3])]])
+        samples_3d = ops.triangulate(torch.from_numpy(kt).to(dev), torch.from_numpy(pair).to(dev), [0, 1])
+        samples_3d = samples_3d.reshape(T, J, N, 3).contiguous()
+        self.samples_3d = samples_3d
+        # targets: camera index 2's means (:802, hard-coded) with camera 0's Σ⁻¹ (quirk F5, :663)
+        g2 = G[:, 2, :, :2].to(dev)
+        cv = G[:, 0, :, 2:].to(dev)
+        c00, c01, c10, c11 = cv[..., 0] + 1e-6, cv[..., 1], cv[..., 2], cv[..., 3] + 1e-6
+        det = c00 * c11 - c01 * c10
+        targets = torch.stack([g2[..., 0], g2[..., 1], c11 / det, -c01 / det, -c10 / det, c00 / det], -1)
+        targets = targets.contiguous()
+        K, dist = self.decomposed_cam_params[ID][0], self.decomposed_cam_params[ID][3]
+
+        const = self._window_costs(G, trajectory[:T], B, lambda_smooth, lambda_body_length)
+        names = ["total_cost"] + list(const.keys()) + ["extrinsic_param_sample_cost"]
+        hist = {n: [] for n in names}          # all_costs and all_costs_total share these lists (F6)
+        best_total = float("inf")
+        no_improve = 0
+        it = 0
+        while no_improve < patience and it <= max_iter:
+            for w in range(n_win):
+                optimizer.zero_grad()
+                Rm = rotation_conversion(Rp, to_vector=False)
+                cam = torch.cat([K.detach().reshape(9), Rm.detach().reshape(9), Tp.detach().reshape(3),
+                                 dist.detach().reshape(5)]).to(torch.float32).to(dev, non_blocking=True)
+                sums = extrinsic_sample_grad(samples_3d, targets, cam, N, ignore_distortions).cpu()
+                cnt = sums[1]
+                ext_cost = (sums[0] / cnt).to(torch.float32)
+                gR = (sums[2:11] / cnt).to(torch.float32).reshape(3, 3)
+                gT = (sums[11:14] / cnt).to(torch.float32)
+                # chain through the (possibly axis-angle) parameterisation exactly as autograd would
+                surrogate = (Rm * gR).sum() + (Tp.reshape(3) * gT).sum()
+                surrogate.backward()
+                costs = {n: torch.tensor(const[n][w]) for n in const}
+                costs["extrinsic_param_sample_cost"] = ext_cost
+                total = torch.sum(torch.stack(list(costs.values())))
+                torch.nn.utils.clip_grad_norm_(learnable, max_norm=1.0)
+                optimizer.step()
+                hist["total_cost"].append(np.float32(total))
+                for n in costs:
+                    hist[n].append(np.float32(costs[n]))
+            for n in names:
+                hist[n].append(np.mean(hist[n], 0))
+            cur = hist["total_cost"][-1]
+            if cur < best_total - tolerance:
+                best_total = cur
+                self.best_trajectory = trajectory.clone().detach()
+                self.best_decomposed_cam_params = {k: [p.clone().detach() for p in v]
+                                                   for k, v in self.decomposed_cam_params.items()}
+                no_improve = 0
+            else:
+                no_improve += 1
+            if no_improve >= patience:
+                break
+            if print_frequency and it % print_frequency == 0 and print_frequency < 10 ** 8:
+                print(f"Iteration {it}: " + ", ".join(f"{n}: {hist[n][-1]:.2e}" for n in names))
+            it += 1
+        self.all_costs_total = hist
+        self.iterations = it
         return self

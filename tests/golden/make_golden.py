@@ -220,6 +220,71 @@ def gen_sgd(pr):
               seeds=np.array([seed]), **{"hist_" + k: v for k, v in hist.items()})
 
 
+def _rotation(rvec):
+    th = np.linalg.norm(rvec)
+    k = np.asarray(rvec) / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+EXTRINSIC_CASES = [
+    # name, seed, learnable ID, GT IDs, (rvec perturbation, T offset), kwargs
+    ("sgd_ext_c2", 81, 2, [0, 1], ([0.02, -0.03, 0.01], [6.0, -4.0, 3.0]),
+     dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100, max_iter=12, batch_size=4,
+          N_sample_points=20)),
+    # camera 0 is R = I, T = 0: every zero entry becomes random.random()/1e6 (:939-940)
+    ("sgd_ext_c0", 82, 0, [1, 2], None,
+     dict(lr=0.02, lambda_smooth=1e-3, lambda_body_length=0.0, patience=3, max_iter=40, batch_size=None,
+          N_sample_points=12, tolerance=1e-3)),
+]
+
+
+def gen_sgd_extrinsic(pr):
+    """sgd_optimize(extrinsic_optimization_IDs=[id], optimize_trajectory=False,
+    GT_camera_IDs=[a, b]) (pose_refinement.py:684-706, :800-831, :894-1096).  The stub
+    cv2.undistortPoints gets the float64 samples cast to float32 (the oracle restates the
+    float32-keypoint path the pipeline uses; real cv2 would keep float64 here)."""
+    import random
+    cv2 = sys.modules["cv2"]
+    und = cv2.undistortPoints
+    cv2.undistortPoints = lambda src, *a, **k: und(np.asarray(src, np.float32), *a, **k)
+    try:
+        for name, seed, ext_id, gt, pert, kw in EXTRINSIC_CASES:
+            kw = dict(kw)
+            T = 9        # time_interval [0, -1] keeps 8 rows: batch_size 4 -> windows [0,4) [2,6) [4,8)
+            cams, gauss, init = sgd_inputs(3, T, seed)
+            params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+            if pert is not None:
+                params[ext_id][1] = _rotation(pert[0]) @ params[ext_id][1]
+                params[ext_id][2] = params[ext_id][2] + np.array(pert[1]).reshape(3, 1)
+            R0 = np.stack([p[1] for p in params.values()])
+            T0 = np.stack([p[2] for p in params.values()])
+            np.random.seed(seed)
+            random.seed(seed + 1)
+            torch.manual_seed(0)
+            n_samples = kw.pop("N_sample_points")   # sgd_optimize's own N_sample_points is unused (:684)
+            opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                                  body_lengths=dict(MY_LENGTHS), N_sample_points=n_samples)
+            full_kw = dict(print_frequency=10 ** 9, extrinsic_optimization_IDs=[ext_id], optimize_trajectory=False,
+                           GT_camera_IDs=gt)
+            full_kw.update(kw)
+            opt.sgd_optimize(**full_kw)
+            hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
+            best = opt.best_decomposed_cam_params[ext_id]
+            fin = opt.decomposed_cam_params[ext_id]
+            _save(f"{name}.npz", gauss=gauss, init=init, K=np.stack([c["K"] for c in cams]), R=R0, T=T0,
+                  dist=np.stack([c["dist"] for c in cams]), ext_id=np.array([ext_id]), gt_ids=np.array(gt),
+                  n_samples=np.array([n_samples]),
+                  samples=opt.samples, samples_3d=opt.samples_3d.numpy(),
+                  best_R=best[1].detach().numpy(), best_T=best[2].detach().numpy(),
+                  final_R=fin[1].detach().numpy(), final_T=fin[2].detach().numpy(),
+                  kw_names=np.array(list(kw.keys())),
+                  kw_vals=np.array([np.nan if v is None else float(v) for v in kw.values()]),
+                  seeds=np.array([seed, seed + 1, 0]), **{"hist_" + k: v for k, v in hist.items()})
+    finally:
+        cv2.undistortPoints = und
+
+
 def gen_interp(pr):
     """pose_refinement.linear_interpolation (pose_refinement.py:15-84) on a noisy
     kpts_3d-like sequence with spikes, a NaN frame and constant stretches."""
@@ -237,7 +302,7 @@ def gen_interp(pr):
     _save("interp.npz", points=pts, seeds=np.array([seed]), **outs)
 
 
-GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "interp")
+GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "sgd_extrinsic", "interp")
 
 
 def main():
@@ -249,7 +314,8 @@ def main():
     from mmpose_pose_estimation import PoseEstimator  # noqa: E402
     gens = {"dlt": lambda: gen_dlt(ref_utils), "pose3d": lambda: gen_pose3d(pose_estimation),
             "moments": lambda: gen_moments(PoseEstimator), "project": lambda: gen_project(pr),
-            "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr), "interp": lambda: gen_interp(pr)}
+            "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr),
+            "sgd_extrinsic": lambda: gen_sgd_extrinsic(pr), "interp": lambda: gen_interp(pr)}
     for name in GENERATORS:
         if name in only:
             gens[name]()

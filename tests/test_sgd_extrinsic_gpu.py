@@ -1,0 +1,150 @@
+"""Extrinsic learning from samples (sgd_optimize(extrinsic_optimization_IDs=[id],
+optimize_trajectory=False, GT_camera_IDs=[a, b]), reference pose_refinement.py:684-706,
+:800-831, :894-1096) against golden runs of the reference itself
+(tests/golden/make_golden.py gen_sgd_extrinsic):
+
+* the Gaussian samples: the reference's np.random.multivariate_normal loop on the global
+  RNG — bit-identical (CPU, no kernel);
+* the triangulated samples (mvp_triangulate on the float32-cast samples; the golden's stub
+  cv2 does the same cast) — within 1e-3 cm: P = K[R|T] is fp64 here and float32 np.dot in
+  the reference;
+* one mvp_extrinsic_sample_grad pass vs a torch fp32 autograd restatement of
+  construct_sample_cost's cost() — cost rtol 1e-5, gradient rtol 1e-4;
+* the whole optimisation: the shared cost / running-mean history (F6), final and best
+  R / T — within f32 reduction-order drift (rtol 2e-3 on costs, 2e-3 on parameters).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from mvpose import refine
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+CASES = ("sgd_ext_c2", "sgd_ext_c0")
+MY_LENGTHS = {"left_shoulder_left_elbow": 38, "left_elbow_left_wrist": 27,
+              "right_shoulder_right_elbow": 38, "right_elbow_right_wrist": 27,
+              "left_hip_left_knee": 51, "left_knee_left_ankle": 40,
+              "right_hip_right_knee": 51, "right_knee_right_ankle": 40,
+              "left_hip_right_hip": 31, "left_shoulder_left_hip": 54,
+              "right_shoulder_right_hip": 54, "left_shoulder_right_shoulder": 47}
+
+
+def _load(name):
+    z = np.load(os.path.join(GOLD, name + ".npz"))
+    kw = {str(k): (None if np.isnan(v) else v) for k, v in zip(z["kw_names"], z["kw_vals"])}
+    for k in ("patience", "max_iter", "batch_size", "N_sample_points"):
+        if kw.get(k) is not None:
+            kw[k] = int(kw[k])
+    return z, kw
+
+
+def _opt(z):
+    params = {i: [z["K"][i], z["R"][i], z["T"][i], z["dist"][i]] for i in range(len(z["K"]))}
+    return refine.Optimized_3d_Pose_Estimation(z["gauss"], z["init"], decomposed_cam_params_initial=params,
+                                               body_lengths=dict(MY_LENGTHS), N_sample_points=int(z["n_samples"][0]))
+
+
+def _seed(z):
+    np.random.seed(int(z["seeds"][0]))
+    random.seed(int(z["seeds"][1]))
+    torch.manual_seed(int(z["seeds"][2]))
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_samples_bitwise(name):
+    z, kw = _load(name)
+    opt = _opt(z)
+    _seed(z)
+    G = opt.gaussians[0:-1]
+    s = opt.sample_gaussians(G, [int(i) for i in z["gt_ids"]], int(z["n_samples"][0]))
+    np.testing.assert_array_equal(s, z["samples"])
+
+
+def _torch_cost(samples_3d, targets_mean, cov_inv, K, R, T, dist):
+    """construct_sample_cost's cost() (:811-829) in torch fp32 autograd: project_points_torch
+    (:94-179) then -nan_mean(-0.5 dᵀΣ⁻¹d)."""
+    P = samples_3d.reshape(-1, 3) @ R.T + T.reshape(1, 3)
+    x, y = P[:, 0] / P[:, 2], P[:, 1] / P[:, 2]
+    k1, k2, p1, p2, k3 = dist.reshape(5)
+    r2 = x * x + y * y
+    rad = 1 + k1 * r2 + k2 * r2 ** 2 + k3 * r2 ** 3
+    xd = x * rad + (2 * p1 * x * y + p2 * (r2 + 2 * x * x))
+    yd = y * rad + (p1 * (r2 + 2 * y * y) + 2 * p2 * x * y)
+    h = torch.stack([xd, yd, torch.ones_like(xd)], 1) @ K.T
+    uv = (h[:, :2] / h[:, 2:3]).reshape(samples_3d.shape[:3] + (2,))
+    d = uv - targets_mean[:, :, None, :]
+    q = -0.5 * torch.einsum("...i,...ij,...j->...", d, cov_inv[:, :, None], d)
+    m = torch.isfinite(q)
+    return -(q[m].sum() / m.sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_sample_cost_and_gradient(name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z, _ = _load(name)
+    ext = int(z["ext_id"][0])
+    s3 = torch.tensor(z["samples_3d"], dtype=torch.float32)
+    G = torch.tensor(z["gauss"][:-1], dtype=torch.float32)
+    mean2 = G[:, 2, :, :2]
+    cov0 = G[:, 0, :, 2:].reshape(*G.shape[:1], G.shape[2], 2, 2) + 1e-6 * torch.eye(2)
+    cinv = torch.linalg.inv(cov0)
+    K = torch.tensor(z["K"][ext], dtype=torch.float32)
+    dist = torch.tensor(z["dist"][ext], dtype=torch.float32)
+    R = torch.tensor(z["final_R"], dtype=torch.float32, requires_grad=True)
+    T = torch.tensor(z["final_T"], dtype=torch.float32, requires_grad=True)
+    ref = _torch_cost(s3, mean2, cinv, K, R, T, dist)
+    ref.backward()
+    targets = torch.cat([mean2, cinv.reshape(*cinv.shape[:2], 4)], -1).cuda().contiguous()
+    cam = torch.cat([K.reshape(9), R.detach().reshape(9), T.detach().reshape(3), dist.reshape(5)]).cuda()
+    sums = refine.extrinsic_sample_grad(s3.cuda().contiguous(), targets, cam, s3.shape[2]).cpu()
+    cnt = sums[1].item()
+    assert cnt == s3.shape[0] * s3.shape[1] * s3.shape[2]
+    np.testing.assert_allclose(sums[0].item() / cnt, ref.item(), rtol=1e-5)
+    np.testing.assert_allclose((sums[2:11] / cnt).reshape(3, 3).numpy(), R.grad.numpy(), rtol=1e-4,
+                               atol=1e-4 * R.grad.abs().max().item())
+    np.testing.assert_allclose((sums[11:14] / cnt).numpy(), T.grad.reshape(3).numpy(), rtol=1e-4,
+                               atol=1e-4 * T.grad.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_extrinsic_optimisation_matches_reference(name):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z, kw = _load(name)
+    ext = int(z["ext_id"][0])
+    opt = _opt(z)
+    _seed(z)
+    opt.sgd_optimize(extrinsic_optimization_IDs=[ext], optimize_trajectory=False,
+                     GT_camera_IDs=[int(i) for i in z["gt_ids"]], print_frequency=10 ** 9, **kw)
+    np.testing.assert_allclose(opt.samples_3d.cpu().numpy(), z["samples_3d"], rtol=0, atol=1e-3)
+    names = [k[5:] for k in z.files if k.startswith("hist_")]
+    assert list(opt.all_costs_total.keys()) == names
+    for n in names:
+        got = np.array(opt.all_costs_total[n], np.float64)
+        assert got.shape == z["hist_" + n].shape, n
+        np.testing.assert_allclose(got, z["hist_" + n], rtol=2e-3, err_msg=n)
+    fin = opt.decomposed_cam_params[ext]
+    best = opt.best_decomposed_cam_params[ext]
+    np.testing.assert_allclose(fin[1].detach().numpy(), z["final_R"], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(fin[2].detach().numpy(), z["final_T"], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(best[1].numpy(), z["best_R"], rtol=0, atol=2e-3)
+    np.testing.assert_allclose(best[2].numpy(), z["best_T"], rtol=2e-3, atol=2e-3)
+
+
+def test_extrinsic_argument_errors():
+    z, _ = _load("sgd_ext_c2")
+    with pytest.raises(TypeError):
+        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=False)
+    with pytest.raises(AssertionError):
+        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[1, 2], optimize_trajectory=False, GT_camera_IDs=[0, 1])
+    with pytest.raises(ValueError):      # 8 frames, batch 3: the reference's einsum fails here
+        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=False, GT_camera_IDs=[0, 1],
+                             batch_size=3)
+    with pytest.raises(NotImplementedError):
+        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=True)
