@@ -241,6 +241,55 @@ def sgd_line(dev):
                                        f"adjoint, {SGD_FLOP_PER_COORD} per coordinate (stencil, segments, Adam)"}}
 
 
+def extrinsic_line(dev, T=1000, N=100, reps=20):
+    """one mvp_extrinsic_sample_grad pass (the per-Adam-step cost + R/T gradient
+    of sgd_optimize(extrinsic_optimization_IDs=[id], optimize_trajectory=False), reference
+    pose_refinement.py:800-831) over T x 17 x N triangulated samples, HBM roofline on the
+    12 B/sample read; plus the whole host-orchestrated step (kernel, 14-double readback,
+    torch CPU Adam on the 12 learnable numbers)."""
+    from mvpose import refine, synthetic as syn
+    cams = syn.make_rig(3, seed=9)
+    poses = syn.make_poses(T, seed=10)
+    rng = np.random.default_rng(11)
+    s3 = torch.tensor(poses[:, :, None, :] + rng.normal(0, 2.0, (T, 17, N, 3)), dtype=torch.float32,
+                      device=dev).contiguous()
+    uv = syn.project(poses, cams[2])
+    tg = np.concatenate([uv, np.full((T, 17, 1), 1 / 9.0), np.zeros((T, 17, 2)), np.full((T, 17, 1), 1 / 9.0)], -1)
+    tg = torch.tensor(tg, dtype=torch.float32, device=dev).contiguous()
+    cam = torch.from_numpy(refine.camera_record(cams[2]["K"], cams[2]["R"], cams[2]["T"], cams[2]["dist"])).to(dev)
+    refine.extrinsic_sample_grad(s3, tg, cam, N)
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(s)
+    for _ in range(reps):
+        refine.extrinsic_sample_grad(s3, tg, cam, N)
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    R = torch.tensor(cams[2]["R"], dtype=torch.float32, requires_grad=True)
+    Tt = torch.tensor(cams[2]["T"], dtype=torch.float32, requires_grad=True)
+    opt = torch.optim.Adam([R, Tt], lr=0.01)
+    for it in range(reps + 3):          # 3 untimed steps (the optimizer's first-step setup)
+        if it == 3:
+            t0 = time.perf_counter()
+        opt.zero_grad()
+        sums = refine.extrinsic_sample_grad(s3, tg, cam, N).cpu()
+        R.grad = (sums[2:11] / sums[1]).to(torch.float32).reshape(3, 3)
+        Tt.grad = (sums[11:14] / sums[1]).to(torch.float32).reshape(3, 1)
+        torch.nn.utils.clip_grad_norm_([R, Tt], max_norm=1.0)
+        opt.step()
+    step_ms = (time.perf_counter() - t0) * 1e3 / reps
+    n = T * 17 * N
+    gbs = n * 12 / (ms * 1e-3) / 1e9
+    return {"workload": f"T={T}, 17 joints, N={N} samples per (t, joint): {n} samples",
+            "kernel": "extrinsic_grad_kernel", "avg_launch_ms": ms, "samples_per_s": n / (ms * 1e-3),
+            "host_step_ms": step_ms,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "bytes_model": "12 B per sample (xyz f32); the 24 B "
+                                                                    "target per (t, joint) is L2-resident"}}
+
+
 def ingest_line(est, V, n_frames=512, batch=128):
     """SURVEY §7 "host frame supply": the same 2D stage fed from HOST memory (decoded
     frames in RAM, as the reference holds whole videos, utils.py:849-909) through the
@@ -334,6 +383,7 @@ def main():
             t4["config"] = "BASELINE config 3: 4-cam overdetermined 8x4 DLT, all views"
             extra["roofline_triangulate_v4"] = t4
             extra["sgd"] = sgd_line(dev)
+            extra["sgd_extrinsic"] = extrinsic_line(dev)
             extra["host_ingest"] = ingest_line(est, V)
 
     if rank == 0:

@@ -171,6 +171,7 @@ struct PPair {
     uint16_t* y2;
     const uint16_t* zero;
     long n_pix;
+    int diag;  // unused (diagnostics slot)
 };
 
 // threads per workgroup (one workgroup per CU, 2 waves per SIMD): 12-wave workgroups
@@ -178,12 +179,21 @@ struct PPair {
 template <int KCH>
 constexpr int pair_threads() { return 512; }
 
-template <int KCH>
-__global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PPair p) {
+// KCH: K chunks of the first GEMM (2: 64 ch, 4: the cat-fused 64 + 64); RES: conv3 adds a
+// residual (the cat-fused join has none: its downsample is folded into K); LA: units of
+// load look-ahead per wave.  This kernel is bound by the bytes each wave keeps in flight
+// (8 waves per CU): with one unit ahead the cat-fused join had 4 KB per wave in flight
+// and moved 2.5 TB/s.
+// SECOND = false: conv3 alone (layer1's last block, whose output goes to transition1),
+// same 256-cout waves and staged stores, no second GEMM.
+template <int KCH, bool RES, int LA, bool SECOND = true>
+__global__ __launch_bounds__(pair_threads<KCH>(), 1) void conv1x1_pair_kernel(PPair p) {
     constexpr int kPairThreads = pair_threads<KCH>();
     constexpr int BM = 256, NCT = BM / 16, CIN = KCH * 32;
-    constexpr int S1 = KCH * 4 * BM;  // expand weight slots [chunk][q][row]
-    constexpr int S2 = 8 * 4 * 64;    // reduce weight slots [chunk][q][row]
+    constexpr int S1 = KCH * 4 * BM;            // expand weight slots [chunk][q][row]
+    constexpr int S2 = SECOND ? 8 * 4 * 64 : 0;  // reduce weight slots [chunk][q][row]
+    constexpr int R = LA + 1;         // register ring of units (current + LA ahead)
+    constexpr int NRQ = RES ? 8 : 1;  // residual uint4 per lane per unit
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     __shared__ float4 sb1[BM / 4];
     __shared__ float4 sb2[16];
@@ -194,29 +204,38 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
         const int sl = s0 + lane;
         const void* src = p.zero;
         if (sl < S1) {
+            // A row r of cout tile c holds cout 128 (c >> 3) + 32 (r >> 2) + 4 (c & 7) + (r & 3):
+            // in half h (tiles 8h .. 8h + 7) lane group g owns couts 128h + 32g .. + 31
             const int co = sl % BM, tq = sl / BM;
             const int c = co >> 4, r = co & 15;
-            src = p.w1 + (size_t)((r >> 2) * (BM / 4) + c * 4 + (r & 3)) * CIN + tq * 8;
+            src = p.w1 + (size_t)(128 * (c >> 3) + 32 * (r >> 2) + 4 * (c & 7) + (r & 3)) * CIN + tq * 8;
         } else if (sl < S1 + S2) {
+            // second GEMM K chunk j, lane group q: channels 128 (j >> 2) + 32 q + 8 (j & 3)
             const int s2 = sl - S1, co = s2 % 64, tq = s2 / 64;  // tq = chunk j * 4 + q
             const int c = co >> 4, r = co & 15, j = tq >> 2, q = tq & 3;
-            src = p.w2 + (size_t)((r >> 2) * 16 + c * 4 + (r & 3)) * 256 + q * 64 + j * 8;
+            src = p.w2 + (size_t)((r >> 2) * 16 + c * 4 + (r & 3)) * 256 + 128 * (j >> 2) + 32 * q + 8 * (j & 3);
         }
         glds16(src, lds + s0 * 16);
     }
     if (tid < BM / 4) sb1[tid] = reinterpret_cast<const float4*>(p.b1)[tid];
-    if (tid < 16) sb2[tid] = reinterpret_cast<const float4*>(p.b2)[tid];
+    if (SECOND && tid < 16) sb2[tid] = reinterpret_cast<const float4*>(p.b2)[tid];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const uint8_t* lds2 = lds + S1 * 16;
+    uint8_t* stg = lds + (S1 + S2) * 16 + wave * 4096;  // this wave's 4 KiB y staging block
 
     const long n_units = (p.n_pix + 15) / 16;
     const long ustep = (long)gridDim.x * NWAVES;
-    // software pipeline: the next unit's input and residual loads are issued before
-    // this unit's MFMAs (both halves' residuals: 2 x 4 x 16 B per lane)
-    bf16x8 bn[KCH];
-    uint4 rn0[4], rn1[4];
-    auto load_unit = [&](long u) {
+    // software pipeline: unit u + LA's input and residual loads are issued before unit u's
+    // MFMAs; ring slot of unit u0 + i * ustep is i % R (all indices compile-time)
+    struct UnitRegs {
+        bf16x8 b[KCH];
+        uint4 r[NRQ];
+    };
+    UnitRegs ring[R];
+    auto load_unit = [&](long u, UnitRegs& ur) {
+        bf16x8 (&bn)[KCH] = ur.b;
+        uint4 (&rn)[NRQ] = ur.r;
         const long pp = u * 16 + (lane & 15);
         const long pix = pp < p.n_pix ? pp : p.n_pix - 1;
         const uint16_t* src = p.x + pix * p.c1 + g * 8;
@@ -224,38 +243,54 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
 #pragma unroll
         for (int ch = 0; ch < KCH; ch++)
             bn[ch] = *reinterpret_cast<const bf16x8*>((ch < p.kch1 ? src : src2) + ch * 32);
-        const uint16_t* rsrc = p.res ? p.res + pix * BM + g * 64 : p.zero + lane * 64;
+        if (RES) {  // coalesced: load 4h + i = pixels 4i .. 4i + 3, couts 128h .. 128h + 127
+            const long pr0 = u * 16 + (lane >> 4);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            rn0[q] = *reinterpret_cast<const uint4*>(rsrc + q * 8);
-            rn1[q] = *reinterpret_cast<const uint4*>(rsrc + 32 + q * 8);
+            for (int q = 0; q < 8; q++) {
+                const long pr = pr0 + 4 * (q & 3);
+                const long pc = pr < p.n_pix ? pr : p.n_pix - 1;
+                rn[q] = *reinterpret_cast<const uint4*>(p.res + pc * BM + 128 * (q >> 2) + (lane & 15) * 8);
+            }
         }
     };
-    long u = (long)blockIdx.x * NWAVES + wave;
-    if (u < n_units) load_unit(u);
-    for (; u < n_units; u += ustep) {
+    // the unit's registers by value: two inlined copies merged by the compiler must select
+    // values, not a pointer into the ring (that sent the ring to scratch)
+    auto process = [&](long u, const UnitRegs cur) {
+        const bf16x8(&b)[KCH] = cur.b;
+        const uint4(&rr)[NRQ] = cur.r;
         const long pp = u * 16 + (lane & 15);
         const bool valid = pp < p.n_pix;
         const long pix = valid ? pp : p.n_pix - 1;
-        bf16x8 b[KCH];
-#pragma unroll
-        for (int ch = 0; ch < KCH; ch++) b[ch] = bn[ch];
-        uint4 rv[4], rv_next[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            rv[q] = rn0[q];
-            rv_next[q] = rn1[q];
-        }
-        if (u + ustep < n_units) load_unit(u + ustep);
-        uint16_t* yrow = p.y + pix * BM + g * 64;
         f32x4 acc2[4];
 #pragma unroll
         for (int c = 0; c < 4; c++) acc2[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // two halves of 8 cout tiles: lane group g's couts 64g + 32h .. 64g + 32h + 31,
-        // i.e. the second GEMM's K chunks j = 4h .. 4h + 3 (register pressure: one half
-        // of the accumulators and packed outputs live at a time)
+        // two halves of 8 cout tiles: lane group g's couts 128h + 32g .. + 31, i.e. the
+        // second GEMM's K chunks j = 4h .. 4h + 3 (register pressure: one half of the
+        // accumulators and packed outputs live at a time)
+        uint4 rhalf[RES ? 4 : 1];
+        if (RES) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) rhalf[i] = rr[i];
+        }
 #pragma unroll 1
         for (int h = 0; h < 2; h++) {
+            // residual of half h: through the staging block into the owner layout (the
+            // inverse of the y staging below; lane group g gets couts 128h + 32g .. + 31)
+            uint4 rv[NRQ > 1 ? 4 : 1];
+            if (RES) {
+                const int k = lane & 15;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const int pr = 4 * i + (lane >> 4);
+                    *reinterpret_cast<uint4*>(stg + pr * 256 + ((k ^ pr) << 4)) = rhalf[i];
+                }
+                const int px = lane & 15;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    rv[q] = *reinterpret_cast<const uint4*>(stg + px * 256 + (((4 * g + q) ^ px) << 4));
+#pragma unroll
+                for (int i = 0; i < 4; i++) rhalf[i] = rr[4 + i];  // the next half's
+            }
             f32x4 acc[NCT / 2];
 #pragma unroll
             for (int c = 0; c < NCT / 2; c++) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -271,28 +306,45 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
             uint32_t o[NCT];
 #pragma unroll
             for (int c = 0; c < NCT / 2; c++) {
-                const float4 bb = sb1[g * (BM / 16) + h * (NCT / 2) + c];
+                const float4 bb = sb1[32 * h + 8 * g + c];
                 float v[4] = {acc[c][0] + bb.x, acc[c][1] + bb.y, acc[c][2] + bb.z, acc[c][3] + bb.w};
-                const uint4 r4 = rv[c >> 1];
-                const uint32_t r0 = (c & 1) ? r4.z : r4.x, r1 = (c & 1) ? r4.w : r4.y;
-                v[0] += bf16_to_f32(r0 & 0xffff);
-                v[1] += bf16_to_f32(r0 >> 16);
-                v[2] += bf16_to_f32(r1 & 0xffff);
-                v[3] += bf16_to_f32(r1 >> 16);
+                if (RES) {
+                    const uint4 r4 = rv[c >> 1];
+                    const uint32_t r0 = (c & 1) ? r4.z : r4.x, r1 = (c & 1) ? r4.w : r4.y;
+                    v[0] += bf16_to_f32(r0 & 0xffff);
+                    v[1] += bf16_to_f32(r0 >> 16);
+                    v[2] += bf16_to_f32(r1 & 0xffff);
+                    v[3] += bf16_to_f32(r1 >> 16);
+                }
 #pragma unroll
                 for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
                 o[2 * c] = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
                 o[2 * c + 1] = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
             }
-            if (valid) {
+            // y stores through the wave's LDS staging block: a half is 16 pixels x 128
+            // contiguous couts (256 B), so 16 lanes store one pixel's run and an instruction
+            // writes 4 whole runs.  Lane-owned 64-B pieces stored directly were 64 separate
+            // 16-B requests per instruction (cat-fused join: 1015 us; 64-B runs: 788 us; 599 us
+            // for the same bytes lane-contiguous).  Pixel px's run at px * 256, 16-B chunk k
+            // (= 4g + q) at slot k ^ px: conflict-free for ds_write_b128 and ds_read_b128.
+            {
+                const int px = lane & 15;
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    *reinterpret_cast<uint4*>(yrow + h * 32 + q * 8) =
+                    *reinterpret_cast<uint4*>(stg + px * 256 + (((4 * g + q) ^ px) << 4)) =
                         uint4{o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
-            }
-            // second GEMM, K chunks j = 4h + jj: this lane group's channels 64g + 8j .. +7
+                const int k = lane & 15;
 #pragma unroll
-            for (int jj = 0; jj < 4; jj++) {
+                for (int i = 0; i < 4; i++) {
+                    const int pr = 4 * i + (lane >> 4);
+                    const long pq = u * 16 + pr;
+                    const uint4 v = *reinterpret_cast<const uint4*>(stg + pr * 256 + ((k ^ pr) << 4));
+                    if (pq < p.n_pix) *reinterpret_cast<uint4*>(p.y + pq * BM + 128 * h + k * 8) = v;
+                }
+            }
+            // second GEMM, K chunks j = 4h + jj: this lane group's channels 128h + 32g + 8jj .. +7
+#pragma unroll
+            for (int jj = 0; jj < (SECOND ? 4 : 0); jj++) {
                 const int j = h * 4 + jj;
                 union {
                     uint4 u;
@@ -306,9 +358,8 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
                     acc2[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bj.v, acc2[c], 0, 0, 0);
                 }
             }
-#pragma unroll
-            for (int q = 0; q < 4; q++) rv[q] = rv_next[q];
         }
+        if (!SECOND) return;
         uint32_t o2[8];
 #pragma unroll
         for (int c = 0; c < 4; c++) {
@@ -322,6 +373,21 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 2) void conv1x1_pair_kernel(PP
             uint16_t* y2row = p.y2 + pix * 64 + g * 16;
             *reinterpret_cast<uint4*>(y2row) = uint4{o2[0], o2[1], o2[2], o2[3]};
             *reinterpret_cast<uint4*>(y2row + 8) = uint4{o2[4], o2[5], o2[6], o2[7]};
+        }
+    };
+    const long u0 = (long)blockIdx.x * NWAVES + wave;
+#pragma unroll
+    for (int i = 0; i < LA; i++)
+        if (u0 + i * ustep < n_units) load_unit(u0 + i * ustep, ring[i]);
+    for (long u = u0; u < n_units; u += R * ustep) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            const long uu = u + r * ustep;
+            if (uu < n_units) {  // (no break: the ring indices must stay compile-time)
+                const long un = uu + LA * ustep;
+                if (un < n_units) load_unit(un, ring[(r + LA) % R]);
+                process(uu, ring[r]);
+            }
         }
     }
 }
@@ -417,8 +483,13 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
     MVP_REQUIRE(c.c1 % 32 == 0 && c.c1 > 0 && (!c.x2 || c.c2 % 32 == 0), "conv1x1_pair: channel split %d/%d", c.c1,
                 c.c2);
     if (c.n_pix == 0) return;
+    static int diag = -1;
+    if (diag < 0) {
+        const char* e = getenv("MVPOSE_PAIR_DIAG");
+        diag = e ? atoi(e) : 0;
+    }
     PPair p{c.x, c.x2, c.c1, c.x2 ? c.c2 : 0, c.c1 / 32, c.w1, c.b1, c.res, c.y, c.w2, c.b2, c.y2,
-            conv_zero_region(), c.n_pix};
+            conv_zero_region(), c.n_pix, diag};
     if (g_cus1 == 0) {
         int dev = 0;
         MVP_HIP(hipGetDevice(&dev));
@@ -427,20 +498,70 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
     const long units = (c.n_pix + 15) / 16;
     auto go = [&](auto kern, int kch) {
         const int kPairThreads = kch == 2 ? pair_threads<2>() : pair_threads<4>();
-        const int lds = (kch * 4 * 256 + 8 * 4 * 64) * 16;
-        static int per_cu[2] = {0, 0};
-        int& pc = per_cu[kch == 4];
-        if (pc == 0) {
-            MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-            MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, kPairThreads, lds));
-            if (pc < 1) pc = 1;
-        }
+        const int lds = (kch * 4 * 256 + 8 * 4 * 64) * 16 + (kPairThreads / 64) * 4096;
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        int pc = 0;
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, kPairThreads, lds));
+        if (pc < 1) pc = 1;
         const long grid = std::min<long>((long)g_cus1 * pc, (units + kPairThreads / 64 - 1) / (kPairThreads / 64));
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kPairThreads), lds, s, p);
     };
-    if (cin == 64) go(conv1x1_pair_kernel<2>, 2);
-    else go(conv1x1_pair_kernel<4>, 4);
+    // look-ahead depth (MVPOSE_PAIR_LA, diagnostics): units in flight per wave
+    static int la = -1;
+    if (la < 0) {
+        const char* e = getenv("MVPOSE_PAIR_LA");
+        la = e ? atoi(e) : 0;
+    }
+    MVP_REQUIRE(c.res || c.x2, "conv1x1_pair: a join without residual must be cat-fused");
+    if (cin == 64) {
+        MVP_REQUIRE(c.res != nullptr, "conv1x1_pair: 64-ch join needs its residual");
+        if (la == 2) go(conv1x1_pair_kernel<2, true, 2>, 2);
+        else go(conv1x1_pair_kernel<2, true, 1>, 2);  // 1496 vs 1575 us per join graph (LA 2)
+    } else if (c.res) {
+        go(conv1x1_pair_kernel<4, true, 1>, 4);
+    } else {
+        if (la == 1) go(conv1x1_pair_kernel<4, false, 1>, 4);
+        else if (la == 2) go(conv1x1_pair_kernel<4, false, 2>, 4);
+        else go(conv1x1_pair_kernel<4, false, 3>, 4);
+    }
     MVP_HIP(hipGetLastError());
+}
+
+// A 1x1 conv 64 -> 256 (or the cat-fused 64 + 64 -> 256) with ReLU, + optional 256-ch
+// residual, on the Bottleneck-join kernel without its second GEMM: one wave owns all 256
+// couts of 16 pixels (input read once instead of once per 128-cout column block) and its
+// residual loads / output stores go through LDS as whole 256-B runs.
+bool launch_conv1x1_wide(const ConvLaunch& c, hipStream_t s) {
+    const int cin = c.Cin;
+    if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cout != 256 || !c.relu) return false;
+    if (!(cin == 64 || (cin == 128 && c.x2 && c.c1 == 64))) return false;
+    if (cin == 64 && !c.res) return false;
+    const char* e = getenv("MVPOSE_NO_WIDE1X1");  // diagnostics/tests: conv1x1_kernel instead
+    if (e && e[0] == '1') return false;
+    const long n_pix = (long)c.N * c.H * c.W;
+    if (n_pix == 0) return true;
+    PPair p{c.x, c.x2, cin == 128 ? 64 : 64, cin == 128 ? 64 : 0, 2, c.w, c.bias, c.res, c.y, nullptr, nullptr,
+            nullptr, conv_zero_region(), n_pix, 0};
+    if (g_cus1 == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_cus1, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const long units = (n_pix + 15) / 16;
+    auto go = [&](auto kern, int kch) {
+        const int lds = kch * 4 * 256 * 16 + 8 * 4096;
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        int pc = 0;
+        MVP_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&pc, kern, 512, lds));
+        if (pc < 1) pc = 1;
+        const long grid = std::min<long>((long)g_cus1 * pc, (units + 7) / 8);
+        hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds, s, p);
+    };
+    if (cin == 64) go(conv1x1_pair_kernel<2, true, 1, false>, 2);
+    else if (c.res) go(conv1x1_pair_kernel<4, true, 1, false>, 4);
+    else go(conv1x1_pair_kernel<4, false, 1, false>, 4);
+    MVP_HIP(hipGetLastError());
+    return true;
 }
 
 bool launch_head1x1(const ConvLaunch& c, hipStream_t s) {
@@ -458,6 +579,7 @@ bool launch_head1x1(const ConvLaunch& c, hipStream_t s) {
 
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
     if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cin % 32 != 0) return false;
+    if (launch_conv1x1_wide(c, s)) return true;
     const int bm = conv_cout_pad(c.Cout) % 128 == 0 && c.Cin <= 64 ? 128 : conv_cout_pad(c.Cout) % 64 == 0 ? 64 : 32;
     if (c.Cout % (bm / 4) != 0) return false;  // lane groups own bm/4 consecutive couts
     static const bool disabled = [] {
