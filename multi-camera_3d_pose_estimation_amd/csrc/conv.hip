@@ -722,29 +722,32 @@ __global__ __launch_bounds__(256) void stem_mfma_kernel(const uint16_t* __restri
 }
 
 // ---------------------------------------------------------------- fuse sum
+// out = act(sum_k nearest_up(in[k], 2^lg[k])), one 16-B channel chunk per lane, f32 sums
+// in input order.  One grid row per crop and 32-bit in-crop indices with power-of-two
+// chunk counts and upsample factors as shifts: the 64-bit divisions of a flat index
+// (5 per lane) made the 64x48 fuse VALU-bound.
 struct FuseParams {
     const uint16_t* in[4];
-    int up[4];
+    int lg[4];
     int n_in;
     uint16_t* out;
-    int N, H, W, C, relu;
+    int H, W, C, lgc, relu;
 };
 
 __global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
-    const int chunks = p.C / 8;
-    const long i = (long)blockIdx.x * 256 + threadIdx.x;
-    const long total = (long)p.N * p.H * p.W * chunks;
-    if (i >= total) return;
-    const int ch = i % chunks;
-    const long pix = i / chunks;
-    const int w = pix % p.W;
-    const int h = (pix / p.W) % p.H;
-    const int n = pix / ((long)p.W * p.H);
+    const int i = blockIdx.x * 256 + threadIdx.x;  // (pixel, chunk) within crop n
+    const int n = blockIdx.y;
+    const int hw = p.H * p.W;
+    if (i >= (hw << p.lgc)) return;
+    const int ch = i & ((1 << p.lgc) - 1);
+    const int pix = i >> p.lgc;
+    const int h = (int)((unsigned)pix / (unsigned)p.W), w = pix - h * p.W;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     for (int k = 0; k < p.n_in; k++) {
-        const int u = p.up[k];
-        const int hs = p.H / u, ws = p.W / u;
-        const uint4 v = *reinterpret_cast<const uint4*>(p.in[k] + (((size_t)n * hs + h / u) * ws + w / u) * p.C + ch * 8);
+        const int lg = p.lg[k];
+        const int hs = p.H >> lg, ws = p.W >> lg;
+        const long src = ((long)n * hs * ws + (h >> lg) * ws + (w >> lg)) * p.C + ch * 8;
+        const uint4 v = *reinterpret_cast<const uint4*>(p.in[k] + src);
         acc[0] += bf16_to_f32(v.x & 0xffff);
         acc[1] += bf16_to_f32(v.x >> 16);
         acc[2] += bf16_to_f32(v.y & 0xffff);
@@ -762,7 +765,7 @@ __global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
     o.y = (uint32_t)f32_to_bf16(acc[2]) | ((uint32_t)f32_to_bf16(acc[3]) << 16);
     o.z = (uint32_t)f32_to_bf16(acc[4]) | ((uint32_t)f32_to_bf16(acc[5]) << 16);
     o.w = (uint32_t)f32_to_bf16(acc[6]) | ((uint32_t)f32_to_bf16(acc[7]) << 16);
-    *reinterpret_cast<uint4*>(p.out + pix * p.C + ch * 8) = o;
+    *reinterpret_cast<uint4*>(p.out + ((long)n * hw + pix) * p.C + ch * 8) = o;
 }
 
 }  // namespace
@@ -843,23 +846,29 @@ void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t*
 void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_t* out, int N, int H, int W, int C,
                      int relu, hipStream_t s) {
     MVP_REQUIRE(n_in >= 1 && n_in <= 4, "fuse: n_in=%d", n_in);
-    MVP_REQUIRE(C % 8 == 0, "fuse: C=%d", C);
+    const int chunks = C / 8;
+    MVP_REQUIRE(C % 8 == 0 && (chunks & (chunks - 1)) == 0, "fuse: C=%d (C/8 must be a power of two)", C);
     FuseParams p{};
     for (int k = 0; k < n_in; k++) {
+        int lg = 0;
+        while ((1 << lg) < up[k]) lg++;
+        MVP_REQUIRE(up[k] == (1 << lg) && H % up[k] == 0 && W % up[k] == 0, "fuse: bad upsample factor %d", up[k]);
         p.in[k] = in[k];
-        p.up[k] = up[k];
-        MVP_REQUIRE(up[k] >= 1 && H % up[k] == 0 && W % up[k] == 0, "fuse: bad upsample factor %d", up[k]);
+        p.lg[k] = lg;
     }
+    int lgc = 0;
+    while ((1 << lgc) < chunks) lgc++;
     p.n_in = n_in;
     p.out = out;
-    p.N = N;
     p.H = H;
     p.W = W;
     p.C = C;
+    p.lgc = lgc;
     p.relu = relu;
-    const long total = (long)N * H * W * (C / 8);
-    if (total == 0) return;
-    hipLaunchKernelGGL(fuse_sum_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p);
+    const long per = (long)H * W * chunks;
+    MVP_REQUIRE(per < (1L << 30) && N < 65536, "fuse: plane too large");
+    if (per == 0 || N == 0) return;
+    hipLaunchKernelGGL(fuse_sum_kernel, dim3((unsigned)((per + 255) / 256), (unsigned)N), dim3(256), 0, s, p);
     MVP_HIP(hipGetLastError());
 }
 
