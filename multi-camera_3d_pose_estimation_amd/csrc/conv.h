@@ -70,6 +70,22 @@ bool launch_tconv(const ConvLaunch& c, hipStream_t s);
 // false when the conv is not one of those planes (or MVPOSE_NO_S2CONV=1).
 bool launch_s2conv(const ConvLaunch& c, hipStream_t s);
 
+// Sibling 3x3/s2 convs on one input (graph sib-fusion, s2conv.hip): up to 3 outputs whose
+// weights are concatenated along cout (w [128][3][3][Cin], zero rows past the last
+// output; bias [128]); output i gets couts [sum_{j<i} cout_j, + cout_i) with its own ReLU.
+struct S2Multi {
+    const uint16_t* x = nullptr;
+    const uint16_t* w = nullptr;
+    const float* bias = nullptr;
+    int N = 0, H = 0, W = 0, Cin = 0;
+    int n_out = 0;
+    uint16_t* y[3] = {nullptr, nullptr, nullptr};
+    int cout[3] = {0, 0, 0};
+    int relu[3] = {0, 0, 0};
+};
+bool s2conv_multi_supported(int H, int W, int Cin, int total_cout);
+void launch_s2conv_multi(const S2Multi& m, hipStream_t s);
+
 // 3x3/s2 stem conv on 4-channel (RGB + zero) bf16 crops, BN folded, ReLU.
 // w: [64][3][3][4] f32, bias [64] f32.  x [N][H][W][4] -> y [N][H/2][W/2][64].
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,

@@ -369,10 +369,28 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 1) void conv1x1_pair_kernel(PP
             o2[2 * c] = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
             o2[2 * c + 1] = (uint32_t)f32_to_bf16(v2) | ((uint32_t)f32_to_bf16(v3) << 16);
         }
-        if (valid) {
+        // y2 (64 ch = 128-B pixel rows) through the staging block too: chunk k = 2g + q of
+        // pixel px at px * 128 + (k ^ px & 7) * 16; then 8 lanes store one whole row and an
+        // instruction 1 KiB of consecutive pixels
+        if (p.diag == 1) {
             uint16_t* y2row = p.y2 + pix * 64 + g * 16;
-            *reinterpret_cast<uint4*>(y2row) = uint4{o2[0], o2[1], o2[2], o2[3]};
-            *reinterpret_cast<uint4*>(y2row + 8) = uint4{o2[4], o2[5], o2[6], o2[7]};
+            if (valid) {
+                *reinterpret_cast<uint4*>(y2row) = uint4{o2[0], o2[1], o2[2], o2[3]};
+                *reinterpret_cast<uint4*>(y2row + 8) = uint4{o2[4], o2[5], o2[6], o2[7]};
+            }
+        } else {
+            const int px = lane & 15;
+            *reinterpret_cast<uint4*>(stg + px * 128 + (((2 * g) ^ px) & 7) * 16) = uint4{o2[0], o2[1], o2[2], o2[3]};
+            *reinterpret_cast<uint4*>(stg + px * 128 + (((2 * g + 1) ^ px) & 7) * 16) =
+                uint4{o2[4], o2[5], o2[6], o2[7]};
+            const int k = lane & 7;
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int pr = 8 * i + (lane >> 3);
+                const long pq = u * 16 + pr;
+                const uint4 v = *reinterpret_cast<const uint4*>(stg + pr * 128 + ((k ^ pr) & 7) * 16);
+                if (pq < p.n_pix) *reinterpret_cast<uint4*>(p.y2 + pq * 64 + k * 8) = v;
+            }
         }
     };
     const long u0 = (long)blockIdx.x * NWAVES + wave;

@@ -32,6 +32,9 @@ struct Graph {
     std::vector<int> pair_tail;   // 1x1 op whose 256->64 successor (absorbed) runs in the same launch (-1: none)
     std::vector<int> stem_head;   // 3x3/s2 conv that also runs the (absorbed) stem op stem_head[k] (-1: none)
     std::vector<int> twin;        // 3x3/s1 conv whose (absorbed) 3x3/s2 sibling on the same input runs in its launch
+    std::vector<std::vector<int>> sib;  // 3x3/s2 conv whose (absorbed) 3x3/s2 siblings on its input run in its launch
+    std::vector<uint16_t*> sib_w;       // their cout-concatenated weights [128][3][3][cin] (owned)
+    std::vector<float*> sib_b;          // and biases [128] (owned)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -271,6 +274,41 @@ void twin_fuse(Graph& g, bool enable) {
     }
 }
 
+// Sibling-fusion pass: in an HRModule fuse layer the branch-0 tensor (32 ch @ 64x48) is the
+// input of up to three 3x3/s2 convs (-> 64 ch for branch 1; -> 32 ch + ReLU starting the
+// chains to branches 2 and 3).  They run as ONE launch over cout-concatenated weights
+// (s2conv_multi): the 201 MB input is read once instead of once per conv.
+void sib_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size();
+    g.sib.assign(no, {});
+    g.sib_w.assign(no, nullptr);
+    g.sib_b.assign(no, nullptr);
+    if (!enable) return;
+    auto plain_s2 = [&](int k) {
+        const mvp_op_desc& op = g.ops[k];
+        return op.kind == MVP_OP_CONV && !g.absorbed[k] && !g.block_head[k] && g.cat_src[k] < 0 &&
+               g.pair_tail[k] < 0 && g.stem_head[k] < 0 && g.twin[k] < 0 && op.ks == 3 && op.stride == 2 &&
+               (op.n_in < 2 || op.in[1] < 0) && op.cout % 32 == 0 && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    for (int a = 0; a < no; a++) {
+        if (!plain_s2(a)) continue;
+        const mvp_op_desc& A = g.ops[a];
+        const mvp_tensor_desc& x = g.tensors[A.in[0]];
+        int tot = A.cout;
+        std::vector<int> list;
+        for (int b = a + 1; b < no && list.size() < 2; b++) {
+            const mvp_op_desc& B = g.ops[b];
+            if (B.in[0] != A.in[0] || !plain_s2(b) || B.segment != A.segment) continue;
+            if (!s2conv_multi_supported(x.h, x.w, x.c, tot + B.cout)) continue;
+            list.push_back(b);
+            tot += B.cout;
+        }
+        if (list.empty()) continue;
+        for (int b : list) g.absorbed[b] = 1;
+        g.sib[a] = list;
+    }
+}
+
 // Device-side concatenated weights / summed biases of the cat-fused ops: allocated at graph
 // create time, filled from the blobs by cat_fill (create and mvp_graph_refresh_weights).
 void cat_alloc(Graph& g) {
@@ -281,6 +319,35 @@ void cat_alloc(Graph& g) {
         const int cp = conv_cout_pad(B.cout), cin = B.cin + g.ops[a].cin;
         MVP_HIP(hipMalloc(&g.cat_w[b], (size_t)cp * cin * sizeof(uint16_t)));
         MVP_HIP(hipMalloc(&g.cat_b[b], (size_t)cp * sizeof(float)));
+    }
+}
+
+void sib_alloc(Graph& g) {
+    for (int a = 0; a < (int)g.ops.size(); a++) {
+        if (g.sib[a].empty()) continue;
+        const int kk = 9 * g.ops[a].cin;
+        MVP_HIP(hipMalloc(&g.sib_w[a], (size_t)128 * kk * sizeof(uint16_t)));
+        MVP_HIP(hipMalloc(&g.sib_b[a], (size_t)128 * sizeof(float)));
+    }
+}
+
+void sib_fill(Graph& g) {
+    for (int a = 0; a < (int)g.ops.size(); a++) {
+        if (g.sib[a].empty()) continue;
+        const int kk = 9 * g.ops[a].cin;
+        MVP_HIP(hipMemset(g.sib_w[a], 0, (size_t)128 * kk * sizeof(uint16_t)));
+        MVP_HIP(hipMemset(g.sib_b[a], 0, (size_t)128 * sizeof(float)));
+        int row = 0;
+        std::vector<int> members{a};
+        members.insert(members.end(), g.sib[a].begin(), g.sib[a].end());
+        for (int m : members) {
+            const mvp_op_desc& op = g.ops[m];
+            MVP_HIP(hipMemcpy(g.sib_w[a] + (size_t)row * kk, g.wb + op.w_off, (size_t)op.cout * kk * sizeof(uint16_t),
+                              hipMemcpyDeviceToDevice));
+            MVP_HIP(hipMemcpy(g.sib_b[a] + row, g.fb + op.b_off, (size_t)op.cout * sizeof(float),
+                              hipMemcpyDeviceToDevice));
+            row += op.cout;
+        }
     }
 }
 
@@ -308,8 +375,14 @@ void cat_free(Graph& g) {
         if (p) (void)hipFree(p);
     for (float* p : g.cat_b)
         if (p) (void)hipFree(p);
+    for (uint16_t* p : g.sib_w)
+        if (p) (void)hipFree(p);
+    for (float* p : g.sib_b)
+        if (p) (void)hipFree(p);
     g.cat_w.clear();
     g.cat_b.clear();
+    g.sib_w.clear();
+    g.sib_b.clear();
 }
 
 // Greedy first-fit placement of tensors in one arena by lifetime [def, last use].
@@ -355,6 +428,13 @@ void plan(Graph& g) {
             seg_of_def[y2] = op.segment;
             touch(y2);
         }
+        for (int b : g.sib[k]) {  // the absorbed siblings' outputs are written here
+            const int y2 = g.ops[b].out;
+            first[y2] = k;
+            if (last[y2] < k) last[y2] = k;
+            seg_of_def[y2] = op.segment;
+            touch(y2);
+        }
         if (g.stem_head[k] >= 0) {  // the absorbed stem's input is read here
             const int x = g.ops[g.stem_head[k]].in[0];
             last[x] = std::max(last[x], k);
@@ -390,6 +470,7 @@ void plan(Graph& g) {
                 widen(op.in[i]);
         if (g.stem_head[k] >= 0) widen(g.ops[g.stem_head[k]].in[0]);
         if (g.twin[k] >= 0) widen(g.ops[g.twin[k]].out);
+        for (int b : g.sib[k]) widen(g.ops[b].out);
         if (g.cat_src[k] >= 0) widen(g.ops[g.cat_src[k]].in[0]);
         if (g.pair_tail[k] >= 0) widen(g.ops[g.pair_tail[k]].out);
     }
@@ -467,8 +548,11 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
         mvp::stem_fuse(*g, !(nf && nf[0] == '1'));
         mvp::twin_fuse(*g, !(nf && nf[0] == '1'));
+        mvp::sib_fuse(*g, !(nf && nf[0] == '1'));
         mvp::cat_alloc(*g);
+        mvp::sib_alloc(*g);
         mvp::cat_fill(*g);
+        mvp::sib_fill(*g);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
             hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
@@ -517,6 +601,28 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             const mvp_op_desc& b = g->ops[g->twin[k]];
             mvp::launch_trans1((const uint16_t*)ptr(op.in[0]), g->wb, op.w_off, g->fb + op.b_off, b.w_off,
                                g->fb + b.b_off, (uint16_t*)ptr(op.out), (uint16_t*)ptr(b.out), nb, s);
+            return;
+        }
+        if (!g->sib[k].empty()) {  // this 3x3/s2 conv and its siblings on the same input
+            const mvp_tensor_desc& x = g->tensors[op.in[0]];
+            mvp::S2Multi m;
+            m.x = (const uint16_t*)ptr(op.in[0]);
+            m.w = g->sib_w[k];
+            m.bias = g->sib_b[k];
+            m.N = nb;
+            m.H = x.h;
+            m.W = x.w;
+            m.Cin = op.cin;
+            std::vector<int> members{k};
+            members.insert(members.end(), g->sib[k].begin(), g->sib[k].end());
+            m.n_out = (int)members.size();
+            for (int i = 0; i < m.n_out; i++) {
+                const mvp_op_desc& o2 = g->ops[members[i]];
+                m.y[i] = (uint16_t*)ptr(o2.out);
+                m.cout[i] = o2.cout;
+                m.relu[i] = o2.relu;
+            }
+            mvp::launch_s2conv_multi(m, s);
             return;
         }
         if (g->stem_head[k] >= 0) {  // stem conv1 + this conv2 in one launch
@@ -603,6 +709,7 @@ extern "C" int mvp_graph_refresh_weights(void* handle) {
     MVP_REQUIRE(g != nullptr, "mvp_graph_refresh_weights: NULL handle");
     MVP_HIP(hipDeviceSynchronize());
     mvp::cat_fill(*g);
+    mvp::sib_fill(*g);
     MVP_HIP(hipDeviceSynchronize());
     MVP_ABI_END
 }

@@ -75,6 +75,11 @@ struct SParams {
     const uint16_t* zero;
     uint16_t* sink;
     int N, Cout, n_tiles, ncb, relu;
+    // sibling outputs (graph sib-fusion): couts [Cout, Cout + c1) go to y1 ([..][c1]) and
+    // [Cout + c1, Cout + c1 + c2) to y2, each with its own ReLU flag; couts beyond are padding
+    uint16_t* y1;
+    uint16_t* y2;
+    int c1, c2, relu1, relu2;
 };
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
@@ -231,15 +236,27 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
 
         if (last) {
             const long pix0 = (long)(n0 * G::HO + ho0) * G::WO;
+            // which output this lane's 16 couts belong to (boundaries are multiples of 32)
+            uint16_t* yb = p.y;
+            int cs = p.Cout, cl = cob, rl = p.relu;
+            bool cok = true;
+            if (cob >= p.Cout) {
+                const bool s1 = cob < p.Cout + p.c1;
+                yb = s1 ? p.y1 : p.y2;
+                cs = s1 ? p.c1 : p.c2;
+                cl = s1 ? cob - p.Cout : cob - p.Cout - p.c1;
+                rl = s1 ? p.relu1 : p.relu2;
+                cok = cob < p.Cout + p.c1 + p.c2;
+            }
 #pragma unroll
             for (int t = 0; t < G::NT; t++) {
-                const bool ok = n0 + enb[t] < p.N;
-                uint16_t* yrow = ok ? p.y + (pix0 + eoff[t]) * p.Cout + cob : p.sink + lane * 16;
+                const bool ok = n0 + enb[t] < p.N && cok;
+                uint16_t* yrow = ok ? yb + (pix0 + eoff[t]) * cs + cl : p.sink + lane * 16;
                 uint32_t o[8];
 #pragma unroll
                 for (int e = 0; e < 8; e++) {
                     float v0 = acc[t][2 * e], v1 = acc[t][2 * e + 1];
-                    if (p.relu) {
+                    if (rl) {
                         v0 = relu1(v0);
                         v1 = relu1(v1);
                     }
@@ -257,6 +274,19 @@ int g_s_cus = 0;
 uint16_t* g_s_sink = nullptr;
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
+void launch_sp(SParams p, hipStream_t s) {
+    using G = SCfg<CIN, H, W, TH, NB, WRES, BM>;
+    auto kern = s2conv_kernel<CIN, H, W, TH, NB, WRES, BM>;
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr = true;
+    }
+    const int grid = std::min(p.n_tiles, g_s_cus);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
+}
+
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
 void launch_s(const ConvLaunch& c, hipStream_t s) {
     using G = SCfg<CIN, H, W, TH, NB, WRES, BM>;
     if (g_s_cus == 0) {
@@ -270,7 +300,8 @@ void launch_s(const ConvLaunch& c, hipStream_t s) {
     MVP_REQUIRE(c.Cin == CIN && c.H == H && c.W == W, "s2conv: plane mismatch");
     const long tiles = (long)((c.N + NB - 1) / NB) * (G::HO / TH) * (c.Cout / BM);
     MVP_REQUIRE(tiles < (1L << 30), "s2conv: too many tiles");
-    SParams p{c.x, c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles, c.Cout / BM, c.relu};
+    SParams p{c.x, c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles, c.Cout / BM, c.relu,
+              nullptr, nullptr, 0, 0, 0, 0};
     auto kern = s2conv_kernel<CIN, H, W, TH, NB, WRES, BM>;
     static bool attr = false;
     if (!attr) {
@@ -281,7 +312,44 @@ void launch_s(const ConvLaunch& c, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
 }
 
+void init_s() {
+    if (g_s_cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_s_cus, hipDeviceAttributeMultiprocessorCount, dev));
+        MVP_HIP(hipMalloc(&g_s_sink, 64 * 32));
+    }
+}
+
 }  // namespace
+
+bool s2conv_multi_supported(int H, int W, int Cin, int total_cout) {
+    const char* e = getenv("MVPOSE_NO_SIBFUSE");  // diagnostics/tests: one launch per sibling
+    if (e && e[0] == '1') return false;
+    return H == 64 && W == 48 && Cin == 32 && total_cout <= 128;
+}
+
+// The sibling 3x3/s2 convs reading the 64x48x32 branch-0 tensor in a fuse layer (-> 64 ch
+// for branch 1, -> 32 ch (ReLU) starting the chains to branches 2 and 3): one launch, one
+// pass over the input, 128-cout tiles (weights concatenated along cout, zero-padded).
+void launch_s2conv_multi(const S2Multi& m, hipStream_t s) {
+    MVP_REQUIRE(m.n_out >= 1 && m.n_out <= 3, "s2conv_multi: %d outputs", m.n_out);
+    int tot = 0;
+    for (int i = 0; i < m.n_out; i++) {
+        MVP_REQUIRE(m.cout[i] % 32 == 0 && m.cout[i] > 0, "s2conv_multi: cout %d", m.cout[i]);
+        tot += m.cout[i];
+    }
+    MVP_REQUIRE(s2conv_multi_supported(m.H, m.W, m.Cin, tot), "s2conv_multi: unsupported plane");
+    init_s();
+    using G = SCfg<32, 64, 48, 8, 1, true, 128>;
+    const long tiles = (long)m.N * (G::HO / 8);
+    SParams p{m.x, m.w, m.bias, m.y[0], conv_zero_region(), g_s_sink, m.N, m.cout[0], (int)tiles, 1, m.relu[0],
+              m.n_out > 1 ? m.y[1] : nullptr, m.n_out > 2 ? m.y[2] : nullptr, m.n_out > 1 ? m.cout[1] : 0,
+              m.n_out > 2 ? m.cout[2] : 0, m.n_out > 1 ? m.relu[1] : 0, m.n_out > 2 ? m.relu[2] : 0};
+    if (tiles == 0) return;
+    launch_sp<32, 64, 48, 8, 1, true, 128>(p, s);
+    MVP_HIP(hipGetLastError());
+}
 
 bool launch_s2conv(const ConvLaunch& c, hipStream_t s) {
     if (c.ks != 3 || c.stride != 2 || c.out_f32_nchw || c.res || c.x2) return false;

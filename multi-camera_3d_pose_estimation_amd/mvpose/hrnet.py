@@ -417,6 +417,28 @@ def transition_spec(seed: int = 0, output: int = 0):
     return g, x, (t0, t1)[output], sd
 
 
+SIBLINGS = (("s1", 64, False), ("s2", 32, True), ("s3", 32, True))
+
+
+def sibling_spec(seed: int = 0, output: int = 0, n: int = 3):
+    """A stage-4 HRModule fuse layer's 3x3/s2 convs on the branch-0 tensor (32 ch @ 64x48):
+    s1 -> 64 ch (BN, no ReLU), s2 / s3 -> 32 ch (BN + ReLU) — the first n of them, the
+    siblings the graph's sibling-fusion pass runs as one launch; the graph output is
+    sibling `output`.  For kernel tests.  Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+    for j, co, _ in SIBLINGS[:n]:
+        sd[f"{j}.weight"] = torch.randn((co, 32, 3, 3), generator=gen) * (2.0 / (9 * 32)) ** 0.5
+        sd[f"{j}bn.weight"] = 1.0 + 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.bias"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_mean"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_var"] = 1.0 + 0.2 * torch.rand((co,), generator=gen)
+    g = GraphSpec()
+    x = g.tensor(64, 48, 32)
+    outs = [g.conv(sd, j, j + "bn", x, 2, relu) for j, _, relu in SIBLINGS[:n]]
+    return g, x, outs[output], sd
+
+
 def conv_spec(cin: int, cout: int, h: int, w: int, k: int = 3, stride: int = 1, relu: bool = True, seed: int = 0):
     """One k x k conv (+ folded BN, optional ReLU) cin -> cout on an h x w plane, for
     kernel tests and per-conv benchmarks.  Returns (spec, input id, output id, state dict)."""

@@ -91,6 +91,7 @@ def test_fused_basic_blocks_bitwise_equal(models, monkeypatch):
     monkeypatch.setenv("MVPOSE_NO_PAIRFUSE", "1")
     monkeypatch.setenv("MVPOSE_NO_STEMFUSE", "1")  # stem2.hip / trans1.hip sum K in their own order
     monkeypatch.setenv("MVPOSE_NO_TRANSFUSE", "1")  # (tolerance tests)
+    monkeypatch.setenv("MVPOSE_NO_SIBFUSE", "1")
     monkeypatch.setenv("MVPOSE_NO_FUSE", "1")
     unfused = hrnet.HRNetBackbone(sd, max_batch=6)
     monkeypatch.delenv("MVPOSE_NO_FUSE")
@@ -175,6 +176,30 @@ def test_stem_fusion_matches_unfused(models, monkeypatch):
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
     assert rel < 2e-2, rel
     assert fused.arena_bytes <= plain.arena_bytes
+
+
+def test_sibling_fusion_matches_unfused(models, monkeypatch):
+    """The fuse layers' 3x3/s2 siblings on the branch-0 tensor in one launch (s2conv_multi):
+    the 32-cout ones leave conv_mfma_kernel's K order, a rounding-level difference through
+    the rest of the network (<= 2e-2 relative, as for the other fusions)."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(41)
+    monkeypatch.setenv("MVPOSE_NO_SIBFUSE", "1")
+    plain = hrnet.HRNetBackbone(sd, max_batch=4)
+    monkeypatch.delenv("MVPOSE_NO_SIBFUSE")
+    fused = hrnet.HRNetBackbone(sd, max_batch=4)
+    g = torch.Generator().manual_seed(42)
+    x = torch.zeros((4, 256, 192, 4))
+    x[..., :3] = torch.randn((4, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = fused.forward(xb)
+    torch.cuda.synchronize()
+    rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    assert rel < 2e-2, rel
+    assert not torch.equal(a, b)
+    # the later siblings' outputs now live from the first sibling's launch on
+    assert fused.arena_bytes <= 1.05 * plain.arena_bytes, (fused.arena_bytes, plain.arena_bytes)
 
 
 def test_head_kernel_matches_generic(models, monkeypatch):

@@ -240,3 +240,36 @@ def test_transition1_vs_reference(fused, output, monkeypatch):
     mx = (dev - ref).abs().max().item()
     print(f"transition1 t{output} fused={fused}: rel L2 {rel:.2e}, max abs {mx:.3e}")
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
+
+
+@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("n_sib,output", [(3, 0), (3, 1), (3, 2), (2, 0), (2, 1)])
+def test_fuse_layer_siblings_vs_reference(fused, n_sib, output, monkeypatch):
+    """A fuse layer's 3x3/s2 convs on the branch-0 tensor (-> 64 no ReLU, -> 32 ReLU, -> 32
+    ReLU; stage 3 has the first two): one launch over cout-concatenated weights
+    (s2conv_multi, graph sibling fusion) and one launch each, against a torch fp32
+    restatement with bf16 weights; ragged batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    monkeypatch.setenv("MVPOSE_NO_SIBFUSE", "0" if fused else "1")
+    spec, xi, yo, sd = hrnet.sibling_spec(seed=61 + n_sib, output=output, n=n_sib)
+    n = 9
+    g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+    gen = torch.Generator().manual_seed(62)
+    x = torch.relu(torch.randn((n, 64, 48, 32), generator=gen)).bfloat16()
+    ho, wo, co = spec.tensors[yo][:3]
+    out = torch.empty((n, ho, wo, co), dtype=torch.bfloat16, device="cuda")
+    g.run(x.cuda(), out)
+    torch.cuda.synchronize()
+    g.close()
+    name, _, relu = hrnet.SIBLINGS[output]
+    wt, b = hrnet.fold_bn(sd, name, name + "bn")
+    wt = _bf(torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 3, 1, 2))).float())
+    z = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), wt, stride=2, padding=1)
+    z = z + torch.from_numpy(b).float()[None, :, None, None]
+    ref = _bf(torch.relu(z) if relu else z).permute(0, 2, 3, 1)
+    dev = out.float().cpu()
+    rel = (torch.linalg.vector_norm(dev - ref) / torch.linalg.vector_norm(ref)).item()
+    mx = (dev - ref).abs().max().item()
+    assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8, (rel, mx)
