@@ -40,13 +40,13 @@ struct PreParams {
     float mean[3], stdv[3];
 };
 
+// one grid row per crop, 32-bit in-crop index (the flat 64-bit index's three divisions
+// per pixel made the kernel VALU-bound)
 __global__ __launch_bounds__(kBlock) void preprocess_kernel(PreParams p) {
-    const long gid = (long)blockIdx.x * kBlock + threadIdx.x;
-    const long total = (long)p.n * p.oh * p.ow;
-    if (gid >= total) return;
-    const int x = gid % p.ow;
-    const int y = (gid / p.ow) % p.oh;
-    const int n = gid / ((long)p.ow * p.oh);
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int n = blockIdx.y;
+    if (i >= p.oh * p.ow) return;
+    const int y = (int)((unsigned)i / (unsigned)p.ow), x = i - y * p.ow;
     const double* M = p.minv + 6 * n;
     // WarpAffineInvoker: X0/Y0 per row, adelta/bdelta per column (cvRound = rint)
     const int X0 = (int)rint((M[1] * y + M[2]) * 1024.0) + 16;
@@ -133,9 +133,14 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(DecodeParams p) {
     float* av = p.avg ? p.avg + map * HW : nullptr;
     float bv = 0.f;
     int bi = 0x7fffffff;
+    int y = lane / p.W, x = lane - y * p.W;  // (y, x) of i, stepped without divisions
     for (int i = lane; i < HW; i += 64) {
-        const int y = i / p.W, x = i - (i / p.W) * p.W;
         const float v = avg_at(p, h, hf, y, x);
+        x += 64;
+        while (x >= p.W) {
+            x -= p.W;
+            y++;
+        }
         if (av) av[i] = v;
         if (bi == 0x7fffffff || better(v, i, bv, bi)) {
             bv = v;
@@ -579,9 +584,9 @@ extern "C" int mvp_preprocess(const uint8_t* frames, int n, int H, int W, const 
         p.mean[c] = mean3[c];
         p.stdv[c] = std3[c];
     }
-    const long total = (long)n * out_h * out_w;
-    hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)((total + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       reinterpret_cast<hipStream_t>(stream), p);
+    MVP_REQUIRE((long)out_h * out_w < (1L << 30) && n < 65536, "mvp_preprocess: sizes");
+    hipLaunchKernelGGL(preprocess_kernel, dim3((unsigned)((out_h * out_w + kBlock - 1) / kBlock), (unsigned)n),
+                       dim3(kBlock), 0, reinterpret_cast<hipStream_t>(stream), p);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END
 }
