@@ -30,6 +30,8 @@ pytestmark = pytest.mark.gpu
 
 T, V = 8, 2
 ARGMAX_MIN = 0.80
+MARGIN = 1e-2          # fp32 top-1 vs top-2 relative lead that bf16 must resolve
+DECIDABLE_MIN = 0.99
 
 
 @pytest.fixture(scope="module")
@@ -52,17 +54,19 @@ def runs():
     M, center, scale = heatmap_ref.topdown_crop_matrix(1280, 720)
     k2 = np.zeros((T, 17, 3, V), np.float32)
     amax = np.zeros((T, V, 17), np.int64)
+    oavg = np.zeros((T, V, 17, 64 * 48), np.float32)
     for t in range(T):
         for v in range(V):
             x = torch.from_numpy(heatmap_ref.preprocess(frames[t, v], M))[None]
             avg, _, _ = hrnet_ref.flip_test_forward(model, x)
+            oavg[t, v] = avg[0].numpy().reshape(17, -1)
             k, s, idx = heatmap_ref.msra_decode(avg[0].numpy())
             k2[t, :, :2, v] = heatmap_ref.keypoints_to_image(k, center, scale)
             k2[t, :, 2, v] = s
             amax[t, v] = idx
     k3 = cv_ref.get_pose_3D(cp, k2, camera_indices=[0, 1])
     gam = np.stack([heatmap_ref.msra_decode(gpu_avg[i])[2] for i in range(T * V)]).reshape(T, V, 17)
-    return dict(gpu=gpu, k2=k2, k3=k3, amax=amax, gamax=gam, scale=scale)
+    return dict(gpu=gpu, k2=k2, k3=k3, amax=amax, gamax=gam, scale=scale, oavg=oavg)
 
 
 def test_argmax_agreement(runs):
@@ -70,6 +74,23 @@ def test_argmax_agreement(runs):
     rate = agree.mean()
     print(f"argmax agreement {rate:.4f} ({agree.sum()}/{agree.size})")
     assert rate >= ARGMAX_MIN
+
+
+def test_argmax_agreement_on_decidable_maps(runs):
+    """Where the fp32 oracle's maximum leads its runner-up cell by more than the bf16
+    path's own error (MARGIN relative), the argmax must agree (>= DECIDABLE_MIN): the
+    disagreements above are near-ties that bf16 compute (the allowed dtype) cannot
+    resolve, not a pipeline error."""
+    o = runs["oavg"]                                                     # (T, V, 17, HW)
+    top2 = -np.sort(-o, axis=-1)[..., :2]
+    margin = (top2[..., 0] - top2[..., 1]) / np.maximum(np.abs(top2[..., 0]), 1e-12)
+    agree = runs["gamax"] == runs["amax"]
+    for m in (0.0, 1e-3, 3e-3, 1e-2, 3e-2, 1e-1):
+        sel = margin > m
+        print(f"margin > {m:g}: {sel.mean():.3f} of maps, argmax agreement {agree[sel].mean() if sel.any() else 1:.4f}")
+    sel = margin > MARGIN
+    assert sel.sum() >= 0.25 * sel.size
+    assert agree[sel].mean() >= DECIDABLE_MIN
 
 
 def _agree(runs):
