@@ -30,8 +30,9 @@ pytestmark = pytest.mark.gpu
 
 T, V = 8, 2
 ARGMAX_MIN = 0.80
-MARGIN = 1e-2          # fp32 top-1 vs top-2 relative lead that bf16 must resolve
+MARGIN = 1e-2              # fp32 top-1 lead over top-2, in units of the map's max|h|
 DECIDABLE_MIN = 0.99
+DECIDABLE_FRACTION = 0.2
 
 
 @pytest.fixture(scope="module")
@@ -78,19 +79,22 @@ def test_argmax_agreement(runs):
 
 def test_argmax_agreement_on_decidable_maps(runs):
     """Where the fp32 oracle's maximum leads its runner-up cell by more than the bf16
-    path's own error (MARGIN relative), the argmax must agree (>= DECIDABLE_MIN): the
-    disagreements above are near-ties that bf16 compute (the allowed dtype) cannot
-    resolve, not a pipeline error."""
+    path's own error, the argmax must agree (>= DECIDABLE_MIN).  The error scale is the
+    map's magnitude: bf16 heatmaps differ from fp32 by ~1-3 % of max|h| per map (measured,
+    tools/e2e_diag.py), so a lead below MARGIN x max|h| is a near-tie that bf16 compute
+    (the allowed dtype) cannot resolve.  Many random-weight maps have no peak at all (all
+    cells below zero, the head bias): their argmax is decided by noise in either dtype."""
     o = runs["oavg"]                                                     # (T, V, 17, HW)
     top2 = -np.sort(-o, axis=-1)[..., :2]
-    margin = (top2[..., 0] - top2[..., 1]) / np.maximum(np.abs(top2[..., 0]), 1e-12)
+    lead = (top2[..., 0] - top2[..., 1]) / np.abs(o).max(axis=-1)
     agree = runs["gamax"] == runs["amax"]
-    for m in (0.0, 1e-3, 3e-3, 1e-2, 3e-2, 1e-1):
-        sel = margin > m
-        print(f"margin > {m:g}: {sel.mean():.3f} of maps, argmax agreement {agree[sel].mean() if sel.any() else 1:.4f}")
-    sel = margin > MARGIN
-    assert sel.sum() >= 0.25 * sel.size
-    assert agree[sel].mean() >= DECIDABLE_MIN
+    for m in (0.0, 1e-3, 1e-2, 2e-2, 5e-2, 1e-1):
+        sel = lead > m
+        print(f"lead > {m:g} max|h|: {sel.mean():.3f} of maps, argmax agreement "
+              f"{agree[sel].mean() if sel.any() else 1:.4f}")
+    sel = lead > MARGIN
+    assert sel.sum() >= DECIDABLE_FRACTION * sel.size, sel.mean()
+    assert agree[sel].mean() >= DECIDABLE_MIN, agree[sel].mean()
 
 
 def _agree(runs):
