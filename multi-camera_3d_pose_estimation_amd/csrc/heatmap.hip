@@ -205,9 +205,11 @@ struct MomParams {
                     // (2: the separable path without the per-run closed forms)
     int jpb;        // joints per workgroup: the warp tables depend on the crop only, so a
                     // workgroup builds them once and reuses them for jpb maps of its crop
+    int mixcf;      // separable path: mixed columns in closed form with a per-row prefix table
 };
 
 constexpr int kMomMaxLds = 64 * 1024;  // dynamic LDS budget: map + 2 int column tables
+constexpr int kMomMaxLdsCf = 96 * 1024;  // ... + the per-row prefix table of the mixed-column closed forms
 constexpr int kMomBlock = 320;         // 5 waves x 4 columns per lane = 1280: every lane busy on 1280-wide frames
 constexpr int kMomCols = 4;            // image columns per lane (separable path)
 constexpr int kMomJointsPerBlock = 17;  // maps per workgroup sharing one set of warp tables (all of a
@@ -235,6 +237,9 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     int* rstart = riy + ((p.img_h + 2) & ~1);
     int* rend = rstart + ((p.h + 2) & ~1);  // even int counts keep rsum 8-B aligned
     double* rsum = reinterpret_cast<double*>(rend + ((p.h + 2) & ~1));
+    // mixed-column closed forms: per image row y, the run-inclusive prefix over the rows of
+    // y's run up to y of gy, fy, gy·yr, fy·yr, gy·yr², fy·yr² (yr = row - run start)
+    double* rpre = rsum + 6 * (p.h + 1);
     __shared__ double red[6][kMomBlock / 64];
     __shared__ int bbox[4];
     const int groups = (p.K + p.jpb - 1) / p.jpb;
@@ -282,6 +287,15 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                 f1 += fy * yr;
                 g2 += gy * yr * yr;
                 f2 += fy * yr * yr;
+                if (p.mixcf) {
+                    double* pr = rpre + 6 * y;
+                    pr[0] = g0;
+                    pr[1] = f0;
+                    pr[2] = g1;
+                    pr[3] = f1;
+                    pr[4] = g2;
+                    pr[5] = f2;
+                }
             }
             // folded with the run's centred offset y0c = start - cy: a closed-form column
             // adds a·q[0] + b·q[1] to S, a·q[2] + b·q[3] to Sy and a·q[4] + b·q[5] to Syy
@@ -401,7 +415,69 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                                     Sy[j] = fma(da, q[2], fma(db, q[3], Sy[j]));
                                     Syy[j] = fma(da, q[4], fma(db, q[5], Syy[j]));
                                 }
-                                const bool walk = !full && !empty;
+                                bool walk = !full && !empty;
+                                // Mixed column in closed form: the walk's pixel value
+                                // v(y) = fy·b + gy·a (f32, gy·a rounded first) is linear in fy,
+                                // and fy grows with y inside a run, so its rows at or above thr
+                                // form a prefix or a suffix of the run.  When |b - a| / 32 (the
+                                // least change of the exact value between rows) exceeds 4 ulps of
+                                // max(|a|, |b|) — twice the evaluation's rounding — the computed
+                                // v is monotone too, so the exact f32 decisions of a binary search
+                                // find the cut, and the above-threshold rows' sums come from the
+                                // run's prefix table: a·G + b·F in fp64 (the walk sums the same
+                                // rows' f32 values in f32).  Otherwise the column walks.
+                                if (walk && p.mixcf) {
+                                    const float mag = fmaxf(fabsf(a), fabsf(b));
+                                    if (fabsf(b - a) > mag * 1.6e-5f) {
+                                        auto above = [&](int y) {
+                                            const float fy = (float)(riy[y] & 31) * (1.f / 32.f), gy = 1.f - fy;
+                                            return __builtin_fmaf(fy, b, gy * a) >= p.thr;
+                                        };
+                                        const bool d0 = above(ys), d1 = above(ye - 1);
+                                        int u0 = ys, u1 = ys;  // above-threshold rows [u0, u1)
+                                        if (d0 && d1) {
+                                            u1 = ye;
+                                        } else if (!d0 && d1) {
+                                            int lo = ys, hi = ye - 1;
+                                            while (hi - lo > 1) {
+                                                const int mid = (lo + hi) >> 1;
+                                                if (above(mid)) hi = mid;
+                                                else lo = mid;
+                                            }
+                                            u0 = hi;
+                                            u1 = ye;
+                                        } else if (d0 && !d1) {
+                                            int lo = ys, hi = ye - 1;
+                                            while (hi - lo > 1) {
+                                                const int mid = (lo + hi) >> 1;
+                                                if (above(mid)) lo = mid;
+                                                else hi = mid;
+                                            }
+                                            u1 = lo + 1;
+                                        }
+                                        if (u1 > u0) {
+                                            const double* pe = rpre + 6 * (u1 - 1);
+                                            double sg0 = pe[0], sf0 = pe[1], sg1 = pe[2], sf1 = pe[3], sg2 = pe[4],
+                                                   sf2 = pe[5];
+                                            if (u0 > ys) {
+                                                const double* pb = rpre + 6 * (u0 - 1);
+                                                sg0 -= pb[0];
+                                                sf0 -= pb[1];
+                                                sg1 -= pb[2];
+                                                sf1 -= pb[3];
+                                                sg2 -= pb[4];
+                                                sf2 -= pb[5];
+                                            }
+                                            const double da = a, db = b;
+                                            const double s0 = da * sg0 + db * sf0, s1 = da * sg1 + db * sf1,
+                                                         s2 = da * sg2 + db * sf2;
+                                            S[j] += s0;
+                                            Sy[j] += y0c * s0 + s1;
+                                            Syy[j] += y0c * y0c * s0 + 2.0 * y0c * s1 + s2;
+                                        }
+                                        walk = false;
+                                    }
+                                }
                                 mixed |= walk;
                                 ra[j / 2][j & 1] = walk ? a : 0.f;
                                 rb[j / 2][j & 1] = walk ? b : 0.f;
@@ -635,10 +711,21 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     MVP_ABI_BEGIN
     MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
     // map, 2 column tables, row table, run starts / ends, run sums (fp64): moments_kernel's layout
-    const size_t lds = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8 + (size_t)((img_h + 2) & ~1) * 4 +
-                       (size_t)((h + 2) & ~1) * 8 + (size_t)(h + 1) * 48;
-    MVP_REQUIRE(lds <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image %dx%d exceed the LDS budget", h, w,
+    const size_t lds0 = (size_t)((h * w + 3) & ~3) * 4 + (size_t)img_w * 8 + (size_t)((img_h + 2) & ~1) * 4 +
+                        (size_t)((h + 2) & ~1) * 8 + (size_t)(h + 1) * 48;
+    MVP_REQUIRE(lds0 <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image %dx%d exceed the LDS budget", h, w,
                 img_h, img_w);
+    // the mixed-column closed forms need a 48-B prefix row per image row (separable == 1 only;
+    // MVPOSE_MOM_NO_MIXCF=1 walks every mixed column, for tests)
+    const char* nm = getenv("MVPOSE_MOM_NO_MIXCF");
+    const bool mixcf = separable == 1 && !(nm && nm[0] == '1') && lds0 + (size_t)img_h * 48 <= kMomMaxLdsCf;
+    const size_t lds = mixcf ? lds0 + (size_t)img_h * 48 : lds0;
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)moments_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    kMomMaxLdsCf));
+        attr = true;
+    }
     if (N == 0) return MVP_OK;
     MVP_REQUIRE(hm && minv && out, "mvp_heatmap_moments: NULL device pointer");
     MomParams p{};
@@ -653,6 +740,7 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     p.img_w = img_w;
     p.thr = thr;
     p.separable = separable;
+    p.mixcf = mixcf ? 1 : 0;
     const char* je = getenv("MVPOSE_MOM_JPB");  // tuning experiments / tests only
     const int jpb_env = je ? atoi(je) : 0;
     p.jpb = jpb_env > 0 ? std::min(jpb_env, K) : std::min(kMomJointsPerBlock, K);
