@@ -133,18 +133,49 @@ __global__ __launch_bounds__(kBlock) void decode_kernel(DecodeParams p) {
     float* av = p.avg ? p.avg + map * HW : nullptr;
     float bv = 0.f;
     int bi = 0x7fffffff;
-    int y = lane / p.W, x = lane - y * p.W;  // (y, x) of i, stepped without divisions
-    for (int i = lane; i < HW; i += 64) {
-        const float v = avg_at(p, h, hf, y, x);
-        x += 64;
-        while (x >= p.W) {
-            x -= p.W;
-            y++;
+    if ((p.W & 3) == 0 && (HW & 255) == 0) {
+        // 4 consecutive cells of one row per lane (16-B loads / stores of the map and the
+        // average, 4 mirrored loads of the flipped map): four times the bytes in flight of
+        // one cell per lane, which left the kernel latency-bound
+        int i0 = lane * 4, y = i0 / p.W, x = i0 - y * p.W;
+        for (; i0 < HW; i0 += 256) {
+            const float4 a4 = *reinterpret_cast<const float4*>(h + i0);
+            float v[4] = {a4.x, a4.y, a4.z, a4.w};
+            if (hf) {
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    int xs = x + e;
+                    if (p.shift && xs >= 1) xs -= 1;  // heatmaps[..., 1:] = heatmaps[..., :-1]
+                    v[e] = __fmul_rn(__fadd_rn(v[e], hf[y * p.W + (p.W - 1 - xs)]), 0.5f);
+                }
+            }
+            if (av) *reinterpret_cast<float4*>(av + i0) = float4{v[0], v[1], v[2], v[3]};
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if (bi == 0x7fffffff || better(v[e], i0 + e, bv, bi)) {
+                    bv = v[e];
+                    bi = i0 + e;
+                }
+            x += 256;
+            while (x >= p.W) {
+                x -= p.W;
+                y++;
+            }
         }
-        if (av) av[i] = v;
-        if (bi == 0x7fffffff || better(v, i, bv, bi)) {
-            bv = v;
-            bi = i;
+    } else {
+        int y = lane / p.W, x = lane - y * p.W;  // (y, x) of i, stepped without divisions
+        for (int i = lane; i < HW; i += 64) {
+            const float v = avg_at(p, h, hf, y, x);
+            x += 64;
+            while (x >= p.W) {
+                x -= p.W;
+                y++;
+            }
+            if (av) av[i] = v;
+            if (bi == 0x7fffffff || better(v, i, bv, bi)) {
+                bv = v;
+                bi = i;
+            }
         }
     }
 #pragma unroll
