@@ -31,6 +31,12 @@ void launch_conv(const ConvLaunch& c, hipStream_t s);
 // Heatmap head (conv1x1.hip): 1x1 32 -> 17 + bias, f32 NCHW output; false otherwise
 // (or MVPOSE_NO_HEAD1X1=1).
 bool launch_head1x1(const ConvLaunch& c, hipStream_t s);
+// The head with the last fuse layer folded in (graph pass head_fuse, conv1x1.hip): in[k]
+// bf16 NHWC [N][H/up_k][W/up_k][32] summed (nearest upsample), optional ReLU, rounded to
+// bf16 (out0 exactly as launch_fuse_sum writes it), then 1x1 32 -> 17 + bias, f32 NCHW y.
+bool head_fuse_supported(int cin, int cout, int n_in);
+void launch_head_fuse(const uint16_t* const* in, const int* up, int n_in, int relu, const uint16_t* w,
+                      const float* bias, float* y, int N, int H, int W, hipStream_t s);
 
 // Direct-load 1x1 conv (conv1x1.hip); false when the conv is not a bf16-output 1x1.
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s);

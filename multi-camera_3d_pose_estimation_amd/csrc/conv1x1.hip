@@ -451,6 +451,68 @@ __global__ __launch_bounds__(256) void head1x1_kernel(const uint16_t* __restrict
     }
 }
 
+// Heatmap head with the last HRModule fuse folded in (graph pass head_fuse): the head's
+// 32-ch input is out0 = act(sum_k nearest_up(in[k], 2^lg[k])) of the last stage's fuse
+// layer; here each lane forms its pixel's out0 exactly as fuse_sum_kernel does (f32 sums
+// in input order, ReLU, bf16 rounding) and feeds those values to head1x1_kernel's FMAs —
+// bit-identical to the two launches, without writing / re-reading out0 (201 MB per 1024
+// crops).  One grid row per crop.
+struct HeadFuse {
+    const uint16_t* in[4];
+    int lg[4];
+    int n_in, relu;
+    const uint16_t* w;
+    const float* bias;
+    float* y;
+    int H, W;
+};
+
+template <int KOUT>
+__global__ __launch_bounds__(256) void head_fuse_kernel(HeadFuse p) {
+    const int hw = p.H * p.W;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    if (i >= hw) return;
+    const int yy = (int)((unsigned)i / (unsigned)p.W), xx = i - yy * p.W;
+    float xv[32];
+#pragma unroll
+    for (int c = 0; c < 32; c++) xv[c] = 0.f;
+    for (int k = 0; k < p.n_in; k++) {
+        const int lg = p.lg[k];
+        const int hs = p.H >> lg, ws = p.W >> lg;
+        const uint4* src =
+            reinterpret_cast<const uint4*>(p.in[k] + ((long)n * hs * ws + (yy >> lg) * ws + (xx >> lg)) * 32);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint4 u = src[q];
+            const uint32_t e[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                xv[q * 8 + 2 * j] += bf16_to_f32(e[j] & 0xffff);
+                xv[q * 8 + 2 * j + 1] += bf16_to_f32(e[j] >> 16);
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 32; c++) {
+        const float v = p.relu ? fmaxf(xv[c], 0.f) : xv[c];
+        xv[c] = bf16_to_f32(f32_to_bf16(v));  // out0 as the fuse stores it
+    }
+    float* out = p.y + (long)n * KOUT * hw + i;
+#pragma unroll
+    for (int k = 0; k < KOUT; k++) {
+        float acc = p.bias[k];
+        const uint32_t* wk = reinterpret_cast<const uint32_t*>(p.w + k * 32);
+#pragma unroll
+        for (int c = 0; c < 16; c++) {
+            const uint32_t wp = wk[c];
+            acc = __builtin_fmaf(bf16_to_f32(wp & 0xffff), xv[2 * c], acc);
+            acc = __builtin_fmaf(bf16_to_f32(wp >> 16), xv[2 * c + 1], acc);
+        }
+        out[(long)k * hw] = acc;
+    }
+}
+
 int g_cus1 = 0;
 
 template <int BM, int KCH>
@@ -593,6 +655,38 @@ bool launch_head1x1(const ConvLaunch& c, hipStream_t s) {
                        c.yf, n_pix, c.H * c.W);
     MVP_HIP(hipGetLastError());
     return true;
+}
+
+bool head_fuse_supported(int cin, int cout, int n_in) {
+    const char* e = getenv("MVPOSE_NO_HEADFUSE");  // diagnostics/tests: fuse_sum + head1x1
+    if (e && e[0] == '1') return false;
+    const char* e2 = getenv("MVPOSE_NO_HEAD1X1");
+    if (e2 && e2[0] == '1') return false;
+    return cin == 32 && cout == 17 && n_in >= 1 && n_in <= 4;
+}
+
+void launch_head_fuse(const uint16_t* const* in, const int* up, int n_in, int relu, const uint16_t* w,
+                      const float* bias, float* y, int N, int H, int W, hipStream_t s) {
+    MVP_REQUIRE(n_in >= 1 && n_in <= 4, "head_fuse: n_in=%d", n_in);
+    HeadFuse p{};
+    for (int k = 0; k < n_in; k++) {
+        int lg = 0;
+        while ((1 << lg) < up[k]) lg++;
+        MVP_REQUIRE(up[k] == (1 << lg) && H % up[k] == 0 && W % up[k] == 0, "head_fuse: upsample factor %d", up[k]);
+        p.in[k] = in[k];
+        p.lg[k] = lg;
+    }
+    p.n_in = n_in;
+    p.relu = relu;
+    p.w = w;
+    p.bias = bias;
+    p.y = y;
+    p.H = H;
+    p.W = W;
+    MVP_REQUIRE((long)H * W < (1L << 30) && N < 65536, "head_fuse: sizes");
+    if (N == 0) return;
+    hipLaunchKernelGGL(head_fuse_kernel<17>, dim3((unsigned)((H * W + 255) / 256), (unsigned)N), dim3(256), 0, s, p);
+    MVP_HIP(hipGetLastError());
 }
 
 bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {

@@ -35,6 +35,7 @@ struct Graph {
     std::vector<std::vector<int>> sib;  // 3x3/s2 conv whose (absorbed) 3x3/s2 siblings on its input run in its launch
     std::vector<uint16_t*> sib_w;       // their cout-concatenated weights [128][3][3][cin] (owned)
     std::vector<float*> sib_b;          // and biases [128] (owned)
+    std::vector<int> head_src;          // heatmap head that also runs the (absorbed) fuse op head_src[k] (-1: none)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -309,6 +310,35 @@ void sib_fuse(Graph& g, bool enable) {
     }
 }
 
+// Head-fusion pass: the last fuse layer's out0 (32 ch @ 64x48) feeds only the heatmap head
+// (1x1 32 -> 17, f32 NCHW); the head kernel forms out0 per pixel itself, so the 201 MB
+// tensor is never written or re-read (bit-identical: same sums, same bf16 rounding).
+void head_fuse(Graph& g, bool enable) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.head_src.assign(no, -1);
+    if (!enable) return;
+    std::vector<int> uses(nt, 0), producer(nt, -1);
+    for (int k = 0; k < no; k++) {
+        const mvp_op_desc& op = g.ops[k];
+        producer[op.out] = k;
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0) uses[op.in[i]]++;
+    }
+    for (int k = 0; k < no; k++) {
+        const mvp_op_desc& H = g.ops[k];
+        if (H.kind != MVP_OP_CONV || g.absorbed[k] || g.tensors[H.out].dtype != MVP_DT_F32_NCHW || H.ks != 1 ||
+            H.relu || (H.n_in > 1 && H.in[1] >= 0))
+            continue;
+        const int f = producer[H.in[0]];
+        if (f < 0 || g.absorbed[f] || g.ops[f].kind != MVP_OP_FUSE || uses[H.in[0]] != 1 || H.in[0] == g.output ||
+            g.ops[f].segment != H.segment)
+            continue;
+        if (!head_fuse_supported(H.cin, H.cout, g.ops[f].n_in)) continue;
+        g.absorbed[f] = 1;
+        g.head_src[k] = f;
+    }
+}
+
 // Device-side concatenated weights / summed biases of the cat-fused ops: allocated at graph
 // create time, filled from the blobs by cat_fill (create and mvp_graph_refresh_weights).
 void cat_alloc(Graph& g) {
@@ -412,6 +442,7 @@ void plan(Graph& g) {
         for (int i = 0; i < op.n_in; i++) {
             if (op.in[i] < 0 || (g.block_head[k] && i == 0)) continue;  // fused: conv1's output is LDS-only
             if (g.stem_head[k] >= 0 && i == 0) continue;                 // fused stem: LDS-only
+            if (g.head_src[k] >= 0 && i == 0) continue;                  // fused head: never materialised
             if (g.cat_src[k] >= 0 && i == 1) continue;                  // cat-fused: never materialised
             last[op.in[i]] = std::max(last[op.in[i]], k);
             touch(op.in[i]);
@@ -440,6 +471,13 @@ void plan(Graph& g) {
             last[x] = std::max(last[x], k);
             touch(x);
         }
+        if (g.head_src[k] >= 0) {  // the absorbed fuse's inputs are read here
+            const mvp_op_desc& f = g.ops[g.head_src[k]];
+            for (int i = 0; i < f.n_in; i++) {
+                last[f.in[i]] = std::max(last[f.in[i]], k);
+                touch(f.in[i]);
+            }
+        }
         if (g.pair_tail[k] >= 0) {  // the absorbed successor's output is written here
             const int y2 = g.ops[g.pair_tail[k]].out;
             first[y2] = k;
@@ -466,8 +504,11 @@ void plan(Graph& g) {
         };
         widen(op.out);
         for (int i = 0; i < op.n_in; i++)
-            if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1) && !(g.stem_head[k] >= 0 && i == 0))
+            if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1) && !(g.stem_head[k] >= 0 && i == 0) &&
+                !(g.head_src[k] >= 0 && i == 0))
                 widen(op.in[i]);
+        if (g.head_src[k] >= 0)
+            for (int i = 0; i < g.ops[g.head_src[k]].n_in; i++) widen(g.ops[g.head_src[k]].in[i]);
         if (g.stem_head[k] >= 0) widen(g.ops[g.stem_head[k]].in[0]);
         if (g.twin[k] >= 0) widen(g.ops[g.twin[k]].out);
         for (int b : g.sib[k]) widen(g.ops[b].out);
@@ -549,6 +590,7 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::stem_fuse(*g, !(nf && nf[0] == '1'));
         mvp::twin_fuse(*g, !(nf && nf[0] == '1'));
         mvp::sib_fuse(*g, !(nf && nf[0] == '1'));
+        mvp::head_fuse(*g, !(nf && nf[0] == '1'));
         mvp::cat_alloc(*g);
         mvp::sib_alloc(*g);
         mvp::cat_fill(*g);
@@ -623,6 +665,15 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
                 m.relu[i] = o2.relu;
             }
             mvp::launch_s2conv_multi(m, s);
+            return;
+        }
+        if (g->head_src[k] >= 0) {  // the last fuse layer's out0, formed per pixel by the head
+            const mvp_op_desc& f = g->ops[g->head_src[k]];
+            const mvp_tensor_desc& fo = g->tensors[f.out];
+            const uint16_t* ins[4];
+            for (int i = 0; i < f.n_in; i++) ins[i] = (const uint16_t*)ptr(f.in[i]);
+            mvp::launch_head_fuse(ins, f.up, f.n_in, f.relu, g->wb + op.w_off, g->fb + op.b_off, (float*)ptr(op.out),
+                                  nb, fo.h, fo.w, s);
             return;
         }
         if (g->stem_head[k] >= 0) {  // stem conv1 + this conv2 in one launch

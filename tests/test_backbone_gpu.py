@@ -202,6 +202,27 @@ def test_sibling_fusion_matches_unfused(models, monkeypatch):
     assert fused.arena_bytes <= 1.05 * plain.arena_bytes, (fused.arena_bytes, plain.arena_bytes)
 
 
+def test_head_fusion_bitwise_equal(models, monkeypatch):
+    """The last fuse layer folded into the heatmap head (graph head fusion: out0 formed per
+    pixel with fuse_sum's arithmetic and bf16 rounding) is bit-identical to the two
+    launches, and out0 is no longer allocated."""
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(43)
+    monkeypatch.setenv("MVPOSE_NO_HEADFUSE", "1")
+    plain = hrnet.HRNetBackbone(sd, max_batch=3)
+    monkeypatch.delenv("MVPOSE_NO_HEADFUSE")
+    fused = hrnet.HRNetBackbone(sd, max_batch=3)
+    g = torch.Generator().manual_seed(44)
+    x = torch.zeros((3, 256, 192, 4))
+    x[..., :3] = torch.randn((3, 256, 192, 3), generator=g)
+    xb = x.bfloat16().cuda()
+    a = plain.forward(xb)
+    b = fused.forward(xb)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    assert fused.arena_bytes <= plain.arena_bytes
+
+
 def test_head_kernel_matches_generic(models, monkeypatch):
     """The dedicated heatmap-head kernel (1x1 32 -> 17, f32 NCHW, VALU FMAs in channel
     order) against the generic MFMA conv on the same bf16 features: f32 summation
