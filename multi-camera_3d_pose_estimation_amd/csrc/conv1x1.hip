@@ -151,13 +151,15 @@ __global__ __launch_bounds__(256, 2) void conv1x1_kernel(P1x1 p) {
 // Layer1 of HRNet-W32 alternates conv3 (64 -> 256, + residual, ReLU) and the next
 // block's conv1 (256 -> 64, ReLU) at 64x48: the 256-ch tensor (1.6 GB per 1024
 // crops) was written by one launch and read straight back by the next.  Here one
-// wave computes all 256 couts of 16 pixels (A rows permuted as in conv1x1_kernel
-// with BM = 256, so lane group g holds couts 64g .. 64g+63 of its pixel), writes
-// them, and feeds the same bf16 values to the second GEMM as B fragments without
-// any lane exchange: the second GEMM's K order is permuted to match — K chunk j,
-// lane group g covers channels 64g + 8j .. 64g + 8j + 7 — by the order the W2
-// slots are DMA'd into LDS.  y is rounded to bf16 before the second GEMM, as in
-// the unfused graph; only the f32 summation order of the second GEMM differs.
+// wave computes all 256 couts of 16 pixels in two halves of 128 (A rows permuted so
+// that in half h lane group g holds couts 128h + 32g .. + 31 of its pixel), stores
+// them (through a per-wave LDS staging block, as whole 256-B runs) and feeds the same
+// bf16 values to the second GEMM as B fragments without any lane exchange: the second
+// GEMM's K order is permuted to match — K chunk j, lane group g covers channels
+// 128 (j >> 2) + 32g + 8 (j & 3) .. + 7 — by the order the W2 slots are DMA'd into
+// LDS.  The residual is loaded coalesced and transposed through the same block.  y is
+// rounded to bf16 before the second GEMM, as in the unfused graph; only the f32
+// summation order of the second GEMM differs.
 struct PPair {
     const uint16_t* x;
     const uint16_t* x2;
@@ -171,7 +173,6 @@ struct PPair {
     uint16_t* y2;
     const uint16_t* zero;
     long n_pix;
-    int diag;  // unused (diagnostics slot)
 };
 
 // threads per workgroup (one workgroup per CU, 2 waves per SIMD): 12-wave workgroups
@@ -258,9 +259,6 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 1) void conv1x1_pair_kernel(PP
     auto process = [&](long u, const UnitRegs cur) {
         const bf16x8(&b)[KCH] = cur.b;
         const uint4(&rr)[NRQ] = cur.r;
-        const long pp = u * 16 + (lane & 15);
-        const bool valid = pp < p.n_pix;
-        const long pix = valid ? pp : p.n_pix - 1;
         f32x4 acc2[4];
 #pragma unroll
         for (int c = 0; c < 4; c++) acc2[c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -372,13 +370,7 @@ __global__ __launch_bounds__(pair_threads<KCH>(), 1) void conv1x1_pair_kernel(PP
         // y2 (64 ch = 128-B pixel rows) through the staging block too: chunk k = 2g + q of
         // pixel px at px * 128 + (k ^ px & 7) * 16; then 8 lanes store one whole row and an
         // instruction 1 KiB of consecutive pixels
-        if (p.diag == 1) {
-            uint16_t* y2row = p.y2 + pix * 64 + g * 16;
-            if (valid) {
-                *reinterpret_cast<uint4*>(y2row) = uint4{o2[0], o2[1], o2[2], o2[3]};
-                *reinterpret_cast<uint4*>(y2row + 8) = uint4{o2[4], o2[5], o2[6], o2[7]};
-            }
-        } else {
+        {
             const int px = lane & 15;
             *reinterpret_cast<uint4*>(stg + px * 128 + (((2 * g) ^ px) & 7) * 16) = uint4{o2[0], o2[1], o2[2], o2[3]};
             *reinterpret_cast<uint4*>(stg + px * 128 + (((2 * g + 1) ^ px) & 7) * 16) =
@@ -563,13 +555,8 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
     MVP_REQUIRE(c.c1 % 32 == 0 && c.c1 > 0 && (!c.x2 || c.c2 % 32 == 0), "conv1x1_pair: channel split %d/%d", c.c1,
                 c.c2);
     if (c.n_pix == 0) return;
-    static int diag = -1;
-    if (diag < 0) {
-        const char* e = getenv("MVPOSE_PAIR_DIAG");
-        diag = e ? atoi(e) : 0;
-    }
     PPair p{c.x, c.x2, c.c1, c.x2 ? c.c2 : 0, c.c1 / 32, c.w1, c.b1, c.res, c.y, c.w2, c.b2, c.y2,
-            conv_zero_region(), c.n_pix, diag};
+            conv_zero_region(), c.n_pix};
     if (g_cus1 == 0) {
         int dev = 0;
         MVP_HIP(hipGetDevice(&dev));
@@ -620,8 +607,8 @@ bool launch_conv1x1_wide(const ConvLaunch& c, hipStream_t s) {
     if (e && e[0] == '1') return false;
     const long n_pix = (long)c.N * c.H * c.W;
     if (n_pix == 0) return true;
-    PPair p{c.x, c.x2, cin == 128 ? 64 : 64, cin == 128 ? 64 : 0, 2, c.w, c.bias, c.res, c.y, nullptr, nullptr,
-            nullptr, conv_zero_region(), n_pix, 0};
+    PPair p{c.x, c.x2, 64, cin == 128 ? 64 : 0, 2, c.w, c.bias, c.res, c.y, nullptr, nullptr,
+            nullptr, conv_zero_region(), n_pix};
     if (g_cus1 == 0) {
         int dev = 0;
         MVP_HIP(hipGetDevice(&dev));
