@@ -9,9 +9,9 @@
   (17, 6) heatmap Gaussians); with a GPU estimator the V frames are one batched run.
 * ``load_frames(recording_paths, start_end_frames)`` (utils.py:849-909): decoded
   frame stacks, one per camera, sliced ``[start:end]`` (the default ``[0, -1]``
-  drops the last frame, quirk F4).  Video decoding itself is outside this
-  package's scope; a recording is a ``.npy`` (T, H, W, 3) uint8
-  array of frames as a video decoder (BGR) returns them.
+  drops the last frame, quirk F4).  A recording is a ``.npy`` (T, H, W, 3) uint8
+  array of frames as a video decoder (BGR) returns them, an MJPEG / uncompressed AVI
+  or a directory of frame<N>.jpg files (``mvpose.video``).
 * ``run_pose_est`` (:157-244) and ``estimate_pose_from_video`` (:259-327): every
   frame of every camera through the batched GPU pipeline (crop, HRNet-W32 with
   flip test, decode, heatmap moments), then get_pose_3D over ``camera_indices=[0, 1]``
@@ -91,7 +91,11 @@ def get_pose_2D(frames, model, confidence=0.5, pose_keypoints=range(17)):
 
 
 def load_frames(recording_paths, start_end_frames=(0, -1)):
-    """{camera: (T', H, W, 3) uint8} memory-mapped, sliced [start:end]."""
+    """{camera: (T', H, W, 3) uint8 BGR} sliced [start:end] (utils.py:903-909 ->
+    frame_generator :849-900).  A recording is a .npy stack (memory-mapped), an MJPEG or
+    uncompressed AVI, a directory of frame<N>.jpg files (mvpose.video), or an in-memory
+    array; other codecs raise NotImplementedError (no decoder in this image)."""
+    from . import video
     if isinstance(recording_paths, (list, tuple)):
         recording_paths = dict(enumerate(recording_paths))
     if not isinstance(recording_paths, dict):
@@ -102,14 +106,7 @@ def load_frames(recording_paths, start_end_frames=(0, -1)):
         if isinstance(path, np.ndarray):                 # already-decoded frames in memory
             out[k] = path[a:b]
             continue
-        if not str(path).endswith(".npy"):
-            raise NotImplementedError(
-                f"{path}: video decoding is not part of the GPU hot path; pass decoded frames as a "
-                ".npy (T, H, W, 3) uint8 array (cv2 BGR order)")
-        arr = np.load(path, mmap_mode="r")
-        if arr.dtype != np.uint8 or arr.ndim != 4 or arr.shape[-1] != 3:
-            raise ValueError(f"{path}: expected (T, H, W, 3) uint8 frames, got {arr.shape} {arr.dtype}")
-        out[k] = arr[a:b]
+        out[k] = video.read_recording(path, a, b)
     return out
 
 
@@ -244,11 +241,11 @@ def estimate_pose_from_video(camera_names, recording_paths, model, detector_mode
     if os.path.exists(existing) and not recompute_kpts_2d:
         kpts_2d = np.load(existing)
     else:
-        if isinstance(model, str):
-            first = np.load(recording_paths[0], mmap_mode="r")
-            model = build_estimator(model, detector_model, model_yaml, frame_hw=first.shape[1:3])
         paths = {i: recording_paths[i] for i in camera_indices}   # as :281 indexes them
+        frames = load_frames(paths, start_end_frames)          # decoded once
+        if isinstance(model, str):
+            model = build_estimator(model, detector_model, model_yaml, frame_hw=frames[camera_indices[0]].shape[1:3])
         kpts_2d, heatmaps = run_pose_est(model, confidence=confidence, camera_indices=camera_indices,
-                                         recording_paths=paths, start_end_frames=start_end_frames)
+                                         recording_paths=frames, start_end_frames=(0, None))
     kpts_3d = get_pose_3D(camera_params, kpts_2d, camera_indices=[0, 1])
     return kpts_2d, heatmaps, kpts_3d

@@ -95,3 +95,22 @@ def test_pose_refinement_cli(project, monkeypatch):
     opt.sgd_optimize(**{**sgd, "print_frequency": 10 ** 9})
     assert got.shape == (23, 17, 3)
     np.testing.assert_allclose(got, opt.best_trajectory.numpy(), rtol=0, atol=1e-5)
+
+
+def test_avi_recordings_match_npy(project, monkeypatch, tmp_path):
+    """The same frames as uncompressed AVIs (bit-exact decode, mvpose.video) give the same
+    2D keypoints and Gaussians as the .npy recordings."""
+    from mvpose import pose_estimation, video
+    _, _, paths, _ = project
+    monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    est = pose_estimation.build_estimator("random", frame_hw=(360, 640), max_frames=16)
+    avis = []
+    for v, p in enumerate(paths):
+        a = str(tmp_path / f"camera{v}.avi")
+        video.write_avi(a, np.load(p), codec="rgb")
+        avis.append(a)
+    k_npy, h_npy = pose_estimation.run_pose_est(est, recording_paths=paths)
+    k_avi, h_avi = pose_estimation.run_pose_est(est, recording_paths=avis)
+    assert k_npy.shape == (3, 17, 3, 2)
+    np.testing.assert_array_equal(k_avi, k_npy)
+    np.testing.assert_array_equal(h_avi, h_npy)
