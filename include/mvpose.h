@@ -191,6 +191,94 @@ int mvp_graph_refresh_weights(void* handle);
 int mvp_graph_destroy(void* handle);
 
 /* ---------------------------------------------------------------------------
+ * Person detector: RTMDet-m (the reference's `detectors.coco_base`,
+ * examples/model_paths.yaml:2-4) as run by PoseEstimator.predict through mmdet's
+ * inference_detector (mmpose_pose_estimation.py:98-99, :234-241), followed by the
+ * reference's hand-off rule (:242-250): the first detection with label 0 and score >
+ * bbox_thr.  After mmdet's NMS the first detection is the highest-scoring prior that
+ * survives score_thr and the min-size filter, so the hot path is: letterbox ->
+ * CSPNeXt-m / CSPNeXtPAFPN / RTMDetSepBNHead -> per-prior score + box -> per-frame
+ * argmax.  A per-frame NMS kernel gives mmdet's full detection list.
+ *
+ * mvp_det_letterbox: frames_dev [n][h][w][3] uint8 -> out_dev [n][size][size][4] bf16:
+ *   mmdet Resize(scale=(size, size), keep_ratio=True) with cv2 INTER_LINEAR semantics
+ *   (exact 2x downscale = INTER_AREA's fast path), Pad(114) bottom / right, then
+ *   (x - mean[c]) / std[c] in f32 (channel 3 = 0).  new_h / new_w are the resized extent
+ *   (mmcv rescale_size: int(h * s + 0.5), s = min(size / long, size / short)).
+ *
+ * Graph ops (views = channel slices of NHWC bf16 tensors: concat is a shared buffer):
+ *   MVP_DET_STEM : 3x3/s2 conv of the 4-channel letterboxed input to 32 channels,
+ *                  f32 weights [32][3][3][4] + bias [32], act.
+ *   MVP_DET_CONV : y = act(conv(x) + bias [+ res]), ks 1|3, stride 1|2, bf16 weights
+ *                  [cout_pad][ks][ks][cin] (cout_pad as mvp_graph), f32 bias.
+ *   MVP_DET_DW   : 5x5 depthwise conv + bias + act, f32 weights [c][25], bias [c].
+ *   MVP_DET_CA   : channel attention in place on `in`: x *= hardsigmoid(W·mean(x) + b),
+ *                  f32 W^T [c][c] (w_off) and b [c].
+ *   MVP_DET_SPP  : `in` = slice 0 (c channels) of a 4c buffer; writes max-pools 5/9/13
+ *                  (stride 1, -inf padding) into slices 1..3.
+ *   MVP_DET_UP2  : out = nearest 2x upsample of in.
+ *   MVP_DET_HEAD : one FPN level's predictions from `in` = [cls feat | reg feat]
+ *                  (c = 2 * 192): f32 weights [5][192] (cls, reg l/t/r/b) + bias [5];
+ *                  writes cand rows [prior][6] = {sigmoid score, x1, y1, x2, y2, logit}
+ *                  at prior offset `aux`, box = prior (x, y) * stride -+ exp(reg) * stride,
+ *                  clipped to [0, size] (mmdet distance2bbox on img_shape).
+ * act: 0 none, 1 ReLU (after a residual add), 2 SiLU (before it: CSPNeXtBlock's
+ * conv2(conv1(x)) + x).
+ * ------------------------------------------------------------------------- */
+#define MVP_DET_STEM 0
+#define MVP_DET_CONV 1
+#define MVP_DET_DW 2
+#define MVP_DET_CA 3
+#define MVP_DET_SPP 4
+#define MVP_DET_UP2 5
+#define MVP_DET_HEAD 6
+
+typedef struct mvp_det_view {
+    int t;    /* tensor id, -1 = none */
+    int coff; /* first channel of the slice */
+    int c;    /* channels of the slice */
+} mvp_det_view;
+
+typedef struct mvp_det_op {
+    int kind;
+    mvp_det_view in, out, res;
+    int ks, stride, act;
+    int64_t w_off, b_off;
+    int64_t aux;
+} mvp_det_op;
+
+int mvp_det_letterbox(const uint8_t* frames_dev, int n, int h, int w, int size, const float* mean3_host,
+                      const float* std3_host, void* out_dev, void* stream);
+/* tensors_host: (h, w, c, unused) per image; tensor `input_tensor` is the letterboxed image
+ * (c = 4).  n_priors = total rows the HEAD ops write. */
+int mvp_det_create(const mvp_tensor_desc* tensors_host, int n_tensors, const mvp_det_op* ops_host, int n_ops,
+                   int input_tensor, int size, int n_priors, const uint16_t* w_bf16_dev, int64_t w_elems,
+                   const float* f32_dev, int64_t f32_elems, int max_batch, void** handle_out);
+/* frames_dev [n][h][w][3] uint8 -> cand_dev [n][n_priors][6] f32 and best_dev [n][6] f32 =
+ * {x1, y1, x2, y2, score, prior} of the highest-scoring prior with score > score_thr and a
+ * positive width / height after rescaling to the frame (x / (new_w / w), y / (new_h / h));
+ * ties -> lowest prior index; score = -1 when none.  letterboxed_dev: NULL (internal) or a
+ * caller buffer [n][size][size][4] bf16 that receives the letterboxed input. */
+int mvp_det_forward(void* handle, const uint8_t* frames_dev, int n, int h, int w, float score_thr, float* cand_dev,
+                    float* best_dev, void* letterboxed_dev, void* stream);
+/* mmdet post-processing on cand_dev from mvp_det_forward: per frame, priors with score >
+ * score_thr, the nms_pre best of each level (level l = prior rows [level_off[l],
+ * level_off[l + 1])), boxes rescaled to the frame, min-size filter, greedy NMS at iou_thr
+ * in descending score order (ties: lower prior first), the first max_det kept ->
+ * dets_dev [n][max_det][5] {x1, y1, x2, y2, score} (score-descending), counts_dev [n]. */
+int mvp_det_nms(const float* cand_dev, int n, int n_priors, const int* level_off_host, int n_levels, int nms_pre,
+                float score_thr, float iou_thr, int max_det, float fx, float fy, float* dets_dev, int* counts_dev,
+                void* stream);
+int mvp_det_arena_bytes(void* handle, int64_t* bytes_out);
+/* Layer-by-layer access for parity tests: mvp_det_run_ops runs the letterbox (when
+ * op_begin == 0) and ops [op_begin, op_end) on the handle's arena; mvp_det_tensor_copy
+ * copies the first n images of arena tensor t to (to_arena = 0) or from (1) buf_dev. */
+int mvp_det_run_ops(void* handle, const uint8_t* frames_dev, int n, int h, int w, int op_begin, int op_end,
+                    float* cand_dev, void* stream);
+int mvp_det_tensor_copy(void* handle, int t, int n, void* buf_dev, int to_arena, void* stream);
+int mvp_det_destroy(void* handle);
+
+/* ---------------------------------------------------------------------------
  * Reprojection-error trajectory refinement (Optimized_3d_Pose_Estimation,
  * reference pose_refinement.py:579-668 + sgd_optimize :894-1096, trajectory-only
  * path the CLI runs at :1210-1214).

@@ -24,9 +24,17 @@ struct ConvLaunch {
     // from x2 [N][H][W][Cin - c1], the first c1 from x
     const uint16_t* x2 = nullptr;
     int c1 = 0;
+    // Channel views (detector graph, detnet.cpp): elements between consecutive pixels of
+    // x / y / res when they are channel slices of wider NHWC tensors (0 = dense: Cin /
+    // Cout).  relu == 2 selects SiLU (x * sigmoid(x)) applied BEFORE the residual add
+    // (CSPNeXtBlock: conv2(conv1(x)) + x); ReLU (1) is applied after it.
+    int x_stride = 0, y_stride = 0, r_stride = 0;
 };
 
 void launch_conv(const ConvLaunch& c, hipStream_t s);
+// The generic implicit-GEMM conv (conv_mfma_kernel) only, with channel views and the
+// SiLU epilogue: no HRNet-plane kernel is tried.  bf16 NHWC output.
+void launch_conv_generic(const ConvLaunch& c, hipStream_t s);
 
 // Heatmap head (conv1x1.hip): 1x1 32 -> 17 + bias, f32 NCHW output; false otherwise
 // (or MVPOSE_NO_HEAD1X1=1).

@@ -34,6 +34,8 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     return __builtin_bit_cast(uint16_t, b);
 }
 
+__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+
 struct ConvParams {
     const uint16_t* __restrict__ x;
     const uint16_t* __restrict__ w;
@@ -45,7 +47,8 @@ struct ConvParams {
     uint16_t* sink;                     // write-only scratch for masked-off lanes' stores
     float* sinkf;
     int N, H, W, Cin, Ho, Wo, Cout, Cout_pad;
-    int relu, out_f32;
+    int xs, ys, rs;  // pixel strides (elements) of x / y / res
+    int relu, out_f32;  // relu: 0 none, 1 ReLU, 2 SiLU
     int tiles_w, tiles_h, n_tiles;
     int wmode;  // WM_ONCE / WM_RESIDENT / WM_STREAM
 };
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
         const int r = pix - nb * (HH * HW);
         const int hh = r / HW, ww = r - (r / HW) * HW;
         hgeo[j] = pix < C::HALO_PIX ? (hh | (ww << 10) | (nb << 20)) : -1;
-        hoff[j] = (int)(((size_t)nb * plane_in + (size_t)hh * p.W + ww) * p.Cin) + q * 8;
+        hoff[j] = (int)(((size_t)nb * plane_in + (size_t)hh * p.W + ww) * p.xs) + q * 8;
     }
     auto issue = [&](int k, int buf) {
         const int tile = blockIdx.x + (k / n_chunks) * gridDim.x, chunk = k % n_chunks;
@@ -202,7 +205,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
         tile_origin(tile, n0, ho0, wo0);
         const int hi0 = ho0 * S - PAD, wi0 = wo0 * S - PAD;
         // element offset of the halo origin (may point before the image; only in-bounds lanes use it)
-        const uint16_t* xb = p.x + ((long)n0 * (long)plane_in + (long)hi0 * p.W + wi0) * p.Cin + chunk * 32;
+        const uint16_t* xb = p.x + ((long)n0 * (long)plane_in + (long)hi0 * p.W + wi0) * p.xs + chunk * 32;
         uint8_t* hb = halo_buf(buf);
 #pragma unroll
         for (int j = 0; j < kHaloOps; j++) {
@@ -285,7 +288,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
             for (int i = 0; i < PTW; i++) {
                 const int g = egeo[i];
                 const bool valid = n0 + (g >> 20) < p.N && ho0 + (g & 1023) < p.Ho && wo0 + ((g >> 10) & 1023) < p.Wo;
-                const uint16_t* rrow = (p.res ? p.res : p.zero) + (size_t)(pix0 + eoff[i]) * p.Cout;
+                const uint16_t* rrow = (p.res ? p.res : p.zero) + (size_t)(pix0 + eoff[i]) * p.rs;
 #pragma unroll
                 for (int c = 0; c < NCT; c++) {
                     const int co = co_l + c * 16;
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
                 const int n = n0 + nb, ho = ho0 + th, wo = wo0 + tw;
                 const bool valid = n < p.N && ho < p.Ho && wo < p.Wo;
                 const int pix = pix0 + eoff[i];
-                uint16_t* yrow = p.y + (size_t)pix * p.Cout;
+                uint16_t* yrow = p.y + (size_t)pix * p.ys;
 #pragma unroll
                 for (int c = 0; c < NCT; c++) {
                     const int co = co_l + c * 16;
@@ -360,6 +363,12 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
                         }
                         continue;
                     }
+                    if (p.relu == 2) {  // SiLU, then the residual (CSPNeXtBlock: conv2(conv1(x)) + x)
+                        v0 = silu(v0);
+                        v1 = silu(v1);
+                        v2 = silu(v2);
+                        v3 = silu(v3);
+                    }
                     {  // + residual (zeros when the conv has none)
                         const uint2 rv = resv[i][c];
                         v0 += bf16_to_f32(rv.x & 0xffff);
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_mfma_kernel(ConvParams p) {
                         v2 += bf16_to_f32(rv.y & 0xffff);
                         v3 += bf16_to_f32(rv.y >> 16);
                     }
-                    if (p.relu) {
+                    if (p.relu == 1) {  // ReLU after the residual (HRNet BasicBlock / Bottleneck)
                         v0 = fmaxf(v0, 0.f);
                         v1 = fmaxf(v1, 0.f);
                         v2 = fmaxf(v2, 0.f);
@@ -774,7 +783,7 @@ const uint16_t* conv_zero_region() { return zero_page(); }
 
 int conv_cout_pad(int cout) { return cout <= 32 ? 32 : ((cout + 63) / 64) * 64; }
 
-void launch_conv(const ConvLaunch& c, hipStream_t s) {
+void launch_conv_impl(const ConvLaunch& c, hipStream_t s, bool generic_only) {
     MVP_REQUIRE(c.Cin % 32 == 0, "conv: Cin=%d must be a multiple of 32", c.Cin);
     MVP_REQUIRE(c.ks == 1 || c.ks == 3, "conv: ks=%d", c.ks);
     MVP_REQUIRE(c.stride == 1 || c.stride == 2, "conv: stride=%d", c.stride);
@@ -790,6 +799,9 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.H = c.H;
     p.W = c.W;
     p.Cin = c.Cin;
+    p.xs = c.x_stride ? c.x_stride : c.Cin;
+    p.ys = c.y_stride ? c.y_stride : c.Cout;
+    p.rs = c.r_stride ? c.r_stride : c.Cout;
     const int pad = c.ks / 2;
     p.Ho = (c.H + 2 * pad - c.ks) / c.stride + 1;
     p.Wo = (c.W + 2 * pad - c.ks) / c.stride + 1;
@@ -798,6 +810,10 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
     p.relu = c.relu;
     p.out_f32 = c.out_f32_nchw;
     if (c.N == 0) return;
+    if (generic_only) {
+        MVP_REQUIRE(!c.x2 && !c.out_f32_nchw, "conv: the generic path takes one bf16 input and output");
+        goto generic;
+    }
     if (c.x2) {  // graph cat-fusion: only the direct 1x1 kernel reads two inputs
         MVP_REQUIRE(c.ks == 1 && launch_conv1x1_direct(c, s), "conv: dual-input conv needs the 1x1 kernel");
         MVP_HIP(hipGetLastError());
@@ -808,6 +824,7 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
         MVP_HIP(hipGetLastError());
         return;
     }
+generic:
     if (c.ks == 3 && c.stride == 1)
         launch_plane<3, 1>(p, s);
     else if (c.ks == 3 && c.stride == 2)
@@ -818,6 +835,13 @@ void launch_conv(const ConvLaunch& c, hipStream_t s) {
         fail(MVP_ERR_ARG, "conv: unsupported ks=%d stride=%d", c.ks, c.stride);
     MVP_HIP(hipGetLastError());
 }
+
+void launch_conv(const ConvLaunch& c, hipStream_t s) {
+    MVP_REQUIRE(!c.x_stride && !c.y_stride && !c.r_stride && c.relu != 2, "conv: views / SiLU need launch_conv_generic");
+    launch_conv_impl(c, s, false);
+}
+
+void launch_conv_generic(const ConvLaunch& c, hipStream_t s) { launch_conv_impl(c, s, true); }
 
 void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t* y, int N, int H, int W,
                  hipStream_t s) {

@@ -1,0 +1,28 @@
+// Internal (not part of the C-ABI): person-detector kernels (det.hip) used by the
+// detector graph runtime (detnet.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mvp {
+
+// mmcv rescale_size for scale (S, S), keep_ratio: the resized extent of an H x W frame.
+void det_rescale_size(int H, int W, int S, int& nh, int& nw);
+void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, const float* mean3, const float* std3,
+                          void* out, hipStream_t s);
+// 3x3/s2 conv 4 -> 32 channels on the letterboxed [n][S][S][4] input, w f32 [32][9][4].
+void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act,
+                     hipStream_t s);
+void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
+                    int C, int act, hipStream_t s);
+// channel attention in place; scratch: [n][C] f32
+void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
+                   hipStream_t s);
+void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s);
+void launch_det_up2(const uint16_t* x, int xs, uint16_t* y, int ys, int n, int H, int W, int C, hipStream_t s);
+void launch_det_head(const uint16_t* x, int xs, int F, const float* w, const float* b, float* cand, int n, int H, int W,
+                     int stride, int size, int n_priors, int prior0, hipStream_t s);
+void launch_det_select(const float* cand, int n, int n_priors, float score_thr, float fx, float fy, float* best,
+                       hipStream_t s);
+
+}  // namespace mvp

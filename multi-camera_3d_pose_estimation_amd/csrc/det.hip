@@ -1,0 +1,685 @@
+// Person detector (RTMDet-m) kernels for gfx950: the parts of the network that are not
+// dense convolutions (those run on conv_mfma_kernel through launch_conv_generic), plus
+// the test pipeline in front of it and the prediction / selection behind it.
+//
+// Reference: PoseEstimator.predict -> mmdet inference_detector (mmpose_pose_estimation.py
+// :98-99, :234-241) and the hand-off rule (:242-250); algorithm restated in
+// oracle/rtmdet_ref.py (mmdet / mmcv / cv2 are absent here: parity unpinned).
+//
+// Layout: bf16 NHWC activations; a "view" is a channel slice [coff, coff + c) of a
+// tensor whose pixels are `stride` elements apart, so concatenation is free (producers
+// write into their slice of the shared buffer).
+#include <algorithm>
+#include <cstdint>
+
+#include "det.h"
+#include "mvp_common.h"
+
+namespace mvp {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ float bf(uint32_t v16) { return __uint_as_float(v16 << 16); }
+__device__ __forceinline__ uint32_t tobf(float f) {
+    __bf16 b = (__bf16)f;  // round to nearest even
+    return (uint32_t)__builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ float act_f(float v, int act) {
+    if (act == 1) return fmaxf(v, 0.f);
+    if (act == 2) return v / (1.f + __expf(-v));
+    return v;
+}
+__device__ __forceinline__ void unpack8(uint4 u, float* f) {
+    f[0] = bf(u.x & 0xffff), f[1] = bf(u.x >> 16), f[2] = bf(u.y & 0xffff), f[3] = bf(u.y >> 16);
+    f[4] = bf(u.z & 0xffff), f[5] = bf(u.z >> 16), f[6] = bf(u.w & 0xffff), f[7] = bf(u.w >> 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+    return uint4{tobf(f[0]) | (tobf(f[1]) << 16), tobf(f[2]) | (tobf(f[3]) << 16), tobf(f[4]) | (tobf(f[5]) << 16),
+                 tobf(f[6]) | (tobf(f[7]) << 16)};
+}
+
+// ------------------------------------------------------------------ letterbox
+// One thread per output pixel.  cv2.resize INTER_LINEAR on uint8 (OpenCV 4.x
+// imgproc/resize.cpp): an exact 2x downscale runs INTER_AREA's fast path,
+// (a + b + c + d + 2) >> 2; otherwise fixed-point bilinear with 11-bit coefficients,
+// exact int32 horizontal pass and the SIMD vertical rounding
+// (((S0 >> 4) * b0 >> 16) + ((S1 >> 4) * b1 >> 16) + 2) >> 2.
+struct LbParams {
+    const uint8_t* f;
+    uint32_t* out;  // [n][S][S] pixels of 4 bf16 (8 B = 2 words)
+    int H, W, S, nh, nw, area2;
+    double scale_x, scale_y;
+    float mean[3], stdv[3];
+};
+
+__device__ __forceinline__ void lin_coef(int d, double scale, int n_src, int& s0, int& s1, int& c0, int& c1) {
+    float fx = (float)((d + 0.5) * scale - 0.5);
+    int sx = (int)floorf(fx);
+    fx -= (float)sx;
+    if (sx < 0) fx = 0.f, sx = 0;
+    if (sx >= n_src - 1) fx = 0.f, sx = n_src - 1;
+    c1 = (int)rintf(fx * 2048.f);
+    c0 = (int)rintf((1.f - fx) * 2048.f);
+    s0 = sx;
+    s1 = min(sx + 1, n_src - 1);
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
+    const int n = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.S * p.S) return;
+    const int y = i / p.S, x = i - y * p.S;
+    int v[3] = {114, 114, 114};
+    const uint8_t* fr = p.f + (size_t)n * p.H * p.W * 3;
+    if (y < p.nh && x < p.nw) {
+        if (p.area2) {
+            const uint8_t* r0 = fr + ((size_t)(2 * y) * p.W + 2 * x) * 3;
+            const uint8_t* r1 = r0 + (size_t)p.W * 3;
+#pragma unroll
+            for (int c = 0; c < 3; c++) v[c] = (r0[c] + r0[3 + c] + r1[c] + r1[3 + c] + 2) >> 2;
+        } else {
+            int x0, x1, a0, a1, y0, y1, b0, b1;
+            lin_coef(x, p.scale_x, p.W, x0, x1, a0, a1);
+            lin_coef(y, p.scale_y, p.H, y0, y1, b0, b1);
+            const uint8_t* r0 = fr + (size_t)y0 * p.W * 3;
+            const uint8_t* r1 = fr + (size_t)y1 * p.W * 3;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                const int h0 = r0[x0 * 3 + c] * a0 + r0[x1 * 3 + c] * a1;
+                const int h1 = r1[x0 * 3 + c] * a0 + r1[x1 * 3 + c] * a1;
+                const int s = (((h0 >> 4) * b0) >> 16) + (((h1 >> 4) * b1) >> 16);
+                v[c] = min(max((s + 2) >> 2, 0), 255);
+            }
+        }
+    }
+    float o[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) o[c] = ((float)v[c] - p.mean[c]) / p.stdv[c];
+    uint32_t* dst = p.out + ((size_t)n * p.S * p.S + i) * 2;
+    *reinterpret_cast<uint2*>(dst) = uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
+}
+
+// ------------------------------------------------------------------ stem conv
+// 3x3/s2 conv 4 -> 32 channels (24 real + zero-weight padding) on v_mfma_f32_16x16x32_bf16:
+// K = 9 taps x 4 channels = 36 padded to 64.  A workgroup computes two output rows; the
+// five input rows they read are staged in LDS with a one-pixel zero border.  A row r of
+// cout tile c is cout (r >> 2) * 8 + 4c + (r & 3), so lane group g owns the 8 consecutive
+// couts 8g..8g+7 of its pixel (one 16-B store).
+__global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, uint16_t* __restrict__ y,
+                                                       int S, int act, long n_tiles) {
+    extern __shared__ uint2 sx[];  // [5][S + 2]
+    const int Wo = S / 2, LW = S + 2;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+    bf16x8 afr[2][2];
+    float4 b4[2];
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const int r = lane & 15, co = (r >> 2) * 8 + 4 * c + (r & 3);
+#pragma unroll
+        for (int kc = 0; kc < 2; kc++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int k = kc * 32 + g * 8 + j, tap = k >> 2, ch = k & 3;
+                afr[c][kc][j] = (__bf16)(tap < 9 ? w[(co * 9 + tap) * 4 + ch] : 0.f);
+            }
+        b4[c] = *reinterpret_cast<const float4*>(bias + g * 8 + 4 * c);
+    }
+    const int tiles = Wo / 2;  // output row pairs per image (Ho = Wo)
+    const int n_pt = Wo * 2 / 16;  // 16-pixel tiles per row pair
+    for (long t = blockIdx.x; t < n_tiles; t += gridDim.x) {
+        const long n = t / tiles;
+        const int ho0 = (int)(t - n * tiles) * 2;
+        const uint2* xin = reinterpret_cast<const uint2*>(x) + (size_t)n * S * S;
+        __syncthreads();
+        for (int i = tid; i < 5 * LW; i += 256) {
+            const int r = i / LW, c = i - r * LW;
+            const int hi = 2 * ho0 - 1 + r, wi = c - 1;
+            sx[i] = (hi >= 0 && hi < S && wi >= 0 && wi < S) ? xin[(size_t)hi * S + wi] : uint2{0u, 0u};
+        }
+        __syncthreads();
+        for (int pt = wave; pt < n_pt; pt += 4) {
+            const int pix = pt * 16 + (lane & 15);
+            const int orow = pix / Wo, ocol = pix - orow * Wo;
+            auto tap_px = [&](int tap) { return sx[(2 * orow + tap / 3) * LW + 2 * ocol + tap % 3]; };
+            const uint2 t0 = tap_px(2 * g), t1 = tap_px(2 * g + 1);
+            const uint2 t8 = g == 0 ? tap_px(8) : uint2{0u, 0u};
+            union {
+                uint4 u;
+                bf16x8 v;
+            } q0, q1;
+            q0.u = uint4{t0.x, t0.y, t1.x, t1.y};
+            q1.u = uint4{t8.x, t8.y, 0u, 0u};
+            uint32_t o[4];
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][0], q0.v, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afr[c][1], q1.v, acc, 0, 0, 0);
+                o[2 * c] = tobf(act_f(acc[0] + b4[c].x, act)) | (tobf(act_f(acc[1] + b4[c].y, act)) << 16);
+                o[2 * c + 1] = tobf(act_f(acc[2] + b4[c].z, act)) | (tobf(act_f(acc[3] + b4[c].w, act)) << 16);
+            }
+            uint16_t* out = y + (((size_t)n * Wo + ho0 + orow) * Wo + ocol) * 32 + g * 8;
+            *reinterpret_cast<uint4*>(out) = uint4{o[0], o[1], o[2], o[3]};
+        }
+    }
+}
+
+// ------------------------------------------------------------------ depthwise 5x5
+// One workgroup = an 8 x 32 output tile of one 8-channel group; the 12 x 36 input halo
+// and the group's 25 x 8 weights are staged in LDS, each thread computes one pixel's 8
+// channels (f32 accumulation in tap order, then bias and activation).
+constexpr int kDwTH = 8, kDwTW = 32, kDwHH = kDwTH + 4, kDwHW = kDwTW + 4;
+
+struct DwParams {
+    const uint16_t* x;
+    uint16_t* y;
+    const float* w;  // [C][25]
+    const float* b;  // [C]
+    int H, W, C, xs, ys, act, tiles_w, tiles_h;
+};
+
+__global__ __launch_bounds__(256) void dw5_kernel(DwParams p) {
+    __shared__ uint4 sh[kDwHH * kDwHW];
+    __shared__ float sw[25][8];
+    __shared__ float sb[8];
+    const int cg = blockIdx.x % (p.C / 8);
+    const int t2 = blockIdx.x / (p.C / 8);
+    const int tw = t2 % p.tiles_w, th = (t2 / p.tiles_w) % p.tiles_h;
+    const int n = blockIdx.y;
+    const int h0 = th * kDwTH - 2, w0 = tw * kDwTW - 2;
+    const int tid = threadIdx.x;
+    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs + cg * 8;
+    for (int i = tid; i < kDwHH * kDwHW; i += 256) {
+        const int r = i / kDwHW, c = i - r * kDwHW;
+        const int hi = h0 + r, wi = w0 + c;
+        sh[i] = (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                    ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs)
+                    : uint4{0u, 0u, 0u, 0u};
+    }
+    if (tid < 200) sw[tid >> 3][tid & 7] = p.w[(size_t)(cg * 8 + (tid & 7)) * 25 + (tid >> 3)];
+    if (tid < 8) sb[tid] = p.b[cg * 8 + tid];
+    __syncthreads();
+    const int ty = tid / kDwTW, tx = tid - ty * kDwTW;
+    const int ho = th * kDwTH + ty, wo = tw * kDwTW + tx;
+    if (ho >= p.H || wo >= p.W) return;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 5; kh++)
+#pragma unroll
+        for (int kw = 0; kw < 5; kw++) {
+            float v[8];
+            unpack8(sh[(ty + kh) * kDwHW + tx + kw], v);
+#pragma unroll
+            for (int c = 0; c < 8; c++) acc[c] = fmaf(v[c], sw[kh * 5 + kw][c], acc[c]);
+        }
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[c] = act_f(acc[c] + sb[c], p.act);
+    *reinterpret_cast<uint4*>(p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + cg * 8) = pack8(acc);
+}
+
+// ------------------------------------------------------------------ channel attention
+// One workgroup per image: channel means over all pixels (f32, per-thread partial sums
+// then an LDS tree), then s = hardsigmoid(W·mean + b) with W^T [C][C] read coalesced.
+struct CaParams {
+    const uint16_t* x;
+    const float* wt;  // W^T [k][c]
+    const float* b;
+    float* s;  // [n][C]
+    int HW, C, xs;
+};
+
+__global__ __launch_bounds__(256) void ca_pool_fc_kernel(CaParams p) {
+    extern __shared__ float red[];  // [rows][C] partial sums, then mean [C]
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const int Q = p.C / 8;
+    const int rows = 256 / Q;  // pixel lanes per chunk
+    const int q = tid % Q, r = tid / Q;
+    const uint16_t* xb = p.x + (size_t)n * p.HW * p.xs + q * 8;
+    if (r < rows) {
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        for (int px = r; px < p.HW; px += rows) {
+            float v[8];
+            unpack8(*reinterpret_cast<const uint4*>(xb + (size_t)px * p.xs), v);
+#pragma unroll
+            for (int c = 0; c < 8; c++) acc[c] += v[c];
+        }
+#pragma unroll
+        for (int c = 0; c < 8; c++) red[r * p.C + q * 8 + c] = acc[c];
+    }
+    __syncthreads();
+    float* mean = red + rows * p.C;
+    for (int c = tid; c < p.C; c += 256) {
+        float sum = 0.f;
+        for (int i = 0; i < rows; i++) sum += red[i * p.C + c];
+        mean[c] = sum / (float)p.HW;
+    }
+    __syncthreads();
+    for (int c = tid; c < p.C; c += 256) {
+        float a = p.b[c];
+        for (int k = 0; k < p.C; k++) a = fmaf(p.wt[(size_t)k * p.C + c], mean[k], a);
+        p.s[(size_t)n * p.C + c] = fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
+    }
+}
+
+__global__ __launch_bounds__(256) void ca_scale_kernel(uint16_t* x, const float* s, int HW, int C, int xs) {
+    const int n = blockIdx.y;
+    const int Q = C / 8;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long)HW * Q) return;
+    const int px = (int)(i / Q), q = (int)(i - (long)px * Q);
+    uint4* ptr = reinterpret_cast<uint4*>(x + ((size_t)n * HW + px) * xs + q * 8);
+    float v[8];
+    unpack8(*ptr, v);
+    const float* sc = s + (size_t)n * C + q * 8;
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] *= sc[c];
+    *ptr = pack8(v);
+}
+
+// ------------------------------------------------------------------ SPP max pools
+// maxpool 9 = maxpool 5 twice, 13 = three times (stride 1, -inf padding: exact), so one
+// workgroup per (image, 8-channel group) keeps the plane in LDS and applies the 5x5 max
+// three times, writing each result into its slice.
+__global__ __launch_bounds__(256) void spp_kernel(uint16_t* buf, int H, int W, int C, int xs) {
+    extern __shared__ uint4 pl[];  // two planes [H*W] of 8 channels
+    const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, HW = H * W;
+    uint16_t* base = buf + (size_t)n * HW * xs + cg * 8;
+    uint4* a = pl;
+    uint4* b = pl + HW;
+    for (int i = tid; i < HW; i += 256) a[i] = *reinterpret_cast<const uint4*>(base + (size_t)i * xs);
+    for (int k = 1; k <= 3; k++) {
+        __syncthreads();
+        for (int i = tid; i < HW; i += 256) {
+            const int y = i / W, x = i - y * W;
+            float m[8];
+            for (int c = 0; c < 8; c++) m[c] = -__builtin_inff();
+            for (int dy = -2; dy <= 2; dy++) {
+                const int yy = y + dy;
+                if (yy < 0 || yy >= H) continue;
+                for (int dx = -2; dx <= 2; dx++) {
+                    const int xx = x + dx;
+                    if (xx < 0 || xx >= W) continue;
+                    float v[8];
+                    unpack8(a[yy * W + xx], v);
+#pragma unroll
+                    for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
+                }
+            }
+            const uint4 o = pack8(m);  // exact: every value is already bf16
+            b[i] = o;
+            *reinterpret_cast<uint4*>(base + (size_t)i * xs + k * C) = o;
+        }
+        uint4* t = a;
+        a = b;
+        b = t;
+    }
+}
+
+// ------------------------------------------------------------------ nearest 2x
+__global__ __launch_bounds__(256) void up2_kernel(const uint16_t* x, int xs, uint16_t* y, int ys, int H, int W, int C) {
+    const int n = blockIdx.y, Q = C / 8;
+    const long i = (long)blockIdx.x * 256 + threadIdx.x;  // output (pixel, chunk)
+    if (i >= (long)4 * H * W * Q) return;
+    const int px = (int)(i / Q), q = (int)(i - (long)px * Q);
+    const int yo = px / (2 * W), xo = px - yo * (2 * W);
+    const uint4 v = *reinterpret_cast<const uint4*>(x + ((size_t)n * H * W + (size_t)(yo >> 1) * W + (xo >> 1)) * xs + q * 8);
+    *reinterpret_cast<uint4*>(y + ((size_t)n * 4 * H * W + px) * ys + q * 8) = v;
+}
+
+// ------------------------------------------------------------------ head predictions
+// One thread per pixel of a level: rtm_cls (1) and rtm_reg (4) 1x1 convs on the [cls |
+// reg] features (f32 dot products, weights in LDS), sigmoid score, exp(reg) * stride,
+// prior (x, y) * stride, distance2bbox clipped to [0, size].
+struct HeadParams {
+    const uint16_t* x;  // [n][H][W] pixels of xs elements: cls feat at 0, reg feat at F
+    const float* w;     // [5][F]
+    const float* b;     // [5]
+    float* cand;        // [n][n_priors][6]
+    int H, W, F, xs, stride, size, n_priors, prior0;
+};
+
+__global__ __launch_bounds__(256) void det_head_kernel(HeadParams p) {
+#pragma clang fp contract(off)  // box arithmetic rounded op by op, as mmdet's torch ops
+    extern __shared__ float swh[];  // [5][F]
+    const int n = blockIdx.y, tid = threadIdx.x;
+    for (int i = tid; i < 5 * p.F; i += 256) swh[i] = p.w[i];
+    __syncthreads();
+    const int px = blockIdx.x * 256 + tid;
+    if (px >= p.H * p.W) return;
+    const uint16_t* xc = p.x + ((size_t)n * p.H * p.W + px) * p.xs;
+    const uint16_t* xr = xc + p.F;
+    float a[5] = {p.b[0], p.b[1], p.b[2], p.b[3], p.b[4]};
+    for (int k = 0; k < p.F; k += 8) {
+        float c[8], r[8];
+        unpack8(*reinterpret_cast<const uint4*>(xc + k), c);
+        unpack8(*reinterpret_cast<const uint4*>(xr + k), r);
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a[0] = fmaf(swh[k + j], c[j], a[0]);
+#pragma unroll
+            for (int o = 1; o < 5; o++) a[o] = fmaf(swh[o * p.F + k + j], r[j], a[o]);
+        }
+    }
+    const int yy = px / p.W, xx = px - yy * p.W;
+    const float s = (float)p.stride;
+    const float pxf = (float)xx * s, pyf = (float)yy * s;
+    const float d0 = expf(a[1]) * s, d1 = expf(a[2]) * s, d2 = expf(a[3]) * s, d3 = expf(a[4]) * s;
+    const float lim = (float)p.size;
+    float* out = p.cand + ((size_t)n * p.n_priors + p.prior0 + px) * 6;
+    out[0] = 1.f / (1.f + expf(-a[0]));
+    out[1] = fminf(fmaxf(pxf - d0, 0.f), lim);
+    out[2] = fminf(fmaxf(pyf - d1, 0.f), lim);
+    out[3] = fminf(fmaxf(pxf + d2, 0.f), lim);
+    out[4] = fminf(fmaxf(pyf + d3, 0.f), lim);
+    out[5] = a[0];
+}
+
+// ------------------------------------------------------------------ per-frame argmax
+// The reference keeps the first detection after mmdet's NMS = the highest-scoring prior
+// that passed score_thr and the min-size filter (NMS never removes the top box).  Ties go
+// to the lowest prior index (level-major, row-major: the order of a stable sort).
+__global__ __launch_bounds__(256) void det_select_kernel(const float* cand, int n_priors, float score_thr, float fx,
+                                                         float fy, float* best) {
+#pragma clang fp contract(off)
+    __shared__ float ss[256];
+    __shared__ int si[256];
+    const int n = blockIdx.x, tid = threadIdx.x;
+    float bs = -1.f;
+    int bi = 0x7fffffff;
+    for (int i = tid; i < n_priors; i += 256) {
+        const float* c = cand + ((size_t)n * n_priors + i) * 6;
+        const float s = c[0];
+        const float x1 = c[1] * fx, y1 = c[2] * fy, x2 = c[3] * fx, y2 = c[4] * fy;
+        if (s > score_thr && x2 - x1 > 0.f && y2 - y1 > 0.f && s > bs) bs = s, bi = i;  // i increases: first max kept
+    }
+    ss[tid] = bs;
+    si[tid] = bi;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) {
+            const float s2 = ss[tid + w];
+            const int i2 = si[tid + w];
+            if (s2 > ss[tid] || (s2 == ss[tid] && i2 < si[tid])) ss[tid] = s2, si[tid] = i2;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        float* o = best + (size_t)n * 6;
+        if (si[0] == 0x7fffffff) {
+            o[0] = o[1] = o[2] = o[3] = 0.f;
+            o[4] = -1.f;
+            o[5] = -1.f;
+        } else {
+            const float* c = cand + ((size_t)n * n_priors + si[0]) * 6;
+            o[0] = c[1] * fx, o[1] = c[2] * fy, o[2] = c[3] * fx, o[3] = c[4] * fy;
+            o[4] = ss[0];
+            o[5] = (float)si[0];
+        }
+    }
+}
+
+// ------------------------------------------------------------------ NMS (full list)
+// One workgroup per frame.  Per level: the priors above score_thr are ranked by
+// (score desc, index asc) with a bitonic sort of (score, index) keys in LDS and the best
+// nms_pre kept; the survivors of all levels are rescaled, min-size filtered, sorted again
+// and suppressed greedily (IoU > iou_thr, mmcv nms with offset 0).
+constexpr int kNmsCap = 8192;  // keys per sort (a level's priors; <= 6400 at size 640)
+
+__device__ void bitonic_desc(unsigned long long* k, int n_pow2) {
+    for (int size = 2; size <= n_pow2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;  // descending in "up" runs
+                    const unsigned long long a = k[i], b = k[j];
+                    if (up ? a < b : a > b) k[i] = b, k[j] = a;
+                }
+            }
+        }
+    __syncthreads();
+}
+
+// key: score bits (positive floats order as unsigned) high, inverted index low, so a
+// descending sort puts higher score first and, for equal scores, the lower index first
+__device__ __forceinline__ unsigned long long nms_key(float s, int i) {
+    return ((unsigned long long)__float_as_uint(s) << 32) | (unsigned)(0x7fffffff - i);
+}
+
+__global__ __launch_bounds__(1024) void det_nms_kernel(const float* cand, int n_priors, const int* level_off, int n_levels,
+                                                       int nms_pre, float score_thr, float iou_thr, int max_det, float fx,
+                                                       float fy, float* dets, int* counts) {
+#pragma clang fp contract(off)  // rescale / IoU rounded op by op (mmcv nms, offset 0)
+    extern __shared__ unsigned long long keys[];  // [kNmsCap]
+    __shared__ int n_sel;
+    __shared__ int sel[3072];  // kept prior ids over the levels (nms_pre <= 1024 each, <= 3 levels)
+    __shared__ float4 bx[3072];
+    __shared__ float sc[3072];
+    __shared__ unsigned char dead[3072];
+    const int n = blockIdx.x, tid = threadIdx.x;
+    const float* cn = cand + (size_t)n * n_priors * 6;
+    if (tid == 0) n_sel = 0;
+    for (int l = 0; l < n_levels; l++) {
+        const int lo = level_off[l], cnt = level_off[l + 1] - lo;
+        int np2 = 1;
+        while (np2 < cnt) np2 <<= 1;
+        for (int i = tid; i < np2; i += blockDim.x) {
+            const float s = i < cnt ? cn[(size_t)(lo + i) * 6] : 0.f;
+            keys[i] = (i < cnt && s > score_thr) ? nms_key(s, lo + i) : 0ull;
+        }
+        bitonic_desc(keys, np2);
+        const int base = n_sel;
+        for (int i = tid; i < nms_pre && i < np2; i += blockDim.x)
+            if (keys[i] != 0ull) {
+                const int idx = 0x7fffffff - (int)(keys[i] & 0xffffffffu);
+                sel[base + i] = idx;
+            } else {
+                sel[base + i] = -1;
+            }
+        __syncthreads();
+        if (tid == 0) {
+            int k = base;
+            for (int i = 0; i < nms_pre && i < np2; i++)
+                if (sel[base + i] >= 0) sel[k++] = sel[base + i];
+            n_sel = k;
+        }
+        __syncthreads();
+    }
+    const int m = n_sel;
+    // rescale + min-size filter, then one global ranking of the survivors
+    int np2 = 1;
+    while (np2 < m) np2 <<= 1;
+    for (int i = tid; i < np2; i += blockDim.x) {
+        unsigned long long key = 0ull;
+        if (i < m) {
+            const float* c = cn + (size_t)sel[i] * 6;
+            const float x1 = c[1] * fx, y1 = c[2] * fy, x2 = c[3] * fx, y2 = c[4] * fy;
+            bx[i] = float4{x1, y1, x2, y2};
+            sc[i] = c[0];
+            if (x2 - x1 > 0.f && y2 - y1 > 0.f) key = nms_key(c[0], i);
+        }
+        keys[i] = key;
+    }
+    bitonic_desc(keys, np2);
+    for (int i = tid; i < m; i += blockDim.x) dead[i] = 0;
+    __syncthreads();
+    int kept = 0;
+    float* out = dets + (size_t)n * max_det * 5;
+    for (int a = 0; a < m && kept < max_det; a++) {
+        const unsigned long long ka = keys[a];
+        if (ka == 0ull) break;
+        const int ia = 0x7fffffff - (int)(ka & 0xffffffffu);
+        if (dead[a]) continue;  // uniform: every thread reads the same flag after the barrier
+        const float4 A = bx[ia];
+        if (tid == 0) {
+            float* o = out + (size_t)kept * 5;
+            o[0] = A.x, o[1] = A.y, o[2] = A.z, o[3] = A.w, o[4] = sc[ia];
+        }
+        kept++;
+        const float area_a = (A.z - A.x) * (A.w - A.y);
+        for (int b = a + 1 + tid; b < m; b += blockDim.x) {
+            const unsigned long long kb = keys[b];
+            if (kb == 0ull || dead[b]) continue;
+            const float4 B = bx[0x7fffffff - (int)(kb & 0xffffffffu)];
+            const float w = fmaxf(fminf(A.z, B.z) - fmaxf(A.x, B.x), 0.f);
+            const float h = fmaxf(fminf(A.w, B.w) - fmaxf(A.y, B.y), 0.f);
+            const float inter = w * h;
+            const float iou = inter / (area_a + (B.z - B.x) * (B.w - B.y) - inter);
+            if (iou > iou_thr) dead[b] = 1;
+        }
+        __syncthreads();
+    }
+    if (tid == 0) counts[n] = kept;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- launchers
+void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, const float* mean3, const float* std3,
+                          void* out, hipStream_t s) {
+    int nh, nw;
+    det_rescale_size(H, W, S, nh, nw);
+    MVP_REQUIRE(nh >= 1 && nw >= 1 && nh <= S && nw <= S, "letterbox: bad size");
+    LbParams p{};
+    p.f = frames;
+    p.out = static_cast<uint32_t*>(out);
+    p.H = H, p.W = W, p.S = S, p.nh = nh, p.nw = nw;
+    p.scale_x = 1.0 / ((double)nw / W);
+    p.scale_y = 1.0 / ((double)nh / H);
+    p.area2 = p.scale_x == 2.0 && p.scale_y == 2.0 && W == 2 * nw && H == 2 * nh;
+    for (int c = 0; c < 3; c++) p.mean[c] = mean3[c], p.stdv[c] = std3[c];
+    if (n == 0) return;
+    hipLaunchKernelGGL(letterbox_kernel, dim3((unsigned)((S * S + 255) / 256), (unsigned)n), dim3(256), 0, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+void det_rescale_size(int H, int W, int S, int& nh, int& nw) {
+    const double sc = std::min((double)S / std::max(H, W), (double)S / std::min(H, W));
+    nh = (int)(H * sc + 0.5);
+    nw = (int)(W * sc + 0.5);
+}
+
+void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act,
+                     hipStream_t s) {
+    MVP_REQUIRE(S % 16 == 0, "det stem: size %d must be a multiple of 16", S);
+    const long n_tiles = (long)n * (S / 4);
+    if (n_tiles == 0) return;
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const size_t lds = (size_t)5 * (S + 2) * sizeof(uint2);
+    const long grid = std::min<long>(n_tiles, (long)cus * 8);
+    hipLaunchKernelGGL(det_stem_kernel, dim3((unsigned)grid), dim3(256), lds, s, x, w, b, y, S, act, n_tiles);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
+                    int C, int act, hipStream_t s) {
+    MVP_REQUIRE(C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0, "dw5: channels / strides must be multiples of 8");
+    DwParams p{x, y, w, b, H, W, C, xs, ys, act, (W + kDwTW - 1) / kDwTW, (H + kDwTH - 1) / kDwTH};
+    const long blocks = (long)p.tiles_w * p.tiles_h * (C / 8);
+    if (n == 0 || blocks == 0) return;
+    MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
+    hipLaunchKernelGGL(dw5_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
+                   hipStream_t s) {
+    MVP_REQUIRE(C % 8 == 0 && C / 8 <= 256 && xs % 8 == 0, "ca: C=%d", C);
+    const int rows = 256 / (C / 8);
+    const size_t lds = ((size_t)rows * C + C) * sizeof(float);
+    MVP_REQUIRE(lds <= 64 * 1024, "ca: C=%d needs too much LDS", C);
+    if (n == 0) return;
+    CaParams p{x, wt, b, scratch, HW, C, xs};
+    hipLaunchKernelGGL(ca_pool_fc_kernel, dim3((unsigned)n), dim3(256), lds, s, p);
+    MVP_HIP(hipGetLastError());
+    const long work = (long)HW * (C / 8);
+    hipLaunchKernelGGL(ca_scale_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, scratch,
+                       HW, C, xs);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s) {
+    MVP_REQUIRE(C % 8 == 0 && xs >= 4 * C && xs % 8 == 0, "spp: C=%d stride=%d", C, xs);
+    const size_t lds = (size_t)2 * H * W * sizeof(uint4);
+    MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large", H, W);
+    if (n == 0) return;
+    hipLaunchKernelGGL(spp_kernel, dim3((unsigned)(C / 8), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_up2(const uint16_t* x, int xs, uint16_t* y, int ys, int n, int H, int W, int C, hipStream_t s) {
+    MVP_REQUIRE(C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0, "up2: C=%d", C);
+    const long work = (long)4 * H * W * (C / 8);
+    if (n == 0 || work == 0) return;
+    hipLaunchKernelGGL(up2_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, xs, y, ys, H,
+                       W, C);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_head(const uint16_t* x, int xs, int F, const float* w, const float* b, float* cand, int n, int H, int W,
+                     int stride, int size, int n_priors, int prior0, hipStream_t s) {
+    MVP_REQUIRE(F % 8 == 0 && xs >= 2 * F && prior0 + H * W <= n_priors, "det head: shape");
+    HeadParams p{x, w, b, cand, H, W, F, xs, stride, size, n_priors, prior0};
+    if (n == 0) return;
+    hipLaunchKernelGGL(det_head_kernel, dim3((unsigned)((H * W + 255) / 256), (unsigned)n), dim3(256),
+                       (size_t)5 * F * sizeof(float), s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_select(const float* cand, int n, int n_priors, float score_thr, float fx, float fy, float* best,
+                       hipStream_t s) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(det_select_kernel, dim3((unsigned)n), dim3(256), 0, s, cand, n_priors, score_thr, fx, fy, best);
+    MVP_HIP(hipGetLastError());
+}
+
+}  // namespace mvp
+
+extern "C" int mvp_det_letterbox(const uint8_t* frames, int n, int h, int w, int size, const float* mean3,
+                                 const float* std3, void* out, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n >= 0 && h > 0 && w > 0 && size > 0 && mean3 && std3, "mvp_det_letterbox: bad arguments");
+    MVP_REQUIRE(n == 0 || (frames && out), "mvp_det_letterbox: NULL buffer");
+    mvp::launch_det_letterbox(frames, n, h, w, size, mean3, std3, out, reinterpret_cast<hipStream_t>(stream));
+    MVP_ABI_END
+}
+
+extern "C" int mvp_det_nms(const float* cand, int n, int n_priors, const int* level_off, int n_levels, int nms_pre,
+                           float score_thr, float iou_thr, int max_det, float fx, float fy, float* dets, int* counts,
+                           void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n >= 0 && n_levels >= 1 && n_levels <= 3 && level_off, "mvp_det_nms: bad levels");
+    MVP_REQUIRE(nms_pre >= 1 && nms_pre <= 1024 && max_det >= 1, "mvp_det_nms: nms_pre must be in [1, 1024]");
+    MVP_REQUIRE(level_off[0] == 0 && level_off[n_levels] == n_priors, "mvp_det_nms: level offsets");
+    int offs[4];
+    for (int l = 0; l <= n_levels; l++) offs[l] = level_off[l];
+    for (int l = 0; l < n_levels; l++)
+        MVP_REQUIRE(offs[l + 1] > offs[l] && offs[l + 1] - offs[l] <= mvp::kNmsCap, "mvp_det_nms: level %d has %d priors",
+                    l, offs[l + 1] - offs[l]);
+    if (n == 0) return MVP_OK;
+    MVP_REQUIRE(cand && dets && counts, "mvp_det_nms: NULL buffer");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int* d_off = nullptr;
+    MVP_HIP(hipMallocAsync((void**)&d_off, sizeof(offs), s));
+    MVP_HIP(hipMemcpyAsync(d_off, offs, sizeof(int) * (n_levels + 1), hipMemcpyHostToDevice, s));
+    const size_t lds = (size_t)mvp::kNmsCap * sizeof(unsigned long long);
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)mvp::det_nms_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL(mvp::det_nms_kernel, dim3((unsigned)n), dim3(1024), lds, s, cand, n_priors, d_off, n_levels,
+                       nms_pre, score_thr, iou_thr, max_det, fx, fy, dets, counts);
+    MVP_HIP(hipGetLastError());
+    MVP_HIP(hipFreeAsync(d_off, s));
+    MVP_ABI_END
+}

@@ -56,6 +56,18 @@ SIGNATURES = {
     "mvp_graph_arena_bytes": (c_int, None),
     "mvp_graph_refresh_weights": (c_int, [c_void_p]),
     "mvp_graph_destroy": (c_int, [c_void_p]),
+    "mvp_det_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, P(c_float), P(c_float), c_void_p,
+                                  c_void_p]),
+    # detector graph argtypes with struct pointers are (re)declared in mvpose/rtmdet.py
+    "mvp_det_create": (c_int, None),
+    "mvp_det_forward": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                c_void_p]),
+    "mvp_det_nms": (c_int, [c_void_p, c_int, c_int, P(c_int), c_int, c_int, c_float, c_float, c_int, c_float,
+                            c_float, c_void_p, c_void_p, c_void_p]),
+    "mvp_det_arena_bytes": (c_int, None),
+    "mvp_det_run_ops": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "mvp_det_tensor_copy": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "mvp_det_destroy": (c_int, [c_void_p]),
     "mvp_sgd_workspace_floats": (c_int, [c_int, c_int, c_int, c_int, P(c_int64)]),
     # mvp_sgd_params struct pointer declared in mvpose/refine.py
     "mvp_sgd_refine": (c_int, None),
