@@ -312,6 +312,51 @@ def ingest_line(est, V, n_frames=512, batch=128):
                     "moments on the compute stream (2D stage only, serial moments)"}
 
 
+def detector_line(dev, est, cams_params, V, batch=128, reps=5):
+    """the person detector the reference runs on every camera-frame
+    (RTMDet-m, mmpose_pose_estimation.py:234-250), alone (letterbox -> graph -> per-frame
+    selection, HIP events on the launch stream) and in front of the 2D->3D pipeline
+    (T = batch / V synchronised frames: detect -> boxes -> crops -> HRNet -> decode ->
+    moments -> DLT).  77.9 GFLOP per 640x640 camera-frame (38.94 GMAC)."""
+    from mvpose.pipeline import MultiViewPipeline
+    from mvpose.rtmdet import RTMDetector
+    det = RTMDetector(seed=0, max_batch=batch, device=dev)
+    g = torch.Generator(device=dev).manual_seed(99)
+    fr = torch.randint(0, 256, (batch, 720, 1280, 3), dtype=torch.uint8, device=dev, generator=g)
+    for _ in range(2):
+        det.detect(fr)
+    s = torch.cuda.current_stream(dev)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    e[0].record(s)
+    for _ in range(reps):
+        det.detect(fr)
+    e[1].record(s)
+    torch.cuda.synchronize()
+    ms = e[0].elapsed_time(e[1]) / reps
+    flops = 2.0 * det.macs_per_frame * batch
+    tf = flops / (ms * 1e-3) / 1e12
+    pipe = MultiViewPipeline(cams_params, estimator=est, device=dev, detector=det)
+    fr2 = fr.reshape(batch // V, V, 720, 1280, 3)
+    out = {}
+    for _ in range(2):
+        pipe.process(fr2, out)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        pipe.process(fr2, out)
+    torch.cuda.synchronize()
+    e2e = (batch // V) * reps / (time.perf_counter() - t0)
+    found = float((det.best[:batch, 4] > 0.3).float().mean())
+    res = {"model": "RTMDet-m 640x640 (CSPNeXt-m / CSPNeXtPAFPN / RTMDetSepBNHead, 1 class), seeded weights with "
+                    "calibrated BN statistics", "batch_camera_frames": batch, "avg_launch_ms": ms,
+           "camera_frames_per_s": batch / (ms * 1e-3), "frames_with_person_box": found,
+           "pipeline_with_detector_frames_per_s": e2e,
+           "roofline": {"bound": "mfma", "achieved": tf, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": tf / BF16_PEAK_TFLOPS, "flops_per_launch": flops}}
+    det.close()
+    return res
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -385,6 +430,7 @@ def main():
             extra["sgd"] = sgd_line(dev)
             extra["sgd_extrinsic"] = extrinsic_line(dev)
             extra["host_ingest"] = ingest_line(est, V)
+            extra["detector"] = detector_line(dev, est, syn.reference_camera_params(cams), V)
 
     if rank == 0:
         traffic, traffic_src = committed_traffic()

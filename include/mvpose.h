@@ -211,7 +211,7 @@ int mvp_graph_destroy(void* handle);
  *                  f32 weights [32][3][3][4] + bias [32], act.
  *   MVP_DET_CONV : y = act(conv(x) + bias [+ res]), ks 1|3, stride 1|2, bf16 weights
  *                  [cout_pad][ks][ks][cin] (cout_pad as mvp_graph), f32 bias.
- *   MVP_DET_DW   : 5x5 depthwise conv + bias + act, f32 weights [c][25], bias [c].
+ *   MVP_DET_DW   : 5x5 depthwise conv + bias + act, f32 weights [c/8][25][8], bias [c].
  *   MVP_DET_CA   : channel attention in place on `in`: x *= hardsigmoid(W·mean(x) + b),
  *                  f32 W^T [c][c] (w_off) and b [c].
  *   MVP_DET_SPP  : `in` = slice 0 (c channels) of a 4c buffer; writes max-pools 5/9/13

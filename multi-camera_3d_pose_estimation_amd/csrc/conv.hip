@@ -522,6 +522,11 @@ template <int KS, int S, int TH, int TW, int NB, int NW>
 void launch_tile(const ConvParams& p, hipStream_t s) {
     const int n_chunks = p.Cin / 32;
     if (p.Cout_pad == 32) return launch_cfg<KS, S, 32, TH, TW, NB, NW>(p, s);
+    static const bool bm64 = [] {
+        const char* e = getenv("MVPOSE_CONV_BM64");  // tuning experiments: streamed 64-cout tiles
+        return e && e[0] == '1';
+    }();
+    if (bm64) return launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
     if (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
         return launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
     if (ConvCfg<KS, S, 32, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
@@ -566,8 +571,18 @@ void launch_plane(const ConvParams& p, hipStream_t s) {
             launch_tile2<KS, S, 16, 12, 1, 16, 12, 2>(p, s);
         else if (p.Wo == 6 && p.Ho == 8)
             launch_tile2<KS, S, 8, 6, 4, 8, 6, 8>(p, s);
-        else
-            launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
+        else {
+            static const int t3 = [] {
+                const char* e = getenv("MVPOSE_DET_TILE3");  // tuning experiments (detector planes)
+                return e ? atoi(e) : 0;
+            }();
+            if (t3 == 8)
+                launch_tile<KS, S, 8, 16, 1, 8>(p, s);
+            else if (t3 == 2)
+                launch_tile2<KS, S, 4, 16, 1, 8, 16, 1>(p, s);
+            else
+                launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
+        }
     } else {
         const char* e = getenv("MVPOSE_S2_TILE");  // tuning experiments only
         const int v = e ? atoi(e) : 0;  // 7: the pre-sweep 4-wave default

@@ -15,6 +15,12 @@ void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t
                      hipStream_t s);
 void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
                     int C, int act, hipStream_t s);
+// conv (1x1, or 3x3 stride 1 / 2, pad ks/2) as a GEMM over the flat output pixels with the
+// im2col gathered by DMA; w [cout_pad(N)][ks][ks][cin] bf16; act as ConvLaunch.relu (2 = SiLU
+// before the residual, 1 = ReLU after it)
+void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
+                          uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
+                          hipStream_t s);
 // channel attention in place; scratch: [n][C] f32
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
                    hipStream_t s);

@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdint>
 
+#include "conv.h"
 #include "det.h"
 #include "mvp_common.h"
 
@@ -167,56 +168,236 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restric
 }
 
 // ------------------------------------------------------------------ depthwise 5x5
-// One workgroup = an 8 x 32 output tile of one 8-channel group; the 12 x 36 input halo
-// and the group's 25 x 8 weights are staged in LDS, each thread computes one pixel's 8
-// channels (f32 accumulation in tap order, then bias and activation).
-constexpr int kDwTH = 8, kDwTW = 32, kDwHH = kDwTH + 4, kDwHW = kDwTW + 4;
+// Memory-bound (25 MACs per element): one workgroup = an 8 x 16 output tile x G channel
+// chunks of 8 (G waves, one chunk per wave).  The 12 x 20 input halo is loaded coalesced
+// (G consecutive 16-B chunks of a pixel per lane group) into LDS stored chunk-major, so a
+// wave's fragment reads are 64 consecutive pixels of its chunk (conflict-free).  Each lane
+// computes two vertically adjacent outputs (6 input rows x 5 taps for 2 outputs); the
+// weights are wave-uniform ([C/8][25][8] f32), read through the scalar cache.
+constexpr int kDwTH = 8, kDwTW = 16, kDwHH = kDwTH + 4, kDwHW = kDwTW + 4;
 
 struct DwParams {
     const uint16_t* x;
     uint16_t* y;
-    const float* w;  // [C][25]
+    const float* w;  // [C/8][25][8]
     const float* b;  // [C]
-    int H, W, C, xs, ys, act, tiles_w, tiles_h;
+    int H, W, C, xs, ys, act, tiles_w;
 };
 
-__global__ __launch_bounds__(256) void dw5_kernel(DwParams p) {
-    __shared__ uint4 sh[kDwHH * kDwHW];
-    __shared__ float sw[25][8];
-    __shared__ float sb[8];
-    const int cg = blockIdx.x % (p.C / 8);
-    const int t2 = blockIdx.x / (p.C / 8);
-    const int tw = t2 % p.tiles_w, th = (t2 / p.tiles_w) % p.tiles_h;
+template <int G>
+__global__ __launch_bounds__(G * 64) void dw5_kernel(DwParams p) {
+    __shared__ uint4 sh[G][kDwHH * kDwHW];
+    const int n_groups = p.C / (8 * G);
+    const int grp = blockIdx.x % n_groups;
+    const int t2 = blockIdx.x / n_groups;
+    const int tw = t2 % p.tiles_w, th = t2 / p.tiles_w;
     const int n = blockIdx.y;
     const int h0 = th * kDwTH - 2, w0 = tw * kDwTW - 2;
     const int tid = threadIdx.x;
-    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs + cg * 8;
-    for (int i = tid; i < kDwHH * kDwHW; i += 256) {
-        const int r = i / kDwHW, c = i - r * kDwHW;
+    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs + grp * 8 * G;
+    for (int i = tid; i < kDwHH * kDwHW * G; i += G * 64) {
+        const int pix = i / G, q = i - pix * G;
+        const int r = pix / kDwHW, c = pix - r * kDwHW;
         const int hi = h0 + r, wi = w0 + c;
-        sh[i] = (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                    ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs)
-                    : uint4{0u, 0u, 0u, 0u};
+        sh[q][pix] = (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                         ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + q * 8)
+                         : uint4{0u, 0u, 0u, 0u};
     }
-    if (tid < 200) sw[tid >> 3][tid & 7] = p.w[(size_t)(cg * 8 + (tid & 7)) * 25 + (tid >> 3)];
-    if (tid < 8) sb[tid] = p.b[cg * 8 + tid];
     __syncthreads();
-    const int ty = tid / kDwTW, tx = tid - ty * kDwTW;
-    const int ho = th * kDwTH + ty, wo = tw * kDwTW + tx;
-    if (ho >= p.H || wo >= p.W) return;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int col = lane & 15, rp = lane >> 4;
+    const int chunk = grp * G + wave;
+    const float* wc = p.w + (size_t)chunk * 200;
+    float a0[8], a1[8];
 #pragma unroll
-    for (int kh = 0; kh < 5; kh++)
+    for (int c = 0; c < 8; c++) a0[c] = a1[c] = 0.f;
+#pragma unroll
+    for (int ir = 0; ir < 6; ir++) {
 #pragma unroll
         for (int kw = 0; kw < 5; kw++) {
             float v[8];
-            unpack8(sh[(ty + kh) * kDwHW + tx + kw], v);
+            unpack8(sh[wave][(2 * rp + ir) * kDwHW + col + kw], v);
+            if (ir < 5) {
 #pragma unroll
-            for (int c = 0; c < 8; c++) acc[c] = fmaf(v[c], sw[kh * 5 + kw][c], acc[c]);
+                for (int c = 0; c < 8; c++) a0[c] = fmaf(v[c], wc[(ir * 5 + kw) * 8 + c], a0[c]);
+            }
+            if (ir >= 1) {
+#pragma unroll
+                for (int c = 0; c < 8; c++) a1[c] = fmaf(v[c], wc[((ir - 1) * 5 + kw) * 8 + c], a1[c]);
+            }
+        }
+    }
+    const int ho = th * kDwTH + 2 * rp, wo = tw * kDwTW + col;
+    if (wo >= p.W) return;
+    const float* bc = p.b + chunk * 8;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        a0[c] = act_f(a0[c] + bc[c], p.act);
+        a1[c] = act_f(a1[c] + bc[c], p.act);
+    }
+    uint16_t* yb = p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + chunk * 8;
+    if (ho < p.H) *reinterpret_cast<uint4*>(yb) = pack8(a0);
+    if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(a1);
+}
+
+// ------------------------------------------------------------------ conv = GEMM
+// Every detector conv is a GEMM over the flat output-pixel index m = (n, ho, wo):
+//   Y[m][cout] = sum_k X~[m][k] W[cout][k],  k = (tap, cin) (weights [cout][kh][kw][cin]),
+// X~ the im2col of the NHWC input view, gathered on the fly: K step (tap, 32-channel chunk)
+// DMAs, for each of the tile's 128 pixels, the 64 bytes of its tap's input pixel (or zeros
+// outside the image) straight into LDS (global_load_lds); a 1x1 conv reads its own pixel.
+// Flat pixels need no masking on 20x20 or 40x40 planes, and the same kernel serves the
+// stride-2 downsamples.  Workgroup tile: 128 pixels x BN couts, 4 waves as 2 (pixels) x 2
+// (couts), operands double-buffered chunk-major in LDS ([k group][row] 16-B slots: every
+// 16-lane fragment read is 256 contiguous bytes), the next K step's DMA in flight under
+// the current step's MFMAs (v_mfma_f32_16x16x32_bf16).  Epilogue: bias, activation (SiLU
+// before the residual, ReLU after it), bf16 stores into the output view.  Workgroups run
+// couts-fastest so the blocks sharing an input tile are co-resident (input from HBM once,
+// taps from L2).
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+__device__ __forceinline__ void glds16_det(const void* src, void* lds_base) {
+    __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)lds_base, 16, 0, 0);
+}
+
+struct GParams {
+    const uint16_t* x;
+    const uint16_t* w;  // [npad][KS*KS*cin]
+    const float* bias;  // [npad]
+    const uint16_t* res;
+    uint16_t* y;
+    const uint16_t* zero;  // >= 16 KiB of zeros
+    long M;                // n * Ho * Wo
+    int cin, N, npad, xs, ys, rs, act, n_nb;
+    int H, W, Ho, Wo;
+};
+
+template <int BN, int KS, int S>
+__global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
+    constexpr int BMP = 128;              // pixels per tile
+    constexpr int A_SLOTS = 4 * BN;       // [kg][cout]
+    constexpr int B_SLOTS = 4 * BMP;      // [kg][pix]
+    constexpr int STAGE = (A_SLOTS + B_SLOTS) * 16;
+    constexpr int WCT = BN / 32;          // cout tiles per wave
+    constexpr int PAD = KS / 2;
+    constexpr int NBUF = 3;               // LDS ring: two K steps in flight under the MFMAs
+    constexpr int OPS = A_SLOTS / 256 + B_SLOTS / 256;  // DMA instructions per thread per K step
+    static_assert(A_SLOTS % 256 == 0, "A slots per thread");
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 1, wc = wave >> 1;  // pixel half, cout half
+    const long tile = blockIdx.x / p.n_nb;
+    const int co0 = (int)(blockIdx.x - tile * p.n_nb) * BN;
+    const long m0 = tile * BMP;
+    const int kc = p.cin / 32;            // chunks per tap
+    const int nk = KS * KS * kc;
+    const int K = nk * 32;
+    // this thread's B slots: pixel tid % 128, k groups tid / 128 and + 2
+    const int bpx = tid % BMP, bkg = tid / BMP;
+    const long bm = m0 + bpx;
+    const bool bvalid = bm < p.M;
+    int bn_ = 0, bho = 0, bwo = 0;
+    if (KS > 1 && bvalid) {
+        const long hw = (long)p.Ho * p.Wo;
+        bn_ = (int)(bm / hw);
+        const int r = (int)(bm - (long)bn_ * hw);
+        bho = r / p.Wo;
+        bwo = r - bho * p.Wo;
+    }
+    auto issue = [&](int k, int buf) {
+        uint8_t* base = lds + buf * STAGE;
+        const int k0 = k * 32;
+#pragma unroll
+        for (int s0 = 0; s0 < A_SLOTS; s0 += 256) {
+            const int sl = s0 + tid;
+            const int co = sl % BN, kg = sl / BN;
+            const void* src = (co0 + co < p.npad) ? (const void*)(p.w + (size_t)(co0 + co) * K + k0 + kg * 8)
+                                                  : (const void*)(p.zero + (sl & 1023) * 8);
+            glds16_det(src, base + (s0 + wave * 64) * 16);
+        }
+        const uint16_t* px = nullptr;
+        if (KS == 1) {
+            if (bvalid) px = p.x + bm * p.xs + k0;
+        } else {
+            const int tap = k / kc, ch = k - tap * kc;
+            const int hi = bho * S - PAD + tap / KS, wi = bwo * S - PAD + tap % KS;
+            if (bvalid && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+                px = p.x + (((size_t)bn_ * p.H + hi) * p.W + wi) * p.xs + ch * 32;
         }
 #pragma unroll
-    for (int c = 0; c < 8; c++) acc[c] = act_f(acc[c] + sb[c], p.act);
-    *reinterpret_cast<uint4*>(p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + cg * 8) = pack8(acc);
+        for (int s0 = 0; s0 < B_SLOTS; s0 += 256) {
+            const int kg = bkg + s0 / BMP;
+            const void* src = px ? (const void*)(px + kg * 8) : (const void*)(p.zero + ((s0 + tid) & 1023) * 8);
+            glds16_det(src, base + (A_SLOTS + s0 + wave * 64) * 16);
+        }
+    };
+    f32x4 acc[4][WCT];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
+    if (nk > 1) {
+        issue(1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");  // step 0 landed, step 1 in flight
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    const int kg = lane >> 4, r16 = lane & 15;
+    int buf = 0;
+    for (int k = 0; k < nk; k++) {
+        // ring slot (k + 2) % 3 was last read in step k - 1, which every wave has finished
+        if (k + 2 < nk) issue(k + 2, buf == 0 ? 2 : buf - 1);
+        const uint8_t* base = lds + buf * STAGE;
+        bf16x8 a[WCT], b[4];
+#pragma unroll
+        for (int c = 0; c < WCT; c++)
+            a[c] = *reinterpret_cast<const bf16x8*>(base + (kg * BN + wc * (BN / 2) + c * 16 + r16) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            b[i] = *reinterpret_cast<const bf16x8*>(base + (A_SLOTS + kg * BMP + wp * 64 + i * 16 + r16) * 16);
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < WCT; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+        // step k + 1 must have landed; step k + 2 (if issued) may stay in flight.  A plain
+        // s_barrier (no release fence: __syncthreads would drain every DMA in flight)
+        if (k + 2 < nk)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        buf = buf == NBUF - 1 ? 0 : buf + 1;
+    }
+    // epilogue: lane holds couts (lane >> 4) * 4 + j of pixel (lane & 15) in each tile
+#pragma unroll
+    for (int c = 0; c < WCT; c++) {
+        const int co = co0 + wc * (BN / 2) + c * 16 + kg * 4;
+        if (co >= p.N) continue;
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const long m = m0 + wp * 64 + i * 16 + r16;
+            if (m >= p.M) continue;
+            float v[4] = {acc[i][c][0] + bb.x, acc[i][c][1] + bb.y, acc[i][c][2] + bb.z, acc[i][c][3] + bb.w};
+            if (p.act == 2)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+            if (p.res) {
+                const uint2 r = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                v[0] += bf(r.x & 0xffff), v[1] += bf(r.x >> 16), v[2] += bf(r.y & 0xffff), v[3] += bf(r.y >> 16);
+            }
+            if (p.act == 1)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+            *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
+                uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+        }
+    }
 }
 
 // ------------------------------------------------------------------ channel attention
@@ -581,12 +762,56 @@ void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t
 
 void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
                     int C, int act, hipStream_t s) {
-    MVP_REQUIRE(C % 8 == 0 && xs % 8 == 0 && ys % 8 == 0, "dw5: channels / strides must be multiples of 8");
-    DwParams p{x, y, w, b, H, W, C, xs, ys, act, (W + kDwTW - 1) / kDwTW, (H + kDwTH - 1) / kDwTH};
-    const long blocks = (long)p.tiles_w * p.tiles_h * (C / 8);
+    MVP_REQUIRE(C % 32 == 0 && xs % 8 == 0 && ys % 8 == 0, "dw5: channels must be a multiple of 32");
+    DwParams p{x, y, w, b, H, W, C, xs, ys, act, (W + kDwTW - 1) / kDwTW};
+    const int G = C % 64 == 0 ? 8 : 4;
+    const long blocks = (long)p.tiles_w * ((H + kDwTH - 1) / kDwTH) * (C / (8 * G));
     if (n == 0 || blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
-    hipLaunchKernelGGL(dw5_kernel, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
+    if (G == 8)
+        hipLaunchKernelGGL(dw5_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
+    else
+        hipLaunchKernelGGL(dw5_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
+                          uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
+                          hipStream_t s) {
+    MVP_REQUIRE(cin % 32 == 0 && N % 4 == 0 && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
+                "det conv: cin=%d cout=%d strides %d/%d", cin, N, xs, ys);
+    MVP_REQUIRE((ks == 1 && stride == 1) || (ks == 3 && (stride == 1 || stride == 2)), "det conv: ks %d stride %d", ks,
+                stride);
+    const int pad = ks / 2;
+    const int Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
+    const int npad = conv_cout_pad(N);
+    const int bn = npad % 128 == 0 ? 128 : npad % 192 == 0 ? 192 : 64;
+    GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
+              (npad + bn - 1) / bn, H, W, Ho, Wo};
+    const long blocks = (p.M + 127) / 128 * p.n_nb;
+    if (blocks == 0) return;
+    MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
+    const dim3 g((unsigned)blocks), t(256);
+#define MVP_DET_CONV_LAUNCH(BN, KS, S) hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S>), g, t, 0, s, p)
+    if (ks == 1 && bn == 128)
+        MVP_DET_CONV_LAUNCH(128, 1, 1);
+    else if (ks == 1 && bn == 192)
+        MVP_DET_CONV_LAUNCH(192, 1, 1);
+    else if (ks == 1)
+        MVP_DET_CONV_LAUNCH(64, 1, 1);
+    else if (stride == 1 && bn == 128)
+        MVP_DET_CONV_LAUNCH(128, 3, 1);
+    else if (stride == 1 && bn == 192)
+        MVP_DET_CONV_LAUNCH(192, 3, 1);
+    else if (stride == 1)
+        MVP_DET_CONV_LAUNCH(64, 3, 1);
+    else if (bn == 128)
+        MVP_DET_CONV_LAUNCH(128, 3, 2);
+    else if (bn == 192)
+        MVP_DET_CONV_LAUNCH(192, 3, 2);
+    else
+        MVP_DET_CONV_LAUNCH(64, 3, 2);
+#undef MVP_DET_CONV_LAUNCH
     MVP_HIP(hipGetLastError());
 }
 

@@ -4,6 +4,7 @@
 // network (CSP layers, SPP, the PAFPN's top-down / bottom-up joins, the head's cls/reg
 // pair) is a shared buffer its producers write into.
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "conv.h"
@@ -237,6 +238,19 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 break;
             case MVP_DET_CONV: {
                 const mvp_tensor_desc& x = T(op.in.t);
+                static const int gemm = [] {
+                    // A/B switch: 0 = the generic conv kernel for everything, 1 = GEMM for 1x1 only,
+                    // 2 (default) = GEMM for every conv
+                    const char* e = getenv("MVPOSE_DET_GEMM");
+                    return e ? atoi(e) : 2;
+                }();
+                if (gemm == 2 || (gemm == 1 && op.ks == 1)) {
+                    launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
+                                         op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
+                                         vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
+                                         op.act, s);
+                    break;
+                }
                 ConvLaunch c{};
                 c.x = vp(op.in);
                 c.x_stride = x.c;

@@ -10,12 +10,16 @@ MSRA decode, revert + heatmap moments, all HIP kernels in libmvpose.so).
   torch.load(weights_only=True); its 'state_dict' if present).  The reference's
   model_paths.yaml holds download URLs; there is no network here, so a URL or a
   missing file raises, unless MVPOSE_RANDOM_WEIGHTS=1 selects seeded random weights.
-* The person detector (RTMDet through mmdet's inference_detector, :234-241) is not
-  part of this package.  `detector=` takes any callable
+* The person detector (RTMDet-m through mmdet's inference_detector, :234-241) is
+  mvpose.rtmdet.RTMDetector (HIP, libmvpose): built from det_checkpoint when that is a
+  LOCAL mmdet checkpoint (.pth, weights_only load), or with seeded synthetic weights
+  under MVPOSE_RANDOM_DETECTOR=1.  `detector=` also takes any callable
   frame -> detections (M, 6) [x1, y1, x2, y2, score, label] (mmdet pred_instances'
-  bboxes | scores | labels); the reference's selection rule then applies (first box
-  with label == det_cat_id and score > bbox_thr, :242-250).  Without a detector —
-  or when no box passes — the crop is the whole image, the reference's own fallback.
+  bboxes | scores | labels).  The reference's selection rule then applies (first box
+  with label == det_cat_id and score > bbox_thr, :242-250); with an RTMDetector the
+  batched path takes it on the device (the per-frame argmax = the first detection after
+  NMS).  Without a detector — or when no box passes — the crop is the whole image, the
+  reference's own fallback.
 * device: the model runs on the GPU whatever is passed (the reference's default
   'cpu' is accepted); there is no CPU path.
 """
@@ -37,6 +41,19 @@ def select_person_bbox(detections, det_cat_id=0, bbox_thr=0.3):
     d = np.asarray(detections, dtype=np.float64).reshape(-1, 6)
     keep = d[(d[:, 5] == det_cat_id) & (d[:, 4] > bbox_thr)]
     return keep[0, :4].astype(np.float32) if len(keep) else None
+
+
+def build_detector(det_checkpoint, device="cuda", max_batch=64, seed=0):
+    """RTMDetector for the reference's det_checkpoint (model_paths.yaml's detectors entry): a
+    LOCAL mmdet RTMDet-m checkpoint (safe loader, its 'state_dict' if present), seeded
+    synthetic weights under MVPOSE_RANDOM_DETECTOR=1, else None (whole-image crops)."""
+    from .rtmdet import RTMDetector
+    if det_checkpoint and os.path.exists(str(det_checkpoint)):
+        blob = torch.load(det_checkpoint, map_location="cpu", weights_only=True)
+        return RTMDetector(blob.get("state_dict", blob), max_batch=max_batch, device=device)
+    if os.environ.get("MVPOSE_RANDOM_DETECTOR") == "1":
+        return RTMDetector(seed=seed, max_batch=max_batch, device=device)
+    return None
 
 
 def load_pose_checkpoint(pose_checkpoint):
@@ -67,6 +84,8 @@ class PoseEstimator:
         self.bbox_thr = bbox_thr
         self.nms_thr = nms_thr
         self.using_detector = using_detector
+        if detector is None and using_detector:
+            detector = build_detector(det_checkpoint, self.device)
         self.detector = detector if using_detector else None
         self._state_dict = state_dict if state_dict is not None else load_pose_checkpoint(pose_checkpoint)
         self._seed = seed
@@ -83,8 +102,20 @@ class PoseEstimator:
         return self._est
 
     def bboxes_for(self, frames):
-        """One xyxy box (or NaNs = whole image) per frame from the detector callable."""
+        """One xyxy box (or NaNs = whole image) per frame from the detector: batched on the
+        device for an RTMDetector (frames a CUDA tensor or numpy), else per frame."""
+        from .rtmdet import RTMDetector
+        if isinstance(self.detector, RTMDetector) and self.det_cat_id == 0:
+            f = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
+            f = f.to(self.device)
+            out = []
+            for i in range(0, f.shape[0], self.detector.max_batch):
+                best = self.detector.detect(f[i:i + self.detector.max_batch])["best"]
+                out.append(RTMDetector.bboxes_for(best, self.bbox_thr))
+            return np.concatenate(out) if out else np.full((0, 4), np.nan)
         out = np.full((len(frames), 4), np.nan)
+        if isinstance(frames, torch.Tensor):
+            frames = frames.cpu().numpy()
         if self.detector is not None:
             for i, f in enumerate(frames):
                 b = select_person_bbox(self.detector(f), self.det_cat_id, self.bbox_thr)
@@ -99,7 +130,7 @@ class PoseEstimator:
         f = f.to(self.device, non_blocking=True).contiguous()
         est = self.estimator(f.shape[1:3])
         if bboxes is None and self.detector is not None:
-            bboxes = self.bboxes_for(frames if not isinstance(frames, torch.Tensor) else frames.cpu().numpy())
+            bboxes = self.bboxes_for(f)
         return est.run(f, bboxes=bboxes, overlap_moments=overlap_moments)
 
     def predict(self, input_file, return_full_heatmaps=False):

@@ -23,9 +23,15 @@ from .hrnet import N_JOINTS
 
 class MultiViewPipeline:
     def __init__(self, camera_params, estimator: BatchPoseEstimator | None = None, camera_indices=(0, 1),
-                 mode: int = ops.TRI_REFERENCE, device="cuda", **estimator_kw):
+                 mode: int = ops.TRI_REFERENCE, device="cuda", detector=None, bbox_thr: float = 0.3,
+                 **estimator_kw):
         """camera_params: {camera key: [K, R, T, dist]} (utils.get_params_from_name order),
-        keys 0..V-1 as the reference assumes (pose_estimation.py:276-280)."""
+        keys 0..V-1 as the reference assumes (pose_estimation.py:276-280).
+        detector: an mvpose.rtmdet.RTMDetector run on every camera-frame before the crops
+        (PoseEstimator.predict, mmpose_pose_estimation.py:234-250: its first person box with
+        score > bbox_thr, else the whole image), or None (whole-image crops)."""
+        self.detector = detector
+        self.bbox_thr = bbox_thr
         self.device = torch.device(device)
         self.n_views = len(camera_params)
         self.cams = torch.tensor(ops.pack_cameras(camera_params), device=self.device)
@@ -49,7 +55,10 @@ class MultiViewPipeline:
         if "kpts_2d" not in out or tuple(out["kpts_2d"].shape) != (T, N_JOINTS, 3, V):
             out["kpts_2d"] = torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)
             out.pop("kpts_3d", None)
-        bb = None if bboxes is None else np.asarray(bboxes, np.float64).reshape(T * V, 4)
+        if bboxes is None and self.detector is not None:
+            bb = self.detect(flat)
+        else:
+            bb = None if bboxes is None else np.asarray(bboxes, np.float64).reshape(T * V, 4)
         r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments, bboxes=bb)
         out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
         if r["moments_done"] is not None:
@@ -59,6 +68,13 @@ class MultiViewPipeline:
         out["kpts_3d"] = ops.triangulate(out["kpts_2d"], self.cams, self.camera_indices, mode=self.mode,
                                          out=out.get("kpts_3d"))
         return out
+
+    def detect(self, flat: torch.Tensor) -> np.ndarray:
+        """(T*V, H, W, 3) camera-frames -> (T*V, 4) person boxes (NaN rows: whole image)."""
+        from .rtmdet import RTMDetector
+        mb = self.detector.max_batch
+        return np.concatenate([RTMDetector.bboxes_for(self.detector.detect(flat[i:i + mb])["best"], self.bbox_thr)
+                               for i in range(0, flat.shape[0], mb)])
 
     @staticmethod
     def wait(out: dict) -> None:

@@ -311,6 +311,7 @@ class DetSpec:
         out = View(self.tensor(h, ww, x.c), 0, x.c, x.cmap)
         ws = np.zeros((x.c, 25))
         ws[x.cmap] = w.reshape(w.shape[0], 25)
+        ws = ws.reshape(x.c // 8, 8, 25).transpose(0, 2, 1)  # [C/8][25 taps][8]: wave-uniform chunks
         bs = np.zeros(x.c)
         bs[x.cmap] = b
         self._op(name, DET_DW, x, out, ks=5, w_off=self._push_f(ws), b_off=self._push_f(bs))

@@ -57,7 +57,7 @@ def apply_op(spec: D.DetSpec, T: list, op, cand: torch.Tensor, device_weights: b
         put(op.out, y if op.act == D.ACT_SILU else _act(y, op.act))
     elif op.kind == D.DET_DW:
         c = op.in_.c
-        w = fb[op.w_off:op.w_off + c * 25].view(c, 1, 5, 5)
+        w = fb[op.w_off:op.w_off + c * 25].view(c // 8, 25, 8).permute(0, 2, 1).reshape(c, 1, 5, 5)
         b = fb[op.b_off:op.b_off + c]
         put(op.out, _act(F.conv2d(get(op.in_), w, b, padding=2, groups=c), op.act))
     elif op.kind == D.DET_CA:

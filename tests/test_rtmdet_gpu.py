@@ -185,3 +185,37 @@ def test_end_to_end_vs_fp32_oracle(sd, det640):
             agree += int(gi == int(t2.indices[0]))
     print(f"same prior {same}/{n}, decided {decided}, agree {agree}")
     assert agree == decided
+
+
+def test_pose_estimator_with_detector(det640):
+    """PoseEstimator(using_detector) crops each frame to the detector's person box: batched
+    (device argmax) and per-frame (NMS list + the reference's hand-off rule) agree, and
+    equal BatchPoseEstimator.run with those boxes."""
+    from mvpose import hrnet, synthetic as syn
+    from mvpose.mmpose_pose_estimation import PoseEstimator
+    from mvpose.pipeline import MultiViewPipeline
+    sd_pose = hrnet.random_state_dict(5)
+    pe = PoseEstimator(None, None, None, None, detector=det640, state_dict=sd_pose, max_frames=4)
+    frames = _frames(4, 720, 1280, seed=31)
+    out = pe.predict_batch(frames)
+    boxes = D.RTMDetector.bboxes_for(det640.detect(torch.from_numpy(frames).cuda())["best"])
+    assert np.isfinite(boxes).any()
+    ref = pe.estimator((720, 1280)).run(torch.from_numpy(frames).cuda(), bboxes=boxes)
+    assert torch.equal(out["keypoints"], ref["keypoints"])
+    # per-frame: the NMS list through the reference's selection = the batched box
+    for i in range(2):
+        dets = det640(frames[i])
+        from mvpose.mmpose_pose_estimation import select_person_bbox
+        b = select_person_bbox(dets)
+        if b is None:
+            assert np.isnan(boxes[i]).all()
+        else:
+            np.testing.assert_array_equal(b, boxes[i].astype(np.float32))
+    # the multi-view pipeline with the detector in front
+    cams = syn.make_rig(2, seed=3)
+    p = MultiViewPipeline(syn.reference_camera_params(cams), estimator=pe.estimator((720, 1280)), detector=det640)
+    fr = torch.from_numpy(frames).cuda().reshape(2, 2, 720, 1280, 3)
+    a = p.process(fr)
+    k2a = a["kpts_2d"].clone()
+    b = p.process(fr, bboxes=boxes.reshape(2, 2, 4))
+    assert torch.equal(k2a, b["kpts_2d"])
