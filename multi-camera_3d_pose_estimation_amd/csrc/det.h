@@ -21,7 +21,7 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
                           hipStream_t s);
-// channel attention in place; scratch: [n][C] f32
+// channel attention in place; scratch: [n][17][C] f32 (per-split partial sums + scales)
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
                    hipStream_t s);
 void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s);

@@ -11,6 +11,7 @@
 // write into their slice of the shared buffer).
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "conv.h"
 #include "det.h"
@@ -185,7 +186,7 @@ struct DwParams {
 };
 
 template <int G>
-__global__ __launch_bounds__(G * 64) void dw5_kernel(DwParams p) {
+__global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
     __shared__ uint4 sh[G][kDwHH * kDwHW];
     const int n_groups = p.C / (8 * G);
     const int grp = blockIdx.x % n_groups;
@@ -211,7 +212,9 @@ __global__ __launch_bounds__(G * 64) void dw5_kernel(DwParams p) {
     float a0[8], a1[8];
 #pragma unroll
     for (int c = 0; c < 8; c++) a0[c] = a1[c] = 0.f;
-#pragma unroll
+    // input rows one at a time (not unrolled): 8 unpacked values live, not 240, so the
+    // kernel fits 8 waves per SIMD and the next block's halo load hides under this one
+#pragma unroll 1
     for (int ir = 0; ir < 6; ir++) {
 #pragma unroll
         for (int kw = 0; kw < 5; kw++) {
@@ -224,6 +227,71 @@ __global__ __launch_bounds__(G * 64) void dw5_kernel(DwParams p) {
             if (ir >= 1) {
 #pragma unroll
                 for (int c = 0; c < 8; c++) a1[c] = fmaf(v[c], wc[((ir - 1) * 5 + kw) * 8 + c], a1[c]);
+            }
+        }
+    }
+    const int ho = th * kDwTH + 2 * rp, wo = tw * kDwTW + col;
+    if (wo >= p.W) return;
+    const float* bc = p.b + chunk * 8;
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        a0[c] = act_f(a0[c] + bc[c], p.act);
+        a1[c] = act_f(a1[c] + bc[c], p.act);
+    }
+    uint16_t* yb = p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + chunk * 8;
+    if (ho < p.H) *reinterpret_cast<uint4*>(yb) = pack8(a0);
+    if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(a1);
+}
+
+// Variant (MVPOSE_DET_DW=1): weights staged in LDS (wave-uniform broadcast reads), loop over
+// the kernel rows outside so each tap row's 40 weights are read once per lane.
+template <int G>
+__global__ __launch_bounds__(G * 64) void dw5b_kernel(DwParams p) {
+    __shared__ uint4 sh[G][kDwHH * kDwHW];
+    __shared__ float4 sw[G][25][2];
+    const int n_groups = p.C / (8 * G);
+    const int grp = blockIdx.x % n_groups;
+    const int t2 = blockIdx.x / n_groups;
+    const int tw = t2 % p.tiles_w, th = t2 / p.tiles_w;
+    const int n = blockIdx.y;
+    const int h0 = th * kDwTH - 2, w0 = tw * kDwTW - 2;
+    const int tid = threadIdx.x;
+    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs + grp * 8 * G;
+    for (int i = tid; i < kDwHH * kDwHW * G; i += G * 64) {
+        const int pix = i / G, q = i - pix * G;
+        const int r = pix / kDwHW, c = pix - r * kDwHW;
+        const int hi = h0 + r, wi = w0 + c;
+        sh[q][pix] = (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                         ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + q * 8)
+                         : uint4{0u, 0u, 0u, 0u};
+    }
+    for (int i = tid; i < G * 50; i += G * 64)
+        (&sw[0][0][0])[i] = reinterpret_cast<const float4*>(p.w + (size_t)grp * G * 200)[i];
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    const int col = lane & 15, rp = lane >> 4;
+    const int chunk = grp * G + wave;
+    float a0[8], a1[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) a0[c] = a1[c] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < 5; kh++) {
+        float w[5][8];
+#pragma unroll
+        for (int kw = 0; kw < 5; kw++) {
+            const float4 u = sw[wave][kh * 5 + kw][0], v = sw[wave][kh * 5 + kw][1];
+            w[kw][0] = u.x, w[kw][1] = u.y, w[kw][2] = u.z, w[kw][3] = u.w;
+            w[kw][4] = v.x, w[kw][5] = v.y, w[kw][6] = v.z, w[kw][7] = v.w;
+        }
+#pragma unroll
+        for (int o = 0; o < 2; o++) {
+#pragma unroll
+            for (int kw = 0; kw < 5; kw++) {
+                float v[8];
+                unpack8(sh[wave][(2 * rp + o + kh) * kDwHW + col + kw], v);
+                float* acc = o ? a1 : a0;
+#pragma unroll
+                for (int c = 0; c < 8; c++) acc[c] = fmaf(v[c], w[kw][c], acc[c]);
             }
         }
     }
@@ -401,26 +469,33 @@ __global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
 }
 
 // ------------------------------------------------------------------ channel attention
-// One workgroup per image: channel means over all pixels (f32, per-thread partial sums
-// then an LDS tree), then s = hardsigmoid(W·mean + b) with W^T [C][C] read coalesced.
+// Channel means: kCaSplit workgroups per image each sum a contiguous pixel range (f32
+// per-thread partial sums, then an LDS tree) into part[n][split][C]; then one workgroup per
+// image adds the splits in order (deterministic), divides by H*W and applies
+// s = hardsigmoid(W.mean + b) with W^T [C][C] read coalesced.
+constexpr int kCaSplit = 16;
+
 struct CaParams {
     const uint16_t* x;
     const float* wt;  // W^T [k][c]
     const float* b;
-    float* s;  // [n][C]
+    float* part;  // [n][kCaSplit][C]
+    float* s;     // [n][C]
     int HW, C, xs;
 };
 
-__global__ __launch_bounds__(256) void ca_pool_fc_kernel(CaParams p) {
-    extern __shared__ float red[];  // [rows][C] partial sums, then mean [C]
-    const int n = blockIdx.x, tid = threadIdx.x;
+__global__ __launch_bounds__(256) void ca_pool_kernel(CaParams p) {
+    extern __shared__ float red[];  // [rows][C]
+    const int n = blockIdx.y, sp = blockIdx.x, tid = threadIdx.x;
     const int Q = p.C / 8;
     const int rows = 256 / Q;  // pixel lanes per chunk
     const int q = tid % Q, r = tid / Q;
+    const int per = (p.HW + kCaSplit - 1) / kCaSplit;
+    const int px0 = sp * per, px1 = min(p.HW, px0 + per);
     const uint16_t* xb = p.x + (size_t)n * p.HW * p.xs + q * 8;
     if (r < rows) {
         float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int px = r; px < p.HW; px += rows) {
+        for (int px = px0 + r; px < px1; px += rows) {
             float v[8];
             unpack8(*reinterpret_cast<const uint4*>(xb + (size_t)px * p.xs), v);
 #pragma unroll
@@ -430,10 +505,19 @@ __global__ __launch_bounds__(256) void ca_pool_fc_kernel(CaParams p) {
         for (int c = 0; c < 8; c++) red[r * p.C + q * 8 + c] = acc[c];
     }
     __syncthreads();
-    float* mean = red + rows * p.C;
     for (int c = tid; c < p.C; c += 256) {
         float sum = 0.f;
         for (int i = 0; i < rows; i++) sum += red[i * p.C + c];
+        p.part[((size_t)n * kCaSplit + sp) * p.C + c] = sum;
+    }
+}
+
+__global__ __launch_bounds__(256) void ca_fc_kernel(CaParams p) {
+    extern __shared__ float mean[];  // [C]
+    const int n = blockIdx.x, tid = threadIdx.x;
+    for (int c = tid; c < p.C; c += 256) {
+        float sum = 0.f;
+        for (int i = 0; i < kCaSplit; i++) sum += p.part[((size_t)n * kCaSplit + i) * p.C + c];
         mean[c] = sum / (float)p.HW;
     }
     __syncthreads();
@@ -768,7 +852,15 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
     const long blocks = (long)p.tiles_w * ((H + kDwTH - 1) / kDwTH) * (C / (8 * G));
     if (n == 0 || blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
-    if (G == 8)
+    static const bool variant = [] {
+        const char* e = getenv("MVPOSE_DET_DW");  // A/B: 1 = LDS-staged weights
+        return e && e[0] == '1';
+    }();
+    if (variant && G == 8)
+        hipLaunchKernelGGL(dw5b_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
+    else if (variant)
+        hipLaunchKernelGGL(dw5b_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
+    else if (G == 8)
         hipLaunchKernelGGL(dw5_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
     else
         hipLaunchKernelGGL(dw5_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
@@ -819,15 +911,19 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
                    hipStream_t s) {
     MVP_REQUIRE(C % 8 == 0 && C / 8 <= 256 && xs % 8 == 0, "ca: C=%d", C);
     const int rows = 256 / (C / 8);
-    const size_t lds = ((size_t)rows * C + C) * sizeof(float);
+    const size_t lds = (size_t)rows * C * sizeof(float);
     MVP_REQUIRE(lds <= 64 * 1024, "ca: C=%d needs too much LDS", C);
     if (n == 0) return;
-    CaParams p{x, wt, b, scratch, HW, C, xs};
-    hipLaunchKernelGGL(ca_pool_fc_kernel, dim3((unsigned)n), dim3(256), lds, s, p);
+    float* part = scratch;                              // [n][kCaSplit][C]
+    float* sc = scratch + (size_t)n * kCaSplit * C;     // [n][C]
+    CaParams p{x, wt, b, part, sc, HW, C, xs};
+    hipLaunchKernelGGL(ca_pool_kernel, dim3(kCaSplit, (unsigned)n), dim3(256), lds, s, p);
+    MVP_HIP(hipGetLastError());
+    hipLaunchKernelGGL(ca_fc_kernel, dim3((unsigned)n), dim3(256), (size_t)C * sizeof(float), s, p);
     MVP_HIP(hipGetLastError());
     const long work = (long)HW * (C / 8);
-    hipLaunchKernelGGL(ca_scale_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, scratch,
-                       HW, C, xs);
+    hipLaunchKernelGGL(ca_scale_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, sc, HW,
+                       C, xs);
     MVP_HIP(hipGetLastError());
 }
 

@@ -205,7 +205,7 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
         if (e != hipSuccess)
             mvp::fail(MVP_ERR_NOMEM, "mvp_det_create: arena of %lld bytes: %s", (long long)g->arena_bytes,
                       hipGetErrorString(e));
-        MVP_HIP(hipMalloc(&g->ca_scratch, (size_t)max_batch * g->max_ca * sizeof(float)));
+        MVP_HIP(hipMalloc(&g->ca_scratch, (size_t)max_batch * 17 * g->max_ca * sizeof(float)));  // launch_det_ca scratch
     } catch (...) {
         if (g->arena) (void)hipFree(g->arena);
         delete g;
