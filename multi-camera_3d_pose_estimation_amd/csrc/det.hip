@@ -340,21 +340,44 @@ struct GParams {
     int H, W, Ho, Wo;
 };
 
-template <int BN, int KS, int S>
-__global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
-    constexpr int BMP = 128;              // pixels per tile
+// s_waitcnt vmcnt(n') for the largest level n' <= n (wave-uniform n): at most n' of this
+// wave's vector-memory operations stay outstanding (rounding down only waits longer)
+__device__ __forceinline__ void wait_vm(int n) {
+    if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+    else if (n >= 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else if (n >= 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else if (n >= 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else if (n >= 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (n >= 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (n >= 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if (n >= 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// PW waves along the pixels (64 each) x 2 along the couts: tile 64*PW pixels x BN couts.
+template <int BN, int KS, int S, int PW, int NBUF>
+__global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams p) {
+    constexpr int NT = 128 * PW;          // threads
+    constexpr int NWV = 2 * PW;           // waves
+    constexpr int BMP = 64 * PW;          // pixels per tile
     constexpr int A_SLOTS = 4 * BN;       // [kg][cout]
     constexpr int B_SLOTS = 4 * BMP;      // [kg][pix]
     constexpr int STAGE = (A_SLOTS + B_SLOTS) * 16;
     constexpr int WCT = BN / 32;          // cout tiles per wave
     constexpr int PAD = KS / 2;
-    constexpr int NBUF = 3;               // LDS ring: two K steps in flight under the MFMAs
-    constexpr int OPS = A_SLOTS / 256 + B_SLOTS / 256;  // DMA instructions per thread per K step
-    static_assert(A_SLOTS % 256 == 0, "A slots per thread");
+    constexpr int D = NBUF - 1;           // LDS ring: D K steps in flight under the MFMAs
+    constexpr int A_R64 = A_SLOTS / 64;   // 64-slot DMA rounds of the weight slice
+    static_assert(A_SLOTS % 64 == 0 && B_SLOTS % NT == 0, "slot rounds");
     __shared__ __attribute__((aligned(1024))) uint8_t lds[NBUF * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wp = wave & 1, wc = wave >> 1;  // pixel half, cout half
+    // DMA instructions this wave issues per K step: its weight rounds + the pixel rounds
+    const int ops = (A_R64 - wave + NWV - 1) / NWV + B_SLOTS / NT;
+    const int wp = wave % PW, wc = wave / PW;  // pixel quarter / half, cout half
     const long tile = blockIdx.x / p.n_nb;
     const int co0 = (int)(blockIdx.x - tile * p.n_nb) * BN;
     const long m0 = tile * BMP;
@@ -373,28 +396,44 @@ __global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
         bho = r / p.Wo;
         bwo = r - bho * p.Wo;
     }
+    // per-thread DMA sources fixed for the launch: the weight rows of this wave's rounds
+    // (advanced by 32 channels per K step), and the pixel's image base (the tap moves it)
+    constexpr int ARW = (A_R64 + NWV - 1) / NWV;
+    const uint16_t* asrc[ARW];
+#pragma unroll
+    for (int j = 0; j < ARW; j++) {
+        const int sl = (wave + j * NWV) * 64 + lane;
+        const int co = sl % BN, kg = sl / BN;
+        asrc[j] = (co0 + co < p.npad) ? p.w + (size_t)(co0 + co) * K + kg * 8 : nullptr;
+    }
+    const uint16_t* bimg = p.x + (size_t)bn_ * p.H * p.W * p.xs;
+    int it_ch = 0, it_kh = 0, it_kw = 0;  // (tap, chunk) of the next issued K step (issued in order)
     auto issue = [&](int k, int buf) {
         uint8_t* base = lds + buf * STAGE;
         const int k0 = k * 32;
 #pragma unroll
-        for (int s0 = 0; s0 < A_SLOTS; s0 += 256) {
-            const int sl = s0 + tid;
-            const int co = sl % BN, kg = sl / BN;
-            const void* src = (co0 + co < p.npad) ? (const void*)(p.w + (size_t)(co0 + co) * K + k0 + kg * 8)
-                                                  : (const void*)(p.zero + (sl & 1023) * 8);
-            glds16_det(src, base + (s0 + wave * 64) * 16);
+        for (int j = 0; j < ARW; j++) {
+            const int r = wave + j * NWV;
+            if (r < A_R64) {  // wave-uniform
+                const void* src = asrc[j] ? (const void*)(asrc[j] + k0)
+                                          : (const void*)(p.zero + ((r * 64 + lane) & 1023) * 8);
+                glds16_det(src, base + r * 64 * 16);
+            }
         }
         const uint16_t* px = nullptr;
         if (KS == 1) {
             if (bvalid) px = p.x + bm * p.xs + k0;
         } else {
-            const int tap = k / kc, ch = k - tap * kc;
-            const int hi = bho * S - PAD + tap / KS, wi = bwo * S - PAD + tap % KS;
+            const int hi = bho * S - PAD + it_kh, wi = bwo * S - PAD + it_kw;
             if (bvalid && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-                px = p.x + (((size_t)bn_ * p.H + hi) * p.W + wi) * p.xs + ch * 32;
+                px = bimg + ((size_t)hi * p.W + wi) * p.xs + it_ch * 32;
+            if (++it_ch == kc) {
+                it_ch = 0;
+                if (++it_kw == KS) it_kw = 0, it_kh++;
+            }
         }
 #pragma unroll
-        for (int s0 = 0; s0 < B_SLOTS; s0 += 256) {
+        for (int s0 = 0; s0 < B_SLOTS; s0 += NT) {
             const int kg = bkg + s0 / BMP;
             const void* src = px ? (const void*)(px + kg * 8) : (const void*)(p.zero + ((s0 + tid) & 1023) * 8);
             glds16_det(src, base + (A_SLOTS + s0 + wave * 64) * 16);
@@ -405,19 +444,14 @@ __global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
     for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    issue(0, 0);
-    if (nk > 1) {
-        issue(1, 1);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");  // step 0 landed, step 1 in flight
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    for (int j = 0; j < D && j < nk; j++) issue(j, j);
+    wait_vm(ops * (min(D, nk) - 1));  // step 0 landed, the others in flight
     __builtin_amdgcn_s_barrier();
     const int kg = lane >> 4, r16 = lane & 15;
     int buf = 0;
     for (int k = 0; k < nk; k++) {
-        // ring slot (k + 2) % 3 was last read in step k - 1, which every wave has finished
-        if (k + 2 < nk) issue(k + 2, buf == 0 ? 2 : buf - 1);
+        // ring slot (k + D) % NBUF was last read in step k - 1, which every wave has finished
+        if (k + D < nk) issue(k + D, buf == 0 ? NBUF - 1 : buf - 1);
         const uint8_t* base = lds + buf * STAGE;
         bf16x8 a[WCT], b[4];
 #pragma unroll
@@ -430,12 +464,9 @@ __global__ __launch_bounds__(256, 2) void det_conv_gemm_kernel(GParams p) {
         for (int i = 0; i < 4; i++)
 #pragma unroll
             for (int c = 0; c < WCT; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
-        // step k + 1 must have landed; step k + 2 (if issued) may stay in flight.  A plain
+        // step k + 1 must have landed; the steps issued after it may stay in flight.  A plain
         // s_barrier (no release fence: __syncthreads would drain every DMA in flight)
-        if (k + 2 < nk)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wait_vm(ops * max(0, min(k + D, nk - 1) - k - 1));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -884,7 +915,20 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
     const dim3 g((unsigned)blocks), t(256);
-#define MVP_DET_CONV_LAUNCH(BN, KS, S) hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S>), g, t, 0, s, p)
+    static const int nbuf = [] {
+        const char* e = getenv("MVPOSE_DET_NBUF");  // tuning: LDS ring depth 3, 4 or 5
+        const int v = e ? atoi(e) : 3;  // 3 measured best (4: +2 %, 5: +18 % time)
+        return v < 3 ? 3 : v > 5 ? 5 : v;
+    }();
+#define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                          \
+    do {                                                                                       \
+        if (nbuf == 3)                                                                         \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3>), g, t, 0, s, p);       \
+        else if (nbuf == 4)                                                                    \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 4>), g, t, 0, s, p);       \
+        else                                                                                   \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 5>), g, t, 0, s, p);       \
+    } while (0)
     if (ks == 1 && bn == 128)
         MVP_DET_CONV_LAUNCH(128, 1, 1);
     else if (ks == 1 && bn == 192)
