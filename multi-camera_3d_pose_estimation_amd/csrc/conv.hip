@@ -34,7 +34,7 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
     return __builtin_bit_cast(uint16_t, b);
 }
 
-__device__ __forceinline__ float silu(float v) { return v / (1.f + __expf(-v)); }
+__device__ __forceinline__ float silu(float v) { return v * __builtin_amdgcn_rcpf(1.f + __expf(-v)); }
 
 struct ConvParams {
     const uint16_t* __restrict__ x;

@@ -30,7 +30,7 @@ __device__ __forceinline__ uint32_t tobf(float f) {
 }
 __device__ __forceinline__ float act_f(float v, int act) {
     if (act == 1) return fmaxf(v, 0.f);
-    if (act == 2) return v / (1.f + __expf(-v));
+    if (act == 2) return v * __builtin_amdgcn_rcpf(1.f + __expf(-v));  // v_exp + v_rcp (1 ulp): output is bf16
     return v;
 }
 __device__ __forceinline__ void unpack8(uint4 u, float* f) {
