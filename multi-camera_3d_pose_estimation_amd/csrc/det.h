@@ -6,6 +6,9 @@
 
 namespace mvp {
 
+// Detector conv weights are padded to whole 32-cout rows ([det_cout_pad(cout)][kh][kw][cin]).
+inline int det_cout_pad(int cout) { return (cout + 31) / 32 * 32; }
+
 // mmcv rescale_size for scale (S, S), keep_ratio: the resized extent of an H x W frame.
 void det_rescale_size(int H, int W, int S, int& nh, int& nw);
 void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, const float* mean3, const float* std3,
@@ -16,7 +19,7 @@ void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t
 void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
                     int C, int act, hipStream_t s);
 // conv (1x1, or 3x3 stride 1 / 2, pad ks/2) as a GEMM over the flat output pixels with the
-// im2col gathered by DMA; w [cout_pad(N)][ks][ks][cin] bf16; act as ConvLaunch.relu (2 = SiLU
+// im2col gathered by DMA; w [det_cout_pad(N)][ks][ks][cin] bf16; act as ConvLaunch.relu (2 = SiLU
 // before the residual, 1 = ReLU after it)
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,

@@ -907,46 +907,35 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
                 stride);
     const int pad = ks / 2;
     const int Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
-    const int npad = conv_cout_pad(N);
-    const int bn = npad % 128 == 0 ? 128 : npad % 192 == 0 ? 192 : 64;
+    const int npad = det_cout_pad(N);
+    const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo};
     const long blocks = (p.M + 127) / 128 * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
     const dim3 g((unsigned)blocks), t(256);
-    static const int nbuf = [] {
-        const char* e = getenv("MVPOSE_DET_NBUF");  // tuning: LDS ring depth 3, 4 or 5
-        const int v = e ? atoi(e) : 3;  // 3 measured best (4: +2 %, 5: +18 % time)
-        return v < 3 ? 3 : v > 5 ? 5 : v;
-    }();
-#define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                          \
-    do {                                                                                       \
-        if (nbuf == 3)                                                                         \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3>), g, t, 0, s, p);       \
-        else if (nbuf == 4)                                                                    \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 4>), g, t, 0, s, p);       \
-        else                                                                                   \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 5>), g, t, 0, s, p);       \
+#define MVP_DET_CONV_LAUNCH(BN, KS, S) hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3>), g, t, 0, s, p)
+#define MVP_DET_CONV_BN(KS, S)              \
+    do {                                    \
+        if (bn == 192)                      \
+            MVP_DET_CONV_LAUNCH(192, KS, S); \
+        else if (bn == 128)                 \
+            MVP_DET_CONV_LAUNCH(128, KS, S); \
+        else if (bn == 96)                  \
+            MVP_DET_CONV_LAUNCH(96, KS, S);  \
+        else if (bn == 64)                  \
+            MVP_DET_CONV_LAUNCH(64, KS, S);  \
+        else                                \
+            MVP_DET_CONV_LAUNCH(32, KS, S);  \
     } while (0)
-    if (ks == 1 && bn == 128)
-        MVP_DET_CONV_LAUNCH(128, 1, 1);
-    else if (ks == 1 && bn == 192)
-        MVP_DET_CONV_LAUNCH(192, 1, 1);
-    else if (ks == 1)
-        MVP_DET_CONV_LAUNCH(64, 1, 1);
-    else if (stride == 1 && bn == 128)
-        MVP_DET_CONV_LAUNCH(128, 3, 1);
-    else if (stride == 1 && bn == 192)
-        MVP_DET_CONV_LAUNCH(192, 3, 1);
+    if (ks == 1)
+        MVP_DET_CONV_BN(1, 1);
     else if (stride == 1)
-        MVP_DET_CONV_LAUNCH(64, 3, 1);
-    else if (bn == 128)
-        MVP_DET_CONV_LAUNCH(128, 3, 2);
-    else if (bn == 192)
-        MVP_DET_CONV_LAUNCH(192, 3, 2);
+        MVP_DET_CONV_BN(3, 1);
     else
-        MVP_DET_CONV_LAUNCH(64, 3, 2);
+        MVP_DET_CONV_BN(3, 2);
+#undef MVP_DET_CONV_BN
 #undef MVP_DET_CONV_LAUNCH
     MVP_HIP(hipGetLastError());
 }

@@ -71,7 +71,7 @@ void validate(DetNet& g, int64_t w_elems, int64_t f_elems) {
                     const mvp_tensor_desc& r = view_ok(op.res, "res", k);
                     MVP_REQUIRE(r.h == y.h && r.w == y.w && op.res.c == op.out.c, "det conv %zu: residual shape", k);
                 }
-                const int64_t cp = conv_cout_pad(op.out.c);
+                const int64_t cp = det_cout_pad(op.out.c);
                 MVP_REQUIRE(op.w_off >= 0 && op.w_off % 8 == 0 && op.w_off + cp * op.ks * op.ks * op.in.c <= w_elems,
                             "det conv %zu: weights out of the bf16 blob", k);
                 f_ok(op.b_off, cp, k);
@@ -238,37 +238,10 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 break;
             case MVP_DET_CONV: {
                 const mvp_tensor_desc& x = T(op.in.t);
-                static const int gemm = [] {
-                    // A/B switch: 0 = the generic conv kernel for everything, 1 = GEMM for 1x1 only,
-                    // 2 (default) = GEMM for every conv
-                    const char* e = getenv("MVPOSE_DET_GEMM");
-                    return e ? atoi(e) : 2;
-                }();
-                if (gemm == 2 || (gemm == 1 && op.ks == 1)) {
-                    launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
-                                         op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
-                                         vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                         op.act, s);
-                    break;
-                }
-                ConvLaunch c{};
-                c.x = vp(op.in);
-                c.x_stride = x.c;
-                c.w = g->wb + op.w_off;
-                c.bias = g->fb + op.b_off;
-                c.res = op.res.t >= 0 ? vp(op.res) : nullptr;
-                c.r_stride = op.res.t >= 0 ? T(op.res.t).c : 0;
-                c.y = vp(op.out);
-                c.y_stride = T(op.out.t).c;
-                c.N = n;
-                c.H = x.h;
-                c.W = x.w;
-                c.Cin = op.in.c;
-                c.Cout = op.out.c;
-                c.ks = op.ks;
-                c.stride = op.stride;
-                c.relu = op.act;
-                launch_conv_generic(c, s);
+                launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
+                                     op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
+                                     vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
+                                     op.act, s);
                 break;
             }
             case MVP_DET_DW: {

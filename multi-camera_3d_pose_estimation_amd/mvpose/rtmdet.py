@@ -36,7 +36,7 @@ import torch
 
 from . import _lib
 from ._lib import call
-from .hrnet import TensorDesc, cout_pad, to_bf16_bits
+from .hrnet import TensorDesc, to_bf16_bits
 
 BN_EPS = 1e-5
 SIZE = 640
@@ -69,6 +69,9 @@ _lib.lib.mvp_det_arena_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.
 
 def pad32(c: int) -> int:
     return (c + 31) // 32 * 32
+
+
+cout_pad = pad32  # detector conv weights: [pad32(cout)][kh][kw][cin] (det_cout_pad in det.h)
 
 
 def rescale_size(h: int, w: int, size: int = SIZE):
