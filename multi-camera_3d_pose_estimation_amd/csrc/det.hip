@@ -359,14 +359,15 @@ __device__ __forceinline__ void wait_vm(int n) {
 }
 
 // PW waves along the pixels (64 each) x 2 along the couts: tile 64*PW pixels x BN couts.
-template <int BN, int KS, int S, int PW, int NBUF>
+template <int BN, int KS, int S, int PW, int NBUF, int CPS>
 __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams p) {
     constexpr int NT = 128 * PW;          // threads
     constexpr int NWV = 2 * PW;           // waves
     constexpr int BMP = 64 * PW;          // pixels per tile
     constexpr int A_SLOTS = 4 * BN;       // [kg][cout]
     constexpr int B_SLOTS = 4 * BMP;      // [kg][pix]
-    constexpr int STAGE = (A_SLOTS + B_SLOTS) * 16;
+    constexpr int SUB = (A_SLOTS + B_SLOTS) * 16;  // one 32-channel K chunk
+    constexpr int STAGE = CPS * SUB;      // CPS chunks per ring slot (per barrier)
     constexpr int WCT = BN / 32;          // cout tiles per wave
     constexpr int PAD = KS / 2;
     constexpr int D = NBUF - 1;           // LDS ring: D K steps in flight under the MFMAs
@@ -376,14 +377,15 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // DMA instructions this wave issues per K step: its weight rounds + the pixel rounds
-    const int ops = (A_R64 - wave + NWV - 1) / NWV + B_SLOTS / NT;
+    const int ops = CPS * ((A_R64 - wave + NWV - 1) / NWV + B_SLOTS / NT);
     const int wp = wave % PW, wc = wave / PW;  // pixel quarter / half, cout half
     const long tile = blockIdx.x / p.n_nb;
     const int co0 = (int)(blockIdx.x - tile * p.n_nb) * BN;
     const long m0 = tile * BMP;
     const int kc = p.cin / 32;            // chunks per tap
-    const int nk = KS * KS * kc;
-    const int K = nk * 32;
+    const int nq = KS * KS * kc;          // 32-channel K chunks
+    const int K = nq * 32;
+    const int nk = (nq + CPS - 1) / CPS;  // ring steps
     // this thread's B slots: pixel tid % 128, k groups tid / 128 and + 2
     const int bpx = tid % BMP, bkg = tid / BMP;
     const long bm = m0 + bpx;
@@ -408,22 +410,24 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
     }
     const uint16_t* bimg = p.x + (size_t)bn_ * p.H * p.W * p.xs;
     int it_ch = 0, it_kh = 0, it_kw = 0;  // (tap, chunk) of the next issued K step (issued in order)
-    auto issue = [&](int k, int buf) {
-        uint8_t* base = lds + buf * STAGE;
-        const int k0 = k * 32;
+    // one 32-channel chunk q into sub-slot `base`; chunks past the end DMA zeros (every step
+    // issues the same number of operations, which the vmcnt accounting relies on)
+    auto issue_chunk = [&](int q, uint8_t* base) {
+        const bool live = q < nq;
+        const int k0 = q * 32;
 #pragma unroll
         for (int j = 0; j < ARW; j++) {
             const int r = wave + j * NWV;
             if (r < A_R64) {  // wave-uniform
-                const void* src = asrc[j] ? (const void*)(asrc[j] + k0)
-                                          : (const void*)(p.zero + ((r * 64 + lane) & 1023) * 8);
+                const void* src = (live && asrc[j]) ? (const void*)(asrc[j] + k0)
+                                                    : (const void*)(p.zero + ((r * 64 + lane) & 1023) * 8);
                 glds16_det(src, base + r * 64 * 16);
             }
         }
         const uint16_t* px = nullptr;
         if (KS == 1) {
-            if (bvalid) px = p.x + bm * p.xs + k0;
-        } else {
+            if (bvalid && live) px = p.x + bm * p.xs + k0;
+        } else if (live) {
             const int hi = bho * S - PAD + it_kh, wi = bwo * S - PAD + it_kw;
             if (bvalid && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
                 px = bimg + ((size_t)hi * p.W + wi) * p.xs + it_ch * 32;
@@ -439,6 +443,10 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
             glds16_det(src, base + (A_SLOTS + s0 + wave * 64) * 16);
         }
     };
+    auto issue = [&](int k, int buf) {
+#pragma unroll
+        for (int c = 0; c < CPS; c++) issue_chunk(k * CPS + c, lds + buf * STAGE + c * SUB);
+    };
     f32x4 acc[4][WCT];
 #pragma unroll
     for (int i = 0; i < 4; i++)
@@ -452,18 +460,22 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
     for (int k = 0; k < nk; k++) {
         // ring slot (k + D) % NBUF was last read in step k - 1, which every wave has finished
         if (k + D < nk) issue(k + D, buf == 0 ? NBUF - 1 : buf - 1);
-        const uint8_t* base = lds + buf * STAGE;
-        bf16x8 a[WCT], b[4];
 #pragma unroll
-        for (int c = 0; c < WCT; c++)
-            a[c] = *reinterpret_cast<const bf16x8*>(base + (kg * BN + wc * (BN / 2) + c * 16 + r16) * 16);
+        for (int cc = 0; cc < CPS; cc++) {
+            const uint8_t* base = lds + buf * STAGE + cc * SUB;
+            bf16x8 a[WCT], b[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++)
-            b[i] = *reinterpret_cast<const bf16x8*>(base + (A_SLOTS + kg * BMP + wp * 64 + i * 16 + r16) * 16);
+            for (int c = 0; c < WCT; c++)
+                a[c] = *reinterpret_cast<const bf16x8*>(base + (kg * BN + wc * (BN / 2) + c * 16 + r16) * 16);
 #pragma unroll
-        for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 4; i++)
+                b[i] = *reinterpret_cast<const bf16x8*>(base + (A_SLOTS + kg * BMP + wp * 64 + i * 16 + r16) * 16);
 #pragma unroll
-            for (int c = 0; c < WCT; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < WCT; c++)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+        }
         // step k + 1 must have landed; the steps issued after it may stay in flight.  A plain
         // s_barrier (no release fence: __syncthreads would drain every DMA in flight)
         wait_vm(ops * max(0, min(k + D, nk - 1) - k - 1));
@@ -915,7 +927,17 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
     const dim3 g((unsigned)blocks), t(256);
-#define MVP_DET_CONV_LAUNCH(BN, KS, S) hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3>), g, t, 0, s, p)
+    static const int cps = [] {
+        const char* e = getenv("MVPOSE_DET_CPS");  // tuning: K chunks per barrier (1: 3-slot ring, 2: 2-slot)
+        return e && atoi(e) == 2 ? 2 : 1;
+    }();
+#define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                           \
+    do {                                                                                        \
+        if (cps == 2)                                                                           \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 2>), g, t, 0, s, p);     \
+        else                                                                                    \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3, 1>), g, t, 0, s, p);     \
+    } while (0)
 #define MVP_DET_CONV_BN(KS, S)              \
     do {                                    \
         if (bn == 192)                      \
