@@ -127,3 +127,57 @@ def test_postprocess_candidates_first_is_argmax():
     i = int(torch.argmax(sc))
     assert torch.equal(b[0], bx[i] * 2) and float(s[0]) == float(sc[i])
     assert len(s) <= 100 and bool((s[:-1] >= s[1:]).all())
+
+
+def _create(spec, ops=None, size=None, n_priors=None, w_elems=None):
+    """mvp_det_create on dummy (never dereferenced) weight pointers: the graph is validated
+    before any HIP call, so argument errors surface here on the CPU."""
+    import ctypes
+    from mvpose import _lib
+    from mvpose.hrnet import TensorDesc
+    ops = list(spec.ops) if ops is None else ops
+    tens = (TensorDesc * len(spec.tensors))(*[TensorDesc(*t) for t in spec.tensors])
+    arr = (D.DetOp * len(ops))(*ops)
+    w, f = spec.blobs()
+    h = ctypes.c_void_p()
+    return _lib.lib.mvp_det_create(tens, len(spec.tensors), arr, len(ops), 0, size or spec.size,
+                                   n_priors if n_priors is not None else spec.n_priors, ctypes.c_void_p(16),
+                                   w.size if w_elems is None else w_elems, ctypes.c_void_p(16), f.size, 4,
+                                   ctypes.byref(h)), h
+
+
+def test_det_create_rejects_malformed_graphs(sd):
+    import copy
+    from mvpose import _lib
+    spec, _ = D.build_rtmdet_m(sd, 128)
+    k = next(i for i, op in enumerate(spec.ops) if op.kind == D.DET_CONV and op.ks == 3 and op.in_.c >= 64)
+    bad = copy.deepcopy(list(spec.ops))
+    bad[k].in_.c = 48  # a valid view, but cin not a multiple of 32
+    rc, _ = _create(spec, bad)
+    assert rc == -1 and "multiple of 32" in _lib.last_error()
+    bad = copy.deepcopy(list(spec.ops))
+    bad[k].out = bad[k].in_  # a conv writing its own input tensor
+    rc, _ = _create(spec, bad)
+    assert rc == -1
+    rc, _ = _create(spec, n_priors=spec.n_priors + 1)  # head rows do not cover n_priors
+    assert rc == -1 and "priors" in _lib.last_error()
+    rc, _ = _create(spec, w_elems=1000)  # weights outside the blob
+    assert rc == -1 and "blob" in _lib.last_error()
+    rc, _ = _create(spec, size=100)
+    assert rc == -1 and "multiple of 32" in _lib.last_error()
+    bad = copy.deepcopy(list(spec.ops))
+    bad[0].kind = 42
+    rc, _ = _create(spec, bad)
+    assert rc == -1 and "unknown kind" in _lib.last_error()
+
+
+def test_det_nms_rejects_bad_levels():
+    import ctypes
+    from mvpose import _lib
+    offs = (ctypes.c_int * 4)(0, 6400, 8000, 8400)
+    # level offsets must start at 0 and end at n_priors; nms_pre <= 1024
+    assert _lib.lib.mvp_det_nms(None, 1, 8000, offs, 3, 1000, 0.05, 0.6, 100, 2.0, 2.0, None, None, None) == -1
+    assert _lib.lib.mvp_det_nms(None, 1, 8400, offs, 3, 2000, 0.05, 0.6, 100, 2.0, 2.0, None, None, None) == -1
+    big = (ctypes.c_int * 2)(0, 9000)
+    assert _lib.lib.mvp_det_nms(None, 1, 9000, big, 1, 1000, 0.05, 0.6, 100, 2.0, 2.0, None, None, None) == -1
+    assert _lib.lib.mvp_det_nms(None, 0, 8400, offs, 3, 1000, 0.05, 0.6, 100, 2.0, 2.0, None, None, None) == 0

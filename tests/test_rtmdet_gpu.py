@@ -130,6 +130,7 @@ def test_select_none_below_score_thr(det640):
         torch.cuda.synchronize()
         assert (out["best"][:, 4] == -1).all()
         assert np.isnan(D.RTMDetector.bboxes_for(out["best"])).all()
+        assert all(len(d) == 0 for d in det640.nms(out))  # NMS over no survivors: empty lists
     finally:
         det640.cfg["score_thr"] = D.TEST_CFG["score_thr"]
 
