@@ -386,29 +386,45 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
     const int nq = KS * KS * kc;          // 32-channel K chunks
     const int K = nq * 32;
     const int nk = (nq + CPS - 1) / CPS;  // ring steps
-    // this thread's B slots: pixel tid % 128, k groups tid / 128 and + 2
-    const int bpx = tid % BMP, bkg = tid / BMP;
-    const long bm = m0 + bpx;
-    const bool bvalid = bm < p.M;
-    int bn_ = 0, bho = 0, bwo = 0;
-    if (KS > 1 && bvalid) {
-        const long hw = (long)p.Ho * p.Wo;
-        bn_ = (int)(bm / hw);
-        const int r = (int)(bm - (long)bn_ * hw);
-        bho = r / p.Wo;
-        bwo = r - bho * p.Wo;
+    // LDS images are row-major with a swizzle: row r (a cout of A, a pixel of B) keeps its
+    // four 16-B K chunks (32 channels) in slots 4r .. 4r+3, chunk kg at 4r + (kg ^ swz(r)),
+    // swz(r) = -(r >> 2) & 3.  A DMA instruction then reads 16 rows x 64 contiguous bytes
+    // (4 lanes per row) instead of 64 rows x 16 B: a quarter of the cache lines per
+    // instruction.  The swizzle keeps the 16-lane fragment reads (16 rows, one chunk)
+    // conflict-free in every ds_read_b128 lane group.
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    constexpr int BR = B_SLOTS / NT;  // pixel rounds per thread (2)
+    long bm[BR];
+    bool bvalid[BR];
+    int bkg[BR], bn_[BR], bho[BR], bwo[BR];
+#pragma unroll
+    for (int j = 0; j < BR; j++) {
+        const int slot = j * NT + tid, row = slot >> 2;
+        bkg[j] = (slot & 3) ^ swz(row);
+        bm[j] = m0 + row;
+        bvalid[j] = bm[j] < p.M;
+        bn_[j] = bho[j] = bwo[j] = 0;
+        if (KS > 1 && bvalid[j]) {
+            const long hw = (long)p.Ho * p.Wo;
+            bn_[j] = (int)(bm[j] / hw);
+            const int r = (int)(bm[j] - (long)bn_[j] * hw);
+            bho[j] = r / p.Wo;
+            bwo[j] = r - bho[j] * p.Wo;
+        }
     }
     // per-thread DMA sources fixed for the launch: the weight rows of this wave's rounds
-    // (advanced by 32 channels per K step), and the pixel's image base (the tap moves it)
+    // (advanced by 32 channels per K step), and each pixel's image base (the tap moves it)
     constexpr int ARW = (A_R64 + NWV - 1) / NWV;
     const uint16_t* asrc[ARW];
 #pragma unroll
     for (int j = 0; j < ARW; j++) {
         const int sl = (wave + j * NWV) * 64 + lane;
-        const int co = sl % BN, kg = sl / BN;
+        const int co = sl >> 2, kg = (sl & 3) ^ swz(co);
         asrc[j] = (co0 + co < p.npad) ? p.w + (size_t)(co0 + co) * K + kg * 8 : nullptr;
     }
-    const uint16_t* bimg = p.x + (size_t)bn_ * p.H * p.W * p.xs;
+    const uint16_t* bimg[BR];
+#pragma unroll
+    for (int j = 0; j < BR; j++) bimg[j] = p.x + (size_t)bn_[j] * p.H * p.W * p.xs;
     int it_ch = 0, it_kh = 0, it_kw = 0;  // (tap, chunk) of the next issued K step (issued in order)
     // one 32-channel chunk q into sub-slot `base`; chunks past the end DMA zeros (every step
     // issues the same number of operations, which the vmcnt accounting relies on)
@@ -424,23 +440,27 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
                 glds16_det(src, base + r * 64 * 16);
             }
         }
-        const uint16_t* px = nullptr;
-        if (KS == 1) {
-            if (bvalid && live) px = p.x + bm * p.xs + k0;
-        } else if (live) {
-            const int hi = bho * S - PAD + it_kh, wi = bwo * S - PAD + it_kw;
-            if (bvalid && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-                px = bimg + ((size_t)hi * p.W + wi) * p.xs + it_ch * 32;
-            if (++it_ch == kc) {
+        int hoff = 0, woff = 0, coff = 0;
+        if (KS > 1) {
+            hoff = it_kh - PAD, woff = it_kw - PAD, coff = it_ch * 32;
+            if (live && ++it_ch == kc) {
                 it_ch = 0;
                 if (++it_kw == KS) it_kw = 0, it_kh++;
             }
         }
 #pragma unroll
-        for (int s0 = 0; s0 < B_SLOTS; s0 += NT) {
-            const int kg = bkg + s0 / BMP;
-            const void* src = px ? (const void*)(px + kg * 8) : (const void*)(p.zero + ((s0 + tid) & 1023) * 8);
-            glds16_det(src, base + (A_SLOTS + s0 + wave * 64) * 16);
+        for (int j = 0; j < BR; j++) {
+            const uint16_t* px = nullptr;
+            if (KS == 1) {
+                if (bvalid[j] && live) px = p.x + bm[j] * p.xs + k0;
+            } else if (live) {
+                const int hi = bho[j] * S + hoff, wi = bwo[j] * S + woff;
+                if (bvalid[j] && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+                    px = bimg[j] + ((size_t)hi * p.W + wi) * p.xs + coff;
+            }
+            const void* src = px ? (const void*)(px + bkg[j] * 8)
+                                 : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
+            glds16_det(src, base + (A_SLOTS + j * NT + wave * 64) * 16);
         }
     };
     auto issue = [&](int k, int buf) {
@@ -456,6 +476,7 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
     wait_vm(ops * (min(D, nk) - 1));  // step 0 landed, the others in flight
     __builtin_amdgcn_s_barrier();
     const int kg = lane >> 4, r16 = lane & 15;
+    const int soff = r16 * 64 + ((kg ^ ((-(r16 >> 2)) & 3)) * 16);  // this lane's (row, chunk) in a 16-row block
     int buf = 0;
     for (int k = 0; k < nk; k++) {
         // ring slot (k + D) % NBUF was last read in step k - 1, which every wave has finished
@@ -466,10 +487,10 @@ __global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams
             bf16x8 a[WCT], b[4];
 #pragma unroll
             for (int c = 0; c < WCT; c++)
-                a[c] = *reinterpret_cast<const bf16x8*>(base + (kg * BN + wc * (BN / 2) + c * 16 + r16) * 16);
+                a[c] = *reinterpret_cast<const bf16x8*>(base + (wc * (BN / 2) + c * 16) * 64 + soff);
 #pragma unroll
             for (int i = 0; i < 4; i++)
-                b[i] = *reinterpret_cast<const bf16x8*>(base + (A_SLOTS + kg * BMP + wp * 64 + i * 16 + r16) * 16);
+                b[i] = *reinterpret_cast<const bf16x8*>(base + A_SLOTS * 16 + (wp * 64 + i * 16) * 64 + soff);
 #pragma unroll
             for (int i = 0; i < 4; i++)
 #pragma unroll
