@@ -47,7 +47,7 @@ using namespace mfma_tile;
 constexpr int kZeroSlots = 4096;  // 16-B slots of the shared zero region
 
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM_ = 64>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM_ = 64, bool PM_ = false>
 struct TCfg {
     static constexpr int NW = 8, NT_THREADS = NW * 64;
     static constexpr int BM = BM_, MG = BM / 32, PG = NW / MG;  // cout groups x pixel groups
@@ -55,8 +55,15 @@ struct TCfg {
     static constexpr int P = NB * TH * W;                        // output pixels per tile
     static constexpr int NCH = CIN / 32;                         // items per tile
     static constexpr int RS = W + 1, HR = TH + 2;                // halo row pitch (slots), rows
-    static constexpr int HS = 1 + NB * HR * RS;                  // slots per 8-channel plane
-    static constexpr int HT = 4 * HS;                            // halo slots per chunk
+    // PM (pixel-major halo): a halo pixel's four 16-B planes are slots 5p .. 5p+3 (5p+4 is a
+    // never-read pad), so a DMA instruction reads ~13 pixels x 64 contiguous bytes instead
+    // of 64 pixels x 16 B (a quarter of the cache lines); the 80-B pixel pitch keeps 16
+    // consecutive pixels' fragment reads on distinct banks.  Plane-major otherwise.
+    static constexpr bool PM = PM_;
+    static constexpr int HS = 1 + NB * HR * RS;                  // halo pixels (incl. the leading zero)
+    static constexpr int HT = PM ? 5 * HS : 4 * HS;              // halo slots per chunk
+    static constexpr int QSTRIDE = PM ? 1 : HS;                  // slots between planes of a pixel
+    static constexpr int PSTRIDE = PM ? 5 : 1;                   // slots between pixels
     static constexpr int WT = 9 * 4 * BM;                        // weight slots per chunk
     static constexpr int ITEM_SLOTS = HT + (WRES ? 0 : WT);
     static constexpr int PPW = (ITEM_SLOTS + 64 * NW - 1) / (64 * NW);  // 1-KiB DMA pieces per wave per item
@@ -67,8 +74,8 @@ struct TCfg {
     static constexpr int STORES = 2 * NT;                        // epilogue stores per wave per tile
     static_assert(P == PG * NT * 32, "tile = pixel groups x 3 fragments x 32 pixels");
     static_assert(H % TH == 0 && CIN % 32 == 0, "tiling");
-    static_assert(LDS <= 160 * 1024, "LDS budget");
-    static_assert((2 * HS + 2 * RS + 2) * 16 < 65536 && (36 * BM) * 16 < 65536, "ds_read offset range");
+    static_assert((2 * QSTRIDE + (2 * RS + 2) * PSTRIDE) * 16 < 65536 && (36 * BM) * 16 < 65536,
+                  "ds_read offset range");
     static_assert(STORES + 2 * NT < 64 && PPW < 64, "vmcnt range");
 };
 
@@ -84,9 +91,9 @@ struct TParams {
     int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 2 = no stores
 };
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM, bool PM>
 __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
-    using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
+    using G = TCfg<CIN, H, W, TH, NB, WRES, BM, PM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -110,8 +117,8 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
         const int s = (j * G::NW + wave) * 64 + lane;  // slot within the ring slot
         int kind = 0, off = 0, nb = 0, hy = 0;
         if (s < G::HT) {
-            const int q = s / G::HS, hs = s - (s / G::HS) * G::HS;
-            if (hs > 0) {
+            const int q = PM ? s % 5 : s / G::HS, hs = PM ? s / 5 : s - (s / G::HS) * G::HS;
+            if (hs > 0 && q < 4) {
                 const int t = hs - 1;
                 nb = t / (G::HR * G::RS);
                 const int rr = t - nb * (G::HR * G::RS);
@@ -160,7 +167,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
         const int pp = frag_pixel<W, TH, NB>(pg * G::NT + t, r32);
         const int nb = pp / (TH * W), rem = pp - nb * (TH * W);
         const int ty = rem / W, x = rem - (rem / W) * W;
-        bv[t] = (h * G::HS + nb * G::HR * G::RS + ty * G::RS + x) * 16;
+        bv[t] = (h * G::QSTRIDE + (nb * G::HR * G::RS + ty * G::RS + x) * G::PSTRIDE) * 16;
         eoff[t] = (nb * H + ty) * W + x;  // output pixel from the tile's (n0, ho0, 0)
         enb[t] = nb;
     }
@@ -254,7 +261,8 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
             a = *reinterpret_cast<const bf16x8*>(lds + ava + (tap * 4 + ks * 2) * G::BM * 16);
 #pragma unroll
             for (int t = 0; t < G::NT; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] + (ks * 2 * G::HS + dy * G::RS + dx) * 16);
+                b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] +
+                                                        (ks * 2 * G::QSTRIDE + (dy * G::RS + dx) * G::PSTRIDE) * 16);
         };
 #pragma unroll
         for (int s0 = 0; s0 < LD; s0++) load(s0, fa[s0], fb[s0]);
@@ -298,10 +306,11 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
 int g_t_cus = 0;
 uint16_t* g_t_sink = nullptr;
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM, bool PM>
 void launch_t_kernel(const TParams& p, hipStream_t s) {
-    using G = TCfg<CIN, H, W, TH, NB, WRES, BM>;
-    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM>;
+    using G = TCfg<CIN, H, W, TH, NB, WRES, BM, PM>;
+    static_assert(G::LDS <= 160 * 1024, "LDS budget");
+    auto kern = tconv_kernel<CIN, H, W, TH, NB, WRES, RES, BM, PM>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -327,10 +336,25 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
     const char* dg = getenv("MVPOSE_TCONV_DIAG");
     TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM,
               dg ? atoi(dg) : 0};
+    // pixel-major halo for the resident-weight planes (streamed weights leave no LDS for it)
+    static const bool pm_env = [] {
+        const char* e = getenv("MVPOSE_TCONV_PM");  // A/B: 0 = plane-major halo everywhere
+        return !(e && e[0] == '0');
+    }();
+    constexpr bool PM_OK = WRES && TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
+    if constexpr (PM_OK) {
+        if (pm_env) {
+            if (c.res)
+                launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM, true>(p, s);
+            else
+                launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM, true>(p, s);
+            return;
+        }
+    }
     if (c.res)
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM, false>(p, s);
     else
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM, false>(p, s);
 }
 
 }  // namespace
