@@ -336,12 +336,12 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
     const char* dg = getenv("MVPOSE_TCONV_DIAG");
     TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM,
               dg ? atoi(dg) : 0};
-    // pixel-major halo for the resident-weight planes (streamed weights leave no LDS for it)
+    // pixel-major halo wherever its 25 % larger ring slot still fits the LDS
     static const bool pm_env = [] {
         const char* e = getenv("MVPOSE_TCONV_PM");  // A/B: 0 = plane-major halo everywhere
         return !(e && e[0] == '0');
     }();
-    constexpr bool PM_OK = WRES && TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
+    constexpr bool PM_OK = TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
     if constexpr (PM_OK) {
         if (pm_env) {
             if (c.res)
