@@ -30,13 +30,20 @@ using namespace mfma_tile;
 
 constexpr int kZeroSlots = 4096;
 
-struct T1 {
+template <bool PM_>
+struct T1C {
     static constexpr int H = 64, W = 48, C = 256, TH = 16;
     static constexpr int NW = 8, NTH = NW * 64;
     static constexpr int NCH = C / 16;                     // 16-channel items per tile
-    static constexpr int RS = W + 1, HR = TH + 2;          // halo row pitch (slots), rows
-    static constexpr int HS = 1 + HR * RS;                 // slots per 8-channel plane
-    static constexpr int WA = 2 * HS;                      // t0 weight slots [9][2][32]
+    static constexpr int RS = W + 1, HR = TH + 2;          // halo row pitch (pixels), rows
+    static constexpr int HS = 1 + HR * RS;                 // halo pixels (incl. the leading zero)
+    // PM (pixel-major halo): a pixel's two 16-B planes are slots 3p, 3p+1 (3p+2 a never-read
+    // pad): a DMA instruction reads ~21 pixels x 32 contiguous bytes instead of 64 pixels x
+    // 16 B (a third of the cache lines); the 48-B pixel pitch keeps 16 consecutive pixels'
+    // fragment reads on distinct banks.  Plane-major otherwise.
+    static constexpr bool PM = PM_;
+    static constexpr int QS = PM ? 1 : HS, PS = PM ? 3 : 1;  // slots between planes / pixels
+    static constexpr int WA = (PM ? 3 : 2) * HS;           // t0 weight slots [9][2][32]
     static constexpr int WB = WA + 9 * 2 * 32;             // t1 weight slots [9][2][64]
     static constexpr int ITEM = WB + 9 * 2 * 64;           // slots per item
     static constexpr int PPW = (ITEM + 64 * NW - 1) / (64 * NW);  // 1-KiB DMA pieces per wave per item
@@ -65,8 +72,9 @@ struct TrParams {
     int N, n_tiles;
 };
 
+template <bool PM>
 __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
-    using G = T1;
+    using G = T1C<PM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -84,8 +92,8 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
         const int s = (j * G::NW + wave) * 64 + lane;
         int kind = 0, off = 0, hy = 0;
         if (s < G::WA) {
-            const int q = s / G::HS, hs = s - q * G::HS;
-            if (hs > 0) {
+            const int q = PM ? s % 3 : s / G::HS, hs = PM ? s / 3 : s - q * G::HS;
+            if (hs > 0 && q < 2) {
                 const int t = hs - 1, yy = t / G::RS, xx = t - yy * G::RS;
                 if (xx < G::W) {
                     kind = 1;
@@ -127,12 +135,12 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
             const int f = (i < G::NF0) ? wave * G::NF0 + i : 0;
             const int pp = frag_pixel<G::W, G::TH, 1>(f, r32);
             const int ty = pp / G::W, x = pp - ty * G::W;
-            bv[i] = (h * G::HS + ty * G::RS + x) * 16;   // tap (0,0) of output (ty, x): slot 1 + (ty-1+1)*RS + x-1
+            bv[i] = (h * G::QS + (ty * G::RS + x) * G::PS) * 16;  // tap (0,0) of (ty, x): pixel 1 + (ty-1+1)*RS + x-1
             eo[i] = ty * G::W + x;
         } else {
             const int pp = i * 32 + r32;                 // t1: 8 rows x 24 columns, generic order
             const int ro = pp / G::W1, c = pp - ro * G::W1;
-            bv[i] = (h * G::HS + 2 * ro * G::RS + 2 * c) * 16;  // y (2ro - 1, 2c - 1): slot 1 + 2ro*RS + 2c - 1
+            bv[i] = (h * G::QS + (2 * ro * G::RS + 2 * c) * G::PS) * 16;  // y (2ro-1, 2c-1): pixel 1 + 2ro*RS + 2c - 1
             eo[i] = ro * G::W1 + c;
         }
     }
@@ -191,7 +199,7 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
                 a = *reinterpret_cast<const bf16x8*>(lds + boff + av + tap * AST);
 #pragma unroll
                 for (int t = 0; t < NF; t++)
-                    b[t] = *reinterpret_cast<const bf16x8*>(lds + boff + bv[t] + (dy * G::RS + dx) * 16);
+                    b[t] = *reinterpret_cast<const bf16x8*>(lds + boff + bv[t] + (dy * G::RS + dx) * G::PS * 16);
             };
             load(0, fa[0], fb[0]);
 #pragma unroll
@@ -233,7 +241,7 @@ int g_tr_cus = 0;
 bool trans1_supported(int H, int W, int C, int cout0, int cout1) {
     const char* e = getenv("MVPOSE_NO_TRANSFUSE");  // diagnostics/tests: the two convs apart
     if (e && e[0] == '1') return false;
-    return H == T1::H && W == T1::W && C == T1::C && cout0 == 32 && cout1 == 64;
+    return H == T1C<true>::H && W == T1C<true>::W && C == T1C<true>::C && cout0 == 32 && cout1 == 64;
 }
 
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
@@ -243,7 +251,10 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     if (N == 0) return;
     static bool attr = false;
     if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)trans1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, T1::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)trans1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    T1C<true>::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)trans1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    T1C<false>::LDS));
         attr = true;
     }
     if (g_tr_cus == 0) {
@@ -251,11 +262,18 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
         MVP_HIP(hipGetDevice(&dev));
         MVP_HIP(hipDeviceGetAttribute(&g_tr_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const long tiles = (long)N * (T1::H / T1::TH);
-    MVP_REQUIRE(tiles * T1::NCH < (1L << 30), "trans1: too many tiles");
+    const long tiles = (long)N * (T1C<true>::H / T1C<true>::TH);
+    MVP_REQUIRE(tiles * T1C<true>::NCH < (1L << 30), "trans1: too many tiles");
     TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles};
     const int grid = (int)std::min<long>(tiles, g_tr_cus);
-    hipLaunchKernelGGL(trans1_kernel, dim3(grid), dim3(T1::NTH), T1::LDS, s, p);
+    static const bool pm = [] {
+        const char* e = getenv("MVPOSE_TRANS1_PM");  // A/B: 0 = plane-major halo
+        return !(e && e[0] == '0');
+    }();
+    if (pm)
+        hipLaunchKernelGGL(trans1_kernel<true>, dim3(grid), dim3(T1C<true>::NTH), T1C<true>::LDS, s, p);
+    else
+        hipLaunchKernelGGL(trans1_kernel<false>, dim3(grid), dim3(T1C<false>::NTH), T1C<false>::LDS, s, p);
     MVP_HIP(hipGetLastError());
 }
 
