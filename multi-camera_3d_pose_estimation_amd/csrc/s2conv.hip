@@ -39,7 +39,7 @@ using namespace mfma_tile;
 
 constexpr int kZeroSlots = 4096;  // 16-B slots of the shared zero region
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM, bool PM_ = false>
 struct SCfg {
     static constexpr int NW = 8, NT_THREADS = NW * 64;
     static constexpr int MG = BM / 32, PG = NW / MG;  // cout groups x pixel groups
@@ -49,8 +49,13 @@ struct SCfg {
     static constexpr int NCH = CIN / 16;              // items per tile
     static constexpr int RS = WO + 1, HR = TH + 1;    // phase-plane row pitch (slots), rows
     static constexpr int PH = HR * RS;                // slots per phase plane
-    static constexpr int HS = NB * 4 * PH;            // slots per 8-channel plane
+    static constexpr int HS = NB * 4 * PH;            // halo pixels per item
     static constexpr int HT = 2 * HS;                 // halo slots per item
+    // PM (pixel-major halo): a pixel's two 16-B planes are adjacent slots (32 B contiguous per
+    // pixel in a DMA instruction, half the cache lines of plane-major) at the price of 2-way
+    // bank conflicts on the fragment reads (16 pixels x 32 B pitch); plane-major otherwise.
+    static constexpr bool PM = PM_;
+    static constexpr int QS = PM ? 1 : HS, PS = PM ? 2 : 1;  // slots between planes / pixels
     static constexpr int WT = 9 * 2 * BM;             // weight slots per item
     static constexpr int ITEM_SLOTS = HT + (WRES ? 0 : WT);
     static constexpr int PPW = (ITEM_SLOTS + 64 * NW - 1) / (64 * NW);  // 1-KiB DMA pieces per wave per item
@@ -62,7 +67,8 @@ struct SCfg {
     static_assert(P == PG * NT * 32, "tile = pixel groups x 3 fragments x 32 pixels");
     static_assert(H % 2 == 0 && W % 2 == 0 && HO % TH == 0 && CIN % 16 == 0, "tiling");
     static_assert(LDS <= 160 * 1024, "LDS budget");
-    static_assert((HS + 3 * PH + RS + 1) * 16 < 65536 && (16 * BM + 2 * BM) * 16 < 65536, "ds_read offset range");
+    static_assert((QS + (3 * PH + RS + 1) * PS) * 16 < 65536 && (16 * BM + 2 * BM) * 16 < 65536,
+                  "ds_read offset range");
     static_assert(STORES < 64 && PPW < 64, "vmcnt range");
     static_assert(2 * TH + 1 < 256, "row index packing");
 };
@@ -82,9 +88,9 @@ struct SParams {
     int c1, c2, relu1, relu2;
 };
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM, bool PM>
 __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
-    using G = SCfg<CIN, H, W, TH, NB, WRES, BM>;
+    using G = SCfg<CIN, H, W, TH, NB, WRES, BM, PM>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -108,7 +114,7 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
         const int s = (j * G::NW + wave) * 64 + lane;
         int kind = 0, off = 0, nb = 0, hy = 0;
         if (s < G::HT) {
-            const int qh = s / G::HS, hs = s - (s / G::HS) * G::HS;
+            const int qh = PM ? s & 1 : s / G::HS, hs = PM ? s >> 1 : s - (s / G::HS) * G::HS;
             nb = hs / (4 * G::PH);
             const int rem = hs - nb * (4 * G::PH);
             const int ph = rem / G::PH, rr = rem - (rem / G::PH) * G::PH;
@@ -157,7 +163,7 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
         const int pp = frag_pixel<G::WO, TH, NB>(pg * G::NT + t, r32);
         const int nb = pp / (TH * G::WO), rem = pp - nb * (TH * G::WO);
         const int ty = rem / G::WO, x = rem - (rem / G::WO) * G::WO;
-        bv[t] = (h * G::HS + nb * 4 * G::PH + ty * G::RS + x) * 16;
+        bv[t] = (h * G::QS + (nb * 4 * G::PH + ty * G::RS + x) * G::PS) * 16;
         eoff[t] = (nb * G::HO + ty) * G::WO + x;
         enb[t] = nb;
     }
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
             const int toff = ((dy & 1) * 2 + (dx & 1)) * G::PH + (dy >> 1) * G::RS + (dx >> 1);
             a = *reinterpret_cast<const bf16x8*>(lds + ava + tap * 2 * BM * 16);
 #pragma unroll
-            for (int t = 0; t < G::NT; t++) b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] + toff * 16);
+            for (int t = 0; t < G::NT; t++) b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] + toff * G::PS * 16);
         };
         load(0, fa[0], fb[0]);
 #pragma unroll
@@ -273,10 +279,18 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
 int g_s_cus = 0;
 uint16_t* g_s_sink = nullptr;
 
-template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
-void launch_sp(SParams p, hipStream_t s) {
-    using G = SCfg<CIN, H, W, TH, NB, WRES, BM>;
-    auto kern = s2conv_kernel<CIN, H, W, TH, NB, WRES, BM>;
+bool s2_pm() {
+    static const bool pm = [] {
+        const char* e = getenv("MVPOSE_S2_PM");  // A/B: 0 = plane-major halo (PM measured +0.7 % frames/s)
+        return !(e && e[0] == '0');
+    }();
+    return pm;
+}
+
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM, bool PM>
+void launch_sp_pm(SParams p, hipStream_t s) {
+    using G = SCfg<CIN, H, W, TH, NB, WRES, BM, PM>;
+    auto kern = s2conv_kernel<CIN, H, W, TH, NB, WRES, BM, PM>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
@@ -284,6 +298,14 @@ void launch_sp(SParams p, hipStream_t s) {
     }
     const int grid = std::min(p.n_tiles, g_s_cus);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
+}
+
+template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
+void launch_sp(SParams p, hipStream_t s) {
+    if (s2_pm())
+        launch_sp_pm<CIN, H, W, TH, NB, WRES, BM, true>(p, s);
+    else
+        launch_sp_pm<CIN, H, W, TH, NB, WRES, BM, false>(p, s);
 }
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
@@ -302,14 +324,7 @@ void launch_s(const ConvLaunch& c, hipStream_t s) {
     MVP_REQUIRE(tiles < (1L << 30), "s2conv: too many tiles");
     SParams p{c.x, c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles, c.Cout / BM, c.relu,
               nullptr, nullptr, 0, 0, 0, 0};
-    auto kern = s2conv_kernel<CIN, H, W, TH, NB, WRES, BM>;
-    static bool attr = false;
-    if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
-        attr = true;
-    }
-    const int grid = (int)std::min<long>(tiles, g_s_cus);
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
+    launch_sp<CIN, H, W, TH, NB, WRES, BM>(p, s);
 }
 
 void init_s() {
