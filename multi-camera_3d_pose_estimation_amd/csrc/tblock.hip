@@ -40,10 +40,15 @@ using namespace mfma_tile;
 constexpr int kZeroSlots = 4096;
 
 
-template <int W, int TH_, bool DB_>
+template <int W, int TH_, bool DB_, bool PAIR_ = false>
 struct TBCfg {
     static constexpr int NW = 8, NTH = NW * 64, TH = TH_;
     static constexpr bool DB = DB_;                       // double-buffered input halo
+    // PAIR: the input halo's planes 2k, 2k+1 interleaved per pixel ([pair][pixel][2] slots):
+    // a DMA instruction reads 32 contiguous bytes per pixel (half the cache lines of
+    // plane-major) for 2-way bank conflicts on the conv1 fragment reads
+    static constexpr bool PAIR = PAIR_;
+    static constexpr int PX = PAIR ? 2 : 1;               // input-halo slots between pixels
     static constexpr int RS = W + 1;
     static constexpr int HSI = 1 + (TH + 4) * RS;        // input halo slots per plane
     static constexpr int HSM = 1 + (TH + 2) * RS;        // intermediate slots per plane
@@ -75,9 +80,9 @@ struct TBParams {
     int N, H, n_tiles;
 };
 
-template <int W, int TH_, bool DB_>
+template <int W, int TH_, bool DB_, bool PAIR>
 __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
-    using G = TBCfg<W, TH_, DB_>;
+    using G = TBCfg<W, TH_, DB_, PAIR>;
     constexpr int TH = G::TH, RS = G::RS;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
@@ -105,7 +110,8 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
         const int s = (j * G::NW + wave) * 64 + lane;
         int g = -1, off = 0;
         if (s < G::XSLOTS) {
-            const int q = s / G::HSI, hs = s - (s / G::HSI) * G::HSI;
+            const int q = PAIR ? (s / (2 * G::HSI)) * 2 + (s & 1) : s / G::HSI;
+            const int hs = PAIR ? (s % (2 * G::HSI)) >> 1 : s - (s / G::HSI) * G::HSI;
             if (hs > 0) {
                 const int t = hs - 1, hy = t / RS, hx = t - (t / RS) * RS;
                 if (hx < W) {
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
         int pp = frag_pixel<W, TH, 1>(wave + 8 * i, r32);
         if (pp >= (TH + 2) * W) pp = 0;  // unused slot
         const int r = pp / W, x = pp - (pp / W) * W;
-        b1v[i] = (h * G::HSI + r * RS + x) * 16;                     // input halo, tap (0,0)
+        b1v[i] = (PAIR ? h + (r * RS + x) * 2 : h * G::HSI + r * RS + x) * 16;  // input halo, tap (0,0)
         m1w[i] = G::MOFF + (2 * h * G::HSM + 1 + r * RS + x) * 16;  // intermediate slot, plane 2h
     }
 #pragma unroll
@@ -147,7 +153,8 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
         if (pp >= TH * W) pp = 0;
         const int r = pp / W, x = pp - (pp / W) * W;
         b2v[i] = G::MOFF + (h * G::HSM + r * RS + x) * 16;              // intermediate, tap (0,0)
-        r2v[i] = (2 * h * G::HSI + 1 + (r + 2) * RS + x) * 16;          // residual: input (r+2, x)
+        // residual: input (r+2, x), planes 2h (first 16 B) and 2h+1 (second, + r2s)
+        r2v[i] = (2 * h * G::HSI + (1 + (r + 2) * RS + x) * G::PX) * 16;
         e2[i] = r * W + x;
     }
     // folded-BN biases in LDS (visible after the first tile's barrier): registers are the scarce resource
@@ -169,7 +176,8 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
     };
 
     // one conv over NF fragments: 9 taps x 2 k-steps, fragments of step s+1 read before step s
-    auto conv = [&](auto nf_tag, int av, const int* bv, int hs, f32x16* acc) {
+    auto conv = [&](auto nf_tag, int av, const int* bv, int hs, auto px_tag, f32x16* acc) {
+        constexpr int PXS = decltype(px_tag)::value;  // slots between pixels of this image
         constexpr int NF = decltype(nf_tag)::value;
         bf16x8 fa[2], fb[2][NF];
         auto load = [&](int step, bf16x8& a, bf16x8 (&b)[NF]) {
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
             a = *reinterpret_cast<const bf16x8*>(lds + av + (tap * 4 + ks * 2) * 32 * 16);
 #pragma unroll
             for (int t = 0; t < NF; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + bv[t] + (ks * 2 * hs + dy * RS + dx) * 16);
+                b[t] = *reinterpret_cast<const bf16x8*>(lds + bv[t] + (ks * 2 * hs + (dy * RS + dx) * PXS) * 16);
         };
         load(0, fa[0], fb[0]);
 #pragma unroll
@@ -224,9 +232,10 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
 #pragma unroll
             for (int i = 0; i < G::MF1; i++) bv[i] = b1v[i] + xoff;
             if (nf1 == G::MF1)
-                conv(std::integral_constant<int, G::MF1>{}, av1, bv, G::HSI, acc);
+                conv(std::integral_constant<int, G::MF1>{}, av1, bv, G::HSI, std::integral_constant<int, G::PX>{}, acc);
             else
-                conv(std::integral_constant<int, G::MF1 - 1>{}, av1, bv, G::HSI, acc);
+                conv(std::integral_constant<int, G::MF1 - 1>{}, av1, bv, G::HSI, std::integral_constant<int, G::PX>{},
+                     acc);
 #pragma unroll
             for (int i = 0; i < G::MF1; i++) {
                 if (i < nf1) {
@@ -248,7 +257,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
 #pragma unroll
             for (int i = 0; i < (G::DB ? 1 : G::MF2); i++) {
                 rv[i][0] = *reinterpret_cast<const uint4*>(lds + r2v[i]);
-                rv[i][1] = *reinterpret_cast<const uint4*>(lds + r2v[i] + G::HSI * 16);
+                rv[i][1] = *reinterpret_cast<const uint4*>(lds + r2v[i] + (PAIR ? 1 : G::HSI) * 16);
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -264,9 +273,10 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
 #pragma unroll
             for (int i = 0; i < G::MF2; i++) acc[i] = b;
             if (nf2 == G::MF2)
-                conv(std::integral_constant<int, G::MF2>{}, av2, b2v, G::HSM, acc);
+                conv(std::integral_constant<int, G::MF2>{}, av2, b2v, G::HSM, std::integral_constant<int, 1>{}, acc);
             else
-                conv(std::integral_constant<int, G::MF2 - 1>{}, av2, b2v, G::HSM, acc);
+                conv(std::integral_constant<int, G::MF2 - 1>{}, av2, b2v, G::HSM, std::integral_constant<int, 1>{},
+                     acc);
             const long pix0 = ((long)n * H + ho0) * W;
 #pragma unroll
             for (int i = 0; i < G::MF2; i++) {
@@ -274,7 +284,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
                     uint4 ra, rb;
                     if (G::DB) {
                         ra = *reinterpret_cast<const uint4*>(lds + xoff + r2v[i]);
-                        rb = *reinterpret_cast<const uint4*>(lds + xoff + r2v[i] + G::HSI * 16);
+                        rb = *reinterpret_cast<const uint4*>(lds + xoff + r2v[i] + (PAIR ? 1 : G::HSI) * 16);
                     } else {
                         ra = rv[G::DB ? 0 : i][0];
                         rb = rv[G::DB ? 0 : i][1];
@@ -305,11 +315,18 @@ bool launch_tblock32(const uint16_t* x, const uint16_t* w1, const float* b1, con
     // TH = 16, single-buffered input halo: 82.7 us/conv at 1024 crops vs 91.0 for TH = 8
     // double-buffered (more conv1 recompute and input re-fetch) — tools/conv_bench.py
     using G = TBCfg<48, 16, false>;
-    auto kern = tblock32_kernel<48, 16, false>;
+    static_assert(TBCfg<48, 16, false, true>::LDS == G::LDS, "paired halo changes only the slot order");
     if (W != 48 || H % G::TH != 0) return false;
     const char* e = getenv("MVPOSE_NO_TBLOCK");  // diagnostics/tests: use basic_block_c32_kernel
     if (e && e[0] == '1') return false;
     if (N == 0) return true;
+    // input halo planes 2k, 2k+1 interleaved per pixel (each DMA instruction touches half the
+    // cache lines); MVPOSE_TBLOCK_PAIR=0 keeps the plane-major halo
+    static const bool pair = [] {
+        const char* v = getenv("MVPOSE_TBLOCK_PAIR");
+        return !(v && v[0] == '0');
+    }();
+    auto kern = pair ? tblock32_kernel<48, 16, false, true> : tblock32_kernel<48, 16, false, false>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
