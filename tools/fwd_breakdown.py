@@ -10,7 +10,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [i for i, r in enumerate(rows) if "stem2_kernel" in r["Kernel_Name"]]
 a = starts[-1]
-b = next((i for i in range(a, len(rows)) if "head1x1" in rows[i]["Kernel_Name"]), len(rows) - 1)
+b = next((i for i in range(a, len(rows)) if "head1x1" in rows[i]["Kernel_Name"] or "head_fuse" in rows[i]["Kernel_Name"]), len(rows) - 1)
 seg = rows[a:b + 1]
 fam = collections.defaultdict(lambda: [0, 0.0])
 for r in seg:
