@@ -377,10 +377,12 @@ bool launch_tconv(const ConvLaunch& c, hipStream_t s) {
         launch_t<64, 64, 48, 8, 1, true>(c, s);
         return true;
     }
-    // 128 ch @ 16x12 (streamed weights) measured level with wsconv (87.9 vs 86.2 us/conv at
-    // 1024 crops); wsconv keeps that plane unless MVPOSE_TCONV128=1
+    // 128 ch @ 16x12 (streamed weights, two crops per tile): level with wsconv on the
+    // plane-major halo (87.9 vs 86.2 us/conv at 1024 crops); with the pixel-major halo (the
+    // ring slot fills the 160 KiB exactly) same-box A/B 10,207 -> 10,479 frames/s, backbone
+    // 24.69 -> 23.82 ms.  MVPOSE_TCONV128=0 hands the plane back to wsconv.
     const char* e128 = getenv("MVPOSE_TCONV128");
-    if (c.Cin == 128 && c.H == 16 && c.W == 12 && e128 && e128[0] == '1') {
+    if (c.Cin == 128 && c.H == 16 && c.W == 12 && !(e128 && e128[0] == '0')) {
         launch_t<128, 16, 12, 16, 2, false>(c, s);
         return true;
     }

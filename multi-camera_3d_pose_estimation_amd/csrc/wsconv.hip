@@ -15,6 +15,8 @@
 // read spread over the bank row.  C = 128 (295 KB of weights) splits K over
 // wave pairs: the second wave of a pair hands its partial sums to the first
 // through LDS (one barrier per round).
+// Since the pixel-major tconv halo, the 128-ch plane runs tconv_kernel by default; this
+// kernel serves it with MVPOSE_TCONV128=0 (and the 64-ch plane with MVPOSE_WSCONV64=1).
 // K order is (tap, cin); conv_mfma_kernel sums the same products in (cin chunk,
 // tap) order, so the two agree to f32 rounding, not bit for bit.
 #include <algorithm>
