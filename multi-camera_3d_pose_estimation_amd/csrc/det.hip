@@ -360,7 +360,9 @@ __device__ __forceinline__ void wait_vm(int n) {
 
 // PW waves along the pixels (64 each) x 2 along the couts: tile 64*PW pixels x BN couts.
 template <int BN, int KS, int S, int PW, int NBUF, int CPS>
-__global__ __launch_bounds__(128 * PW, 4 / PW) void det_conv_gemm_kernel(GParams p) {
+// (a 2-slot ring with one chunk per step leaves LDS for three workgroups per CU)
+__global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 4 / PW) void det_conv_gemm_kernel(
+    GParams p) {
     constexpr int NT = 128 * PW;          // threads
     constexpr int NWV = 2 * PW;           // waves
     constexpr int BMP = 64 * PW;          // pixels per tile
@@ -944,17 +946,33 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo};
-    const long blocks = (p.M + 127) / 128 * p.n_nb;
-    if (blocks == 0) return;
-    MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
-    const dim3 g((unsigned)blocks), t(256);
     static const int cps = [] {
         const char* e = getenv("MVPOSE_DET_CPS");  // tuning: K chunks per barrier (1: 3-slot ring, 2: 2-slot)
         return e && atoi(e) == 2 ? 2 : 1;
     }();
+    static const int pw_env = [] {
+        const char* e = getenv("MVPOSE_DET_PW");  // tuning: 4 = 256-pixel tiles (8 waves) for >= 96 couts
+        return e && atoi(e) == 4 ? 4 : 2;
+    }();
+    const int pw = bn >= 96 ? pw_env : 2;
+    static const int ring = [] {
+        // tuning: LDS ring slots (2: three workgroups per CU; 4: three K steps in flight)
+        const char* e = getenv("MVPOSE_DET_RING");
+        return e ? atoi(e) : 3;
+    }();
+    const long blocks = (p.M + 64 * pw - 1) / (64 * pw) * p.n_nb;
+    if (blocks == 0) return;
+    MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
+    const dim3 g((unsigned)blocks), t(128 * pw);
 #define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                           \
     do {                                                                                        \
-        if (cps == 2)                                                                           \
+        if (pw == 4)                                                                            \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 4, 3, 1>), g, t, 0, s, p);     \
+        else if (ring == 2)                                                                     \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 1>), g, t, 0, s, p);     \
+        else if (ring == 4)                                                                     \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 4, 1>), g, t, 0, s, p);     \
+        else if (cps == 2)                                                                      \
             hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 2>), g, t, 0, s, p);     \
         else                                                                                    \
             hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3, 1>), g, t, 0, s, p);     \
