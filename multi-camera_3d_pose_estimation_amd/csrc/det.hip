@@ -358,14 +358,15 @@ __device__ __forceinline__ void wait_vm(int n) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// PW waves along the pixels (64 each) x 2 along the couts: tile 64*PW pixels x BN couts.
-template <int BN, int KS, int S, int PW, int NBUF, int CPS>
-// (a 2-slot ring with one chunk per step leaves LDS for three workgroups per CU)
-__global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 4 / PW) void det_conv_gemm_kernel(
-    GParams p) {
+// PW waves along the pixels (16*FP each) x 2 along the couts: tile 16*FP*PW pixels x BN couts.
+// (a 2-slot ring with one chunk per step leaves LDS for three workgroups per CU; FP = 8
+// holds a 128 x BN/2 accumulator tile per wave, one wave per SIMD)
+template <int BN, int KS, int S, int PW, int NBUF, int CPS, int FP = 4>
+__global__ __launch_bounds__(128 * PW, FP == 8 ? 1 : (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 4 / PW) void
+det_conv_gemm_kernel(GParams p) {
     constexpr int NT = 128 * PW;          // threads
     constexpr int NWV = 2 * PW;           // waves
-    constexpr int BMP = 64 * PW;          // pixels per tile
+    constexpr int BMP = 16 * FP * PW;     // pixels per tile
     constexpr int A_SLOTS = 4 * BN;       // [kg][cout]
     constexpr int B_SLOTS = 4 * BMP;      // [kg][pix]
     constexpr int SUB = (A_SLOTS + B_SLOTS) * 16;  // one 32-channel K chunk
@@ -395,7 +396,7 @@ __global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 
     // instruction.  The swizzle keeps the 16-lane fragment reads (16 rows, one chunk)
     // conflict-free in every ds_read_b128 lane group.
     auto swz = [](int r) { return (-(r >> 2)) & 3; };
-    constexpr int BR = B_SLOTS / NT;  // pixel rounds per thread (2)
+    constexpr int BR = B_SLOTS / NT;  // pixel rounds per thread (FP / 2)
     long bm[BR];
     bool bvalid[BR];
     int bkg[BR], bn_[BR], bho[BR], bwo[BR];
@@ -469,9 +470,9 @@ __global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 
 #pragma unroll
         for (int c = 0; c < CPS; c++) issue_chunk(k * CPS + c, lds + buf * STAGE + c * SUB);
     };
-    f32x4 acc[4][WCT];
+    f32x4 acc[FP][WCT];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int i = 0; i < FP; i++)
 #pragma unroll
         for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int j = 0; j < D && j < nk; j++) issue(j, j);
@@ -486,15 +487,15 @@ __global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 
 #pragma unroll
         for (int cc = 0; cc < CPS; cc++) {
             const uint8_t* base = lds + buf * STAGE + cc * SUB;
-            bf16x8 a[WCT], b[4];
+            bf16x8 a[WCT], b[FP];
 #pragma unroll
             for (int c = 0; c < WCT; c++)
                 a[c] = *reinterpret_cast<const bf16x8*>(base + (wc * (BN / 2) + c * 16) * 64 + soff);
 #pragma unroll
-            for (int i = 0; i < 4; i++)
-                b[i] = *reinterpret_cast<const bf16x8*>(base + A_SLOTS * 16 + (wp * 64 + i * 16) * 64 + soff);
+            for (int i = 0; i < FP; i++)
+                b[i] = *reinterpret_cast<const bf16x8*>(base + A_SLOTS * 16 + (wp * 16 * FP + i * 16) * 64 + soff);
 #pragma unroll
-            for (int i = 0; i < 4; i++)
+            for (int i = 0; i < FP; i++)
 #pragma unroll
                 for (int c = 0; c < WCT; c++)
                     acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
@@ -514,8 +515,8 @@ __global__ __launch_bounds__(128 * PW, (PW == 2 && NBUF == 2 && CPS == 1) ? 3 : 
         if (co >= p.N) continue;
         const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const long m = m0 + wp * 64 + i * 16 + r16;
+        for (int i = 0; i < FP; i++) {
+            const long m = m0 + wp * 16 * FP + i * 16 + r16;
             if (m >= p.M) continue;
             float v[4] = {acc[i][c][0] + bb.x, acc[i][c][1] + bb.y, acc[i][c][2] + bb.z, acc[i][c][3] + bb.w};
             if (p.act == 2)
@@ -943,7 +944,15 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const int pad = ks / 2;
     const int Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
     const int npad = det_cout_pad(N);
-    const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
+    static const int bn_max = [] {
+        const char* e = getenv("MVPOSE_DET_BN");  // tuning: the widest cout tile (192 default; 96: more workgroups per CU)
+        return e ? atoi(e) : 192;
+    }();
+    const int bn = npad % 192 == 0 && bn_max >= 192   ? 192
+                   : npad % 128 == 0 && bn_max >= 128 ? 128
+                   : npad % 96 == 0 && bn_max >= 96   ? 96
+                   : npad % 64 == 0                   ? 64
+                                                      : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo};
     static const int cps = [] {
@@ -955,18 +964,25 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
         return e && atoi(e) == 4 ? 4 : 2;
     }();
     const int pw = bn >= 96 ? pw_env : 2;
+    static const int fp = [] {
+        const char* e = getenv("MVPOSE_DET_FP");  // tuning: 8 = 256-pixel tiles of 4 waves (128 px each)
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    const int px = fp == 8 && bn >= 96 ? 256 : 64 * pw;
     static const int ring = [] {
         // tuning: LDS ring slots (2: three workgroups per CU; 4: three K steps in flight)
         const char* e = getenv("MVPOSE_DET_RING");
         return e ? atoi(e) : 3;
     }();
-    const long blocks = (p.M + 64 * pw - 1) / (64 * pw) * p.n_nb;
+    const long blocks = (p.M + px - 1) / px * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
     const dim3 g((unsigned)blocks), t(128 * pw);
 #define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                           \
     do {                                                                                        \
-        if (pw == 4)                                                                            \
+        if (px == 256 && pw == 2)                                                               \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3, 1, 8>), g, t, 0, s, p);  \
+        else if (pw == 4)                                                                       \
             hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 4, 3, 1>), g, t, 0, s, p);     \
         else if (ring == 2)                                                                     \
             hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 1>), g, t, 0, s, p);     \
