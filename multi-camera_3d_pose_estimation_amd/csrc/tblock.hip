@@ -40,7 +40,7 @@ using namespace mfma_tile;
 constexpr int kZeroSlots = 4096;
 
 
-template <int W, int TH_, bool DB_, bool PAIR_ = false>
+template <int W, int TH_, bool DB_, bool PAIR_ = false, bool SWZ_ = false>
 struct TBCfg {
     static constexpr int NW = 8, NTH = NW * 64, TH = TH_;
     static constexpr bool DB = DB_;                       // double-buffered input halo
@@ -49,6 +49,10 @@ struct TBCfg {
     // plane-major) for 2-way bank conflicts on the conv1 fragment reads
     static constexpr bool PAIR = PAIR_;
     static constexpr int PX = PAIR ? 2 : 1;               // input-halo slots between pixels
+    // SWZ (with PAIR): the two planes of pixel slot hs swap places when bit 3 of hs is set, so
+    // 16 pixels distinct mod 16 hit 16 distinct 16-B bank positions (conflict-free conv1
+    // fragment reads) at the price of per-tap address arithmetic
+    static constexpr bool SWZ = SWZ_ && PAIR_;
     static constexpr int RS = W + 1;
     static constexpr int HSI = 1 + (TH + 4) * RS;        // input halo slots per plane
     static constexpr int HSM = 1 + (TH + 2) * RS;        // intermediate slots per plane
@@ -67,6 +71,7 @@ struct TBCfg {
     static_assert((2 * HSI + 2 * RS + 2) * 16 < 65536, "ds_read offset range");
     static_assert(TH + 4 < 31 && (TH + 2) * W * 32 < (1 << 25), "packed DMA geometry");
     static_assert(2 * MF2 < 16 && XPPW < 64, "vmcnt range");
+    static_assert(!SWZ || !DB, "the swizzled halo is single-buffered");
 };
 
 struct TBParams {
@@ -80,9 +85,9 @@ struct TBParams {
     int N, H, n_tiles;
 };
 
-template <int W, int TH_, bool DB_, bool PAIR>
+template <int W, int TH_, bool DB_, bool PAIR, bool SWZ = false>
 __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
-    using G = TBCfg<W, TH_, DB_, PAIR>;
+    using G = TBCfg<W, TH_, DB_, PAIR, SWZ>;
     constexpr int TH = G::TH, RS = G::RS;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
@@ -110,8 +115,8 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
         const int s = (j * G::NW + wave) * 64 + lane;
         int g = -1, off = 0;
         if (s < G::XSLOTS) {
-            const int q = PAIR ? (s / (2 * G::HSI)) * 2 + (s & 1) : s / G::HSI;
             const int hs = PAIR ? (s % (2 * G::HSI)) >> 1 : s - (s / G::HSI) * G::HSI;
+            const int q = PAIR ? (s / (2 * G::HSI)) * 2 + ((s & 1) ^ (G::SWZ ? (hs >> 3) & 1 : 0)) : s / G::HSI;
             if (hs > 0) {
                 const int t = hs - 1, hy = t / RS, hx = t - (t / RS) * RS;
                 if (hx < W) {
@@ -154,7 +159,8 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
         const int r = pp / W, x = pp - (pp / W) * W;
         b2v[i] = G::MOFF + (h * G::HSM + r * RS + x) * 16;              // intermediate, tap (0,0)
         // residual: input (r+2, x), planes 2h (first 16 B) and 2h+1 (second, + r2s)
-        r2v[i] = (2 * h * G::HSI + (1 + (r + 2) * RS + x) * G::PX) * 16;
+        const int hr = 1 + (r + 2) * RS + x;
+        r2v[i] = (2 * h * G::HSI + hr * G::PX + (G::SWZ ? (hr >> 3) & 1 : 0)) * 16;
         e2[i] = r * W + x;
     }
     // folded-BN biases in LDS (visible after the first tile's barrier): registers are the scarce resource
@@ -184,8 +190,16 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
             const int tap = step >> 1, ks = step & 1, dy = tap / 3, dx = tap % 3;
             a = *reinterpret_cast<const bf16x8*>(lds + av + (tap * 4 + ks * 2) * 32 * 16);
 #pragma unroll
-            for (int t = 0; t < NF; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + bv[t] + (ks * 2 * hs + (dy * RS + dx) * PXS) * 16);
+            for (int t = 0; t < NF; t++) {
+                if constexpr (G::SWZ && PXS == 2) {
+                    int bt = bv[t];
+                    asm volatile("" : "+v"(bt));  // per-step address math: 36 hoisted tap addresses spill
+                    const int a = bt + (dy * RS + dx) * 32;  // (2*slot + h) * 16, unswizzled
+                    b[t] = *reinterpret_cast<const bf16x8*>(lds + (a ^ ((a >> 4) & 16)) + ks * 2 * hs * 16);
+                } else {
+                    b[t] = *reinterpret_cast<const bf16x8*>(lds + bv[t] + (ks * 2 * hs + (dy * RS + dx) * PXS) * 16);
+                }
+            }
         };
         load(0, fa[0], fb[0]);
 #pragma unroll
@@ -257,7 +271,7 @@ __global__ __launch_bounds__(512, 1) void tblock32_kernel(TBParams p) {
 #pragma unroll
             for (int i = 0; i < (G::DB ? 1 : G::MF2); i++) {
                 rv[i][0] = *reinterpret_cast<const uint4*>(lds + r2v[i]);
-                rv[i][1] = *reinterpret_cast<const uint4*>(lds + r2v[i] + (PAIR ? 1 : G::HSI) * 16);
+                rv[i][1] = *reinterpret_cast<const uint4*>(lds + (G::SWZ ? r2v[i] ^ 16 : r2v[i] + (PAIR ? 1 : G::HSI) * 16));
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -322,11 +336,13 @@ bool launch_tblock32(const uint16_t* x, const uint16_t* w1, const float* b1, con
     if (N == 0) return true;
     // input halo planes 2k, 2k+1 interleaved per pixel (each DMA instruction touches half the
     // cache lines); MVPOSE_TBLOCK_PAIR=0 keeps the plane-major halo
-    static const bool pair = [] {
-        const char* v = getenv("MVPOSE_TBLOCK_PAIR");
-        return !(v && v[0] == '0');
+    static const int pair = [] {
+        const char* v = getenv("MVPOSE_TBLOCK_PAIR");  // 0 plane-major, 1 paired (default), 2 paired + swizzle
+        return v ? atoi(v) : 1;
     }();
-    auto kern = pair ? tblock32_kernel<48, 16, false, true> : tblock32_kernel<48, 16, false, false>;
+    auto kern = pair == 2   ? tblock32_kernel<48, 16, false, true, true>
+                : pair == 1 ? tblock32_kernel<48, 16, false, true>
+                            : tblock32_kernel<48, 16, false, false>;
     static bool attr = false;
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
