@@ -792,6 +792,49 @@ __global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
     *reinterpret_cast<uint4*>(p.out + ((long)n * hw + pix) * p.C + ch * 8) = o;
 }
 
+// the same with the input count a template parameter: all NI 16-B loads issue before the
+// first sum (the runtime-count loop waited for each load in turn); sums in input order, so
+// bit-identical to fuse_sum_kernel
+template <int NI>
+__global__ __launch_bounds__(256) void fuse_sum_n_kernel(FuseParams p) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n = blockIdx.y;
+    const int hw = p.H * p.W;
+    if (i >= (hw << p.lgc)) return;
+    const int ch = i & ((1 << p.lgc) - 1);
+    const int pix = i >> p.lgc;
+    const int h = (int)((unsigned)pix / (unsigned)p.W), w = pix - h * p.W;
+    uint4 v[NI];
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+        const int lg = p.lg[k];
+        const int hs = p.H >> lg, ws = p.W >> lg;
+        const long src = ((long)n * hs * ws + (h >> lg) * ws + (w >> lg)) * p.C + ch * 8;
+        v[k] = *reinterpret_cast<const uint4*>(p.in[k] + src);
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < NI; k++) {
+        acc[0] += bf16_to_f32(v[k].x & 0xffff);
+        acc[1] += bf16_to_f32(v[k].x >> 16);
+        acc[2] += bf16_to_f32(v[k].y & 0xffff);
+        acc[3] += bf16_to_f32(v[k].y >> 16);
+        acc[4] += bf16_to_f32(v[k].z & 0xffff);
+        acc[5] += bf16_to_f32(v[k].z >> 16);
+        acc[6] += bf16_to_f32(v[k].w & 0xffff);
+        acc[7] += bf16_to_f32(v[k].w >> 16);
+    }
+    if (p.relu)
+#pragma unroll
+        for (int q = 0; q < 8; q++) acc[q] = fmaxf(acc[q], 0.f);
+    uint4 o;
+    o.x = (uint32_t)f32_to_bf16(acc[0]) | ((uint32_t)f32_to_bf16(acc[1]) << 16);
+    o.y = (uint32_t)f32_to_bf16(acc[2]) | ((uint32_t)f32_to_bf16(acc[3]) << 16);
+    o.z = (uint32_t)f32_to_bf16(acc[4]) | ((uint32_t)f32_to_bf16(acc[5]) << 16);
+    o.w = (uint32_t)f32_to_bf16(acc[6]) | ((uint32_t)f32_to_bf16(acc[7]) << 16);
+    *reinterpret_cast<uint4*>(p.out + ((long)n * hw + pix) * p.C + ch * 8) = o;
+}
+
 }  // namespace
 
 const uint16_t* conv_zero_region() { return zero_page(); }
@@ -907,7 +950,21 @@ void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_
     const long per = (long)H * W * chunks;
     MVP_REQUIRE(per < (1L << 30) && N < 65536, "fuse: plane too large");
     if (per == 0 || N == 0) return;
-    hipLaunchKernelGGL(fuse_sum_kernel, dim3((unsigned)((per + 255) / 256), (unsigned)N), dim3(256), 0, s, p);
+    const dim3 g((unsigned)((per + 255) / 256), (unsigned)N);
+    static const bool loop = [] {
+        const char* e = getenv("MVPOSE_FUSE_LOOP");  // A/B: 1 = the runtime-count loop kernel
+        return e && e[0] == '1';
+    }();
+    if (loop)
+        hipLaunchKernelGGL(fuse_sum_kernel, g, dim3(256), 0, s, p);
+    else if (n_in == 1)
+        hipLaunchKernelGGL(fuse_sum_n_kernel<1>, g, dim3(256), 0, s, p);
+    else if (n_in == 2)
+        hipLaunchKernelGGL(fuse_sum_n_kernel<2>, g, dim3(256), 0, s, p);
+    else if (n_in == 3)
+        hipLaunchKernelGGL(fuse_sum_n_kernel<3>, g, dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL(fuse_sum_n_kernel<4>, g, dim3(256), 0, s, p);
     MVP_HIP(hipGetLastError());
 }
 
