@@ -535,6 +535,103 @@ det_conv_gemm_kernel(GParams p) {
     }
 }
 
+// 3x3/s1 convs with one 32-channel input chunk (the 320x320 stem / stage-1 planes, 24 -> 32
+// padded channels): im2col re-DMAs every input pixel once per tap while a tap's K work is a
+// single chunk, so the GEMM kernel above is DMA-issue bound there.  Here a tile is 2 output
+// rows x 64 columns of one frame; its 4 x 66 input halo (64 B per pixel) and all 9 taps'
+// weights arrive in one DMA phase, and the taps are LDS offsets.  Same swizzled row-major
+// images as the GEMM kernel (row = halo pixel / cout, 4 16-B chunks per row); the
+// workgroup then runs its 9 K-steps without another barrier (3 workgroups per CU hide the
+// DMA).  K order (tap, channel) as the GEMM kernel: identical sums.
+template <int BN>
+__global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
+    constexpr int TR = 2, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;  // halo pixels
+    constexpr int A_SLOTS = 9 * 4 * BN, A_R64 = A_SLOTS / 64;
+    constexpr int B_R64 = (HP * 4 + 63) / 64;
+    constexpr int WCT = BN / 32;
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[(A_SLOTS + B_R64 * 64) * 16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 1, wc = wave >> 1;  // output row of the tile, cout half
+    const int tiles_w = (p.W + TW - 1) / TW, tiles_h = (p.H + TR - 1) / TR;
+    const int per = tiles_w * tiles_h;
+    const int n = blockIdx.x / per, t = blockIdx.x - n * per;
+    const int ho0 = (t / tiles_w) * TR, wo0 = (t - (t / tiles_w) * tiles_w) * TW;
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    // weights: slot s of tap tp = tp * 4BN + 4co + (kg ^ swz(co))
+    for (int r = wave; r < A_R64; r += 4) {
+        const int sl = r * 64 + lane, tp = sl / (4 * BN), rem = sl - tp * (4 * BN);
+        const int co = rem >> 2, kg = (rem & 3) ^ swz(co);
+        glds16_det(p.w + (size_t)co * 288 + tp * 32 + kg * 8, lds + r * 64 * 16);
+    }
+    // input halo: slot s = 4hp + (kg ^ swz(hp)), hp = halo row * 66 + halo col
+    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
+    for (int r = wave; r < B_R64; r += 4) {
+        const int sl = r * 64 + lane, hp = sl >> 2, kg = (sl & 3) ^ swz(hp);
+        const int hy = hp / HW_, hx = hp - hy * HW_;
+        const int gy = ho0 + hy - 1, gx = wo0 + hx - 1;
+        const bool in = hp < HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
+        const void* src = in ? (const void*)(xb + ((size_t)gy * p.W + gx) * p.xs + kg * 8)
+                             : (const void*)(p.zero + (sl & 1023) * 8);
+        glds16_det(src, lds + (A_SLOTS + r * 64) * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const int kg = lane >> 4, r16 = lane & 15;
+    const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
+    f32x4 acc[4][WCT];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tp = 0; tp < 9; tp++) {
+        const int dy = tp / 3, dx = tp % 3;
+        bf16x8 a[WCT], b[4];
+#pragma unroll
+        for (int c = 0; c < WCT; c++)
+            a[c] = *reinterpret_cast<const bf16x8*>(lds + tp * 4 * BN * 16 + (wc * (BN / 2) + c * 16) * 64 + soff);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int hp = (wp + dy) * HW_ + i * 16 + r16 + dx;
+            b[i] = *reinterpret_cast<const bf16x8*>(lds + A_SLOTS * 16 + hp * 64 + ((kg ^ swz(hp)) * 16));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < WCT; c++)
+                acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+    }
+    const int ho = ho0 + wp;
+    if (ho >= p.H) return;
+#pragma unroll
+    for (int c = 0; c < WCT; c++) {
+        const int co = wc * (BN / 2) + c * 16 + kg * 4;
+        if (co >= p.N) continue;
+        const float4 bb = *reinterpret_cast<const float4*>(p.bias + co);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int wo = wo0 + i * 16 + r16;
+            if (wo >= p.W) continue;
+            const long m = ((long)n * p.H + ho) * p.W + wo;
+            float v[4] = {acc[i][c][0] + bb.x, acc[i][c][1] + bb.y, acc[i][c][2] + bb.z, acc[i][c][3] + bb.w};
+            if (p.act == 2)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+            if (p.res) {
+                const uint2 r = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                v[0] += bf(r.x & 0xffff), v[1] += bf(r.x >> 16), v[2] += bf(r.y & 0xffff), v[3] += bf(r.y >> 16);
+            }
+            if (p.act == 1)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+            *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
+                uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+        }
+    }
+}
+
 // ------------------------------------------------------------------ channel attention
 // Channel means: kCaSplit workgroups per image each sum a contiguous pixel range (f32
 // per-thread partial sums, then an LDS tree) into part[n][split][C]; then one workgroup per
@@ -955,6 +1052,23 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
                                                       : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo};
+    // halo-tile kernel for the 32-channel 3x3/s1 convs: 14.03 -> 13.77 ms per 64 frames
+    // (same-box tools/det_ab.sh); MVPOSE_DET_HALO=0 keeps the im2col GEMM for them
+    static const bool halo_env = [] {
+        const char* e = getenv("MVPOSE_DET_HALO");
+        return !(e && e[0] == '0');
+    }();
+    if (halo_env && ks == 3 && stride == 1 && cin == 32 && npad <= 64) {
+        const long tiles = (long)n * ((H + 1) / 2) * ((W + 63) / 64);
+        MVP_REQUIRE(tiles < (1L << 31), "det conv: grid too large");
+        if (tiles == 0) return;
+        if (npad == 64)
+            hipLaunchKernelGGL(det_conv_halo_kernel<64>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+        else
+            hipLaunchKernelGGL(det_conv_halo_kernel<32>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+        MVP_HIP(hipGetLastError());
+        return;
+    }
     static const int cps = [] {
         const char* e = getenv("MVPOSE_DET_CPS");  // tuning: K chunks per barrier (1: 3-slot ring, 2: 2-slot)
         return e && atoi(e) == 2 ? 2 : 1;
