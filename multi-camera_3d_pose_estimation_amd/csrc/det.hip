@@ -542,8 +542,9 @@ det_conv_gemm_kernel(GParams p) {
 // weights arrive in one DMA phase, and the taps are LDS offsets.  Same swizzled row-major
 // images as the GEMM kernel (row = halo pixel / cout, 4 16-B chunks per row); the
 // workgroup then runs its 9 K-steps without another barrier (3 workgroups per CU hide the
-// DMA).  K order (tap, channel) as the GEMM kernel: identical sums.
-template <int BN>
+// DMA).  One chunk: K order (tap, channel) as the GEMM kernel, identical sums; two chunks
+// (64 channels, one DMA + compute phase each): chunk-major K order, equal to f32 rounding.
+template <int BN, int NCK>  // NCK 32-channel input chunks, one DMA + compute phase each
 __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
     constexpr int TR = 2, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;  // halo pixels
     constexpr int A_SLOTS = 9 * 4 * BN, A_R64 = A_SLOTS / 64;
@@ -558,26 +559,7 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
     const int n = blockIdx.x / per, t = blockIdx.x - n * per;
     const int ho0 = (t / tiles_w) * TR, wo0 = (t - (t / tiles_w) * tiles_w) * TW;
     auto swz = [](int r) { return (-(r >> 2)) & 3; };
-    // weights: slot s of tap tp = tp * 4BN + 4co + (kg ^ swz(co))
-    for (int r = wave; r < A_R64; r += 4) {
-        const int sl = r * 64 + lane, tp = sl / (4 * BN), rem = sl - tp * (4 * BN);
-        const int co = rem >> 2, kg = (rem & 3) ^ swz(co);
-        glds16_det(p.w + (size_t)co * 288 + tp * 32 + kg * 8, lds + r * 64 * 16);
-    }
-    // input halo: slot s = 4hp + (kg ^ swz(hp)), hp = halo row * 66 + halo col
     const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
-    for (int r = wave; r < B_R64; r += 4) {
-        const int sl = r * 64 + lane, hp = sl >> 2, kg = (sl & 3) ^ swz(hp);
-        const int hy = hp / HW_, hx = hp - hy * HW_;
-        const int gy = ho0 + hy - 1, gx = wo0 + hx - 1;
-        const bool in = hp < HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
-        const void* src = in ? (const void*)(xb + ((size_t)gy * p.W + gx) * p.xs + kg * 8)
-                             : (const void*)(p.zero + (sl & 1023) * 8);
-        glds16_det(src, lds + (A_SLOTS + r * 64) * 16);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
     const int kg = lane >> 4, r16 = lane & 15;
     const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
     f32x4 acc[4][WCT];
@@ -585,6 +567,27 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
     for (int i = 0; i < 4; i++)
 #pragma unroll
         for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < NCK; q++) {
+    if (q > 0) __builtin_amdgcn_s_barrier();  // every wave is done with chunk q-1's images
+    // weights: slot s of tap tp = tp * 4BN + 4co + (kg ^ swz(co))
+    for (int r = wave; r < A_R64; r += 4) {
+        const int sl = r * 64 + lane, tp = sl / (4 * BN), rem = sl - tp * (4 * BN);
+        const int co = rem >> 2, kq = (rem & 3) ^ swz(co);
+        glds16_det(p.w + (size_t)co * (288 * NCK) + tp * (32 * NCK) + q * 32 + kq * 8, lds + r * 64 * 16);
+    }
+    // input halo: slot s = 4hp + (kg ^ swz(hp)), hp = halo row * 66 + halo col
+    for (int r = wave; r < B_R64; r += 4) {
+        const int sl = r * 64 + lane, hp = sl >> 2, kq = (sl & 3) ^ swz(hp);
+        const int hy = hp / HW_, hx = hp - hy * HW_;
+        const int gy = ho0 + hy - 1, gx = wo0 + hx - 1;
+        const bool in = hp < HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)p.W;
+        const void* src = in ? (const void*)(xb + ((size_t)gy * p.W + gx) * p.xs + q * 32 + kq * 8)
+                             : (const void*)(p.zero + (sl & 1023) * 8);
+        glds16_det(src, lds + (A_SLOTS + r * 64) * 16);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
 #pragma unroll
     for (int tp = 0; tp < 9; tp++) {
         const int dy = tp / 3, dx = tp % 3;
@@ -602,6 +605,8 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
 #pragma unroll
             for (int c = 0; c < WCT; c++)
                 acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
     const int ho = ho0 + wp;
     if (ho >= p.H) return;
@@ -1058,14 +1063,22 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
         const char* e = getenv("MVPOSE_DET_HALO");
         return !(e && e[0] == '0');
     }();
-    if (halo_env && ks == 3 && stride == 1 && cin == 32 && npad <= 64) {
+    static const bool halo64 = [] {
+        const char* e = getenv("MVPOSE_DET_HALO64");  // A/B: 1 = also the 64-channel convs (2 chunk phases)
+        return e && e[0] == '1';
+    }();
+    if (halo_env && ks == 3 && stride == 1 && (cin == 32 || (cin == 64 && halo64)) && npad <= 64) {
         const long tiles = (long)n * ((H + 1) / 2) * ((W + 63) / 64);
         MVP_REQUIRE(tiles < (1L << 31), "det conv: grid too large");
         if (tiles == 0) return;
-        if (npad == 64)
-            hipLaunchKernelGGL(det_conv_halo_kernel<64>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+        if (cin == 64 && npad == 64)
+            hipLaunchKernelGGL((det_conv_halo_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+        else if (cin == 64)
+            hipLaunchKernelGGL((det_conv_halo_kernel<32, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+        else if (npad == 64)
+            hipLaunchKernelGGL((det_conv_halo_kernel<64, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
         else
-            hipLaunchKernelGGL(det_conv_halo_kernel<32>, dim3((unsigned)tiles), dim3(256), 0, s, p);
+            hipLaunchKernelGGL((det_conv_halo_kernel<32, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
         MVP_HIP(hipGetLastError());
         return;
     }
