@@ -1064,8 +1064,9 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
         return !(e && e[0] == '0');
     }();
     static const bool halo64 = [] {
-        const char* e = getenv("MVPOSE_DET_HALO64");  // A/B: 1 = also the 64-channel convs (2 chunk phases)
-        return e && e[0] == '1';
+        // also the 64-channel convs (2 chunk phases): 13.90 -> 13.86 ms per 64 frames; =0 disables
+        const char* e = getenv("MVPOSE_DET_HALO64");
+        return !(e && e[0] == '0');
     }();
     if (halo_env && ks == 3 && stride == 1 && (cin == 32 || (cin == 64 && halo64)) && npad <= 64) {
         const long tiles = (long)n * ((H + 1) / 2) * ((W + 63) / 64);
