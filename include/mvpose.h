@@ -106,7 +106,9 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
  *   enabling the column-resident fast path (per run of rows sharing a source
  *   row, columns whose taps are all clearly above / below thr are summed in
  *   closed form); separable == 2 runs that path walking every row of every
- *   column (diagnostics, tests).
+ *   column (diagnostics, tests).  separable_dev (nullable) [N] int: per-crop flags
+ *   from mvp_bbox_geometry; crops flagged 0 take the general path, the others the
+ *   `separable` mode.
  * ------------------------------------------------------------------------- */
 int mvp_preprocess(const uint8_t* frames_dev, int n, int H, int W, const double* minv_dev, int out_h, int out_w,
                    const float* mean3_host, const float* std3_host, int swap_rb, int with_flip, uint16_t* out_dev,
@@ -122,7 +124,21 @@ int mvp_warp_is_separable(const double* minv_host, int img_h, int img_w, int* se
 int mvp_heatmap_revert(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
                        int img_w, float* out_dev, void* stream);
 int mvp_heatmap_moments(const float* hm_dev, int N, int K, int h, int w, const double* minv_dev, int img_h,
-                        int img_w, float thr, int separable, double* out_dev, void* stream);
+                        int img_w, float thr, int separable, const int* separable_dev, double* out_dev,
+                        void* stream);
+/* mvp_bbox_geometry: the reference's detector -> inference_topdown hand-off and TopdownAffine
+ *   geometry on the device (replaces mmpose_pose_estimation.py:242-253 + mmpose bbox_xyxy2cs /
+ *   _fix_aspect_ratio / get_warp_matrix -> cv2.getAffineTransform (cv::solve LU) and
+ *   warpAffine's inversion).  Row i of boxes_dev ([n][stride] f32: x1, y1, x2, y2, ...) is the
+ *   person box when its four coordinates are finite and (score_col < 0 or
+ *   row[score_col] > bbox_thr), else the whole frame_w x frame_h image.  Writes crop_minv_dev
+ *   [n][6] f64 (crop -> image, for mvp_preprocess), revert_minv_dev [n][6] f64 (image ->
+ *   heatmap, for mvp_heatmap_moments / revert), center_scale_dev [n][4] f32 (for
+ *   mvp_heatmap_decode) and separable_dev [n] int (mvp_warp_is_separable of the revert map).
+ *   Fed directly with mvp_det_forward's best_dev (stride 6, score_col 4). */
+int mvp_bbox_geometry(const float* boxes_dev, int stride, int n, int score_col, float bbox_thr, int frame_h,
+                      int frame_w, double* crop_minv_dev, double* revert_minv_dev, float* center_scale_dev,
+                      int* separable_dev, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Backbone graph runtime (replaces the HRNet-W32 forward inside mmpose's

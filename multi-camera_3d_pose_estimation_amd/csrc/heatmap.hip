@@ -234,6 +234,8 @@ struct MomParams {
     float thr;
     int separable;  // host-verified: source column depends on x only, source row on y only
                     // (2: the separable path without the per-run closed forms)
+    const int* __restrict__ sep;  // nullable: per-crop flags (mvp_bbox_geometry); a crop whose flag
+                                  // is 0 takes the general path, the others `separable`
     int jpb;        // joints per workgroup: the warp tables depend on the crop only, so a
                     // workgroup builds them once and reuses them for jpb maps of its crop
     int mixcf;      // separable path: mixed columns in closed form with a per-row prefix table
@@ -277,13 +279,14 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
     const int n = blockIdx.x / groups;
     const int k0 = (blockIdx.x - n * groups) * p.jpb, k1 = min(p.K, k0 + p.jpb);
     const double* M = p.minv + 6 * n;
+    const int separable = (p.sep && !p.sep[n]) ? 0 : p.separable;
     for (int x = threadIdx.x; x < p.img_w; x += kMomBlock) {
         sad[x] = (int)rint(M[0] * x * 1024.0);
         sbd[x] = (int)rint(M[3] * x * 1024.0);
     }
     __syncthreads();
     const double cx = 0.5 * p.img_w, cy = 0.5 * p.img_h;  // centred coordinates (cancellation)
-    if (p.separable) {
+    if (separable) {
         // Row table: source row iy and weight index fq of every image row (uniform per row).
         // packed (iy + 4096) << 5 | fq, one word per row
         for (int r = threadIdx.x; r <= p.h; r += kMomBlock) {
@@ -384,7 +387,7 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
         r1 = bbox[3];
         double t[6] = {0, 0, 0, 0, 0, 0};
         if (c1 >= 0) {
-            if (p.separable) {
+            if (separable) {
                 // Lanes own column pairs (packed f32 math).  Per run, a column's two
                 // x-interpolated source rows a = v00 gx + v01 fx and b = v10 gx + v11 fx are
                 // formed once; the pixel value is OpenCV's bilinear remap value (its fixed-point
@@ -397,7 +400,7 @@ __global__ __launch_bounds__(kMomBlock) void moments_kernel(MomParams p) {
                 constexpr int NP = kMomCols / 2;
                 const int X0 = (int)rint((M[1] * 0 + M[2]) * 1024.0) + 16;
                 const float thr_hi = p.thr * (1.f + 2e-6f), thr_lo2 = p.thr * (1.f - 2e-6f);
-                const bool closed = p.separable != 2;  // 2: walk every column (diagnostics / tests)
+                const bool closed = separable != 2;  // 2: walk every column (diagnostics / tests)
                 for (int xb = threadIdx.x; xb < p.img_w; xb += kMomBlock * kMomCols) {
 #pragma clang fp contract(off)
                     int ix[kMomCols];
@@ -738,7 +741,8 @@ extern "C" int mvp_heatmap_decode(const float* hm, const float* hm_flip, int N, 
 }
 
 extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, const double* minv, int img_h,
-                                   int img_w, float thr, int separable, double* out, void* stream) {
+                                   int img_w, float thr, int separable, const int* separable_dev, double* out,
+                                   void* stream) {
     MVP_ABI_BEGIN
     MVP_REQUIRE(N >= 0 && K > 0 && h > 0 && w > 0 && img_h > 0 && img_w > 0, "mvp_heatmap_moments: bad sizes");
     // map, 2 column tables, row table, run starts / ends, run sums (fp64): moments_kernel's layout
@@ -771,6 +775,7 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
     p.img_w = img_w;
     p.thr = thr;
     p.separable = separable;
+    p.sep = separable_dev;
     p.mixcf = mixcf ? 1 : 0;
     const char* je = getenv("MVPOSE_MOM_JPB");  // tuning experiments / tests only
     const int jpb_env = je ? atoi(je) : 0;

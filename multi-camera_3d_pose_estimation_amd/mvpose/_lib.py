@@ -49,7 +49,9 @@ SIGNATURES = {
     "mvp_heatmap_revert": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                                    c_void_p]),
     "mvp_heatmap_moments": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float,
-                                    c_int, c_void_p, c_void_p]),
+                                    c_int, c_void_p, c_void_p, c_void_p]),
+    "mvp_bbox_geometry": (c_int, [c_void_p, c_int, c_int, c_int, c_float, c_int, c_int, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p]),
     # graph argtypes with struct pointers are (re)declared in mvpose/hrnet.py
     "mvp_graph_create": (c_int, None),
     "mvp_graph_forward": (c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p]),

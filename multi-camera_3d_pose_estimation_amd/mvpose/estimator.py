@@ -81,14 +81,19 @@ class BatchPoseEstimator:
                      for _ in range(2)]
         self._avg_busy = [None, None]   # side-stream event after the last moments read of each buffer
         self._avg_k = 1                 # buffer the last run wrote
-        # per-crop bbox geometry (run(bboxes=...)), double-buffered like the heatmaps: the side-stream
-        # moments of run i read revert_minv while run i+1 uploads its own; pinned host staging
+        # per-crop bbox geometry (run(bboxes=...)), formed on the device by mvp_bbox_geometry and
+        # double-buffered like the heatmaps: the side-stream moments of run i read revert_minv /
+        # the separability flags while run i+1 writes its own.  Host boxes go up through pinned
+        # staging.
         self._geo_dev = [(torch.empty((n, 6), dtype=torch.float64, device=self.device),
                           torch.empty((n, 6), dtype=torch.float64, device=self.device),
-                          torch.empty((n, 4), dtype=torch.float32, device=self.device)) for _ in range(2)]
-        self._geo_host = [None, None]
-        self._geo_copied = [None, None]  # event after the last H2D copy out of each host buffer
+                          torch.empty((n, 4), dtype=torch.float32, device=self.device),
+                          torch.empty((n,), dtype=torch.int32, device=self.device)) for _ in range(2)]
+        self._box_dev = [torch.empty((n, 4), dtype=torch.float32, device=self.device) for _ in range(2)]
+        self._box_host = [None, None]
+        self._box_copied = [None, None]  # event after the last H2D copy out of each host buffer
         self._side = None
+        self._last_revert = self.revert_minv
         self._mean = (ctypes.c_float * 3)(*MEAN)
         self._std = (ctypes.c_float * 3)(*STD)
         self._flip = (ctypes.c_int * N_JOINTS)(*COCO_FLIP_INDICES)
@@ -98,39 +103,50 @@ class BatchPoseEstimator:
         """Flip-averaged heatmaps of the last run (valid until the run after next)."""
         return self._avg[self._avg_k]
 
-    def _bbox_geometry(self, k: int, n: int, bboxes):
-        """Upload the crop geometry of n bboxes (xyxy; a row with a non-finite value = no
-        detection = the whole image) into geometry buffer k; returns (crop_minv,
-        revert_minv, center_scale, separable) device views."""
-        bb = np.array(bboxes, dtype=np.float64).reshape(-1, 4)
-        if bb.shape[0] != n:
-            raise ValueError(f"bboxes: {bb.shape[0]} boxes for {n} frames")
-        miss = ~np.isfinite(bb).all(axis=1)
-        bb[miss] = (0.0, 0.0, float(self.frame_w), float(self.frame_h))
-        cm, rm, cs = geometry.crop_geometry_batch(bb)
-        sep = all(warp_is_separable(m, self.frame_h, self.frame_w) for m in np.unique(rm, axis=0))
-        if self._geo_host[k] is None:
-            m = self.max_frames
-            self._geo_host[k] = (torch.empty((m, 6), dtype=torch.float64).pin_memory(),
-                                 torch.empty((m, 6), dtype=torch.float64).pin_memory(),
-                                 torch.empty((m, 4), dtype=torch.float32).pin_memory())
-        if self._geo_copied[k] is not None:     # the previous upload out of host buffer k is done
-            self._geo_copied[k].synchronize()
-        dev = self._geo_dev[k]
-        for host, d, a in zip(self._geo_host[k], dev, (cm, rm, cs)):
-            host[:n].copy_(torch.from_numpy(a))
-            d[:n].copy_(host[:n], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self._geo_copied[k] = ev
-        return dev[0][:n], dev[1][:n], dev[2][:n], sep
+    def _bbox_geometry(self, k: int, n: int, bboxes, bbox_thr):
+        """Crop geometry of n person boxes into geometry buffer k, on the device
+        (mvp_bbox_geometry): returns (crop_minv, revert_minv, center_scale, separable flags)
+        device views.  bboxes: a CUDA float32 tensor (n, >=4) — e.g. RTMDetector.detect's
+        per-frame best rows {x1, y1, x2, y2, score, prior}, used when score > bbox_thr — or
+        host (n, 4) xyxy boxes (a row with a non-finite value = no detection = the whole
+        image), uploaded through pinned staging."""
+        if isinstance(bboxes, torch.Tensor) and bboxes.is_cuda:
+            bx = bboxes
+            if bx.dtype != torch.float32 or bx.dim() != 2 or bx.shape[1] < 4 or not bx.is_contiguous():
+                raise ValueError("device bboxes must be a contiguous float32 (N, >=4) tensor")
+            score_col = 4 if (bbox_thr is not None and bx.shape[1] >= 5) else -1
+        else:
+            bb = np.asarray(bboxes.cpu() if isinstance(bboxes, torch.Tensor) else bboxes,
+                            dtype=np.float64).reshape(-1, 4).astype(np.float32)
+            if self._box_host[k] is None:
+                self._box_host[k] = torch.empty((self.max_frames, 4), dtype=torch.float32).pin_memory()
+            if self._box_copied[k] is not None:  # the previous upload out of host buffer k is done
+                self._box_copied[k].synchronize()
+            if bb.shape[0] != n:
+                raise ValueError(f"bboxes: {bb.shape[0]} boxes for {n} frames")
+            self._box_host[k][:n].copy_(torch.from_numpy(bb))
+            bx = self._box_dev[k][:n]
+            bx.copy_(self._box_host[k][:n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            self._box_copied[k] = ev
+            score_col = -1
+        if bx.shape[0] != n:
+            raise ValueError(f"bboxes: {bx.shape[0]} boxes for {n} frames")
+        cm, rm, cs, sep = (t[:n] for t in self._geo_dev[k])
+        call("mvp_bbox_geometry", _ptr(bx), int(bx.shape[1]), n, score_col,
+             ctypes.c_float(0.0 if bbox_thr is None else float(bbox_thr)), self.frame_h, self.frame_w, _ptr(cm),
+             _ptr(rm), _ptr(cs), _ptr(sep), _stream(self.device))
+        return cm, rm, cs, sep
 
     def run(self, frames: torch.Tensor, n_views: int = 1, kpts_tkv: torch.Tensor | None = None,
-            argmax: bool = False, overlap_moments: bool = False, bboxes=None):
+            argmax: bool = False, overlap_moments: bool = False, bboxes=None, bbox_thr: float | None = None):
         """frames: (N, H, W, 3) uint8 on the GPU, ordered (t, v) when n_views > 1.
-        bboxes: None (every crop = the whole image) or (N, 4) xyxy image boxes, one per
-        frame (a row of NaNs = no detection = the whole image), as the reference's
-        detector stage hands them to inference_topdown (mmpose_pose_estimation.py:242-253).
+        bboxes: None (every crop = the whole image), (N, 4) host xyxy image boxes (a row of
+        NaNs = no detection = the whole image), or a CUDA float32 (N, >=4) tensor such as the
+        detector's per-frame best rows, whose score column 4 is held against bbox_thr — the
+        reference's detector hand-off to inference_topdown (mmpose_pose_estimation.py:242-253).
+        Device boxes keep the whole run free of host synchronisation.
         Returns dict: keypoints (N,17,2) f32 image px, scores (N,17) f32,
         gaussians (N,17,6) f64 [mx,my,vxx,vxy,vxy,vyy], and optionally argmax.
         overlap_moments: gaussians are produced on a side stream; read them only after
@@ -149,12 +165,13 @@ class BatchPoseEstimator:
         main = torch.cuda.current_stream(dev)
         if bboxes is None:
             crop_minv, revert_minv, center_scale = self.crop_minv, self.revert_minv, self.center_scale
-            separable = self.separable
+            separable, sep_flags = int(self.separable), None
         else:
             if self._avg_busy[k] is not None:   # moments of two runs ago still reading geometry buffer k
                 main.wait_event(self._avg_busy[k])
                 self._avg_busy[k] = None
-            crop_minv, revert_minv, center_scale, separable = self._bbox_geometry(k, n, bboxes)
+            crop_minv, revert_minv, center_scale, sep_flags = self._bbox_geometry(k, n, bboxes, bbox_thr)
+            separable = 1
         call("mvp_preprocess", _ptr(frames), n, h, w, _ptr(crop_minv), INPUT_HW[0], INPUT_HW[1], self._mean,
              self._std, int(self.swap_rb), int(self.flip_test), _ptr(crops), s)
         hm = self.backbone.forward(crops, out=self.heatmaps[:nc])
@@ -182,24 +199,22 @@ class BatchPoseEstimator:
         else:
             ms = s
         call("mvp_heatmap_moments", _ptr(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(revert_minv),
-             h, w, ctypes.c_float(HEATMAP_THR), int(separable), _ptr(gauss), ms)
+             h, w, ctypes.c_float(HEATMAP_THR), separable, _ptr(sep_flags), _ptr(gauss), ms)
         if overlap_moments:
             done = torch.cuda.Event()
             done.record(self._side)
             self._avg_busy[k] = done
+        self._last_revert = revert_minv
         out = {"keypoints": kp, "scores": sc, "gaussians": gauss, "heatmaps": avg, "moments_done": done}
         if argmax:
             out["argmax"] = am
         return out
 
-    def revert_heatmaps(self, bbox=None, index: int = 0) -> np.ndarray:
-        """The last run's flip-averaged maps of frame `index`, reverted to the image
-        (mvp_heatmap_revert): (17, H, W) f32 numpy — mmpose's _pred_heatmaps for that crop."""
-        if bbox is None:
-            minv = self.revert_minv[:1]
-        else:
-            _, rm, _ = geometry.crop_geometry_batch([bbox])
-            minv = torch.tensor(rm, device=self.device)
+    def revert_heatmaps(self, index: int = 0) -> np.ndarray:
+        """The last run's flip-averaged maps of frame `index`, reverted to the image with that
+        run's crop geometry (mvp_heatmap_revert): (17, H, W) f32 numpy — mmpose's
+        _pred_heatmaps for that crop."""
+        minv = self._last_revert[index:index + 1]
         src = self.avg[index:index + 1].contiguous()
         out = torch.empty((1, N_JOINTS, self.frame_h, self.frame_w), dtype=torch.float32, device=self.device)
         call("mvp_heatmap_revert", _ptr(src), 1, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1], _ptr(minv), self.frame_h,
@@ -215,13 +230,14 @@ class BatchPoseEstimator:
     # ---- the reference's per-frame callable contract (pose_estimation.py:88, :104-110)
     def predict(self, frame, return_full_heatmaps=False, bbox=None):
         """Single frame (H, W, 3) uint8 numpy/tensor -> (pred_instances, heatmaps (17,6) f64)
-        with pred_instances['keypoints'] (1,17,2) f32 and ['keypoint_scores'] (1,17) f32.
+        with pred_instances['keypoints'] (1,17,2) f32 and ['keypoint_scores'] (1,17) f32;
+        with return_full_heatmaps the maps reverted to the image, (17, H, W) f32.
         bbox: optional xyxy person box (None = the whole image)."""
         f = torch.as_tensor(np.ascontiguousarray(frame), device=self.device).reshape(1, *np.shape(frame))
         r = self.run(f.contiguous(), bboxes=None if bbox is None else [bbox])
         inst = {"keypoints": r["keypoints"].cpu().numpy(), "keypoint_scores": r["scores"].cpu().numpy()}
         if return_full_heatmaps:
-            return inst, r["heatmaps"][0].cpu().numpy()
+            return inst, self.revert_heatmaps(0)
         return inst, r["gaussians"][0].cpu().numpy()
 
     __call__ = predict

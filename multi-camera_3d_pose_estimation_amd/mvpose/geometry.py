@@ -109,7 +109,7 @@ def save_camera_names(extrinsic_params_dir, index_name, origin_name):
 
 # ------------------------------------------------------------ top-down crops
 def bbox_center_scale(bbox_xyxy, padding=BBOX_PADDING):
-    x1, y1, x2, y2 = [float(v) for v in bbox_xyxy]
+    x1, y1, x2, y2 = [float(np.float32(v)) for v in bbox_xyxy]
     center = (np.array([x1 + x2, y1 + y2], np.float32) * 0.5).astype(np.float32)
     scale = (np.array([x2 - x1, y2 - y1], np.float32) * padding).astype(np.float32)
     return center, scale
@@ -120,17 +120,59 @@ def fix_aspect_ratio(scale, aspect_ratio):
     return np.array([w, w / aspect_ratio] if w > h * aspect_ratio else [h * aspect_ratio, h], np.float32)
 
 
-def affine_from_points(src, dst):
-    """The 6x6 system cv2.getAffineTransform solves (float32 points, fp64 solve)."""
-    src = np.asarray(src, np.float32).astype(np.float64)
-    dst = np.asarray(dst, np.float32).astype(np.float64)
-    A = np.zeros((6, 6))
-    b = np.zeros(6)
+def lu_solve_batch(A, b):
+    """cv::solve(DECOMP_LU) for N m x m systems at once: OpenCV's hal::LU64f (LUImpl,
+    modules/core/src/matrix_decomp.cpp) — the pivot is the first row with the largest
+    |a| of the column, d = -1 / pivot, rows updated a += (a_ji·d)·a_i, back substitution
+    s -= a_ik·b_k then s / a_ii; a pivot below 100·DBL_EPSILON = failure = zeros.  numpy
+    elementwise fp64 (no FMA), so the roundings are OpenCV's; mvp_bbox_geometry does the
+    same on the device.  A (N, m, m), b (N, m) float64 -> (N, m)."""
+    a = np.array(A, np.float64, copy=True)
+    x = np.array(b, np.float64, copy=True)
+    n, m = x.shape
+    rows = np.arange(n)
+    bad = np.zeros(n, bool)
+    for i in range(m):
+        k = i + np.argmax(np.abs(a[:, i:, i]), axis=1)      # first maximum = OpenCV's strict '>' scan
+        bad |= np.abs(a[rows, k, i]) < 100 * np.finfo(np.float64).eps
+        ai, ak = a[rows, i].copy(), a[rows, k].copy()
+        a[rows, i], a[rows, k] = ak, ai
+        xi, xk = x[rows, i].copy(), x[rows, k].copy()
+        x[rows, i], x[rows, k] = xk, xi
+        with np.errstate(divide="ignore", invalid="ignore"):
+            d = -1.0 / a[:, i, i]
+            for j in range(i + 1, m):
+                alpha = a[:, j, i] * d
+                a[:, j, i + 1:] += alpha[:, None] * a[:, i, i + 1:]
+                x[:, j] += alpha * x[:, i]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        for i in range(m - 1, -1, -1):
+            s = x[:, i].copy()
+            for c in range(i + 1, m):
+                s -= a[:, i, c] * x[:, c]
+            x[:, i] = s / a[:, i, i]
+    x[bad] = 0.0
+    return x
+
+
+def _affine_system(src, dst):
+    """cv2.getAffineTransform's 6x6 system for N point triples: src, dst (N, 3, 2) f32."""
+    s = np.asarray(src, np.float32).astype(np.float64)
+    d = np.asarray(dst, np.float32).astype(np.float64)
+    n = s.shape[0]
+    A = np.zeros((n, 6, 6))
+    b = np.zeros((n, 6))
     for i in range(3):
-        A[2 * i, :3] = (src[i, 0], src[i, 1], 1.0)
-        A[2 * i + 1, 3:] = (src[i, 0], src[i, 1], 1.0)
-        b[2 * i], b[2 * i + 1] = dst[i]
-    return np.linalg.solve(A, b).reshape(2, 3)
+        A[:, 2 * i, 0], A[:, 2 * i, 1], A[:, 2 * i, 2] = s[:, i, 0], s[:, i, 1], 1.0
+        A[:, 2 * i + 1, 3], A[:, 2 * i + 1, 4], A[:, 2 * i + 1, 5] = s[:, i, 0], s[:, i, 1], 1.0
+        b[:, 2 * i], b[:, 2 * i + 1] = d[:, i, 0], d[:, i, 1]
+    return A, b
+
+
+def affine_from_points(src, dst):
+    """cv2.getAffineTransform (imgwarp.cpp): the 6x6 system solved by cv::solve's LU."""
+    A, b = _affine_system(np.asarray(src)[None], np.asarray(dst)[None])
+    return lu_solve_batch(A, b)[0].reshape(2, 3)
 
 
 def warp_matrix(center, scale, output_size, inv=False):
@@ -186,17 +228,8 @@ def _warp_points(center, scale_w, out_w, out_h):
 
 
 def _affine_batch(src, dst):
-    """affine_from_points for N point triples (the same 6x6 systems, solved batched)."""
-    s = src.astype(np.float64)
-    d = dst.astype(np.float64)
-    n = s.shape[0]
-    A = np.zeros((n, 6, 6))
-    b = np.zeros((n, 6))
-    for i in range(3):
-        A[:, 2 * i, 0], A[:, 2 * i, 1], A[:, 2 * i, 2] = s[:, i, 0], s[:, i, 1], 1.0
-        A[:, 2 * i + 1, 3], A[:, 2 * i + 1, 4], A[:, 2 * i + 1, 5] = s[:, i, 0], s[:, i, 1], 1.0
-        b[:, 2 * i], b[:, 2 * i + 1] = d[:, i, 0], d[:, i, 1]
-    return np.linalg.solve(A, b[..., None])[..., 0]
+    """affine_from_points for N point triples."""
+    return lu_solve_batch(*_affine_system(src, dst))
 
 
 def _inverse_map_batch(M):
@@ -219,8 +252,9 @@ def crop_geometry_batch(bboxes_xyxy, padding=BBOX_PADDING):
     """Vectorised CropGeometry for N boxes: (crop_minv (N,6) f64, revert_minv (N,6) f64,
     center_scale (N,4) f32) — the same numbers CropGeometry(box) gives one box at a time
     (mmpose bbox_xyxy2cs -> TopdownAffine -> get_warp_matrix, mmpose_pose_estimation.py:253)."""
-    bb = np.asarray(bboxes_xyxy, np.float64).reshape(-1, 4)
-    x1, y1, x2, y2 = (bb[:, i] for i in range(4))   # sums in fp64, then f32 (bbox_center_scale)
+    # mmdet's boxes are float32; the f32 sums / differences are formed exactly in fp64 and rounded once
+    bb = np.asarray(bboxes_xyxy, np.float64).reshape(-1, 4).astype(np.float32).astype(np.float64)
+    x1, y1, x2, y2 = (bb[:, i] for i in range(4))
     center = (np.stack([x1 + x2, y1 + y2], 1).astype(np.float32) * np.float32(0.5)).astype(np.float32)
     scale = (np.stack([x2 - x1, y2 - y1], 1).astype(np.float32) * np.float32(padding)).astype(np.float32)
     ar = INPUT_SIZE[0] / INPUT_SIZE[1]

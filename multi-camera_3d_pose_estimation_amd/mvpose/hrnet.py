@@ -155,6 +155,25 @@ def random_state_dict(seed: int = 0, stable: bool = True):
     return sd
 
 
+PEAKED_BASE_SEED = 21
+PEAKED_WEIGHTS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "hrnet_w32_peaked.npz")
+
+
+def peaked_state_dict():
+    """random_state_dict(PEAKED_BASE_SEED) with the last stage-4 module's high-resolution branch,
+    its fuse projections and the HeatmapHead replaced by tensors fitted on rendered skeleton
+    frames (tools/train_peaked_hrnet.py; data/hrnet_w32_peaked.npz, loaded without pickle):
+    heatmaps with one clear, trained-model-like peak per joint on
+    synthetic.make_skeleton_frames inputs, for parity tests that must not sit on near-ties."""
+    sd = random_state_dict(PEAKED_BASE_SEED)
+    with np.load(PEAKED_WEIGHTS, allow_pickle=False) as z:
+        for k in z.files:
+            if k not in sd or tuple(sd[k].shape) != z[k].shape:
+                raise ValueError(f"{PEAKED_WEIGHTS}: unexpected tensor {k} {z[k].shape}")
+            sd[k] = torch.from_numpy(z[k].copy())
+    return sd
+
+
 def fold_bn(sd, conv, bn):
     """conv weight (cout,cin,k,k) + eval BatchNorm -> (w (cout,k,k,cin) f64, b (cout,) f64)."""
     w = sd[conv + ".weight"].double().numpy()

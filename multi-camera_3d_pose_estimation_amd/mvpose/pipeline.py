@@ -32,6 +32,7 @@ class MultiViewPipeline:
         score > bbox_thr, else the whole image), or None (whole-image crops)."""
         self.detector = detector
         self.bbox_thr = bbox_thr
+        self._best = None
         self.device = torch.device(device)
         self.n_views = len(camera_params)
         self.cams = torch.tensor(ops.pack_cameras(camera_params), device=self.device)
@@ -45,7 +46,8 @@ class MultiViewPipeline:
 
     def process(self, frames: torch.Tensor, out: dict | None = None, overlap_moments: bool = False,
                 bboxes=None) -> dict:
-        """bboxes: None (whole-image crops) or (T, V, 4) xyxy person boxes (NaN row = none)."""
+        """bboxes: None (the detector's boxes, or whole-image crops without one), host (T, V, 4)
+        xyxy person boxes (NaN row = none), or device rows (T, V, >=4) f32 used as given."""
         T, V = frames.shape[:2]
         if V != self.n_views:
             raise ValueError(f"frames carry {V} views, pipeline has {self.n_views} cameras")
@@ -55,11 +57,15 @@ class MultiViewPipeline:
         if "kpts_2d" not in out or tuple(out["kpts_2d"].shape) != (T, N_JOINTS, 3, V):
             out["kpts_2d"] = torch.empty((T, N_JOINTS, 3, V), dtype=torch.float32, device=self.device)
             out.pop("kpts_3d", None)
+        thr = None
         if bboxes is None and self.detector is not None:
-            bb = self.detect(flat)
+            bb, thr = self.detect(flat), self.bbox_thr       # device rows: no host round trip
+        elif isinstance(bboxes, torch.Tensor) and bboxes.is_cuda:
+            bb = bboxes.reshape(T * V, -1)
         else:
             bb = None if bboxes is None else np.asarray(bboxes, np.float64).reshape(T * V, 4)
-        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments, bboxes=bb)
+        r = self.estimator.run(flat, n_views=V, kpts_tkv=out["kpts_2d"], overlap_moments=overlap_moments, bboxes=bb,
+                               bbox_thr=thr)
         out["heatmaps_2d"] = r["gaussians"].reshape(T, V, N_JOINTS, 6)
         if r["moments_done"] is not None:
             out["moments_done"] = r["moments_done"]
@@ -69,12 +75,17 @@ class MultiViewPipeline:
                                          out=out.get("kpts_3d"))
         return out
 
-    def detect(self, flat: torch.Tensor) -> np.ndarray:
-        """(T*V, H, W, 3) camera-frames -> (T*V, 4) person boxes (NaN rows: whole image)."""
-        from .rtmdet import RTMDetector
+    def detect(self, flat: torch.Tensor) -> torch.Tensor:
+        """(T*V, H, W, 3) camera-frames -> the detector's per-frame best rows (T*V, 6) f32 on the
+        device {x1, y1, x2, y2, score, prior}; BatchPoseEstimator.run applies score > bbox_thr
+        and derives the crops there (mvp_bbox_geometry)."""
+        n = flat.shape[0]
+        if self._best is None or self._best.shape[0] < n:
+            self._best = torch.empty((n, 6), dtype=torch.float32, device=self.device)
         mb = self.detector.max_batch
-        return np.concatenate([RTMDetector.bboxes_for(self.detector.detect(flat[i:i + mb])["best"], self.bbox_thr)
-                               for i in range(0, flat.shape[0], mb)])
+        for i in range(0, n, mb):
+            self.detector.detect(flat[i:i + mb], best_out=self._best[i:min(n, i + mb)])
+        return self._best[:n]
 
     @staticmethod
     def wait(out: dict) -> None:

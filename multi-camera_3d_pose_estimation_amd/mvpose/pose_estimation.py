@@ -13,9 +13,10 @@
   array of frames as a video decoder (BGR) returns them, an MJPEG / uncompressed AVI
   or a directory of frame<N>.jpg files (``mvpose.video``).
 * ``run_pose_est`` (:157-244) and ``estimate_pose_from_video`` (:259-327): every
-  frame of every camera through the batched GPU pipeline (crop, HRNet-W32 with
-  flip test, decode, heatmap moments), then get_pose_3D over ``camera_indices=[0, 1]``
-  as the reference hard-codes (:319).
+  frame of every camera through the batched GPU pipeline (RTMDet-m person box ->
+  crop, HRNet-W32 with flip test, decode, heatmap moments), then get_pose_3D over
+  ``camera_indices=[0, 1]`` as the reference hard-codes (:319).  A model name builds
+  PoseEstimator(detector, pose model) from model_yaml exactly as :290-297 does.
 """
 from __future__ import annotations
 
@@ -55,22 +56,18 @@ def get_pose_3D(camera_params, all_kpts_2d, world_trans_rot=None, camera_indices
 def get_pose_2D(frames, model, confidence=0.5, pose_keypoints=range(17)):
     """pose_estimation.py:71-151.  frames: V frames (H, W, 3) uint8 of one time step.
 
-    model: a BatchPoseEstimator / mvpose PoseEstimator (the V frames go through the GPU
-    in ONE batched run), or any per-frame callable with the reference's contract
+    model: a BatchPoseEstimator / mvpose PoseEstimator or one's bound predict (the V frames
+    go through the GPU in ONE batched run, detector included), or any per-frame callable with the reference's contract
     (model(frame) -> (pred_instances, heatmaps); an onepose-style model's dict output
     with 'points' / 'confidence' is parsed as the reference does, :99-101).
     Returns (results_stacked (17, 3, V) float32, heatmaps list of V arrays).
     confidence and pose_keypoints select only the keypoints the reference DRAWS on the
     frames (:117-131, then discarded with the GUI window), so they do not change the
     output — as in the reference."""
-    from .mmpose_pose_estimation import PoseEstimator
-    if isinstance(model, (BatchPoseEstimator, PoseEstimator)):
-        est = model if isinstance(model, BatchPoseEstimator) else None
+    est = resolve_estimator(model)
+    if est is not None:
         batch = np.ascontiguousarray(np.stack([np.asarray(f) for f in frames]))
-        if est is None:
-            r = model.predict_batch(batch)
-        else:
-            r = est.run(torch.from_numpy(batch).to(est.device).contiguous())
+        r = est.run(torch.from_numpy(batch).to(est.device).contiguous())
         pts = r["keypoints"].cpu().numpy()
         conf = r["scores"].cpu().numpy()
         heat = list(r["gaussians"].cpu().numpy())
@@ -110,28 +107,42 @@ def load_frames(recording_paths, start_end_frames=(0, -1)):
     return out
 
 
+def resolve_estimator(model):
+    """The GPU estimator behind the reference's `model` argument, or None: a BatchPoseEstimator
+    or mvpose PoseEstimator, or one's bound predict (what estimate_pose_from_video passes,
+    `model = model_structure.predict`, pose_estimation.py:297)."""
+    from .mmpose_pose_estimation import PoseEstimator
+    obj = getattr(model, "__self__", model)
+    return obj if isinstance(obj, (BatchPoseEstimator, PoseEstimator)) else None
+
+
 def build_estimator(model, detector_model="coco_base", model_yaml="", frame_hw=(720, 1280), max_frames=256,
                     device=None):
-    """A BatchPoseEstimator for the reference's model argument: an estimator instance, or a
-    model name looked up in model_yaml (pose_estimators: {name: [config, checkpoint]}) whose
-    checkpoint is a LOCAL mmpose HRNet-W32 .pth (loaded with weights_only=True).
-    MVPOSE_RANDOM_WEIGHTS=1 selects seeded random weights (synthetic runs/tests)."""
-    if isinstance(model, BatchPoseEstimator):
-        return model
+    """The estimator estimate_pose_from_video builds for a model NAME (pose_estimation.py:
+    290-297): PoseEstimator(det_cfg, det_ckpt, pose_cfg, pose_ckpt) from model_yaml's
+    detectors[detector_model] and pose_estimators[model] entries — a detector always sits in
+    front, as in the reference.  Checkpoints must be LOCAL files (weights_only loads);
+    MVPOSE_RANDOM_WEIGHTS=1 / MVPOSE_RANDOM_DETECTOR=1 select seeded synthetic weights (the yaml
+    may then be absent), MVPOSE_NO_DETECTOR=1 opts out of the detector (whole-image crops).
+    An estimator object (or its bound predict) is returned as is.  frame_hw is accepted for
+    compatibility: the estimator sizes itself to the first frames it sees."""
+    from .mmpose_pose_estimation import PoseEstimator
+    est = resolve_estimator(model)
+    if est is not None:
+        return est
     dev = torch.device(device if device is not None else "cuda")
-    sd = None
-    if os.environ.get("MVPOSE_RANDOM_WEIGHTS") != "1":
-        if not model_yaml or not os.path.exists(model_yaml):
-            raise FileNotFoundError(f"model_yaml {model_yaml!r} not found (set MVPOSE_RANDOM_WEIGHTS=1 for "
-                                    "random weights)")
+    det_cfg = det_ckpt = pose_cfg = pose_ckpt = None
+    if model_yaml and os.path.exists(model_yaml):
         with open(model_yaml) as f:
-            paths = yaml.safe_load(f)
-        _, ckpt = paths["pose_estimators"][model]
-        if not os.path.exists(ckpt):
-            raise FileNotFoundError(f"pose checkpoint {ckpt!r} is not a local file (no network here)")
-        blob = torch.load(ckpt, map_location="cpu", weights_only=True)
-        sd = blob.get("state_dict", blob)
-    return BatchPoseEstimator(sd, max_frames=max_frames, frame_hw=tuple(frame_hw), swap_rb=False, device=dev)
+            paths = yaml.safe_load(f) or {}
+        det_cfg, det_ckpt = paths.get("detectors", {}).get(detector_model, (None, None))
+        if model not in paths.get("pose_estimators", {}) and os.environ.get("MVPOSE_RANDOM_WEIGHTS") != "1":
+            raise KeyError(f"pose estimator {model!r} not in {model_yaml}'s pose_estimators")
+        pose_cfg, pose_ckpt = paths.get("pose_estimators", {}).get(model, (None, None))
+    elif os.environ.get("MVPOSE_RANDOM_WEIGHTS") != "1":
+        raise FileNotFoundError(f"model_yaml {model_yaml!r} not found (set MVPOSE_RANDOM_WEIGHTS=1 for random "
+                                "weights)")
+    return PoseEstimator(det_cfg, det_ckpt, pose_cfg, pose_ckpt, device=dev, max_frames=max_frames)
 
 
 class FrameStreamer:
@@ -142,23 +153,37 @@ class FrameStreamer:
     frames into a PINNED staging buffer (numpy copies release the GIL), the H2D copy runs
     on a dedicated copy stream, and the estimator consumes the device buffer on the
     compute stream — so chunk i+1's gather and copy overlap chunk i's kernels.  Two pinned
-    and two device buffers; every hand-off is an event (no host synchronisation inside the
-    loop).  Outputs accumulate on the device and come back with one copy at the end."""
+    and two device buffers (each capped at `max_staging_bytes`); every hand-off is an event
+    (no host synchronisation inside the loop).  With a PoseEstimator the detector runs on
+    each chunk on the device and its boxes crop the frames (mmpose_pose_estimation.py:
+    234-253).  Outputs accumulate on the device and come back with one copy at the end.
+    Use as a context manager (or call close()) to release the gather threads."""
 
-    def __init__(self, est: BatchPoseEstimator, n_views: int, frame_hw, batch_frames: int = 128,
-                 gather_threads: int = 8):
+    def __init__(self, est, n_views: int, frame_hw, batch_frames: int = 128, gather_threads: int = 8,
+                 max_staging_bytes: int = 512 << 20):
         from concurrent.futures import ThreadPoolExecutor
         self.est = est
         self.pool = ThreadPoolExecutor(max_workers=max(1, min(int(gather_threads), os.cpu_count() or 1)))
         self.V = int(n_views)
         self.H, self.W = (int(v) for v in frame_hw)
-        self.step = max(1, min(int(batch_frames), est.max_frames // self.V))
+        per_frame = self.V * self.H * self.W * 3
+        self.step = max(1, min(int(batch_frames), est.max_frames // self.V, int(max_staging_bytes) // per_frame))
         shape = (self.step, self.V, self.H, self.W, 3)
+        self.device = est.device
         self.host = [torch.empty(shape, dtype=torch.uint8).pin_memory() for _ in range(2)]
-        self.dev = [torch.empty(shape, dtype=torch.uint8, device=est.device) for _ in range(2)]
-        self.copy_stream = torch.cuda.Stream(est.device)
+        self.dev = [torch.empty(shape, dtype=torch.uint8, device=self.device) for _ in range(2)]
+        self.copy_stream = torch.cuda.Stream(self.device)
         self.copied = [None, None]     # copy-stream event: H2D of buffer k done (host buffer reusable)
         self.consumed = [None, None]   # compute-stream event: kernels done reading device buffer k
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     def _gather(self, stacks, t0, t1, k):
         """Chunk [t0, t1) of every camera into pinned buffer k, in pieces of 4 frames over the
@@ -177,7 +202,7 @@ class FrameStreamer:
         device tensors kpts_2d (T, 17, 3, V) f32 and heatmaps (T, V, 17, 6) f64."""
         from concurrent.futures import ThreadPoolExecutor
         T = min(len(s) for s in stacks) if n_frames is None else int(n_frames)
-        dev = self.est.device
+        dev = self.device
         kp = torch.empty((T, N_JOINTS, 3, self.V), dtype=torch.float32, device=dev)
         hm = torch.empty((T, self.V, N_JOINTS, 6), dtype=torch.float64, device=dev)
         chunks = [(t, min(T, t + self.step)) for t in range(0, T, self.step)]
@@ -212,15 +237,27 @@ class FrameStreamer:
 
 def run_pose_est(model, confidence=0.5, camera_indices=None, recording_paths=None, start_end_frames=(0, -1),
                  frame_shape=(1080, 1920), batch_frames=128):
-    """-> kpts_2d (T, 17, 3, V) float32, heatmaps (T, V, 17, 6) float64 (numpy).
-    recording_paths values may also be in-memory (T, H, W, 3) uint8 arrays."""
+    """pose_estimation.py:157-244 -> kpts_2d (T, 17, 3, V) float32, heatmaps (T, V, 17, 6)
+    float64 (numpy).  recording_paths values may also be in-memory (T, H, W, 3) uint8 arrays.
+
+    model: a PoseEstimator (detector in front) / BatchPoseEstimator or one's bound predict ->
+    every frame through the batched GPU path (FrameStreamer); a model name -> build_estimator;
+    any other per-frame callable with the reference's contract -> get_pose_2D frame by frame,
+    as the reference loops (:184-190).  confidence does not change the output (it only
+    selects what the reference draws, :117-131)."""
     frames = load_frames(recording_paths, start_end_frames)
     cams = list(frames.keys()) if camera_indices is None else list(camera_indices)
     stacks = [frames[c] for c in cams]
     V = len(stacks)
     H, W = stacks[0].shape[1:3]
-    est = model if isinstance(model, BatchPoseEstimator) else build_estimator(model, frame_hw=(H, W))
-    kp, hm = FrameStreamer(est, V, (H, W), batch_frames).run(stacks)
+    est = build_estimator(model, frame_hw=(H, W)) if isinstance(model, str) else resolve_estimator(model)
+    if est is None:                                   # a generic per-frame callable
+        T = min(len(s) for s in stacks)
+        res = [get_pose_2D([s[t] for s in stacks], model, confidence) for t in range(T)]
+        return (np.array([r[0] for r in res], dtype=np.float32).reshape(T, N_JOINTS, 3, V),
+                np.array([r[1] for r in res]))
+    with FrameStreamer(est, V, (H, W), batch_frames) as fs:
+        kp, hm = fs.run(stacks)
     return kp.cpu().numpy(), hm.cpu().numpy()
 
 
@@ -243,7 +280,7 @@ def estimate_pose_from_video(camera_names, recording_paths, model, detector_mode
     else:
         paths = {i: recording_paths[i] for i in camera_indices}   # as :281 indexes them
         frames = load_frames(paths, start_end_frames)          # decoded once
-        if isinstance(model, str):
+        if isinstance(model, str):                             # :290-297: detector + pose model from the yaml
             model = build_estimator(model, detector_model, model_yaml, frame_hw=frames[camera_indices[0]].shape[1:3])
         kpts_2d, heatmaps = run_pose_est(model, confidence=confidence, camera_indices=camera_indices,
                                          recording_paths=frames, start_end_frames=(0, None))

@@ -474,7 +474,12 @@ class RTMDetector:
         nh, nw = rescale_size(h, w, self.size)
         return float(np.float32(1.0 / (nw / w))), float(np.float32(1.0 / (nh / h)))
 
-    def detect(self, frames: torch.Tensor, letterboxed: torch.Tensor | None = None) -> dict:
+    def detect(self, frames: torch.Tensor, letterboxed: torch.Tensor | None = None,
+               best_out: torch.Tensor | None = None) -> dict:
+        """Stream-ordered detection of up to max_batch camera-frames.  The returned 'cand' (and
+        'best', unless best_out is given) are VIEWS of this detector's persistent buffers:
+        the next detect() overwrites them, so clone what must outlive it.  best_out: a
+        caller-owned contiguous float32 (N, 6) CUDA tensor that receives the best rows."""
         if frames.dtype != torch.uint8 or not frames.is_cuda or frames.dim() != 4 or frames.shape[3] != 3:
             raise ValueError("frames must be a (N, H, W, 3) uint8 CUDA tensor")
         frames = frames.contiguous()
@@ -482,6 +487,11 @@ class RTMDetector:
         if n > self.max_batch:
             raise ValueError(f"batch {n} > max_batch {self.max_batch}")
         cand, best = self.cand[:n], self.best[:n]
+        if best_out is not None:
+            if (best_out.dtype != torch.float32 or tuple(best_out.shape) != (n, 6) or not best_out.is_contiguous()
+                    or not best_out.is_cuda):
+                raise ValueError(f"best_out must be a contiguous float32 ({n}, 6) CUDA tensor")
+            best = best_out
         lb = ctypes.c_void_p(letterboxed.data_ptr()) if letterboxed is not None else None
         call("mvp_det_forward", self._h, ctypes.c_void_p(frames.data_ptr()), n, h, w,
              ctypes.c_float(self.cfg["score_thr"]), ctypes.c_void_p(cand.data_ptr()),

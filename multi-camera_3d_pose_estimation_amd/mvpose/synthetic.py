@@ -142,3 +142,85 @@ def make_frames(n: int, seed: int = 0, h: int = FRAME_H, w: int = FRAME_W):
     """(n, H, W, 3) uint8 uniform random frames."""
     rng = np.random.default_rng(seed)
     return rng.integers(0, 256, (n, h, w, 3), dtype=np.uint8)
+
+
+# ------------------------------------------------------------- rendered people --
+# Colour per COCO joint pair (nose alone): a joint and its left / right partner share a
+# colour and the subject's LEFT joint is the one further right in the image (a frontal
+# person), so the flip test's left/right swap is consistent with what the picture shows.
+_PAIR_COLORS = np.array([[230, 40, 40], [40, 220, 40], [50, 80, 240], [235, 225, 40], [225, 50, 220],
+                         [40, 220, 225], [245, 245, 245], [245, 140, 30], [140, 60, 200]], np.uint8)
+_PAIR_OF_JOINT = np.array([0, 1, 1, 2, 2, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8])
+HEATMAP_OFFSET = (0.0, 0.25)   # sub-cell (x, y) position of the rendered joints on the heatmap grid
+
+
+def _whole_image_heatmap_to_image(h: int, w: int):
+    """(scale, offset) of the whole-image crop's heatmap -> image map (mmpose restore:
+    kp / input_size * scale + center - scale / 2 with kp = 4 * heatmap cell)."""
+    sw, sh = 1.25 * w, 1.25 * h
+    sw, sh = (sw, sw / 0.75) if sw > sh * 0.75 else (sh * 0.75, sh)
+    return np.array([sw / 48.0, sh / 64.0]), np.array([w / 2.0 - sw / 2.0, h / 2.0 - sh / 2.0])
+
+
+def skeleton_layout(rng, h: int = FRAME_H, w: int = FRAME_W, min_dist: float = 3.0):
+    """17 joint positions on the heatmap grid of the whole-image crop (cells + HEATMAP_OFFSET),
+    inside the frame, pairwise >= min_dist cells apart, each left joint 2-7 cells to the
+    image right of its right partner."""
+    k, off = _whole_image_heatmap_to_image(h, w)
+    lo = np.ceil((np.array([40.0, 40.0]) - off) / k).astype(int)
+    hi = np.floor((np.array([w - 40.0, h - 40.0]) - off) / k).astype(int)
+    for _ in range(1000):
+        pts = np.zeros((N_JOINTS, 2))
+        placed = []
+        ok = True
+        for j in [0] + list(range(2, N_JOINTS, 2)):      # the nose, then each right joint with its left partner
+            for _try in range(200):
+                p = rng.integers(lo, hi + 1).astype(float)
+                cand = [p]
+                if j > 0:
+                    q = p + np.array([rng.integers(2, 8), rng.integers(-2, 3)])
+                    if not ((lo <= q).all() and (q <= hi).all()):
+                        continue
+                    cand.append(q)
+                if all(np.hypot(*(c - d)) >= min_dist for c in cand for d in placed):
+                    break
+            else:
+                ok = False
+                break
+            placed += cand
+            if j == 0:
+                pts[0] = p
+            else:
+                pts[j], pts[j - 1] = p, cand[1]              # right joint j, left joint j - 1 (to its image right)
+        if ok:
+            return pts + np.array(HEATMAP_OFFSET)
+    raise RuntimeError("skeleton_layout: no layout found")
+
+
+def make_skeleton_frames(n: int, seed: int = 0, h: int = FRAME_H, w: int = FRAME_W, radius: float = 0.9):
+    """(frames (n, H, W, 3) uint8, joints (n, 17, 2) heatmap-grid cells of the whole-image crop):
+    dark noisy backgrounds with one coloured disc per COCO joint (radius in heatmap cells), laid
+    out by skeleton_layout.  The test / training input for weights with trained-model-like
+    peaked heatmaps (tools/train_peaked_hrnet.py, tests/test_e2e_parity_gpu.py)."""
+    rng = np.random.default_rng(seed)
+    k, off = _whole_image_heatmap_to_image(h, w)
+    frames = np.empty((n, h, w, 3), np.uint8)
+    joints = np.empty((n, N_JOINTS, 2))
+    ys, xs = np.mgrid[0:h, 0:w]
+    for i in range(n):
+        base = rng.integers(20, 90, 3)
+        img = np.clip(base + rng.normal(0.0, 6.0, (h, w, 3)), 0, 255)
+        cells = skeleton_layout(rng, h, w)
+        # the crop samples pixel centres: heatmap position c <-> image coordinate c * k + off
+        centers = cells * k + off
+        r = radius * k[0]
+        for j in range(N_JOINTS):
+            cx, cy = centers[j]
+            x0, x1 = int(max(0, cx - r - 1)), int(min(w, cx + r + 2))
+            y0, y1 = int(max(0, cy - r - 1)), int(min(h, cy + r + 2))
+            m = (xs[y0:y1, x0:x1] - cx) ** 2 + (ys[y0:y1, x0:x1] - cy) ** 2 <= r * r
+            col = _PAIR_COLORS[_PAIR_OF_JOINT[j]].astype(float) + rng.normal(0.0, 6.0, 3)
+            img[y0:y1, x0:x1][m] = col
+        frames[i] = img.astype(np.uint8)
+        joints[i] = cells
+    return frames, joints

@@ -37,8 +37,9 @@ STD_RGB = np.array([58.395, 57.12, 57.375], np.float32)
 
 # ---------------------------------------------------------------- geometry --
 def bbox_xyxy2cs(bbox, padding=1.25):
-    """mmpose bbox_xyxy2cs: (x1,y1,x2,y2) -> center, scale (float32)."""
-    x1, y1, x2, y2 = [float(v) for v in bbox]
+    """mmpose bbox_xyxy2cs: (x1,y1,x2,y2) -> center, scale (float32).  The box is
+    mmdet's float32 bboxes row (mmpose_pose_estimation.py:242-253)."""
+    x1, y1, x2, y2 = [float(np.float32(v)) for v in bbox]
     center = np.array([x1 + x2, y1 + y2], np.float32) * 0.5
     scale = np.array([x2 - x1, y2 - y1], np.float32) * padding
     return center.astype(np.float32), scale.astype(np.float32)
@@ -58,9 +59,43 @@ def fix_aspect_ratio(scale, aspect_ratio):
     return np.array([h * aspect_ratio, h], np.float32)
 
 
+def cv_lu_solve(a, b):
+    """cv::solve(DECOMP_LU) on an m x m system: OpenCV 4.9 hal::LU64f -> LUImpl
+    (modules/core/src/matrix_decomp.cpp; external, parity unpinned — OpenCV is absent
+    here): column pivot = the first row with the largest |a| (strict >), d = -1/pivot,
+    row update a[j][k] += (a[j][i]·d)·a[i][k], back substitution s -= a[i][k]·b[k],
+    b[i] = s / a[i][i].  A pivot below 100·DBL_EPSILON makes solve() fail and return
+    zeros.  Plain Python floats (IEEE fp64, no FMA), so every rounding is OpenCV's."""
+    a = [[float(v) for v in row] for row in np.asarray(a, np.float64)]
+    b = [float(v) for v in np.asarray(b, np.float64).ravel()]
+    m = len(b)
+    for i in range(m):
+        k = i
+        for j in range(i + 1, m):
+            if abs(a[j][i]) > abs(a[k][i]):
+                k = j
+        if abs(a[k][i]) < 100 * np.finfo(np.float64).eps:
+            return np.zeros(m)
+        if k != i:
+            a[i], a[k] = a[k], a[i]
+            b[i], b[k] = b[k], b[i]
+        d = -1.0 / a[i][i]
+        for j in range(i + 1, m):
+            alpha = a[j][i] * d
+            for c in range(i + 1, m):
+                a[j][c] += alpha * a[i][c]
+            b[j] += alpha * b[i]
+    for i in range(m - 1, -1, -1):
+        s = b[i]
+        for c in range(i + 1, m):
+            s -= a[i][c] * b[c]
+        b[i] = s / a[i][i]
+    return np.array(b)
+
+
 def get_affine_transform(src, dst):
-    """cv2.getAffineTransform: the 6x6 system OpenCV builds, solved by LU with
-    partial pivoting (numpy/LAPACK dgesv stands in for cv::solve(DECOMP_LU))."""
+    """cv2.getAffineTransform (imgwarp.cpp): the 6x6 system OpenCV builds (rows
+    (x, y, 1, 0, 0, 0) and (0, 0, 0, x, y, 1) per point), solved by cv::solve's LU."""
     src = np.asarray(src, np.float32).astype(np.float64)
     dst = np.asarray(dst, np.float32).astype(np.float64)
     a = np.zeros((6, 6))
@@ -70,7 +105,7 @@ def get_affine_transform(src, dst):
         a[2 * i + 1, 3:6] = [src[i, 0], src[i, 1], 1.0]
         b[2 * i] = dst[i, 0]
         b[2 * i + 1] = dst[i, 1]
-    return np.linalg.solve(a, b).reshape(2, 3)
+    return cv_lu_solve(a, b).reshape(2, 3)
 
 
 def _rotate_point(pt, angle_rad):

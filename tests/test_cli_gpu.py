@@ -1,6 +1,6 @@
 """GPU: the drop-in command lines end to end on a synthetic project directory.
 
-record_and_estimate_pose (random weights, 2 cameras, decoded frames as .npy)
+record_and_estimate_pose (random pose + detector weights, 2 cameras, decoded frames as .npy)
 must write the reference's four outputs with the reference's shapes/dtypes,
 and its kpts_3d must be the oracle's get_pose_3D of its kpts_2d (1e-4);
 pose_refinement must then write kpts_3d_linear_interpolation.npy and
@@ -49,6 +49,7 @@ def test_record_and_estimate_pose_cli(project, monkeypatch):
     from mvpose import cli
     root, names, paths, cams = project
     monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    monkeypatch.setenv("MVPOSE_RANDOM_DETECTOR", "1")
     monkeypatch.chdir(root)
     log = cli.record_and_estimate_pose_main(["--camera_names", *names, "--configuration_number", "1",
                                              "--recording_paths", *paths])
@@ -103,6 +104,7 @@ def test_avi_recordings_match_npy(project, monkeypatch, tmp_path):
     from mvpose import pose_estimation, video
     _, _, paths, _ = project
     monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    monkeypatch.setenv("MVPOSE_NO_DETECTOR", "1")
     est = pose_estimation.build_estimator("random", frame_hw=(360, 640), max_frames=16)
     avis = []
     for v, p in enumerate(paths):
@@ -114,3 +116,51 @@ def test_avi_recordings_match_npy(project, monkeypatch, tmp_path):
     assert k_npy.shape == (3, 17, 3, 2)
     np.testing.assert_array_equal(k_avi, k_npy)
     np.testing.assert_array_equal(h_avi, h_npy)
+
+
+def test_cli_runs_the_detector_like_the_reference(project, monkeypatch, tmp_path):
+    """record_and_estimate_pose builds PoseEstimator(detector, pose model) from the model name
+    (ref pose_estimation.py:290-297) and crops every camera-frame to its first person box
+    (ref mmpose_pose_estimation.py:234-253).  With the seeded synthetic detector, the CLI's
+    kpts_2d.npy / heatmaps_2d.npy equal the reference's own loop — get_pose_2D calling
+    PoseEstimator.predict frame by frame (ref pose_estimation.py:184-190, :88) — bit for bit;
+    frames with a box differ from the whole-frame run (MVPOSE_NO_DETECTOR=1), the others
+    equal it."""
+    from mvpose import cli
+    from mvpose.mmpose_pose_estimation import PoseEstimator
+    from mvpose.pose_estimation import get_pose_2D
+    root, names, _, _ = project
+    rec = root / "configurations" / "1" / "recordings" / "det"
+    rec.mkdir(parents=True, exist_ok=True)
+    rng = np.random.default_rng(7)
+    stacks, paths = [], []
+    for v in range(2):
+        s = rng.integers(0, 256, (4, 720, 1280, 3), dtype=np.uint8)
+        p = rec / f"camera{v}.npy"
+        np.save(p, s)
+        stacks.append(s)
+        paths.append(str(p))
+    monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    monkeypatch.setenv("MVPOSE_RANDOM_DETECTOR", "1")
+    monkeypatch.delenv("MVPOSE_NO_DETECTOR", raising=False)
+    monkeypatch.chdir(root)
+    argv = ["--camera_names", *names, "--configuration_number", "1", "--recording_paths", *paths]
+    log = cli.record_and_estimate_pose_main(argv)
+    k2, hm = np.load(log["kpts_2d"]), np.load(log["heatmaps_2d"])
+    assert k2.shape == (3, 17, 3, 2)
+    pe = PoseEstimator(None, None, None, None, max_frames=2)        # the same seeded detector + pose weights
+    assert pe.detector is not None
+    for t in range(3):
+        s2, h2 = get_pose_2D([stacks[0][t], stacks[1][t]], lambda f: pe.predict(f))
+        np.testing.assert_array_equal(k2[t], s2, err_msg=f"frame {t}")
+        np.testing.assert_array_equal(hm[t], np.stack(h2), err_msg=f"frame {t}")
+    best = pe.bboxes_for(torch.from_numpy(np.stack([stacks[v][t] for t in range(3) for v in range(2)])).cuda())
+    has_box = (best[:, 4] > 0.3).cpu().numpy().reshape(3, 2)
+    monkeypatch.setenv("MVPOSE_NO_DETECTOR", "1")
+    whole = np.load(cli.record_and_estimate_pose_main(argv)["kpts_2d"])
+    print(f"camera-frames with a person box: {int(has_box.sum())}/6")
+    assert has_box.any()
+    for t in range(3):
+        for v in range(2):
+            same = np.array_equal(whole[t, :, :, v], k2[t, :, :, v])
+            assert same != bool(has_box[t, v]), (t, v, bool(has_box[t, v]))

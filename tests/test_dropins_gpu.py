@@ -54,7 +54,9 @@ def test_pose_estimator_signature_and_checkpoint(env):
     from mvpose.estimator import BatchPoseEstimator
     from mvpose.mmpose_pose_estimation import PoseEstimator
     sd, ck, syn = env
-    pe = PoseEstimator("rtmdet_m.py", "rtmdet_m.pth", "td-hm_hrnet-w32.py", ck)   # device='cpu' default
+    with pytest.raises(FileNotFoundError):   # the detector checkpoint is not a local file
+        PoseEstimator("rtmdet_m.py", "rtmdet_m.pth", "td-hm_hrnet-w32.py", ck)
+    pe = PoseEstimator("rtmdet_m.py", "rtmdet_m.pth", "td-hm_hrnet-w32.py", ck, using_detector=False)   # device='cpu'
     frame = syn.make_frames(1, seed=12)[0]
     inst, hm = pe(frame)
     ref = BatchPoseEstimator(sd, max_frames=1, swap_rb=False)

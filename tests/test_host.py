@@ -85,3 +85,81 @@ def test_camera_names_loader_rejects_code(tmp_path):
         pickle.dump(({0: Evil()}, "a"), f)
     with pytest.raises(pickle.UnpicklingError):
         geometry.load_camera_names(str(d))
+
+
+def _random_boxes(n, seed):
+    rng = np.random.default_rng(seed)
+    x1 = rng.uniform(-150, 1250, n)
+    y1 = rng.uniform(-100, 700, n)
+    return np.stack([x1, y1, x1 + rng.uniform(0.5, 1400, n), y1 + rng.uniform(0.5, 800, n)], 1).astype(np.float32)
+
+
+def test_crop_geometry_batch_matches_oracle_per_box():
+    """geometry.crop_geometry_batch (the host twin of mvp_bbox_geometry) = the oracle's
+    mmpose bbox_xyxy2cs -> _fix_aspect_ratio -> get_warp_matrix (OpenCV LU) ->
+    warpAffine inversion, bit for bit, box by box (f32 boxes as mmdet returns them)."""
+    bb = _random_boxes(200, 1)
+    cm, rm, cs = geometry.crop_geometry_batch(bb)
+    for i in range(len(bb)):
+        c, s = heatmap_ref.bbox_xyxy2cs(bb[i])
+        s = heatmap_ref.fix_aspect_ratio(s, 192 / 256)
+        np.testing.assert_array_equal(cs[i], np.r_[c, s].astype(np.float32))
+        np.testing.assert_array_equal(cm[i], heatmap_ref.invert_affine(heatmap_ref.get_warp_matrix(c, s, 0.0, (192, 256))))
+        np.testing.assert_array_equal(
+            rm[i], heatmap_ref.invert_affine(heatmap_ref.get_warp_matrix(c, s, 0.0, (48, 64), inv=True)))
+
+
+def test_lu_solve_batch_is_opencv_lu():
+    """The vectorised LU = the oracle's scalar OpenCV LUImpl restatement on general systems
+    (pivoting exercised), and a singular system gives zeros like cv::solve's failure."""
+    rng = np.random.default_rng(2)
+    A = rng.normal(size=(50, 6, 6)) * rng.uniform(0.1, 100, (50, 1, 6))
+    b = rng.normal(size=(50, 6))
+    A[7] = 0.0
+    A[7, :, 0] = 1.0
+    got = geometry.lu_solve_batch(A, b)
+    for i in range(50):
+        np.testing.assert_array_equal(got[i], heatmap_ref.cv_lu_solve(A[i], b[i]))
+    assert not got[7].any()
+    np.testing.assert_allclose(got[:7], np.linalg.solve(A[:7], b[:7, :, None])[..., 0], rtol=1e-9, atol=1e-12)
+
+
+def test_detector_checkpoint_must_be_local(monkeypatch):
+    """The reference always builds its detector (mmpose_pose_estimation.py:98-99): a
+    det_checkpoint that is not a local file raises instead of silently cropping the whole
+    image; MVPOSE_NO_DETECTOR=1 / using_detector=False are the explicit opt-outs."""
+    from mvpose.mmpose_pose_estimation import PoseEstimator, build_detector
+    monkeypatch.delenv("MVPOSE_RANDOM_DETECTOR", raising=False)
+    url = "https://download.openmmlab.com/mmpose/v1/projects/rtmpose/rtmdet_m_8xb32-100e_coco-obj365-person.pth"
+    with pytest.raises(FileNotFoundError):
+        build_detector(url)
+    with pytest.raises(FileNotFoundError):
+        PoseEstimator("rtmdet_m.py", url, "hrnet.py", "hrnet.pth")
+    monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    monkeypatch.setenv("MVPOSE_NO_DETECTOR", "1")
+    pe = PoseEstimator("rtmdet_m.py", url, "hrnet.py", "hrnet.pth")
+    assert pe.detector is None and not pe.using_detector
+
+
+def test_build_estimator_from_model_yaml(tmp_path, monkeypatch):
+    """estimate_pose_from_video's model-name path (pose_estimation.py:290-297): the detector
+    and the pose model come from model_yaml; estimator objects and their bound predict pass
+    through unchanged (no yaml lookup)."""
+    import yaml as _yaml
+    from mvpose import pose_estimation as pe_mod
+    from mvpose.mmpose_pose_estimation import PoseEstimator
+    y = tmp_path / "model_paths.yaml"
+    _yaml.safe_dump({"detectors": {"coco_base": ["rtmdet_m.py", str(tmp_path / "missing_det.pth")]},
+                     "pose_estimators": {"coco_base": ["hrnet.py", str(tmp_path / "missing_pose.pth")]}},
+                    open(y, "w"))
+    monkeypatch.delenv("MVPOSE_RANDOM_DETECTOR", raising=False)
+    monkeypatch.delenv("MVPOSE_NO_DETECTOR", raising=False)
+    monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    with pytest.raises(FileNotFoundError, match="detector checkpoint"):
+        pe_mod.build_estimator("coco_base", "coco_base", str(y))
+    monkeypatch.setenv("MVPOSE_NO_DETECTOR", "1")
+    est = pe_mod.build_estimator("coco_base", "coco_base", str(y), max_frames=8)
+    assert isinstance(est, PoseEstimator) and est.detector is None
+    assert pe_mod.build_estimator(est) is est
+    assert pe_mod.build_estimator(est.predict) is est
+    assert pe_mod.resolve_estimator(lambda f: None) is None

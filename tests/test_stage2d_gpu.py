@@ -107,7 +107,7 @@ def _moments(_lib, hm, minv, img_h, img_w, separable=None):
     md = torch.tensor(np.tile(minv, (N, 1)), device="cuda")
     out = torch.empty((N, K, 6), dtype=torch.float64, device="cuda")
     _lib.call("mvp_heatmap_moments", _p(hd), N, K, h, w, _p(md), img_h, img_w, ctypes.c_float(0.01), int(separable),
-              _p(out), _s())
+              None, _p(out), _s())
     torch.cuda.synchronize()
     return out.cpu().numpy()
 
@@ -226,7 +226,7 @@ def test_moments_joints_per_block_bit_identical(lib, jpb, separable, monkeypatch
         monkeypatch.setenv("MVPOSE_MOM_JPB", str(j))
         out = torch.full((3, 17, 6), float("nan"), dtype=torch.float64, device="cuda")
         _lib.call("mvp_heatmap_moments", _p(hd), 3, 17, 64, 48, _p(md), 720, 1280, ctypes.c_float(0.01),
-                  separable, _p(out), _s())
+                  separable, None, _p(out), _s())
         torch.cuda.synchronize()
         return out.cpu().numpy()
 

@@ -26,7 +26,7 @@ for jpb in (1, 2, 3, 6, 9, 17):
             e0.record()
         estimator.call("mvp_heatmap_moments", ctypes.c_void_p(hm.data_ptr()), n, 17, 64, 48,
                        ctypes.c_void_p(est.revert_minv.data_ptr()), 720, 1280, ctypes.c_float(0.01),
-                       int(est.separable), ctypes.c_void_p(out.data_ptr()), s)
+                       int(est.separable), None, ctypes.c_void_p(out.data_ptr()), s)
     e1.record()
     torch.cuda.synchronize()
     if ref is None:

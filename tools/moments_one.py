@@ -23,7 +23,7 @@ for r in range(reps + 1):
         e0.record()
     estimator.call("mvp_heatmap_moments", ctypes.c_void_p(hm.data_ptr()), n, 17, 64, 48,
                    ctypes.c_void_p(est.revert_minv.data_ptr()), 720, 1280, ctypes.c_float(0.01),
-                   int(est.separable), ctypes.c_void_p(out.data_ptr()), s)
+                   int(est.separable), None, ctypes.c_void_p(out.data_ptr()), s)
 e1.record()
 torch.cuda.synchronize()
 print(f"moments: {e0.elapsed_time(e1) / reps:.3f} ms per launch of {n} camera-frames", flush=True)

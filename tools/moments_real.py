@@ -33,7 +33,7 @@ for sep in (1, 2):
             e0.record()
         estimator.call("mvp_heatmap_moments", ctypes.c_void_p(avg.data_ptr()), B * V, 17, 64, 48,
                        ctypes.c_void_p(est.revert_minv.data_ptr()), 720, 1280, ctypes.c_float(0.01), sep,
-                       ctypes.c_void_p(out.data_ptr()), s)
+                       None, ctypes.c_void_p(out.data_ptr()), s)
     e1.record()
     torch.cuda.synchronize()
     print(f"separable={sep}: {e0.elapsed_time(e1) / reps:.3f} ms", flush=True)

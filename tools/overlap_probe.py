@@ -22,7 +22,7 @@ s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 def moments(stream):
     estimator.call("mvp_heatmap_moments", ctypes.c_void_p(hm.data_ptr()), 512, 17, 64, 48,
                    ctypes.c_void_p(est.revert_minv.data_ptr()), 720, 1280, ctypes.c_float(0.01),
-                   int(est.separable), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
+                   int(est.separable), None, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(stream.cuda_stream))
 
 
 def timed(fn, reps=5):
