@@ -142,8 +142,15 @@ def cpu_baseline(n_frames, n_frames_1t, views):
         dt1 = _cpu_path(n_frames_1t, views) if n_frames_1t > 0 else None
     finally:
         torch.set_num_threads(n_threads)
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
     out = {"value": n_frames / dt, "unit": "frames/s", "cores": n_threads, "kind": "port",
-           "host_cpu_count": os.cpu_count(), "cpu_model": _cpu_model(),
+           "host_cpu_count": os.cpu_count(), "usable_cpus": usable, "cpu_model": _cpu_model(),
+           "threads_note": "cores = torch.get_num_threads() = the intra-op threads the sample ran on; torch takes "
+                           "it from OMP_NUM_THREADS, which the GPU box sets to its per-GPU CPU share (16); "
+                           "usable_cpus = this process's affinity mask (the box's whole machine is shared)",
            "sample": f"{n_frames} of config 1's 50 synthetic {views}-cam 1280x720 frames, batch 1 per camera, "
                      f"flip test, {dt:.1f} s on {n_threads} threads (oracle/ restatement: torch-CPU fp32 "
                      f"HRNet-W32 + numpy decode/revert/moments + OpenCV-4.9-semantics triangulation in C)"}
@@ -396,10 +403,16 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    rank_ms = [1e3 * elapsed / args.steps]
+    rccl_world = 1
     if world > 1:
+        # every rank's own step time to rank 0 (shows a lagging rank), then the max = the job's time
+        rccl_world = torch.distributed.get_world_size()
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        elapsed = t.item()
+        parts = [torch.empty_like(t) for _ in range(rccl_world)]
+        torch.distributed.all_gather(parts, t)
+        rank_ms = [1e3 * float(p.item()) / args.steps for p in parts]
+        elapsed = max(float(p.item()) for p in parts)
 
     # ---- per-kernel timing with HIP events on the launch stream (not part of the timed region)
     s = torch.cuda.current_stream(dev)
@@ -451,6 +464,8 @@ def main():
             "config": {"workload": f"BASELINE config 2: {V}-cam HRNet-W32 256x192 bf16 (flip test) + batched "
                                    f"4x4 DLT-SVD triangulation", "frames_per_step_per_gpu": B, "views": V,
                        "crops_per_step_per_gpu": 2 * B * V, "parallelism": f"dp{world} (frame-sharded)"},
+            "rccl_world": rccl_world,
+            "rank_ms_per_step": {"min": min(rank_ms), "max": max(rank_ms), "per_rank": rank_ms},
             "roofline": {"bound": "mfma", "kernel": "HRNet-W32 conv graph (one graph forward = one launch)",
                          "achieved": bb_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": bb_tflops / BF16_PEAK_TFLOPS,

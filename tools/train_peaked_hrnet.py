@@ -65,6 +65,28 @@ def trainable_forward(model, feats):
     return model.head(F.relu(y))
 
 
+def calibrate_bn(model, feats, n=128):
+    """Running statistics of the trainable part's BatchNorms from these inputs (the random
+    ones were drawn for unit-variance noise): each BN in forward order sees its input's batch
+    mean / variance, so the fit starts from O(1) activations.  (The GPU graph folds whatever
+    statistics the state dict holds.)"""
+    last = model.backbone.stage4[-1]
+    bns = [mod for blk in last.branches[0] for mod in (blk.bn1, blk.bn2)]
+    bns += [last.fuse_layers[0][j][1] for j in (1, 2, 3)]
+    hooks = []
+
+    def pre(mod, inp):
+        x = inp[0]
+        mod.running_mean.copy_(x.mean((0, 2, 3)))
+        mod.running_var.copy_(x.var((0, 2, 3)))
+    for b in bns:
+        hooks.append(b.register_forward_pre_hook(pre))
+    with torch.no_grad():
+        trainable_forward(model, [f[:n] for f in feats])
+    for h in hooks:
+        h.remove()
+
+
 def targets(joints, flipped):
     """(n, 17, 64, 48) Gaussian maps; flipped crops: joint k's disc sits at 47.75 - x and is
     the flip test's channel FLIP[k]."""
@@ -135,11 +157,12 @@ def main():
         p.requires_grad_(False)
     for p in params:
         p.requires_grad_(True)
+    calibrate_bn(model, feats)
     with torch.no_grad():   # a fresh head (the random one is biased to -0.15)
         model.head.final_layer.weight.normal_(0.0, 0.01)
         model.head.final_layer.bias.zero_()
-    epochs, bs = int(os.environ.get("EPOCHS", "60")), 32
-    opt = torch.optim.Adam(params, lr=2e-3)
+    epochs, bs = int(os.environ.get("EPOCHS", "60")), int(os.environ.get("BATCH", "16"))
+    opt = torch.optim.Adam(params, lr=float(os.environ.get("LR", "5e-4")))
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, epochs)
     n = tgt.shape[0]
     g = torch.Generator().manual_seed(1)
@@ -155,7 +178,7 @@ def main():
             opt.zero_grad()
             loss.backward()
             opt.step()
-            tot += float(loss) * len(idx)
+            tot += float(loss.detach()) * len(idx)
         sched.step()
         if ep % 5 == 4 or ep == epochs - 1:
             dec, acc, peak = evaluate(model, va_o, va_f, jv)
@@ -166,7 +189,7 @@ def main():
     sd = model.state_dict()
     keys = [k for k in sd if k.startswith("backbone.stage4.2.branches.0.") or k.startswith("head.")
             or any(k.startswith(f"backbone.stage4.2.fuse_layers.0.{j}.") for j in (1, 2, 3))]
-    keys = [k for k in keys if not k.endswith("num_batches_tracked")]
+    keys = [k for k in keys if not k.endswith("num_batches_tracked")]   # incl. the recalibrated BN statistics
     np.savez(OUT, **{k: sd[k].detach().numpy().astype(np.float32) for k in keys})
     print(f"wrote {len(keys)} tensors ({sum(sd[k].numel() for k in keys)} values) to {OUT}")
 
