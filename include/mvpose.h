@@ -75,6 +75,11 @@ int mvp_camera_pack(const double* K_host, const double* dist5_host, const double
 /* OR-ed into mode: solve every point with the exact JacobiSVDImpl_ restatement
  * (default: QR + inverse iteration, Jacobi only where that has not converged). */
 #define MVP_TRI_EXACT_JACOBI 0x10
+/* OR-ed into mode: throughput solver validated to <= 1e-4 world units against the exact
+ * path (mixed f32/fp64 undistortion, normal-equation inverse iteration; the exact path for
+ * any point that has not provably converged).  Reference mode with 2 listed cameras; other
+ * cases run the default solver. */
+#define MVP_TRI_TOLERANCE 0x20
 
 int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double* cams_dev,
                     int n_cams, const int* cam_idx_host, int n_cam_idx, int mode,
@@ -348,6 +353,17 @@ int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, in
 int mvp_extrinsic_sample_grad(const float* samples_dev, const float* targets_dev, int n_samples, int64_t n_points,
                               const float* cam_dev, int ignore_distortions, int n_blocks, double* partial_dev,
                               void* stream);
+/* One Adam step of that branch on the device (pose_refinement.py:1039-1050, learnable R as a
+ * 3x3 matrix and T): reduces partial_dev [n_blocks][14] of mvp_extrinsic_sample_grad, casts
+ * cost and gradient to f32 like the host path, clip_grad_norm_([R, T], max_norm), torch
+ * single-tensor Adam on R and T with state_dev [m (12) | v (12) | step (int32)] (zero it before
+ * the first step), and updates R (cam_dev[9..18)) and T (cam_dev[18..21)) in place, so the next
+ * mvp_extrinsic_sample_grad sees the new camera.  The step's cost goes to cost_hist_dev[step-1]
+ * and the new R, T (12 floats) to param_hist_dev[step-1][12]: the host reads the history every
+ * few iterations for the early-stop bookkeeping instead of once per step. */
+int mvp_extrinsic_adam_step(const double* partial_dev, int n_blocks, float* cam_dev, float* state_dev, double lr,
+                            double beta1, double beta2, double adam_eps, double max_norm, float* cost_hist_dev,
+                            float* param_hist_dev, void* stream);
 int mvp_project_points(const float* pts, int64_t n, const float* cam, int ignore_distortions, float* uv,
                        void* stream);
 

@@ -547,6 +547,78 @@ __global__ __launch_bounds__(kExtBlock) void extrinsic_grad_kernel(const float* 
     }
 }
 
+// ---- one Adam step of the extrinsic-from-samples branch on the device (pose_refinement.py:
+// 1039-1050 with the learnable R (3x3 matrix) and T): the partial sums of the pass above ->
+// cost / gradient (f32 casts of the fp64 means, as the host path), clip_grad_norm_([R, T],
+// 1.0) (per-tensor norms then the norm of norms, accumulated in fp64 and cast to f32, like
+// ATen's CPU reduction), torch single-tensor Adam per tensor; the camera record the next pass
+// reads is updated in place and the step's cost and parameters are appended to the history.
+// One workgroup; state = [m (12) | v (12) | step (as float bits)].
+constexpr int kAdamBlock = 256;
+
+__global__ __launch_bounds__(kAdamBlock) void extrinsic_adam_kernel(const double* __restrict__ partial, int n_blocks,
+                                                                    float* __restrict__ cam, float* __restrict__ state,
+                                                                    double lr, double beta1, double beta2,
+                                                                    double adam_eps, double max_norm,
+                                                                    float* __restrict__ cost_hist,
+                                                                    float* __restrict__ param_hist) {
+    __shared__ double red[kAdamBlock / 64][8];
+    __shared__ double sums[kExtSums];
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        double v[7];
+#pragma unroll
+        for (int k = 0; k < 7; k++) v[k] = 0.0;
+        for (int b = threadIdx.x; b < n_blocks; b += kAdamBlock)
+#pragma unroll
+            for (int k = 0; k < 7; k++) v[k] += partial[(long)b * kExtSums + 7 * half + k];
+        block_sum<kAdamBlock, 7>(v, red);
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int k = 0; k < 7; k++) sums[7 * half + k] = v[k];
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    int* stepp = reinterpret_cast<int*>(state + 24);
+    const int step = *stepp + 1;
+    *stepp = step;
+    const double cnt = sums[1];
+    float g[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) g[k] = (float)(sums[2 + k] / cnt);
+    double nR = 0.0, nT = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) nR += (double)g[k] * g[k];
+#pragma unroll
+    for (int k = 9; k < 12; k++) nT += (double)g[k] * g[k];
+    const float fR = (float)sqrt(nR), fT = (float)sqrt(nT);
+    const float total = (float)sqrt((double)fR * fR + (double)fT * fT);
+    const float coef = fminf((float)max_norm / (total + 1e-6f), 1.f);
+    const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2);
+    const double bc1 = 1.0 - pow(beta1, (double)step), bc2 = 1.0 - pow(beta2, (double)step);
+    const float nstep = (float)(-(lr / bc1));
+    const float bc2s = (float)sqrt(bc2);
+    const float eps = (float)adam_eps;
+    float* m = state;
+    float* vv = state + 12;
+    // learnable values live in the camera record: R at [9, 18), T at [18, 21)
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+        const float gk = g[k] * coef;
+        float mv = m[k];
+        mv = (w1 < 0.5f) ? mv + w1 * (gk - mv) : gk - (gk - mv) * (1.f - w1);
+        float ve = vv[k] * b2;
+        ve = ve + w2 * gk * gk;
+        m[k] = mv;
+        vv[k] = ve;
+        const float denom = sqrtf(ve) / bc2s + eps;
+        cam[9 + k] = cam[9 + k] + nstep * mv / denom;
+    }
+    cost_hist[step - 1] = (float)(sums[0] / cnt);
+#pragma unroll
+    for (int k = 0; k < 12; k++) param_hist[(long)(step - 1) * 12 + k] = cam[9 + k];
+}
+
 }  // namespace
 
 extern "C" int mvp_sgd_workspace_floats(int M, int T, int V, int J, int64_t* out) {
@@ -636,6 +708,18 @@ extern "C" int mvp_extrinsic_sample_grad(const float* samples, const float* targ
     MVP_REQUIRE(samples && targets && cam && partial, "mvp_extrinsic_sample_grad: NULL device pointer");
     hipLaunchKernelGGL(extrinsic_grad_kernel, dim3((unsigned)n_blocks), dim3(kExtBlock), 0, (hipStream_t)stream,
                        samples, targets, n_samples, (long)n_points, cam, ignore_distortions, partial);
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_extrinsic_adam_step(const double* partial, int n_blocks, float* cam, float* state, double lr,
+                                       double beta1, double beta2, double adam_eps, double max_norm,
+                                       float* cost_hist, float* param_hist, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n_blocks > 0 && partial && cam && state && cost_hist && param_hist,
+                "mvp_extrinsic_adam_step: bad arguments");
+    hipLaunchKernelGGL(extrinsic_adam_kernel, dim3(1), dim3(kAdamBlock), 0, (hipStream_t)stream, partial, n_blocks,
+                       cam, state, lr, beta1, beta2, adam_eps, max_norm, cost_hist, param_hist);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END
 }

@@ -391,6 +391,157 @@ __device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], CamFa
     __syncthreads();
 }
 
+// ----------------------------------------------------------------- tolerance mode
+// MVP_TRI_TOLERANCE: the same problem solved for throughput, validated to <= 1e-4 world
+// units against the exact-rounding path (and bit-identical to it on almost every point).
+//   * undistortion: OpenCV's 5 fixed iterations, the first 3 in f32 (both views packed in
+//     one v_pk_* instruction stream), the last 2 in fp64 — the fixed-point map contracts by
+//     ~|k1|·r² per step, so the f32 rounding of the early iterates is damped ~100x before
+//     the f32 output rounding; FMA contraction, hardware reciprocals with Newton steps;
+//   * null vector: normal equations M = AᵀA (fp64), LDLᵀ, three inverse-iteration steps
+//     from e₄ — each shrinks the off-null component by λ₄/λ₃ = (σ₄/σ₃)² (~4e-7 on the
+//     synthetic rigs; σ₁/σ₃ ~ 200, so the squared condition costs ~1e-12 of direction);
+//   * a lane whose last step still moved the unit vector by > 1e-12 (σ₄ ≈ σ₃ geometry,
+//     NaN / Inf input) re-solves its point on the exact path (same kernel, rare branch).
+// The result is then normalised and dehomogenised through OpenCV's f32 chain.
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct CamTol {        // per-camera constants for the f32 iterations
+    float k0, k1, k4, k2x2, k3x2, k2, k3;
+};
+
+// r = 1/b to ~1 ulp: v_rcp_f64 + two Newton steps (no IEEE-division scaling)
+__device__ __forceinline__ double rcp_nr(double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    return __builtin_fma(r, e, r);
+}
+
+// Both views of a point: (u, v) pixels -> undistorted pixels (P = K), OpenCV's iteration.
+__device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const float (&v)[2],
+                                                   const double* __restrict__ c0, const double* __restrict__ c1,
+                                                   const CamFast& f0, const CamFast& f1, const CamTol& t0,
+                                                   const CamTol& t1, float (&ox)[2], float (&oy)[2]) {
+#pragma clang fp contract(fast)
+    const double* cc[2] = {c0, c1};
+    double x0[2], y0[2];
+    x0[0] = ((double)u[0] - c0[2]) * f0.ifx;
+    y0[0] = ((double)v[0] - c0[5]) * f0.ify;
+    x0[1] = ((double)u[1] - c1[2]) * f1.ifx;
+    y0[1] = ((double)v[1] - c1[5]) * f1.ify;
+    const f2v X0 = {(float)x0[0], (float)x0[1]}, Y0 = {(float)y0[0], (float)y0[1]};
+    const f2v K0 = {t0.k0, t1.k0}, K1 = {t0.k1, t1.k1}, K4 = {t0.k4, t1.k4};
+    const f2v K2x2 = {t0.k2x2, t1.k2x2}, K3x2 = {t0.k3x2, t1.k3x2}, K2 = {t0.k2, t1.k2}, K3 = {t0.k3, t1.k3};
+    const f2v one = {1.f, 1.f}, two = {2.f, 2.f};
+    f2v x = X0, y = Y0;
+    bool neg0 = false, neg1 = false;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        const f2v r2 = __builtin_elementwise_fma(x, x, y * y);
+        const f2v den = __builtin_elementwise_fma(__builtin_elementwise_fma(__builtin_elementwise_fma(K4, r2, K1), r2, K0),
+                                                  r2, one);
+        f2v ic;
+        ic.x = __builtin_amdgcn_rcpf(den.x);
+        ic.y = __builtin_amdgcn_rcpf(den.y);
+        neg0 |= ic.x < 0.f;
+        neg1 |= ic.y < 0.f;
+        const f2v xy = x * y;
+        const f2v dX = __builtin_elementwise_fma(K2x2, xy, K3 * __builtin_elementwise_fma(two * x, x, r2));
+        const f2v dY = __builtin_elementwise_fma(K2, __builtin_elementwise_fma(two * y, y, r2), K3x2 * xy);
+        x = (X0 - dX) * ic;
+        y = (Y0 - dY) * ic;
+    }
+    double xd[2] = {(double)x.x, (double)x.y}, yd[2] = {(double)y.x, (double)y.y};
+    bool neg[2] = {neg0, neg1};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const double* c = cc[q];
+            const double k0 = c[9], k1 = c[10], k2 = c[11], k3 = c[12], k4 = c[13];
+            const double r2 = xd[q] * xd[q] + yd[q] * yd[q];
+            const double ic = rcp_nr(1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+            neg[q] = neg[q] || ic < 0;
+            const double dX = 2 * k2 * xd[q] * yd[q] + k3 * (r2 + 2 * xd[q] * xd[q]);
+            const double dY = k2 * (r2 + 2 * yd[q] * yd[q]) + 2 * k3 * xd[q] * yd[q];
+            xd[q] = (x0[q] - dX) * ic;
+            yd[q] = (y0[q] - dY) * ic;
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const double* c = cc[q];
+        const double xx = neg[q] ? x0[q] : xd[q], yy = neg[q] ? y0[q] : yd[q];
+        const double ww = rcp_nr(c[6] * xx + c[7] * yy + c[8]);
+        ox[q] = (float)((c[0] * xx + c[1] * yy + c[2]) * ww);
+        oy[q] = (float)((c[3] * xx + c[4] * yy + c[5]) * ww);
+    }
+}
+
+// Null vector of A (M x 4) by LDLᵀ inverse iteration on AᵀA; false = not provably converged.
+template <int M>
+__device__ __forceinline__ bool normal_eq_null_vector(const double (&A)[M][4], double (&nv)[4]) {
+#pragma clang fp contract(fast)
+    double m[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) {
+            double s = A[0][i] * A[0][j];
+#pragma unroll
+            for (int r = 1; r < M; r++) s += A[r][i] * A[r][j];
+            m[i][j] = s;
+        }
+    // LDLᵀ (lower triangle of m)
+    const double D0 = m[0][0], r0 = rcp_nr(D0);
+    const double l10 = m[1][0] * r0, l20 = m[2][0] * r0, l30 = m[3][0] * r0;
+    const double a11 = m[1][1] - l10 * m[1][0], a21 = m[2][1] - l20 * m[1][0], a31 = m[3][1] - l30 * m[1][0];
+    const double a22 = m[2][2] - l20 * m[2][0], a32 = m[3][2] - l30 * m[2][0], a33 = m[3][3] - l30 * m[3][0];
+    const double r1 = rcp_nr(a11);
+    const double l21 = a21 * r1, l31 = a31 * r1;
+    const double b22 = a22 - l21 * a21, b32 = a32 - l31 * a21, b33 = a33 - l31 * a31;
+    const double r2 = rcp_nr(b22);
+    const double l32 = b32 * r2;
+    double D3 = b33 - l32 * b32;
+    // an exactly singular M (noise-free data): a pivot far below the factorisation's rounding
+    // keeps the solves finite and changes nothing else
+    if (!(fabs(D3) >= 1e-30 * D0)) D3 = 1e-30 * D0;
+    const double r3 = rcp_nr(D3);
+    auto solve = [&](double (&y)[4]) {  // y <- M⁻¹ y
+        const double z1 = y[1] - l10 * y[0];
+        const double z2 = y[2] - l20 * y[0] - l21 * z1;
+        const double z3 = y[3] - l30 * y[0] - l31 * z1 - l32 * z2;
+        y[3] = z3 * r3;
+        y[2] = z2 * r2 - l32 * y[3];
+        y[1] = z1 * r1 - l21 * y[2] - l31 * y[3];
+        y[0] = y[0] * r0 - l10 * y[1] - l20 * y[2] - l30 * y[3];
+    };
+    double y[4];
+    y[3] = r3;  // M⁻¹ e₄
+    y[2] = -l32 * y[3];
+    y[1] = -l21 * y[2] - l31 * y[3];
+    y[0] = -l10 * y[1] - l20 * y[2] - l30 * y[3];
+    solve(y);
+    const double n2 = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    double x2[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) x2[q] = y[q] * n2;
+    solve(y);
+    const double n3 = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+    double dd = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        nv[q] = y[q] * n3;
+        const double e = nv[q] - x2[q];
+        dd += e * e;
+    }
+    // (M⁻¹ is positive definite up to the pivot clamp: no sign flip between iterates)
+    return dd <= 1e-24;
+}
+
 // Solver stages.  kExact: the restatement for every lane (OpenCV undistortion
 // with IEEE divisions, Jacobi SVD).  kFast: fast undistortion + QR / inverse
 // iteration, with the Jacobi restatement (on the same A) for the lanes whose
@@ -400,7 +551,7 @@ __device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], CamFa
 // fallback to a second launch over marked lanes cuts the fast kernel from 110 to
 // 66 VGPRs (4 -> 7 waves per SIMD) but made it slower (69 vs 58 us; VALU busy
 // 59 % vs 73 %), and the marker sweep cost another 23 us.
-enum Stage { kExact = 0, kFast = 1 };
+enum Stage { kExact = 0, kFast = 1, kTol = 2 };
 
 template <int S>
 __device__ __forceinline__ void undistort_view(float u, float v, const double* __restrict__ c, const CamFast& cf,
@@ -510,6 +661,64 @@ __global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
     triangulate_all_views_body<S, NV>(kpts, n, V, cams, n_cams, ci, out, out4);
 }
 
+// MVP_TRI_REFERENCE | MVP_TRI_TOLERANCE with camera_indices of length 2 (the reference's
+// hard-coded [0, 1]): the top-2 rule reduces to one comparison (np.argsort of two values:
+// [0, 1] unless conf[1] < conf[0], NaN sorts last).
+__global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
+    float* __restrict__ out, double* __restrict__ out4) {
+    __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
+    __shared__ CamFast sfast[kMaxCams];
+    __shared__ CamTol stol[2];
+    load_cams(scam, sfast, cams, n_cams);
+    if (threadIdx.x < 2) {
+        const double* c = cams + threadIdx.x * MVP_CAM_DOUBLES;
+        stol[threadIdx.x] = CamTol{(float)c[9], (float)c[10], (float)c[13], (float)(2 * c[11]), (float)(2 * c[12]),
+                                   (float)c[11], (float)c[12]};
+    }
+    __syncthreads();
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const float* __restrict__ kp = kpts + p * 3 * V;
+    const int ca = ci.v[0], cb = ci.v[1];
+    const float conf_a = kp[2 * V + ca], conf_b = kp[2 * V + cb];
+    // stable ascending argsort of (conf_a, conf_b), NaN last: swapped iff conf_b sorts before conf_a
+    const bool swap = isnan(conf_a) ? !isnan(conf_b) : (conf_b < conf_a);
+    // selection position 0 = the lower-confidence camera (its params: camera key 0), 1 = the other
+    const int col0 = swap ? cb : ca, col1 = swap ? ca : cb;
+    const float u[2] = {kp[col0], kp[col1]}, v[2] = {kp[V + col0], kp[V + col1]};
+    float ux[2], uy[2];
+    undistort_pair_tol(u, v, scam[0], scam[1], sfast[0], sfast[1], stol[0], stol[1], ux, uy);
+    double A[4][4];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const double* P = scam[q] + 26;
+        const double x = ux[q], y = uy[q];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            A[2 * q][k] = __builtin_fma(x, P[8 + k], -P[0 + k]);
+            A[2 * q + 1][k] = __builtin_fma(y, P[8 + k], -P[4 + k]);
+        }
+    }
+    double nv[4];
+    if (!normal_eq_null_vector<4>(A, nv)) {
+        // not provably converged (or non-finite): the exact path for this point
+        float e0x, e0y, e1x, e1y;
+        undistort_point(u[0], v[0], scam[0], e0x, e0y);
+        undistort_point(u[1], v[1], scam[1], e1x, e1y);
+        double E[4][4];
+        add_view_rows(E, 0, e0x, e0y, scam[0] + 26);
+        add_view_rows(E, 2, e1x, e1y, scam[1] + 26);
+        double At[4][4];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) At[c][r] = E[r][c];
+        jacobi_null_vector<4>(At, nv);
+    }
+    write_result(nv, p, out, out4);
+}
+
 }  // namespace
 
 extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const double* cams, int n_cams,
@@ -534,12 +743,17 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
     const int64_t blocks = (n_points + kBlock - 1) / kBlock;
     MVP_REQUIRE(blocks < (1LL << 31), "mvp_triangulate: too many points");
     const bool exact = (mode & MVP_TRI_EXACT_JACOBI) != 0;
-    mode &= ~MVP_TRI_EXACT_JACOBI;
+    const bool tol = (mode & MVP_TRI_TOLERANCE) != 0;
+    MVP_REQUIRE(!(exact && tol), "mvp_triangulate: MVP_TRI_EXACT_JACOBI and MVP_TRI_TOLERANCE exclude each other");
+    mode &= ~(MVP_TRI_EXACT_JACOBI | MVP_TRI_TOLERANCE);
     const dim3 grid((unsigned)blocks), block(kBlock);
     if (mode == MVP_TRI_REFERENCE) {
         MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
                     "n_cam_idx <= n_cams");
-        if (exact)
+        if (tol && n_cam_idx == 2)
+            hipLaunchKernelGGL(triangulate_tol2_kernel, grid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
+                               out_xyz, out_xyzw);
+        else if (exact)
             hipLaunchKernelGGL(triangulate_reference_kernel<kExact>, grid, block, 0, s, kpts, n_points, V, cams,
                                n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
         else

@@ -75,6 +75,8 @@ SIGNATURES = {
     "mvp_sgd_refine": (c_int, None),
     "mvp_extrinsic_sample_grad": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_void_p,
                                           c_void_p]),
+    "mvp_extrinsic_adam_step": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_double, c_double, c_double, c_double,
+                                        c_double, c_void_p, c_void_p, c_void_p]),
     "mvp_project_points": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
     "mvp_linear_interpolation": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_float, c_float, c_int, c_int,
                                          c_void_p, c_void_p]),

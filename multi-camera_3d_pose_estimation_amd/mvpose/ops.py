@@ -19,6 +19,7 @@ CAM_DOUBLES = 40
 TRI_REFERENCE = 0
 TRI_ALL_VIEWS = 1
 TRI_EXACT_JACOBI = 0x10  # mode flag: exact Jacobi SVD for every point (mvpose.h)
+TRI_TOLERANCE = 0x20     # mode flag: throughput solver validated to <= 1e-4 world units (mvpose.h)
 
 
 def _stream(device=None) -> ctypes.c_void_p:
@@ -72,13 +73,20 @@ def pack_cameras(camera_params) -> np.ndarray:
 
 def triangulate(kpts: torch.Tensor, cams: torch.Tensor, cam_idx: Sequence[int] = (0, 1),
                 mode: int = TRI_REFERENCE, out: torch.Tensor | None = None,
-                return_xyzw: bool = False, exact: bool = False):
+                return_xyzw: bool = False, exact: bool = False, tolerance: bool = False):
     """kpts (..., 3, V) float32 on GPU (reference layout) -> (..., 3) float32.
 
-    cams: (n_cams, 40) float64 on GPU (pack_cameras).  exact=True solves every
-    point with the JacobiSVDImpl_ restatement instead of QR + inverse iteration."""
+    cams: (n_cams, 40) float64 on GPU (pack_cameras).  Default: OpenCV's rounding sequence
+    (bit-identical to the restatement), QR + inverse iteration with the Jacobi restatement
+    where that has not converged; exact=True: the JacobiSVDImpl_ restatement for every point;
+    tolerance=True: the throughput solver (MVP_TRI_TOLERANCE, reference mode with two listed
+    cameras), within 1e-4 world units of the exact path."""
+    if exact and tolerance:
+        raise ValueError("exact and tolerance exclude each other")
     if exact:
         mode = int(mode) | TRI_EXACT_JACOBI
+    if tolerance:
+        mode = int(mode) | TRI_TOLERANCE
     _require(kpts, torch.float32, "kpts")
     _require(cams, torch.float64, "cams")
     if kpts.dim() < 2 or kpts.shape[-2] != 3:

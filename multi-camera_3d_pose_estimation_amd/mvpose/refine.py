@@ -245,6 +245,11 @@ def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=N
 class Optimized_3d_Pose_Estimation:
     """GPU drop-in for pose_refinement.Optimized_3d_Pose_Estimation (:579-668)."""
 
+    # extrinsic-from-samples branch: Adam steps on the device (mvp_extrinsic_adam_step) when the
+    # learnable R is a 3x3 matrix; False = the host loop (torch CPU Adam per step), kept for
+    # axis-angle R and as the tests' comparison
+    device_adam = True
+
     def __init__(self, gaussians, initial_trajectory, decomposed_cam_params_initial=None, body_lengths=None,
                  camera_IDs=None, R_initial=None, T_initial=None, N_sample_points=100, torch_dtype=torch.float32,
                  device=None):
@@ -337,17 +342,18 @@ class Optimized_3d_Pose_Estimation:
     # optimize_trajectory=False): sample_gaussians (:684-706), construct_sample_cost
     # (:800-831), the Adam loop (:1000-1089).
     def sample_gaussians(self, G, GT, N):
-        """:684-706 — np.random.multivariate_normal per (t, GT camera, joint) in the reference's
-        loop order on the global numpy RNG (so seeded runs draw the same samples); returns
-        (T, J, N, 2 cams, 2) float64."""
+        """:684-706 — np.random.multivariate_normal per (t, GT camera, joint) on the global numpy
+        RNG, vectorised: the reference's T·2·J calls each draw N·2 standard normals in loop order
+        (an even count, so the legacy Gaussian cache never carries over) and map them by its own
+        svd(cov) -> x @ (sqrt(s)[:, None] * v) + mean; one standard_normal draw of the whole
+        (T, 2, J, N, 2) block and the same per-matrix LAPACK SVD / BLAS products on the stacked
+        covariances give bit-identical samples.  Returns (T, J, N, 2 cams, 2) float64."""
         T, J = G.shape[0], G.shape[2]
-        means = G[:, GT, :, :2]
-        covs = G[:, GT, :, 2:].reshape(T, 2, J, 2, 2)
-        samples = np.empty((T, 2, J, N, 2))
-        for t in range(T):
-            for c in range(2):
-                for j in range(J):
-                    samples[t, c, j] = np.random.multivariate_normal(means[t, c, j].numpy(), covs[t, c, j].numpy(), N)
+        means = G[:, GT, :, :2].numpy().astype(np.float64)
+        covs = G[:, GT, :, 2:].reshape(T, 2, J, 2, 2).numpy().astype(np.float64)
+        x = np.random.standard_normal((T, 2, J, N, 2))
+        _, s, v = np.linalg.svd(covs)
+        samples = np.matmul(x, np.sqrt(s)[..., :, None] * v) + means[..., None, :]
         return np.transpose(samples, (0, 2, 3, 1, 4))
 
     def _window_costs(self, G, X, B, lambda_smooth, lambda_body_length):
@@ -443,6 +449,13 @@ class Optimized_3d_Pose_Estimation:
         best_total = float("inf")
         no_improve = 0
         it = 0
+        if self.device_adam and Rp.shape == (3, 3) and tuple(Tp.shape) in ((3, 1), (3,)):
+            it, _ = self._sgd_extrinsic_device(samples_3d, targets, K, dist, Rp, Tp, const, names, hist, lr, betas,
+                                               patience, tolerance, max_iter, n_win, N, ignore_distortions,
+                                               trajectory, print_frequency)
+            self.all_costs_total = hist
+            self.iterations = it
+            return self
         while no_improve < patience and it <= max_iter:
             for w in range(n_win):
                 optimizer.zero_grad()
@@ -484,3 +497,83 @@ class Optimized_3d_Pose_Estimation:
         self.all_costs_total = hist
         self.iterations = it
         return self
+
+    def _sgd_extrinsic_device(self, samples_3d, targets, K, dist, Rp, Tp, const, names, hist, lr, betas, patience,
+                              tolerance, max_iter, n_win, N, ignore_distortions, trajectory, print_frequency,
+                              chunk_iters=8):
+        """The Adam loop of _sgd_extrinsic with every step on the device (learnable R a 3x3
+        matrix, the reference's default): per window one mvp_extrinsic_sample_grad pass and one
+        mvp_extrinsic_adam_step (clip + Adam, camera record updated in place) — no host round
+        trip per step.  Every `chunk_iters` iterations one read-back of the per-step costs and
+        parameters replays the reference's shared-list running means and early stop (F6) on the
+        host; the best / final parameters are taken from the parameter history (iterations the
+        device ran past the stopping point are discarded)."""
+        dev = self.device
+        cam = torch.cat([K.detach().reshape(9), Rp.detach().reshape(9), Tp.detach().reshape(3),
+                         dist.detach().reshape(5)]).to(torch.float32).to(dev).contiguous()
+        state = torch.zeros(25, dtype=torch.float32, device=dev)
+        max_steps = (int(max_iter) + 1) * n_win
+        cost_hist = torch.zeros(max_steps, dtype=torch.float32, device=dev)
+        param_hist = torch.zeros((max_steps, 12), dtype=torch.float32, device=dev)
+        n_pts = samples_3d.numel() // 3
+        n_blocks = max(1, min(1024, (n_pts + 255) // 256))
+        part = torch.empty((n_blocks, EXT_SUMS), dtype=torch.float64, device=dev)
+        s = _stream(dev)
+
+        def launch_step(step):
+            call("mvp_extrinsic_sample_grad", _ptr(samples_3d), _ptr(targets), int(N), int(n_pts), _ptr(cam),
+                 int(bool(ignore_distortions)), int(n_blocks), _ptr(part), s)
+            call("mvp_extrinsic_adam_step", _ptr(part), int(n_blocks), _ptr(cam), _ptr(state), float(lr),
+                 float(betas[0]), float(betas[1]), 1e-8, 1.0, _ptr(cost_hist), _ptr(param_hist), s)
+
+        best_total = float("inf")
+        no_improve = 0
+        it = 0
+        launched = 0          # iterations launched on the device
+        done = False
+        final_params = None
+        while not done:
+            n_new = min(chunk_iters, int(max_iter) + 1 - launched)
+            for _ in range(n_new * n_win):
+                launch_step(None)
+            launched += n_new
+            costs_h = cost_hist[:launched * n_win].cpu().numpy()
+            params_h = param_hist[:launched * n_win].cpu()
+            while it < launched:
+                for w in range(n_win):
+                    k = it * n_win + w
+                    costs = {n: torch.tensor(const[n][w]) for n in const}
+                    costs["extrinsic_param_sample_cost"] = torch.tensor(costs_h[k])
+                    total = torch.sum(torch.stack(list(costs.values())))
+                    hist["total_cost"].append(np.float32(total))
+                    for n in costs:
+                        hist[n].append(np.float32(costs[n]))
+                for n in names:
+                    hist[n].append(np.mean(hist[n], 0))
+                last = params_h[(it + 1) * n_win - 1]
+                final_params = last
+                cur = hist["total_cost"][-1]
+                if cur < best_total - tolerance:
+                    best_total = cur
+                    self.best_trajectory = trajectory.clone().detach()
+                    self.best_decomposed_cam_params = {k2: [p.clone().detach() for p in v]
+                                                       for k2, v in self.decomposed_cam_params.items()}
+                    ID = [k2 for k2, v in self.decomposed_cam_params.items() if v[1] is Rp][0]
+                    self.best_decomposed_cam_params[ID][1] = last[:9].reshape(3, 3).clone()
+                    self.best_decomposed_cam_params[ID][2] = last[9:].reshape(Tp.shape).clone()
+                    no_improve = 0
+                else:
+                    no_improve += 1
+                if no_improve >= patience:
+                    done = True
+                    break
+                if print_frequency and it % print_frequency == 0 and print_frequency < 10 ** 8:
+                    print(f"Iteration {it}: " + ", ".join(f"{n}: {hist[n][-1]:.2e}" for n in names))
+                it += 1
+                if it > max_iter:
+                    done = True
+                    break
+        with torch.no_grad():
+            Rp.copy_(final_params[:9].reshape(3, 3))
+            Tp.copy_(final_params[9:].reshape(Tp.shape))
+        return it, final_params

@@ -206,10 +206,10 @@ def make_skeleton_frames(n: int, seed: int = 0, h: int = FRAME_H, w: int = FRAME
     k, off = _whole_image_heatmap_to_image(h, w)
     frames = np.empty((n, h, w, 3), np.uint8)
     joints = np.empty((n, N_JOINTS, 2))
-    ys, xs = np.mgrid[0:h, 0:w]
+    ys, xs = np.mgrid[0:h, 0:w].astype(np.float32)
     for i in range(n):
-        base = rng.integers(20, 90, 3)
-        img = np.clip(base + rng.normal(0.0, 6.0, (h, w, 3)), 0, 255)
+        base = rng.integers(20, 90, 3).astype(np.int16)
+        img = (base + rng.integers(-10, 11, (h, w, 3), dtype=np.int16)).astype(np.uint8)   # 10..99: no clipping
         cells = skeleton_layout(rng, h, w)
         # the crop samples pixel centres: heatmap position c <-> image coordinate c * k + off
         centers = cells * k + off
@@ -219,8 +219,8 @@ def make_skeleton_frames(n: int, seed: int = 0, h: int = FRAME_H, w: int = FRAME
             x0, x1 = int(max(0, cx - r - 1)), int(min(w, cx + r + 2))
             y0, y1 = int(max(0, cy - r - 1)), int(min(h, cy + r + 2))
             m = (xs[y0:y1, x0:x1] - cx) ** 2 + (ys[y0:y1, x0:x1] - cy) ** 2 <= r * r
-            col = _PAIR_COLORS[_PAIR_OF_JOINT[j]].astype(float) + rng.normal(0.0, 6.0, 3)
-            img[y0:y1, x0:x1][m] = col
-        frames[i] = img.astype(np.uint8)
+            col = np.clip(_PAIR_COLORS[_PAIR_OF_JOINT[j]].astype(np.int16) + rng.integers(-8, 9, 3), 0, 255)
+            img[y0:y1, x0:x1][m] = col.astype(np.uint8)
+        frames[i] = img
         joints[i] = cells
     return frames, joints

@@ -5,20 +5,25 @@ frames and the same cameras (oracle/heatmap_ref.preprocess -> hrnet_ref
 flip_test_forward -> msra_decode / keypoints_to_image -> cv_ref.get_pose_3D), the
 reference's pose_estimation.py:88-135 + :319-322 loop.
 
-The weights are mvpose.hrnet.random_state_dict's activation-stable seeded weights
-(O(0.1) heatmaps, a few per cent of cells above the 0.01 threshold), so argmax and
-threshold decisions are realistic.  bf16 weights/activations through ~90 layers move
-the heatmaps by ~1e-2 relative, so an argmax can move where two cells are within that
-of each other; random weights have no trained-model peak (a trained peak's neighbour
-sits ~12 % below it), so the agreement rate here is a pessimistic figure.
-Asserted (tolerances written here):
-* argmax agreement >= ARGMAX_MIN of all (frame, view, joint) heatmaps (measured rate
-  printed and recorded in DESIGN.md);
-* where the argmax agrees (and the max's sign, which decides MSRA's -1 marker), the decoded keypoint differs from the oracle's only by the
-  +-0.25-cell MSRA refinement step's sign (|dx|, |dy| in {0, one step}); where, in
-  addition, the refinement agrees, x and y are bit-exact;
+Two workloads (module fixture `runs`, parametrised):
+* "peaked" — the headline parity case: mvpose.hrnet.peaked_state_dict (seeded random
+  convolutions with BatchNorms, stem, last high-resolution branch and head fitted on
+  rendered skeleton frames, tools/train_peaked_hrnet.py) on synthetic.make_skeleton_frames:
+  one trained-model-like peak per joint, so argmax parity is measured on decidable maps;
+* "random" — random_state_dict's activation-stable seeded weights on uniform-noise frames:
+  O(0.1) maps, many without any peak, so most argmaxes are near-ties (a pessimistic figure).
+bf16 weights/activations through ~90 layers move the heatmaps by ~1e-2 relative, so an
+argmax can only move where two cells are within that of each other.
+Asserted per workload (tolerances in LIMITS; measured rates printed and recorded in DESIGN §5):
+* argmax agreement >= argmax_min of all (frame, view, joint) heatmaps;
+* >= decidable_fraction of maps lead their runner-up by > MARGIN of the map's max|h| in
+  fp32, and there the argmax agrees on >= DECIDABLE_MIN;
+* where the argmax agrees (and the max's sign, which decides MSRA's -1 marker), the decoded
+  keypoint differs from the oracle's only by the +-0.25-cell MSRA refinement step's sign
+  (|dx|, |dy| in {0, one step}), and is bit-exact on >= exact_min of those maps;
 * where both views' x, y are bit-exact and the camera order (ascending score, the
-  reference's top-2 rule) agrees, kpts_3d is within 1e-4 world units.
+  reference's top-2 rule) agrees, kpts_3d is within 1e-4 world units — on >= k3_min of
+  all joints.
 """
 import numpy as np
 import pytest
@@ -29,21 +34,27 @@ from oracle import cv_ref, heatmap_ref, hrnet_ref
 pytestmark = pytest.mark.gpu
 
 T, V = 8, 2
-ARGMAX_MIN = 0.80
 MARGIN = 1e-2              # fp32 top-1 lead over top-2, in units of the map's max|h|
 DECIDABLE_MIN = 0.99
-DECIDABLE_FRACTION = 0.2
+LIMITS = {
+    "peaked": dict(argmax_min=0.99, decidable_fraction=0.80, exact_min=0.99, k3_min=0.90),
+    "random": dict(argmax_min=0.80, decidable_fraction=0.20, exact_min=0.50, k3_min=0.0),
+}
 
 
-@pytest.fixture(scope="module")
-def runs():
+@pytest.fixture(scope="module", params=["peaked", "random"])
+def runs(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet, pipeline, synthetic as syn
-    sd = hrnet.random_state_dict(21)
+    if request.param == "peaked":
+        sd = hrnet.peaked_state_dict()
+        frames = syn.make_skeleton_frames(T * V, seed=31)[0].reshape(T, V, 720, 1280, 3)
+    else:
+        sd = hrnet.random_state_dict(21)
+        frames = syn.make_frames(T * V, seed=31).reshape(T, V, 720, 1280, 3)
     cams = syn.make_rig(V, seed=4)
     cp = syn.reference_camera_params(cams)
-    frames = syn.make_frames(T * V, seed=31).reshape(T, V, 720, 1280, 3)
     p = pipeline.MultiViewPipeline(cp, max_frames=T * V, state_dict=sd)
     out = p.process(torch.tensor(frames, device="cuda"))
     torch.cuda.synchronize()
@@ -67,14 +78,15 @@ def runs():
             amax[t, v] = idx
     k3 = cv_ref.get_pose_3D(cp, k2, camera_indices=[0, 1])
     gam = np.stack([heatmap_ref.msra_decode(gpu_avg[i])[2] for i in range(T * V)]).reshape(T, V, 17)
-    return dict(gpu=gpu, k2=k2, k3=k3, amax=amax, gamax=gam, scale=scale, oavg=oavg)
+    return dict(gpu=gpu, k2=k2, k3=k3, amax=amax, gamax=gam, scale=scale, oavg=oavg, name=request.param,
+                lim=LIMITS[request.param])
 
 
 def test_argmax_agreement(runs):
     agree = runs["gamax"] == runs["amax"]
     rate = agree.mean()
-    print(f"argmax agreement {rate:.4f} ({agree.sum()}/{agree.size})")
-    assert rate >= ARGMAX_MIN
+    print(f"[{runs['name']}] argmax agreement {rate:.4f} ({agree.sum()}/{agree.size})")
+    assert rate >= runs["lim"]["argmax_min"]
 
 
 def test_argmax_agreement_on_decidable_maps(runs):
@@ -90,10 +102,10 @@ def test_argmax_agreement_on_decidable_maps(runs):
     agree = runs["gamax"] == runs["amax"]
     for m in (0.0, 1e-3, 1e-2, 2e-2, 5e-2, 1e-1):
         sel = lead > m
-        print(f"lead > {m:g} max|h|: {sel.mean():.3f} of maps, argmax agreement "
+        print(f"[{runs['name']}] lead > {m:g} max|h|: {sel.mean():.3f} of maps, argmax agreement "
               f"{agree[sel].mean() if sel.any() else 1:.4f}")
     sel = lead > MARGIN
-    assert sel.sum() >= DECIDABLE_FRACTION * sel.size, sel.mean()
+    assert sel.sum() >= runs["lim"]["decidable_fraction"] * sel.size, sel.mean()
     assert agree[sel].mean() >= DECIDABLE_MIN, agree[sel].mean()
 
 
@@ -115,8 +127,9 @@ def test_keypoints_where_argmax_agrees(runs):
     ok = (d <= 1.01 * step) | (d == 0)
     assert ok.transpose(0, 1, 3, 2)[agree].all()
     exact = (d == 0).all(axis=2) & agree
-    print(f"kpts_2d bit-exact {exact.mean():.4f} of all, {exact.sum() / max(1, agree.sum()):.4f} where argmax agrees")
-    assert exact.sum() >= 0.5 * agree.sum()
+    print(f"[{runs['name']}] kpts_2d bit-exact {exact.mean():.4f} of all, "
+          f"{exact.sum() / max(1, agree.sum()):.4f} where argmax agrees")
+    assert exact.sum() >= runs["lim"]["exact_min"] * agree.sum()
 
 
 def test_kpts_3d_where_inputs_agree(runs):
@@ -125,6 +138,7 @@ def test_kpts_3d_where_inputs_agree(runs):
     order_same = (g2[:, :, 2, 0] < g2[:, :, 2, 1]) == (o2[:, :, 2, 0] < o2[:, :, 2, 1])
     sel = xy_exact & order_same
     d = np.abs(runs["gpu"]["kpts_3d"] - runs["k3"])[sel]
-    print(f"kpts_3d compared on {sel.sum()}/{sel.size} joints, max |d| {np.nanmax(d) if d.size else 0:.3g}")
-    assert sel.sum() > 0
+    print(f"[{runs['name']}] kpts_3d compared on {sel.sum()}/{sel.size} joints, "
+          f"max |d| {np.nanmax(d) if d.size else 0:.3g}")
+    assert sel.sum() > 0 and sel.sum() >= runs["lim"]["k3_min"] * sel.size
     np.testing.assert_allclose(runs["gpu"]["kpts_3d"][sel], runs["k3"][sel], rtol=0, atol=1e-4)

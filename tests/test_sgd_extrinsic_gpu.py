@@ -7,7 +7,9 @@ optimize_trajectory=False, GT_camera_IDs=[a, b]), reference pose_refinement.py:6
   RNG — bit-identical (CPU, no kernel);
 * the triangulated samples (mvp_triangulate on the float32-cast samples; the golden's stub
   cv2 does the same cast) — within 1e-3 cm: P = K[R|T] is fp64 here and float32 np.dot in
-  the reference;
+  the reference.  PARITY UNPINNED for this leg: real cv2 keeps the float64 samples in float64
+  through undistortPoints / triangulatePoints, so the goldens restate the float32-keypoint
+  path the pipeline uses, not the reference's exact numbers (DESIGN §5);
 * one mvp_extrinsic_sample_grad pass vs a torch fp32 autograd restatement of
   construct_sample_cost's cost() — cost rtol 1e-5, gradient rtol 1e-4;
 * the whole optimisation: the shared cost / running-mean history (F6), final and best
@@ -111,30 +113,69 @@ def test_sample_cost_and_gradient(name):
                                atol=1e-4 * T.grad.abs().max().item())
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("name", CASES)
-def test_extrinsic_optimisation_matches_reference(name):
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    z, kw = _load(name)
+def _run_opt(z, kw, device_adam):
     ext = int(z["ext_id"][0])
     opt = _opt(z)
+    opt.device_adam = device_adam
     _seed(z)
     opt.sgd_optimize(extrinsic_optimization_IDs=[ext], optimize_trajectory=False,
                      GT_camera_IDs=[int(i) for i in z["gt_ids"]], print_frequency=10 ** 9, **kw)
+    return opt, ext
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("device_adam", [True, False])
+@pytest.mark.parametrize("name", CASES)
+def test_extrinsic_optimisation_matches_reference(name, device_adam):
+    """Both step drivers (Adam on the device, the default; torch CPU Adam per step) against the
+    reference's golden run; measured deviations are printed (DESIGN §5 records them)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z, kw = _load(name)
+    opt, ext = _run_opt(z, kw, device_adam)
     np.testing.assert_allclose(opt.samples_3d.cpu().numpy(), z["samples_3d"], rtol=0, atol=1e-3)
     names = [k[5:] for k in z.files if k.startswith("hist_")]
     assert list(opt.all_costs_total.keys()) == names
+    worst = 0.0
     for n in names:
         got = np.array(opt.all_costs_total[n], np.float64)
         assert got.shape == z["hist_" + n].shape, n
+        worst = max(worst, float(np.max(np.abs(got - z["hist_" + n]) / np.maximum(np.abs(z["hist_" + n]), 1e-30))))
         np.testing.assert_allclose(got, z["hist_" + n], rtol=2e-3, err_msg=n)
     fin = opt.decomposed_cam_params[ext]
     best = opt.best_decomposed_cam_params[ext]
+    dev = {"final_R": np.abs(fin[1].detach().numpy() - z["final_R"]).max(),
+           "final_T": np.abs(fin[2].detach().numpy() - z["final_T"]).max(),
+           "best_R": np.abs(best[1].numpy() - z["best_R"]).max(),
+           "best_T": np.abs(best[2].numpy() - z["best_T"]).max()}
+    print(f"[{name} device_adam={device_adam}] cost history max rel dev {worst:.3g}; "
+          + ", ".join(f"{k} {v:.3g}" for k, v in dev.items()))
     np.testing.assert_allclose(fin[1].detach().numpy(), z["final_R"], rtol=0, atol=2e-3)
     np.testing.assert_allclose(fin[2].detach().numpy(), z["final_T"], rtol=2e-3, atol=2e-3)
     np.testing.assert_allclose(best[1].numpy(), z["best_R"], rtol=0, atol=2e-3)
     np.testing.assert_allclose(best[2].numpy(), z["best_T"], rtol=2e-3, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_device_adam_matches_host_adam(name):
+    """mvp_extrinsic_adam_step (reduction, f32 casts, clip_grad_norm_, single-tensor Adam on the
+    device) vs the host loop (the same gradient pass, torch CPU clip + Adam): the same number of
+    iterations and histories / parameters equal to f32 reduction-order rounding."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    z, kw = _load(name)
+    a, ext = _run_opt(z, kw, True)
+    b, _ = _run_opt(z, kw, False)
+    assert a.iterations == b.iterations
+    for n in a.all_costs_total:
+        np.testing.assert_allclose(np.array(a.all_costs_total[n], np.float64),
+                                   np.array(b.all_costs_total[n], np.float64), rtol=1e-5, err_msg=n)
+    for k in (1, 2):
+        np.testing.assert_allclose(a.decomposed_cam_params[ext][k].detach().numpy(),
+                                   b.decomposed_cam_params[ext][k].detach().numpy(), rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(a.best_decomposed_cam_params[ext][k].numpy(),
+                                   b.best_decomposed_cam_params[ext][k].numpy(), rtol=1e-5, atol=1e-6)
 
 
 def test_extrinsic_argument_errors():

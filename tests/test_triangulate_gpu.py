@@ -164,3 +164,81 @@ def test_full_size_roundtrip_property(ops):
     k2[:, :, 2, :] = k[:, :, 2, ::-1]  # flip the confidence order -> swapped camera order
     out2 = _run(ops, cp, k2, [0, 1])
     np.testing.assert_allclose(out2, out, atol=ATOL)
+
+
+# ------------------------------------------------------------------ tolerance mode
+def _tol_vs_exact(ops, cp, k, ci=(0, 1)):
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    kd = torch.tensor(np.ascontiguousarray(k), device="cuda")
+    tol = ops.triangulate(kd, cams_d, list(ci), tolerance=True).cpu().numpy()
+    ex = ops.triangulate(kd, cams_d, list(ci), exact=True).cpu().numpy()
+    return tol, ex
+
+
+@pytest.mark.parametrize("seed,noise", [(51, 1.0), (52, 0.0), (53, 40.0), (54, 3.0)])
+def test_tolerance_mode_vs_exact(ops, seed, noise):
+    """MVP_TRI_TOLERANCE (mixed f32/fp64 undistortion + normal-equation inverse iteration)
+    vs the exact-rounding restatement on the same points: <= 1e-4 world units (the
+    north_star contract), and bit-identical on >= 95 % of coordinates — noise-free
+    (singular A), 1-3 px and badly inconsistent (40 px) views."""
+    cams = syn.make_rig(2, seed=seed)
+    k = syn.make_kpts_2d(syn.make_poses(3000, seed=seed + 1), cams, seed=seed + 2, noise_px=noise)
+    tol, ex = _tol_vs_exact(ops, syn.reference_camera_params(cams), k)
+    d = np.abs(tol - ex)
+    print(f"tolerance vs exact (noise {noise} px): max |d| {np.nanmax(d):.3g}, bit-identical {np.mean(d == 0):.4f}")
+    np.testing.assert_allclose(tol, ex, rtol=0, atol=ATOL, equal_nan=True)
+    assert np.mean(d == 0) >= 0.95
+
+
+@pytest.mark.parametrize("tag,ign", [("01", False), ("01_nodist", True)])
+def test_tolerance_mode_golden(ops, tag, ign):
+    """The reference's own get_pose_3D golden vectors (pose3d_select.npz), camera_indices [0, 1]."""
+    d = np.load(os.path.join(GOLDEN, "pose3d_select.npz"))
+    cp = _cams(d)
+    if ign:
+        cp = {k: [K, R, T, np.asarray(dist) * 0] for k, (K, R, T, dist) in cp.items()}
+    cams = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    out = ops.triangulate(torch.tensor(d["kpts"], device="cuda"), cams, [0, 1], tolerance=True).cpu().numpy()
+    np.testing.assert_allclose(out, d["out_" + tag], rtol=0, atol=ATOL, equal_nan=True)
+
+
+def test_tolerance_mode_ties_nans_degenerate(ops):
+    """Equal confidences (np.argsort keeps [0, 1]), NaN / Inf coordinates and confidences,
+    geometrically inconsistent random points: the same answer as the exact path (NaN where
+    it gives NaN; <= 1e-4 elsewhere, away from points at infinity)."""
+    cams = syn.make_rig(2, seed=61)
+    rng = np.random.default_rng(62)
+    k = syn.make_kpts_2d(syn.make_poses(400, seed=63), cams, seed=64)
+    k[::4, :, 2, 1] = k[::4, :, 2, 0]                       # ties
+    k[5, 3, 2, 0] = np.nan                                  # NaN confidence sorts last
+    k[6, 4, 2, 1] = np.nan
+    k[7, 3, 0, 1] = np.nan
+    k[9, 4, 1, 0] = np.inf
+    k[200:] = 0
+    k[200:, :, 0] = rng.uniform(0, 1280, (200, 17, 2))      # random, inconsistent views
+    k[200:, :, 1] = rng.uniform(0, 720, (200, 17, 2))
+    k[200:, :, 2] = rng.uniform(0.3, 1, (200, 17, 2))
+    cp = syn.reference_camera_params(cams)
+    tol, ex = _tol_vs_exact(ops, cp, k)
+    ref = cv_ref.get_pose_3D(cp, k, camera_indices=[0, 1])
+    np.testing.assert_array_equal(np.isnan(tol), np.isnan(ex))
+    np.testing.assert_allclose(ex[:200], ref[:200], rtol=0, atol=ATOL, equal_nan=True)
+    np.testing.assert_allclose(tol[:200], ex[:200], rtol=0, atol=ATOL, equal_nan=True)
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    _, ew = ops.triangulate(torch.tensor(k, device="cuda"), cams_d, [0, 1], exact=True, return_xyzw=True)
+    far = (np.abs(ew.cpu().numpy()[..., 3]) < 1e-6)[200:]
+    np.testing.assert_allclose(tol[200:][~far], ex[200:][~far], rtol=1e-5, atol=ATOL)
+
+
+def test_tolerance_mode_full_size(ops):
+    """BASELINE config 4 size (100 k frames x 17 joints): tolerance vs exact within 1e-4
+    on every coordinate, and noise-free projections triangulate back to the poses."""
+    cams = syn.make_rig(2, seed=71)
+    poses = syn.make_poses(100_000, seed=72)
+    k = syn.make_kpts_2d(poses, cams, seed=73, noise_px=0.5)
+    tol, ex = _tol_vs_exact(ops, syn.reference_camera_params(cams), k)
+    d = np.abs(tol - ex)
+    print(f"100k frames: max |d| {d.max():.3g}, bit-identical {np.mean(d == 0):.5f}")
+    assert np.isfinite(tol).all()
+    np.testing.assert_allclose(tol, ex, rtol=0, atol=ATOL)
+    np.testing.assert_allclose(tol, poses, atol=0.5)

@@ -7,7 +7,10 @@ OUT=$ROOT/gpurun_out/$N
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-ARGS=("$@")
+ARGS=()
+for a in "$@"; do
+    if [ -e "$ROOT/${a%%::*}" ]; then ARGS+=("$ROOT/$a"); else ARGS+=("$a"); fi
+done
 [ ${#ARGS[@]} -eq 0 ] && ARGS=("$ROOT/tests")
 timeout -k 10 900 python3 -u -m pytest "${ARGS[@]}" -m gpu -q -rs -p no:cacheprovider --timeout 120 \
     --timeout-method thread -s > "$OUT/pytest_gpu.log" 2>&1

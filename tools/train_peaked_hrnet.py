@@ -1,25 +1,33 @@
-"""Seeded CPU fine-tuning that gives the synthetic HRNet-W32 trained-model-like, PEAKED heatmaps.
+"""Seeded fine-tuning that gives the synthetic HRNet-W32 trained-model-like, PEAKED heatmaps.
 
 The end-to-end parity test (tests/test_e2e_parity_gpu.py) compares the bf16 GPU pipeline with
 the fp32 oracle on identical frames.  With purely random weights most heatmaps have no peak,
 so argmax parity would be measured on near-ties.  This script keeps mvpose.hrnet's seeded
-random weights (random_state_dict(BASE_SEED)) for the whole network except the last stage-4
-HRModule's high-resolution branch (4 BasicBlocks), its three fuse projections into that branch
-and the HeatmapHead, and fits those (~88 k parameters) on rendered skeleton frames
-(mvpose.synthetic.make_skeleton_frames) with the standard top-down target: a Gaussian
-(sigma 2 heatmap cells) per joint, MSE loss (mmpose MSRAHeatmap + KeypointMSELoss).
-Training includes the flipped crops with the flip test's left/right-swapped targets, so the
-flip-averaged maps the pipeline decodes have one clear maximum per joint.
+random convolution weights (random_state_dict(PEAKED_BASE_SEED)) and fits a small set of
+parameters on rendered skeleton frames (mvpose.synthetic.make_skeleton_frames: one coloured
+disc per COCO joint) with the standard top-down target — a Gaussian (sigma 2 heatmap cells)
+per joint, MSE loss (mmpose MSRAHeatmap + KeypointMSELoss):
 
-Run once in the build container (CPU, ~10-20 min):
-    python tools/train_peaked_hrnet.py
-It writes multi-camera_3d_pose_estimation_amd/mvpose/data/hrnet_w32_peaked.npz (the trained
-tensors only, mmpose state-dict names; loaded by mvpose.hrnet.peaked_state_dict with
-numpy's pickle-free loader).  Everything is seeded; the fit is deterministic on one thread
-count.
+* every BatchNorm's affine parameters and running statistics (the network's routing: random
+  convolutions with trained BatchNorm alone already learn real tasks),
+* the two stem convolutions, the last stage-4 module's high-resolution branch (4 BasicBlocks)
+  and its three fuse projections, and the HeatmapHead.
+
+Training includes flipped crops with the flip test's left/right-swapped targets, so the
+flip-averaged maps the pipeline decodes have one clear maximum per joint.  It runs in torch
+on one MI355X in a few minutes (the crops come from libmvpose's mvp_preprocess, the same
+kernel the pipeline uses):
+
+    gpurun -- python tools/train_peaked_hrnet.py
+It writes gpurun_out/peaked/hrnet_w32_peaked.npz (the fitted tensors only, mmpose state-dict
+names); committed as multi-camera_3d_pose_estimation_amd/mvpose/data/hrnet_w32_peaked.npz and
+loaded by mvpose.hrnet.peaked_state_dict with numpy's pickle-free loader.  Seeded (data,
+initialisation, batch order); GPU atomics in the backward pass make the fit reproducible to
+rounding, not bit for bit.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import sys
 import time
@@ -31,60 +39,28 @@ import torch.nn.functional as F
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd")]
 
-from mvpose import hrnet, synthetic as syn  # noqa: E402
+from mvpose import geometry, hrnet, synthetic as syn  # noqa: E402
+from mvpose._lib import call  # noqa: E402
+from mvpose.estimator import MEAN, STD  # noqa: E402
 from oracle import heatmap_ref, hrnet_ref  # noqa: E402
 
-BASE_SEED = hrnet.PEAKED_BASE_SEED
-OUT = os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd", "mvpose", "data", "hrnet_w32_peaked.npz")
+OUT_DIR = os.path.join(ROOT, "gpurun_out", "peaked")
 SIGMA = 2.0
 FLIP = heatmap_ref.COCO_FLIP_INDICES
 
 
-def frozen_features(bb, x):
-    """Inputs of the last stage-4 module: branch 0's input, branches 1-3 after their blocks."""
-    x = F.relu(bb.bn1(bb.conv1(x)))
-    x = F.relu(bb.bn2(bb.conv2(x)))
-    x = bb.layer1(x)
-    ys = [x]
-    for s in range(3):
-        trans = getattr(bb, f"transition{s + 1}")
-        xs = [ys[i] if t is None else t(ys[-1]) for i, t in enumerate(trans)]
-        mods = getattr(bb, f"stage{s + 2}")
-        for m in (mods if s < 2 else mods[:-1]):
-            xs = m(xs)
-        ys = xs
-    last = bb.stage4[-1]
-    return [xs[0]] + [last.branches[j](xs[j]) for j in (1, 2, 3)]
-
-
-def trainable_forward(model, feats):
-    last = model.backbone.stage4[-1]
-    y = last.branches[0](feats[0])
-    for j in (1, 2, 3):
-        y = y + last.fuse_layers[0][j](feats[j])
-    return model.head(F.relu(y))
-
-
-def calibrate_bn(model, feats, n=128):
-    """Running statistics of the trainable part's BatchNorms from these inputs (the random
-    ones were drawn for unit-variance noise): each BN in forward order sees its input's batch
-    mean / variance, so the fit starts from O(1) activations.  (The GPU graph folds whatever
-    statistics the state dict holds.)"""
-    last = model.backbone.stage4[-1]
-    bns = [mod for blk in last.branches[0] for mod in (blk.bn1, blk.bn2)]
-    bns += [last.fuse_layers[0][j][1] for j in (1, 2, 3)]
-    hooks = []
-
-    def pre(mod, inp):
-        x = inp[0]
-        mod.running_mean.copy_(x.mean((0, 2, 3)))
-        mod.running_var.copy_(x.var((0, 2, 3)))
-    for b in bns:
-        hooks.append(b.register_forward_pre_hook(pre))
-    with torch.no_grad():
-        trainable_forward(model, [f[:n] for f in feats])
-    for h in hooks:
-        h.remove()
+def crops_on_device(frames: np.ndarray, dev) -> torch.Tensor:
+    """Whole-image TopdownAffine crops by mvp_preprocess (swap_rb=1, as BatchPoseEstimator's
+    default and the e2e test) -> (n, 3, 256, 192) float32 on the device."""
+    n, h, w, _ = frames.shape
+    g = geometry.CropGeometry.whole_image(w, h)
+    fd = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    minv = torch.tensor(np.tile(g.crop_minv, (n, 1)), dtype=torch.float64, device=dev)
+    out = torch.empty((n, 256, 192, 4), dtype=torch.bfloat16, device=dev)
+    mean, std = (ctypes.c_float * 3)(*MEAN), (ctypes.c_float * 3)(*STD)
+    call("mvp_preprocess", ctypes.c_void_p(fd.data_ptr()), n, h, w, ctypes.c_void_p(minv.data_ptr()), 256, 192,
+         mean, std, 1, 0, ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    return out[..., :3].float().permute(0, 3, 1, 2).contiguous()
 
 
 def targets(joints, flipped):
@@ -103,95 +79,101 @@ def targets(joints, flipped):
     return t
 
 
-def crops_of(frames):
-    M, _, _ = heatmap_ref.topdown_crop_matrix(frames.shape[2], frames.shape[1])
-    return np.stack([heatmap_ref.preprocess(f, M) for f in frames])
+def trainable_params(model):
+    bb = model.backbone
+    last = bb.stage4[-1]
+    mods = [bb.conv1, bb.conv2, last.branches[0], model.head]
+    mods += [last.fuse_layers[0][j] for j in (1, 2, 3)]
+    ps = {id(p): p for m in mods for p in m.parameters()}
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            for p in m.parameters():
+                ps[id(p)] = p
+    return list(ps.values())
 
 
-def evaluate(model, feats_o, feats_f, joints):
+def flip_avg(model, x):
+    h = model(x)
+    hf = model(x.flip(-1)).flip(-1)[:, FLIP].clone()
+    hf[..., 1:] = hf[..., :-1].clone()
+    return (h + hf) * 0.5
+
+
+def evaluate(model, x, joints):
+    model.eval()
     with torch.no_grad():
-        h = trainable_forward(model, feats_o)
-        hf = trainable_forward(model, feats_f)
-    hfb = hf.flip(-1)[:, FLIP].clone()
-    hfb[..., 1:] = hfb[..., :-1].clone()
-    avg = ((h + hfb) * 0.5).reshape(h.shape[0], 17, -1).numpy()
+        avg = torch.cat([flip_avg(model, x[i:i + 16]) for i in range(0, x.shape[0], 16)]).cpu().numpy()
+    avg = avg.reshape(avg.shape[0], 17, -1)
     top2 = -np.sort(-avg, axis=-1)[..., :2]
     lead = (top2[..., 0] - top2[..., 1]) / np.abs(avg).max(axis=-1)
-    am = avg.argmax(-1)
-    want = np.round(joints[..., 1] - 0.25).astype(int) * 48 + np.round(joints[..., 0]).astype(int)
-    return (lead > 1e-2).mean(), (am == want).mean(), float(np.median(top2[..., 0]))
+    want = np.round(joints[..., 1] - syn.HEATMAP_OFFSET[1]).astype(int) * 48 + np.round(joints[..., 0]).astype(int)
+    return round(float((lead > 1e-2).mean()), 4), round(float((avg.argmax(-1) == want).mean()), 4), \
+        round(float(np.median(top2[..., 0])), 4)
 
 
 def main():
+    dev = torch.device("cuda")
     torch.manual_seed(0)
-    torch.set_num_threads(int(os.environ.get("TRAIN_THREADS", "6")))
-    model = hrnet_ref.build(hrnet.random_state_dict(BASE_SEED))
-    bb = model.backbone
-    n_train, n_val = int(os.environ.get("N_TRAIN", "384")), 48
+    n_train, n_val = int(os.environ.get("N_TRAIN", "2048")), 64
+    steps, bs = int(os.environ.get("STEPS", "3000")), int(os.environ.get("BATCH", "32"))
     t0 = time.time()
     fr, jt = syn.make_skeleton_frames(n_train, seed=1000)
     fv, jv = syn.make_skeleton_frames(n_val, seed=2000)
     print(f"rendered {n_train + n_val} frames in {time.time() - t0:.1f}s", flush=True)
-
-    def cache(frames):
-        outs_o, outs_f = [[] for _ in range(4)], [[] for _ in range(4)]
-        for i in range(0, len(frames), 16):
-            x = torch.from_numpy(crops_of(frames[i:i + 16]))
-            with torch.no_grad():
-                for outs, xin in ((outs_o, x), (outs_f, x.flip(-1))):
-                    for k, f in enumerate(frozen_features(bb, xin)):
-                        outs[k].append(f)
-        return [torch.cat(o) for o in outs_o], [torch.cat(o) for o in outs_f]
-
-    t0 = time.time()
-    tr_o, tr_f = cache(fr)
-    va_o, va_f = cache(fv)
-    print(f"cached frozen features in {time.time() - t0:.1f}s", flush=True)
-    feats = [torch.cat([a, b]) for a, b in zip(tr_o, tr_f)]
-    tgt = torch.from_numpy(np.concatenate([targets(jt, False), targets(jt, True)]))
-    last = bb.stage4[-1]
-    params = list(last.branches[0].parameters()) + list(model.head.parameters())
-    for j in (1, 2, 3):
-        params += list(last.fuse_layers[0][j].parameters())
+    xtr = torch.cat([crops_on_device(fr[i:i + 128], dev) for i in range(0, n_train, 128)])
+    xva = crops_on_device(fv, dev)
+    del fr
+    ttr = torch.from_numpy(np.stack([targets(jt, False), targets(jt, True)], 1)).to(dev)   # (n, 2, 17, 64, 48)
+    model = hrnet_ref.build(hrnet.random_state_dict(hrnet.PEAKED_BASE_SEED)).to(dev)
     for p in model.parameters():
         p.requires_grad_(False)
+    params = trainable_params(model)
     for p in params:
         p.requires_grad_(True)
-    calibrate_bn(model, feats)
     with torch.no_grad():   # a fresh head (the random one is biased to -0.15)
         model.head.final_layer.weight.normal_(0.0, 0.01)
         model.head.final_layer.bias.zero_()
-    epochs, bs = int(os.environ.get("EPOCHS", "60")), int(os.environ.get("BATCH", "16"))
-    opt = torch.optim.Adam(params, lr=float(os.environ.get("LR", "5e-4")))
-    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, epochs)
-    n = tgt.shape[0]
-    g = torch.Generator().manual_seed(1)
-    model.eval()   # BN with its running statistics (affine parameters are trained)
-    for ep in range(epochs):
-        t0 = time.time()
-        perm = torch.randperm(n, generator=g)
-        tot = 0.0
-        for i in range(0, n, bs):
-            idx = perm[i:i + bs]
-            out = trainable_forward(model, [f[idx] for f in feats])
-            loss = F.mse_loss(out, tgt[idx]) * 1e3
-            opt.zero_grad()
-            loss.backward()
-            opt.step()
-            tot += float(loss.detach()) * len(idx)
+    print(f"{sum(p.numel() for p in params)} trainable values; val before: {evaluate(model, xva, jv)}", flush=True)
+    lr = float(os.environ.get("LR", "1e-3"))
+    opt = torch.optim.Adam(params, lr=lr)
+    sched = torch.optim.lr_scheduler.OneCycleLR(opt, max_lr=lr, total_steps=steps, pct_start=0.05)
+    g = torch.Generator(device="cpu").manual_seed(1)
+    t0 = time.time()
+    for it in range(steps):
+        model.train()
+        idx = torch.randint(0, n_train, (bs,), generator=g).to(dev)
+        flip = torch.randint(0, 2, (bs,), generator=g).to(dev)
+        x = xtr[idx]
+        x = torch.where(flip.bool()[:, None, None, None], x.flip(-1), x)
+        tgt = ttr[idx, flip]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = model(x)
+        loss = F.mse_loss(out.float(), tgt) * 1e3
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
         sched.step()
-        if ep % 5 == 4 or ep == epochs - 1:
-            dec, acc, peak = evaluate(model, va_o, va_f, jv)
-            print(f"epoch {ep + 1}: loss {tot / n:.4f}  val decidable {dec:.3f} argmax-at-joint {acc:.3f} "
-                  f"median peak {peak:.3f}  ({time.time() - t0:.1f}s/epoch)", flush=True)
-        else:
-            print(f"epoch {ep + 1}: loss {tot / n:.4f} ({time.time() - t0:.1f}s)", flush=True)
-    sd = model.state_dict()
-    keys = [k for k in sd if k.startswith("backbone.stage4.2.branches.0.") or k.startswith("head.")
-            or any(k.startswith(f"backbone.stage4.2.fuse_layers.0.{j}.") for j in (1, 2, 3))]
-    keys = [k for k in keys if not k.endswith("num_batches_tracked")]   # incl. the recalibrated BN statistics
-    np.savez(OUT, **{k: sd[k].detach().numpy().astype(np.float32) for k in keys})
-    print(f"wrote {len(keys)} tensors ({sum(sd[k].numel() for k in keys)} values) to {OUT}")
+        if it % 250 == 0 or it == steps - 1:
+            print(f"step {it}: loss {float(loss):.4f}  val {evaluate(model, xva, jv)}  ({time.time() - t0:.0f}s)",
+                  flush=True)
+    # exact running statistics for inference: cumulative averages over training crops
+    for m in model.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.reset_running_stats()
+            m.momentum = None
+    model.train()
+    with torch.no_grad():
+        for i in range(0, min(n_train, 1024), 32):
+            model(torch.cat([xtr[i:i + 32], xtr[i:i + 32].flip(-1)]))
+    dec, acc, peak = evaluate(model, xva, jv)
+    print(f"final (eval mode, fp32, flip test): val decidable {dec:.3f}, argmax at the joint {acc:.3f}, "
+          f"median peak {peak:.3f}", flush=True)
+    base = hrnet.random_state_dict(hrnet.PEAKED_BASE_SEED)
+    sd = {k: v.detach().float().cpu() for k, v in model.state_dict().items() if not k.endswith("num_batches_tracked")}
+    keep = {k: v.numpy() for k, v in sd.items() if not torch.equal(v, base[k].float())}
+    os.makedirs(OUT_DIR, exist_ok=True)
+    np.savez(os.path.join(OUT_DIR, "hrnet_w32_peaked.npz"), **keep)
+    print(f"wrote {len(keep)} tensors ({sum(v.size for v in keep.values())} values)", flush=True)
 
 
 if __name__ == "__main__":
