@@ -142,5 +142,10 @@ bool launch_tblock32(const uint16_t* x, const uint16_t* w1, const float* b1, con
                      uint16_t* y, int N, int H, int W, hipStream_t s);
 void launch_basic_block_c32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,
                             const float* b2, uint16_t* y, int N, int H, int W, hipStream_t s);
+// The same block on 64 channels at 32x24 (tblock64.hip, warp-specialised, weights in
+// registers); bit-identical to the two tconv launches.  Supported unless MVPOSE_NO_TBLOCK64=1.
+bool tblock64_supported(int H, int W);
+void launch_tblock64(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                     uint16_t* y, int N, int H, int W, hipStream_t s);
 
 }  // namespace mvp

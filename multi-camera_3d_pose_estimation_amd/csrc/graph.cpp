@@ -121,8 +121,9 @@ void validate(Graph& g, int64_t w_elems, int64_t f_elems) {
 }
 
 // Fusion pass: a 3x3 conv pair conv1 (relu) -> conv2 (+ conv1's input as residual,
-// relu) on 32 channels whose intermediate feeds nothing else becomes one fused
-// BasicBlock launch; the intermediate tensor is then never allocated.
+// relu) on 32 channels (64x48 plane) or 64 channels (32x24 plane, tblock64.hip) whose
+// intermediate feeds nothing else becomes one fused BasicBlock launch; the intermediate
+// tensor is then never allocated.
 void fuse(Graph& g, bool enable) {
     const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
     g.absorbed.assign(no, 0);
@@ -132,19 +133,20 @@ void fuse(Graph& g, bool enable) {
     for (const mvp_op_desc& op : g.ops)
         for (int i = 0; i < op.n_in; i++)
             if (op.in[i] >= 0) uses[op.in[i]]++;
-    auto is_c32_conv3 = [&](const mvp_op_desc& op) {
-        return op.kind == MVP_OP_CONV && op.ks == 3 && op.stride == 1 && op.cin == 32 && op.cout == 32 && op.relu &&
-               g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    auto is_block_conv3 = [&](const mvp_op_desc& op) {
+        return op.kind == MVP_OP_CONV && op.ks == 3 && op.stride == 1 && (op.cin == 32 || op.cin == 64) &&
+               op.cout == op.cin && op.relu && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
     };
     for (int k = 0; k + 1 < no; k++) {
         const mvp_op_desc& a = g.ops[k];
         const mvp_op_desc& b = g.ops[k + 1];
-        if (g.absorbed[k] || g.block_head[k] || !is_c32_conv3(a) || !is_c32_conv3(b)) continue;
+        if (g.absorbed[k] || g.block_head[k] || !is_block_conv3(a) || !is_block_conv3(b) || a.cin != b.cin) continue;
         const bool a_plain = a.n_in == 1 || a.in[1] < 0;
         const bool b_res = b.n_in > 1 && b.in[1] == a.in[0];
         const mvp_tensor_desc& t = g.tensors[a.out];
         if (!a_plain || !b_res || b.in[0] != a.out || uses[a.out] != 1 || a.out == g.output) continue;
-        if (a.segment != b.segment || !basic_block_c32_supported(t.h, t.w)) continue;
+        const bool ok = a.cin == 32 ? basic_block_c32_supported(t.h, t.w) : tblock64_supported(t.h, t.w);
+        if (a.segment != b.segment || !ok) continue;
         g.absorbed[k] = 1;
         g.block_head[k + 1] = 1;
         k++;
@@ -635,8 +637,9 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         if (g->absorbed[k]) return;
         if (g->block_head[k]) {
             const mvp_op_desc& c1 = g->ops[k - 1];
-            mvp::launch_basic_block_c32((const uint16_t*)ptr(op.in[1]), g->wb + c1.w_off, g->fb + c1.b_off,
-                                        g->wb + op.w_off, g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, o.h, o.w, s);
+            auto launch = c1.cin == 32 ? mvp::launch_basic_block_c32 : mvp::launch_tblock64;
+            launch((const uint16_t*)ptr(op.in[1]), g->wb + c1.w_off, g->fb + c1.b_off, g->wb + op.w_off,
+                   g->fb + op.b_off, (uint16_t*)ptr(op.out), nb, o.h, o.w, s);
             return;
         }
         if (g->twin[k] >= 0) {  // transition1: this 3x3/s1 conv and its 3x3/s2 sibling, one pass

@@ -398,11 +398,11 @@ __device__ __forceinline__ void load_cams(double (*scam)[MVP_CAM_DOUBLES], CamFa
 //     one v_pk_* instruction stream), the last 2 in fp64 — the fixed-point map contracts by
 //     ~|k1|·r² per step, so the f32 rounding of the early iterates is damped ~100x before
 //     the f32 output rounding; FMA contraction, hardware reciprocals with Newton steps;
-//   * null vector: normal equations M = AᵀA (fp64), LDLᵀ, three inverse-iteration steps
-//     from e₄ — each shrinks the off-null component by λ₄/λ₃ = (σ₄/σ₃)² (~4e-7 on the
-//     synthetic rigs; σ₁/σ₃ ~ 200, so the squared condition costs ~1e-12 of direction);
-//   * a lane whose last step still moved the unit vector by > 1e-12 (σ₄ ≈ σ₃ geometry,
-//     NaN / Inf input) re-solves its point on the exact path (same kernel, rare branch).
+//   * null vector: normal equations M = AᵀA (fp64), LDLᵀ, inverse iteration from M⁻¹e₄
+//     until the geometric convergence estimate is <= 1e-13 (2-5 steps; each shrinks the
+//     off-null component by λ₄/λ₃ = (σ₄/σ₃)², median 4e-7, max ~2e-5 on the synthetic rigs);
+//   * a lane that is not contracting (σ₄ ≈ σ₃ geometry, NaN / Inf input) re-solves its
+//     point on the exact path (same kernel, rare branch).
 // The result is then normalised and dehomogenised through OpenCV's f32 chain.
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -519,27 +519,42 @@ __device__ __forceinline__ bool normal_eq_null_vector(const double (&A)[M][4], d
         y[1] = z1 * r1 - l21 * y[2] - l31 * y[3];
         y[0] = y[0] * r0 - l10 * y[1] - l20 * y[2] - l30 * y[3];
     };
-    double y[4];
-    y[3] = r3;  // M⁻¹ e₄
-    y[2] = -l32 * y[3];
-    y[1] = -l21 * y[2] - l31 * y[3];
-    y[0] = -l10 * y[1] - l20 * y[2] - l30 * y[3];
-    solve(y);
-    const double n2 = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
-    double x2[4];
+    double x[4];
+    x[3] = r3;  // M⁻¹ e₄
+    x[2] = -l32 * x[3];
+    x[1] = -l21 * x[2] - l31 * x[3];
+    x[0] = -l10 * x[1] - l20 * x[2] - l30 * x[3];
+    {
+        const double is = rsqrt_fast(x[0] * x[0] + x[1] * x[1] + x[2] * x[2] + x[3] * x[3]);
 #pragma unroll
-    for (int q = 0; q < 4; q++) x2[q] = y[q] * n2;
-    solve(y);
-    const double n3 = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
-    double dd = 0;
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-        nv[q] = y[q] * n3;
-        const double e = nv[q] - x2[q];
-        dd += e * e;
+        for (int q = 0; q < 4; q++) x[q] *= is;
     }
-    // (M⁻¹ is positive definite up to the pivot clamp: no sign flip between iterates)
-    return dd <= 1e-24;
+    // e₄ is a poor start (the null vector is (X, Y, Z, 1)/|.| with |X, Y, Z| ~ 1e2-1e3 world
+    // units, so its e₄ component is ~1/350) and λ₄/λ₃ reaches ~2e-5 on the synthetic rigs:
+    // three fixed steps left a third of the points unconverged.  Iterate to a geometric
+    // convergence test instead (remaining error ≈ step · step / previous step <= 1e-13).
+    double prev = 1.0;
+    for (int it = 0; it < 8; it++) {
+        double y[4] = {x[0], x[1], x[2], x[3]};
+        solve(y);
+        const double is = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
+        double dd = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            y[q] *= is;  // M⁻¹ is positive definite (up to the pivot clamp): no sign flip
+            const double e = y[q] - x[q];
+            dd += e * e;
+            x[q] = y[q];
+        }
+        if (dd <= 1e-26 || (dd <= 1e-16 && dd * dd <= 1e-26 * prev)) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) nv[q] = x[q];
+            return true;
+        }
+        if (it >= 2 && !(dd < 0.25 * prev)) return false;  // not contracting (or NaN)
+        prev = dd;
+    }
+    return false;
 }
 
 // Solver stages.  kExact: the restatement for every lane (OpenCV undistortion
@@ -684,15 +699,18 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     const float conf_a = kp[2 * V + ca], conf_b = kp[2 * V + cb];
     // stable ascending argsort of (conf_a, conf_b), NaN last: swapped iff conf_b sorts before conf_a
     const bool swap = isnan(conf_a) ? !isnan(conf_b) : (conf_b < conf_a);
-    // selection position 0 = the lower-confidence camera (its params: camera key 0), 1 = the other
-    const int col0 = swap ? cb : ca, col1 = swap ? ca : cb;
+    // rows of the lower-confidence camera first; each view's point comes from its column
+    // ci.v[pos] and its parameters from camera key = its position pos in camera_indices
+    const int pos0 = swap ? 1 : 0, pos1 = swap ? 0 : 1;
+    const int col0 = ci.v[pos0], col1 = ci.v[pos1];
     const float u[2] = {kp[col0], kp[col1]}, v[2] = {kp[V + col0], kp[V + col1]};
+    const double* cp[2] = {scam[pos0], scam[pos1]};
     float ux[2], uy[2];
-    undistort_pair_tol(u, v, scam[0], scam[1], sfast[0], sfast[1], stol[0], stol[1], ux, uy);
+    undistort_pair_tol(u, v, cp[0], cp[1], sfast[pos0], sfast[pos1], stol[pos0], stol[pos1], ux, uy);
     double A[4][4];
 #pragma unroll
     for (int q = 0; q < 2; q++) {
-        const double* P = scam[q] + 26;
+        const double* P = cp[q] + 26;
         const double x = ux[q], y = uy[q];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -704,11 +722,11 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     if (!normal_eq_null_vector<4>(A, nv)) {
         // not provably converged (or non-finite): the exact path for this point
         float e0x, e0y, e1x, e1y;
-        undistort_point(u[0], v[0], scam[0], e0x, e0y);
-        undistort_point(u[1], v[1], scam[1], e1x, e1y);
+        undistort_point(u[0], v[0], cp[0], e0x, e0y);
+        undistort_point(u[1], v[1], cp[1], e1x, e1y);
         double E[4][4];
-        add_view_rows(E, 0, e0x, e0y, scam[0] + 26);
-        add_view_rows(E, 2, e1x, e1y, scam[1] + 26);
+        add_view_rows(E, 0, e0x, e0y, cp[0] + 26);
+        add_view_rows(E, 2, e1x, e1y, cp[1] + 26);
         double At[4][4];
 #pragma unroll
         for (int c = 0; c < 4; c++)

@@ -1,7 +1,9 @@
 """GPU parity of the bf16 HRNet-W32 graph (libmvpose) vs the torch fp32 oracle
 (oracle/hrnet_ref.py) on the same seeded weights and the same (bf16) input.
 Tolerance: bf16 activations/weights through ~90 conv layers — relative L2
-error of the heatmaps <= 3e-2 and >= 0.99 cosine similarity per crop."""
+error of the heatmaps <= 1.5e-2 (measured 7e-3, ~2x) and >= 0.99 cosine similarity per
+crop.  Fused-vs-unfused graph tolerances are ~1.5-3x their measured deviations, which
+every test prints (profiles/r03_tolerances.log)."""
 import numpy as np
 import pytest
 import torch
@@ -37,7 +39,7 @@ def test_backbone_vs_fp32_oracle(models):
     rel = (torch.linalg.vector_norm(o - r) / torch.linalg.vector_norm(r)).item()
     cos = torch.nn.functional.cosine_similarity(o.reshape(5, -1), r.reshape(5, -1)).min().item()
     print(f"backbone rel L2 err {rel:.3e}, min cosine {cos:.6f}, max|ref| {r.abs().max():.3f}")
-    assert rel <= 3e-2 and cos >= 0.99
+    assert rel <= 1.5e-2 and cos >= 0.99
 
 
 def test_backbone_batch_consistency(models):
@@ -125,6 +127,7 @@ def test_cat_fusion_matches_unfused(models, monkeypatch):
     b = fused.forward(xb)
     torch.cuda.synchronize()
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    print(f"cat fusion vs unfused: rel L2 {rel:.3e}")
     assert rel < 1e-2, rel
 
 
@@ -150,6 +153,7 @@ def test_pair_fusion_matches_unfused(models, monkeypatch):
     b = fused.forward(xb)
     torch.cuda.synchronize()
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    print(f"pair fusion vs unfused: rel L2 {rel:.3e}")
     assert rel < 2e-2, rel
     assert not torch.equal(a, b)  # the fused path ran (its summation order shows somewhere)
     assert fused.arena_bytes <= plain.arena_bytes
@@ -174,6 +178,7 @@ def test_stem_fusion_matches_unfused(models, monkeypatch):
     b = fused.forward(xb)
     torch.cuda.synchronize()
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    print(f"stem fusion vs unfused: rel L2 {rel:.3e}")
     assert rel < 2e-2, rel
     assert fused.arena_bytes <= plain.arena_bytes
 
@@ -196,6 +201,7 @@ def test_sibling_fusion_matches_unfused(models, monkeypatch):
     b = fused.forward(xb)
     torch.cuda.synchronize()
     rel = (torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(a)).item()
+    print(f"sibling fusion vs unfused: rel L2 {rel:.3e}")
     assert rel < 2e-2, rel
     assert not torch.equal(a, b)
     # the later siblings' outputs now live from the first sibling's launch on

@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]
 # environment per kernel family: the 32-channel plane runs the fused block,
-# basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv")
+# basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv"); the 64-channel plane at
+# 32x24 runs tblock64 in "tconv" mode
 _OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_WSCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
 MODES = {
     "generic": dict(_OFF),
@@ -78,6 +79,36 @@ def test_basic_block_vs_reference(c, h, w, monkeypatch):
         print(f"C={c} {h}x{w} {mode}: rel L2 {rel:.2e}, max abs {mx:.3e} (max|ref| {scale:.2f})")
         assert rel <= 4e-3
         assert mx <= 3 * scale * 2.0 ** -8
+
+
+@pytest.mark.parametrize("n", [37, 301])
+def test_tblock64_bitwise_equals_two_tconv_launches(n, monkeypatch):
+    """The fused 64-channel BasicBlock (tblock64.hip: warp-specialised conv1 / conv2 waves,
+    the intermediate only in LDS) reproduces the two separate tconv launches bit for bit —
+    same MFMA sequence per accumulator, same epilogues.  n = 37: fewer tiles than CUs (one per
+    workgroup); n = 301: the persistent loop with its ring / intermediate double buffers."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    _set_mode(monkeypatch, "tconv")
+    spec, xi, yo, _ = hrnet.basic_block_spec(64, 32, 24, seed=13, n_blocks=2)
+    gen = torch.Generator().manual_seed(14)
+    x = torch.randn((n, 32, 24, 64), generator=gen).bfloat16().cuda()
+    outs = []
+    for off in ("1", "0"):
+        monkeypatch.setenv("MVPOSE_NO_TBLOCK64", off)
+        g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+        out = torch.empty_like(x)
+        g.run(x, out)
+        torch.cuda.synchronize()
+        outs.append((out, g.arena_bytes))
+        g.close()
+    (a, arena_a), (b, arena_b) = outs
+    d = (a.float() - b.float()).abs()
+    print(f"tblock64 n={n}: max |fused - unfused| {d.max().item():.3g}, identical {(d == 0).float().mean().item():.6f}, "
+          f"arena {arena_b} vs {arena_a}")
+    assert torch.equal(a, b)
+    assert arena_b < arena_a
 
 
 @pytest.mark.parametrize("mode", ["wsconv", "tconv"])

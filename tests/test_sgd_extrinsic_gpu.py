@@ -13,7 +13,8 @@ optimize_trajectory=False, GT_camera_IDs=[a, b]), reference pose_refinement.py:6
 * one mvp_extrinsic_sample_grad pass vs a torch fp32 autograd restatement of
   construct_sample_cost's cost() — cost rtol 1e-5, gradient rtol 1e-4;
 * the whole optimisation: the shared cost / running-mean history (F6), final and best
-  R / T — within f32 reduction-order drift (rtol 2e-3 on costs, 2e-3 on parameters).
+  R / T — within f32 reduction-order drift (HIST_RTOL on costs, R_ATOL / T_ATOL on the
+  parameters: ~3x the measured deviations).
 """
 import os
 import random
@@ -26,6 +27,9 @@ from mvpose import refine
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 CASES = ("sgd_ext_c2", "sgd_ext_c0")
+# ~3x the measured deviations from the golden runs (profiles/r03_sgd_extrinsic.log: cost history
+# <= 8.2e-5 relative, R <= 1.0e-5, T <= 1.9e-6 over both cases and both step drivers)
+HIST_RTOL, R_ATOL, T_ATOL = 2.5e-4, 3e-5, 6e-6
 MY_LENGTHS = {"left_shoulder_left_elbow": 38, "left_elbow_left_wrist": 27,
               "right_shoulder_right_elbow": 38, "right_elbow_right_wrist": 27,
               "left_hip_left_knee": 51, "left_knee_left_ankle": 40,
@@ -141,7 +145,7 @@ def test_extrinsic_optimisation_matches_reference(name, device_adam):
         got = np.array(opt.all_costs_total[n], np.float64)
         assert got.shape == z["hist_" + n].shape, n
         worst = max(worst, float(np.max(np.abs(got - z["hist_" + n]) / np.maximum(np.abs(z["hist_" + n]), 1e-30))))
-        np.testing.assert_allclose(got, z["hist_" + n], rtol=2e-3, err_msg=n)
+        np.testing.assert_allclose(got, z["hist_" + n], rtol=HIST_RTOL, err_msg=n)
     fin = opt.decomposed_cam_params[ext]
     best = opt.best_decomposed_cam_params[ext]
     dev = {"final_R": np.abs(fin[1].detach().numpy() - z["final_R"]).max(),
@@ -150,10 +154,10 @@ def test_extrinsic_optimisation_matches_reference(name, device_adam):
            "best_T": np.abs(best[2].numpy() - z["best_T"]).max()}
     print(f"[{name} device_adam={device_adam}] cost history max rel dev {worst:.3g}; "
           + ", ".join(f"{k} {v:.3g}" for k, v in dev.items()))
-    np.testing.assert_allclose(fin[1].detach().numpy(), z["final_R"], rtol=0, atol=2e-3)
-    np.testing.assert_allclose(fin[2].detach().numpy(), z["final_T"], rtol=2e-3, atol=2e-3)
-    np.testing.assert_allclose(best[1].numpy(), z["best_R"], rtol=0, atol=2e-3)
-    np.testing.assert_allclose(best[2].numpy(), z["best_T"], rtol=2e-3, atol=2e-3)
+    np.testing.assert_allclose(fin[1].detach().numpy(), z["final_R"], rtol=0, atol=R_ATOL)
+    np.testing.assert_allclose(fin[2].detach().numpy(), z["final_T"], rtol=0, atol=T_ATOL)
+    np.testing.assert_allclose(best[1].numpy(), z["best_R"], rtol=0, atol=R_ATOL)
+    np.testing.assert_allclose(best[2].numpy(), z["best_T"], rtol=0, atol=T_ATOL)
 
 
 @pytest.mark.gpu
