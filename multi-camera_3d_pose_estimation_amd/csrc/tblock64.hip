@@ -10,20 +10,28 @@
 //               -> the intermediate (bias, ReLU, bf16; rows outside the image = 0 = conv2's
 //               zero padding) in LDS;
 //   waves 2, 3  conv2 of the PREVIOUS tile from the other intermediate buffer, + b2 +
-//               residual (global, issued before the DMA) + ReLU -> output, and the input
+//               residual (read from the input ring) + ReLU -> output, and the input
 //               halo DMA of the NEXT tile into the idle ring slot.
 // So each phase (one barrier) runs conv1 of tile k beside conv2 of tile k-1 on the other
 // two SIMDs, and the halo of tile k+1 streams in under both.  Each wave keeps its conv's
 // 32 couts x 576 K of weights in registers (144 VGPRs, loaded once per launch: no weight
 // traffic in the loop and only B fragments are read from LDS, one ds_read_b128 per MFMA).
-// LDS: input halo ring 2 x 42 KiB (channel pairs interleaved per pixel, as tblock32) +
-// intermediate 2 x 31.4 KiB (plane-major, row pitch W+1 with a zero pad slot).
+//
+// LDS images (input halo ring 2 x 40 KiB, intermediate 2 x 32.5 KiB) are plane-major
+// (8 planes of 8 channels, 16-B slots) with a row pitch of 26 slots (zero pad | 24 pixels |
+// zero pad).  A fragment's 32 pixels are an 8-row x 4-column block whose even rows go to
+// one ds_read_b128 lane group of the half-wave ({0-3,12-15,20-27}) and odd rows to the
+// other: with the pitch = 10 (mod 16) every group reads 16 distinct bank quads for every
+// tap, so the B-operand reads are conflict-free (the first layout — channel pairs
+// interleaved per pixel, raster fragments across the pad slots — measured 2.6-way,
+// SQ_LDS_BANK_CONFLICT 56 % of the LDS cycles).  conv1's rows 8-9 use 2 x 16 blocks.
 //
 // Every accumulator sees tconv_kernel's MFMA sequence (bias start, K order (32-channel
 // chunk, tap, 16-channel half)) and its epilogue, so the result is bit-identical to the two
-// separate tconv launches (tests/test_backbone_gpu.py, tests/test_conv_planes_gpu.py).
+// separate tconv launches (tests/test_conv_planes_gpu.py, tests/test_backbone_gpu.py).
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv.h"
 #include "mfma_tile.h"
@@ -37,28 +45,61 @@ using namespace mfma_tile;
 constexpr int kZeroSlots = 4096;  // 16-B slots of the shared zero region
 
 struct B64 {
-    static constexpr int H = 32, W = 24, TH = 8, RS = W + 1;
+    static constexpr int H = 32, W = 24, TH = 8, RS = W + 2;
     static constexpr int TILES_H = H / TH;
-    static constexpr int R1 = TH + 2;                         // conv1 rows (the intermediate)
-    static constexpr int F1 = (R1 * W + 31) / 32;             // 8 fragments (the last 16 pixels pad)
-    static constexpr int F2 = TH * W / 32;                    // 6 fragments
-    static constexpr int HR = TH + 5;                         // input halo rows: 2 above, 2 below, 1 for the pad pixels
-    static constexpr int HS = 1 + HR * RS;                    // input pixel slots (incl. the leading zero)
-    static constexpr int HSM = 1 + R1 * RS;                   // intermediate slots per plane
-    static constexpr int XSLOTS = 8 * HS;                     // 4 channel pairs x HS pixels x 2
-    static constexpr int NDW = 2;                             // DMA-issuing waves
-    static constexpr int XPPW = (XSLOTS + 64 * NDW - 1) / (64 * NDW);  // 1-KiB pieces per DMA wave
-    static constexpr int XBYTES = XPPW * NDW * 1024;          // one input ring slot
-    static constexpr int MBYTES = 8 * HSM * 16;               // one intermediate buffer
+    static constexpr int R1 = TH + 2;            // conv1 rows (the intermediate)
+    static constexpr int F1 = 8;                 // 6 blocks of 8x4 (rows 0-7) + 2 of 2x16 (rows 8-9)
+    static constexpr int F2 = 6;                 // 6 blocks of 8x4
+    static constexpr int HR = TH + 4;            // input halo rows: 2 above, 2 below
+    static constexpr int HSP = 320;              // input slots per plane (HR * RS = 312 used; 64-slot DMA blocks)
+    static constexpr int HSM = R1 * RS;          // intermediate slots per plane
+    static constexpr int NB = (HSP + 63) / 64;   // 64-slot DMA blocks per plane
+    static constexpr int NPIECE = 8 * NB;        // 1-KiB DMA pieces per tile
+    static constexpr int NDW = 2;                // DMA-issuing waves
+    static constexpr int XPPW = NPIECE / NDW;    // pieces per DMA wave
+    static constexpr int XBYTES = 8 * HSP * 16;  // one ring slot
+    static constexpr int MBYTES = 8 * HSM * 16;  // one intermediate buffer
     static constexpr int MOFF = 2 * XBYTES;
-    static constexpr int LDS = MOFF + 2 * MBYTES;
-    static constexpr int KS = 36;                              // k-steps: 2 chunks x 9 taps x 2 halves
+    static constexpr int BOFF = MOFF + 2 * MBYTES;  // b1 | b2 (f32)
+    static constexpr int LDS = BOFF + 2 * 64 * 4;
+    static constexpr int KS = 36;                // k-steps: 2 chunks x 9 taps x 2 halves
     static_assert(LDS <= 160 * 1024, "LDS budget");
-    static_assert(R1 * W > (F1 - 1) * 32 && F2 * 32 == TH * W, "fragments");
-    static_assert((3 * 2 * HS + (2 * RS + 2) * 2) * 16 < 65536 && (7 * HSM + 2 * RS + 2) * 16 < 65536,
-                  "ds_read offset range");
-    static_assert(HR < 31 && 2 * F2 + XPPW < 64, "packed DMA geometry / vmcnt range");
+    static_assert(RS % 16 == 10, "conflict-free 8x4 blocks need a row pitch of 10 (mod 16)");
+    static_assert(HSP >= HR * RS && HSP % 64 == 0 && HSP % 16 == 0, "plane stride: whole DMA blocks, bank-neutral");
+    static_assert(NPIECE % NDW == 0 && 2 * F2 + XPPW < 64 && XPPW == 4 * NB, "DMA split / vmcnt range");
+    static_assert((6 * HSP + 2 * RS + 2) * 16 < 65536 && (6 * HSM + 2 * RS + 2) * 16 < 65536, "ds_read offset range");
 };
+
+// Lane r32 of a half-wave -> pixel of an 8x4 block: block b = r32 / 4 of 4 lanes; the
+// groups {0-3,12-15,20-27} (b = 0, 3, 5, 6) take rows 0, 2, 4, 6 and {4-11,16-19,28-31}
+// (b = 1, 2, 4, 7) rows 1, 3, 5, 7.  grp = the lane group, pos = rank within it (0-15).
+__device__ __forceinline__ int lane_grp(int r32) { return (0x96 >> (r32 >> 2)) & 1; }
+__device__ __forceinline__ int lane_pos(int r32) { return 4 * (r32 >> 3) + (r32 & 3); }
+__device__ __forceinline__ int blk_row(int r32) { return 2 * (r32 >> 3) + lane_grp(r32); }
+__device__ __forceinline__ int blk_col(int r32) { return r32 & 3; }
+
+// Intermediate / output pixel (row r, column x) of fragment t for lane r32; pad = a
+// duplicate lane of conv1's last fragment (reads a real lane's address, never written).
+__device__ __forceinline__ void frag_pixel64(int t, int r32, int& r, int& x, bool& pad) {
+    pad = false;
+    if (t < 6) {
+        r = blk_row(r32);
+        x = 4 * t + blk_col(r32);
+    } else {
+        r = 8 + lane_grp(r32);
+        const int pos = lane_pos(r32);
+        x = t == 6 ? pos : 16 + (pos & 7);
+        pad = t == 7 && pos >= 8;
+    }
+}
+
+// s_waitcnt through the builtin, so the compiler's own wait insertion sees it (an asm
+// s_waitcnt is opaque: the weight loads issued before the tile loop then looked pending on
+// every iteration and put a vmcnt(0) in front of the first MFMA).  gfx9 encoding: vmcnt in
+// bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8.
+constexpr int wait_vm(int n) { return ((n >> 4) << 14) | 0x0F70 | (n & 15); }
+constexpr int kWaitLgkm0 = 0xC07F;
+constexpr int kWaitAll = 0x0070;
 
 struct TB64Params {
     const uint16_t* x;
@@ -69,6 +110,9 @@ struct TB64Params {
     uint16_t* y;
     const uint16_t* zero;
     int N, n_tiles;
+#ifdef TB64_STAMPS
+    unsigned long long* stamps;  // [block][wave][phase < 16][4] s_memtime (tools/tb64_stamps.hip)
+#endif
 };
 
 // Weights of one conv's cout group, in registers for the launch: A fragment of k-step
@@ -84,20 +128,46 @@ __device__ __forceinline__ void load_weights(const uint16_t* __restrict__ w, int
     }
 }
 
-// The accumulators start at the bias (couts 32cg + 16h .. +15), reloaded per tile (L2).
-__device__ __forceinline__ f32x16 bias_acc(const float* __restrict__ b, int cg, int h) {
-    const float* bp = b + 32 * cg + 16 * h;
-    f32x16 a;
+// The accumulators start at the bias (couts 32cg + 16h .. +15), read per tile from the LDS
+// copy.  Inline asm with its own lgkmcnt wait: as a plain LDS load the compiler puts a
+// vmcnt(0) in front of it (the previous phase's halo DMA is an LDS write it cannot see
+// completed), which in the conv2 waves also waited for the residual loads just issued.
+__device__ __forceinline__ f32x16 bias_acc(const uint8_t* lds, int conv, int cg, int h) {
+    const uint32_t a = (uint32_t)reinterpret_cast<uintptr_t>(lds) + B64::BOFF + (64 * conv + 32 * cg + 16 * h) * 4;
+    float4 q0, q1, q2, q3;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %4 offset:16\n\t"
+        "ds_read_b128 %2, %4 offset:32\n\t"
+        "ds_read_b128 %3, %4 offset:48\n\t"
+        "s_waitcnt lgkmcnt(0)"  // (this asm's own wait: the compiler does not track these reads)
+        : "=&v"(q0), "=&v"(q1), "=&v"(q2), "=&v"(q3)  // early clobber: not the address register
+        : "v"(a)
+        : "memory");
+    f32x16 r;
+    const float4 q[4] = {q0, q1, q2, q3};
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-        const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * j);
-        a[4 * j] = b4.x;
-        a[4 * j + 1] = b4.y;
-        a[4 * j + 2] = b4.z;
-        a[4 * j + 3] = b4.w;
+        r[4 * j] = q[j].x;
+        r[4 * j + 1] = q[j].y;
+        r[4 * j + 2] = q[j].z;
+        r[4 * j + 3] = q[j].w;
     }
-    return a;
+    return r;
 }
+
+#ifdef TB64_STAMPS
+#define TB64_STAMP(k, i)                                                                                     \
+    do {                                                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
+        if ((k) < 16 && (threadIdx.x & 63) == 0)                                                             \
+            p.stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (k)) * 4 + (i)] = t_;                    \
+    } while (0)
+#else
+#define TB64_STAMP(k, i) \
+    do {                 \
+    } while (0)
+#endif
 
 __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
@@ -105,179 +175,254 @@ __device__ __forceinline__ void barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E) — the step index is a
+// constant expression inside f (waitcnt immediates, buffer and fragment selection).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// Both roles run their K loop as 72 steps: the first 36 accumulate the fragments of half A,
+// the last 36 those of half B (weights in registers, so the split costs no extra reads),
+// with the B operand prefetched PF = 2 steps ahead across the halves.  Half A's epilogue
+// (bias is already in the accumulator; ReLU, bf16, store) runs in the MFMA shadow of half
+// B's steps; only half B's epilogue is exposed.
+#ifndef TB64_PF
+#define TB64_PF 2
+#endif
+constexpr int kPF = TB64_PF;
+
 // conv1 waves: tile k's 10 intermediate rows from input ring slot k & 1 into intermediate
-// buffer k & 1, then the phase barrier.  n_items + 1 barriers, as the conv2 waves.
+// buffer k & 1, then the phase barrier.  n_items + 2 barriers, as the conv2 waves.
+// Fragments 0-3 are half A, 4-7 half B; half A's epilogues at steps 40, 47, 54, 61.
 __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items) {
     using G = B64;
-    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS;
+    constexpr int H = G::H, TH = G::TH, RS = G::RS, NF = G::F1 / 2;
     const int h = lane >> 5, r32 = lane & 31;
     bf16x8 wa[G::KS];
     load_weights(p.w1, cg, r32, h, wa);
-    // fragment t, lane r32: intermediate pixel pp = 32t + r32 of the 10 x 24 rows (pp >= 240:
-    // padding pixels, computed on the spare halo row, never written)
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    // fragment t, lane r32: intermediate pixel (r, x) (frag_pixel64); its input tap (0, 0) is
+    // halo pixel (r, x - 1) = slot r * RS + x, and it lands in intermediate slot r * RS + x + 1
     int bv1[G::F1], mw[G::F1];
 #pragma unroll
     for (int t = 0; t < G::F1; t++) {
-        const int pp = 32 * t + r32, r = pp / W, x = pp - (pp / W) * W;
-        bv1[t] = ((r * RS + x) * 2 + h) * 16;                                  // input halo, tap (0, 0)
-        mw[t] = G::MOFF + ((4 * cg + 2 * h) * G::HSM + 1 + r * RS + x) * 16;  // intermediate, plane 4cg + 2h
+        int r, x;
+        bool pad;
+        frag_pixel64(t, r32, r, x, pad);
+        bv1[t] = (h * G::HSP + r * RS + x) * 16;
+        mw[t] = pad ? -1 : G::MOFF + ((4 * cg + 2 * h) * G::HSM + r * RS + x + 1) * 16;
     }
     barrier();  // prologue: tile 0's halo and the zeroed intermediate
     for (int k = 0; k < n_items; k++) {
+        TB64_STAMP(k, 0);
         const int tile = blockIdx.x + k * gridDim.x;
         const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * TH;
-        f32x16 acc[G::F1];
-        acc[0] = bias_acc(p.b1, cg, h);
+        f32x16 accA[NF], accB[NF];
+        accA[0] = bias_acc(lds, 0, cg, h);
 #pragma unroll
-        for (int t = 1; t < G::F1; t++) acc[t] = acc[0];
-        const int xo = (k & 1) * G::XBYTES;
-        bf16x8 fb[2][G::F1];
-        auto load = [&](int s, bf16x8 (&b)[G::F1]) {
-            const int c = s / 18, tap = (s % 18) >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
+        for (int t = 0; t < NF; t++) accB[t] = accA[0];
 #pragma unroll
-            for (int t = 0; t < G::F1; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + xo + bv1[t] + ((c * 2 + ks) * 2 * G::HS) * 16 +
-                                                        (dy * RS + dx) * 32);
+        for (int t = 1; t < NF; t++) accA[t] = accA[0];
+        const int xo = (k & 1) * G::XBYTES, mo = (k & 1) * G::MBYTES;
+        bf16x8 fb[kPF + 1][NF];
+        auto load = [&](auto Gs) {  // B operands of step g (half g / 36, k-step g % 36)
+            constexpr int g = Gs, s = g % 36, t0 = (g / 36) * NF;
+            constexpr int c = s / 18, tap = (s % 18) >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
+#pragma unroll
+            for (int t = 0; t < NF; t++)
+                fb[g % (kPF + 1)][t] = *reinterpret_cast<const bf16x8*>(
+                    lds + xo + bv1[t0 + t] + ((4 * c + 2 * ks) * G::HSP + dy * RS + dx) * 16);
         };
-        load(0, fb[0]);
+        auto epilogue = [&](int t, const f32x16& a) {
+            if (mw[t] < 0) return;
+            int r, x;
+            bool pad;
+            frag_pixel64(t, r32, r, x, pad);
+            // rows outside the image are conv2's zero padding
+            const bool live = (unsigned)(ho0 - 1 + r) < (unsigned)H;
+            uint32_t o[8];
 #pragma unroll
-        for (int s = 0; s < G::KS; s++) {
-            if (s + 1 < G::KS) load(s + 1, fb[(s + 1) & 1]);
+            for (int e = 0; e < 8; e++) o[e] = live ? pack_bf16x2(relu1(a[2 * e]), relu1(a[2 * e + 1])) : 0u;
+            *reinterpret_cast<uint4*>(lds + mw[t] + mo) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(lds + mw[t] + mo + G::HSM * 16) = uint4{o[4], o[5], o[6], o[7]};
+        };
+        static_for<0, kPF>(load);
+        static_for<0, 72>([&](auto Gs) {
+            constexpr int g = Gs, s = g % 36;
+            if constexpr (g + kPF < 72) load(std::integral_constant<int, g + kPF>{});
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int t = 0; t < G::F1; t++)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[s & 1][t], acc[t], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        const int mo = (k & 1) * G::MBYTES;
-#pragma unroll
-        for (int t = 0; t < G::F1; t++) {
-            const int pp = 32 * t + r32;
-            if (pp < G::R1 * W) {
-                // rows outside the image are conv2's zero padding
-                const bool live = (unsigned)(ho0 - 1 + pp / W) < (unsigned)H;
-                uint32_t o[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-                    o[e] = live ? pack_bf16x2(relu1(acc[t][2 * e]), relu1(acc[t][2 * e + 1])) : 0u;
-                *reinterpret_cast<uint4*>(lds + mw[t] + mo) = uint4{o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<uint4*>(lds + mw[t] + mo + G::HSM * 16) = uint4{o[4], o[5], o[6], o[7]};
+            for (int t = 0; t < NF; t++) {
+                if constexpr (g < 36)
+                    accA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accA[t], 0, 0, 0);
+                else
+                    accB[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accB[t], 0, 0, 0);
             }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g >= 40 && (g - 40) % 7 == 0 && (g - 40) / 7 < NF) epilogue((g - 40) / 7, accA[(g - 40) / 7]);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        TB64_STAMP(k, 1);
+#pragma unroll
+        for (int t = 0; t < NF; t++) epilogue(NF + t, accB[t]);
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        TB64_STAMP(k, 2);
         barrier();
     }
     barrier();  // the conv2 waves' last phase
 }
 
-// Input halo of tile k into ring slot buf, by the two conv2 waves (dw = 0, 1): ring slot
-// 16-B slot s = pair pp, pixel pix, plane e -> channels 16pp + 8e of halo pixel pix (0 = the
-// leading zero; row hy = image row ho0 - 2 + hy; column hx = W is the zero pad).
-__device__ __forceinline__ void issue_halo(const TB64Params& p, uint8_t* lds, int dw, int lane, const uint16_t* zl,
-                                           int k, int buf) {
+// Input halo of tile k into ring slot buf, by the two conv2 waves (dw = 0, 1).  Piece
+// (block b, plane q) fills ring slots q * HSP + 64 b + lane with plane q of halo pixel
+// p = 64 b + lane: row hy = p / RS (image row ho0 - 2 + hy), column p % RS - 1 (0 and RS - 1
+// are the zero pads; p >= HR * RS is unused).  Wave dw issues planes dw, dw + 2, dw + 4,
+// dw + 6 of every block, block-major (piece j = 4 b + q / 2), so a block's lane addresses
+// are computed once and its 8 planes (the same 128-B pixel lines) are fetched together.
+// valid = false (no tile k): zeros, so every phase issues the same VMEM ops.
+struct HaloSrc {
+    const uint16_t* xb;
+    int ho0, buf;
+    bool valid;
+};
+__device__ __forceinline__ HaloSrc halo_src(const TB64Params& p, int k, int buf, bool valid) {
     using G = B64;
-    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS;
     const int tile = blockIdx.x + k * gridDim.x;
-    const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * TH;
-    const uint16_t* xb = p.x + ((long)n * H + ho0) * W * 64;
+    const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * G::TH;
+    return HaloSrc{p.x + ((long)n * G::H + ho0) * G::W * 64, ho0, buf, valid};
+}
+__device__ __forceinline__ const uint16_t* halo_block(const HaloSrc& hs, int lane, const uint16_t* zl, int b) {
+    using G = B64;
+    const int px = 64 * b + lane, hy = px / G::RS, hx = px - hy * G::RS - 1;
+    const bool in = hs.valid && px < G::HR * G::RS && (unsigned)hx < (unsigned)G::W &&
+                    (unsigned)(hs.ho0 + hy - 2) < (unsigned)G::H;
+    return in ? hs.xb + ((hy - 2) * G::W + hx) * 64 : zl;  // + 8 q per plane (zl: 64 KiB of zeros)
+}
+__device__ __forceinline__ void halo_piece(const HaloSrc& hs, const uint16_t* blk, uint8_t* lds, int dw, int j) {
+    using G = B64;
+    const int b = j / 4, q = 2 * (j % 4) + dw;
+    glds16(blk + q * 8, lds + hs.buf * G::XBYTES + (q * G::HSP + 64 * b) * 16);
+}
+__device__ __forceinline__ void issue_halo(const HaloSrc& hs, uint8_t* lds, int dw, int lane, const uint16_t* zl) {
+    const uint16_t* blk = nullptr;
 #pragma unroll
-    for (int j = 0; j < G::XPPW; j++) {
-        const int s = (j * G::NDW + dw) * 64 + lane;
-        const int pp = s / (2 * G::HS), rem = s - pp * (2 * G::HS), pix = rem >> 1, e = rem & 1;
-        const int t = pix - 1, hy = t / RS, hx = t - hy * RS;
-        const bool in = s < G::XSLOTS && pix > 0 && hx < W && (unsigned)(ho0 + hy - 2) < (unsigned)H;
-        glds16(in ? xb + ((hy - 2) * W + hx) * 64 + pp * 16 + e * 8 : zl,
-               lds + buf * G::XBYTES + (j * G::NDW + dw) * 1024);
+    for (int j = 0; j < B64::XPPW; j++) {
+        if (j % 4 == 0) blk = halo_block(hs, lane, zl, j / 4);
+        halo_piece(hs, blk, lds, dw, j);
     }
 }
 
-// conv2 waves: in phase k, the residual of tile k-1 (global), the halo DMA of tile k+1, conv2
-// of tile k-1 from intermediate buffer (k-1) & 1 + bias + residual + ReLU -> y.
+// conv2 schedule over the 72 steps: DMA piece j at step 2 + 3j; half A's epilogue (fragments
+// 0-2) at steps 40, 46, 52.
+constexpr int kDmaStep0 = 2, kDmaStride = 3;
+static_assert(kDmaStep0 + kDmaStride * (B64::XPPW - 1) < 72, "DMA pieces fit the steps");
+
+// conv2 waves: in phase k, the halo DMA of tile k+1 and conv2 of tile k-1 from intermediate
+// buffer (k-1) & 1 + bias + residual (from the input ring) + ReLU -> y.
 __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items,
                                            const uint16_t* zl) {
     using G = B64;
-    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS;
+    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS, NF = G::F2 / 2;
     const int h = lane >> 5, r32 = lane & 31, dw = cg;
     bf16x8 wa[G::KS];
     load_weights(p.w2, cg, r32, h, wa);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    // fragment t, lane r32: output pixel (r, x) = (blk_row, 4t + blk_col); its tap (0, 0) is
+    // intermediate pixel (r, x - 1) = slot r * RS + x
     int bv2[G::F2];
+    const int er = blk_row(r32), ex = blk_col(r32);
 #pragma unroll
-    for (int t = 0; t < G::F2; t++) {
-        const int pp = 32 * t + r32, r = pp / W, x = pp - (pp / W) * W;
-        bv2[t] = G::MOFF + (h * G::HSM + r * RS + x) * 16;  // intermediate, tap (0, 0), plane h
-    }
-    issue_halo(p, lds, dw, lane, zl, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (int t = 0; t < G::F2; t++) bv2[t] = G::MOFF + (h * G::HSM + er * RS + 4 * t + ex) * 16;
+    issue_halo(halo_src(p, 0, 0, true), lds, dw, lane, zl);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // prologue
-    for (int k = 0; k <= n_items; k++) {
-        const bool conv = k >= 1, dma = k + 1 < n_items;
-        if (!conv) {
-            if (dma) issue_halo(p, lds, dw, lane, zl, k + 1, (k + 1) & 1);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            barrier();
-            continue;
-        }
+    issue_halo(halo_src(p, 1, 1, n_items > 1), lds, dw, lane, zl);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    barrier();  // phase 0: conv1 of tile 0 only
+    for (int k = 1; k <= n_items; k++) {
+        TB64_STAMP(k, 0);
         const int kp = k - 1;
         const int tile = blockIdx.x + kp * gridDim.x;
         const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * TH;
         const long pix0 = ((long)n * H + ho0) * W;
-        f32x16 acc[G::F2];
-        acc[0] = bias_acc(p.b2, cg, h);
-        // the residual, issued before the DMA so the epilogue never waits for the halo
+        f32x16 accA[NF], accB[NF];
+        accA[0] = bias_acc(lds, 1, cg, h);
+        // the residual = tile k-1's input, still in ring slot (k-1) & 1 (halo rows 2-9): read
+        // before this phase's DMA pieces start overwriting that slot with tile k+1
         uint4 rv[G::F2][2];
+        {
+            const uint8_t* rb = lds + (kp & 1) * G::XBYTES + ((4 * cg + 2 * h) * G::HSP + (er + 2) * RS + ex + 1) * 16;
 #pragma unroll
-        for (int t = 0; t < G::F2; t++) {
-            const uint16_t* rs = p.x + (pix0 + 32 * t + r32) * 64 + 32 * cg + 16 * h;
-            rv[t][0] = *reinterpret_cast<const uint4*>(rs);
-            rv[t][1] = *reinterpret_cast<const uint4*>(rs + 8);
+            for (int t = 0; t < G::F2; t++) {
+                rv[t][0] = *reinterpret_cast<const uint4*>(rb + 4 * t * 16);
+                rv[t][1] = *reinterpret_cast<const uint4*>(rb + (G::HSP + 4 * t) * 16);
+            }
         }
 #pragma unroll
-        for (int t = 1; t < G::F2; t++) acc[t] = acc[0];
-        asm volatile("" ::: "memory");
-        if (dma) issue_halo(p, lds, dw, lane, zl, k + 1, (k + 1) & 1);
-        asm volatile("" ::: "memory");
+        for (int t = 0; t < NF; t++) accB[t] = accA[0];
+#pragma unroll
+        for (int t = 1; t < NF; t++) accA[t] = accA[0];
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        __builtin_amdgcn_sched_barrier(0);
+        const HaloSrc hn = halo_src(p, k + 1, (k + 1) & 1, k + 1 < n_items);
+        const uint16_t* blk = nullptr;
         const int mo = (kp & 1) * G::MBYTES;
-        bf16x8 fb[2][G::F2];
-        auto load = [&](int s, bf16x8 (&b)[G::F2]) {
-            const int c = s / 18, tap = (s % 18) >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
+        bf16x8 fb[kPF + 1][NF];
+        auto load = [&](auto Gs) {
+            constexpr int g = Gs, s = g % 36, t0 = (g / 36) * NF;
+            constexpr int c = s / 18, tap = (s % 18) >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
 #pragma unroll
-            for (int t = 0; t < G::F2; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + mo + bv2[t] +
-                                                        ((c * 4 + ks * 2) * G::HSM + dy * RS + dx) * 16);
+            for (int t = 0; t < NF; t++)
+                fb[g % (kPF + 1)][t] = *reinterpret_cast<const bf16x8*>(
+                    lds + mo + bv2[t0 + t] + ((4 * c + 2 * ks) * G::HSM + dy * RS + dx) * 16);
         };
-        load(0, fb[0]);
-#pragma unroll
-        for (int s = 0; s < G::KS; s++) {
-            if (s + 1 < G::KS) load(s + 1, fb[(s + 1) & 1]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int t = 0; t < G::F2; t++)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[s & 1][t], acc[t], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // the residual loads are older than the DMA pieces
-        if (dma)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::XPPW) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-        for (int t = 0; t < G::F2; t++) {
+        auto epilogue = [&](int t, const f32x16& a) {
             uint32_t o[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) {
                 const uint4 rr = rv[t][e >> 2];
                 const uint32_t u = (e & 3) == 0 ? rr.x : (e & 3) == 1 ? rr.y : (e & 3) == 2 ? rr.z : rr.w;
-                o[e] = pack_bf16x2(relu1(acc[t][2 * e] + lo_bf16(u)), relu1(acc[t][2 * e + 1] + hi_bf16(u)));
+                o[e] = pack_bf16x2(relu1(a[2 * e] + lo_bf16(u)), relu1(a[2 * e + 1] + hi_bf16(u)));
             }
-            uint16_t* yp = p.y + (pix0 + 32 * t + r32) * 64 + 32 * cg + 16 * h;
+            uint16_t* yp = p.y + (pix0 + er * W + 4 * t + ex) * 64 + 32 * cg + 16 * h;
             *reinterpret_cast<uint4*>(yp) = uint4{o[0], o[1], o[2], o[3]};
             *reinterpret_cast<uint4*>(yp + 8) = uint4{o[4], o[5], o[6], o[7]};
-        }
-        // the next tile's halo has landed (only this tile's stores may still be in flight)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::F2) : "memory");
+        };
+        static_for<0, kPF>(load);
+        static_for<0, 72>([&](auto Gs) {
+            constexpr int g = Gs, s = g % 36;
+            if constexpr (g + kPF < 72) load(std::integral_constant<int, g + kPF>{});
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < NF; t++) {
+                if constexpr (g < 36)
+                    accA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accA[t], 0, 0, 0);
+                else
+                    accB[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accB[t], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g >= kDmaStep0 && (g - kDmaStep0) % kDmaStride == 0 &&
+                          (g - kDmaStep0) / kDmaStride < G::XPPW) {
+                constexpr int j = (g - kDmaStep0) / kDmaStride;
+                if constexpr (j % 4 == 0) blk = halo_block(hn, lane, zl, j / 4);
+                halo_piece(hn, blk, lds, dw, j);
+            }
+            if constexpr (g >= 40 && (g - 40) % 6 == 0 && (g - 40) / 6 < NF) epilogue((g - 40) / 6, accA[(g - 40) / 6]);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        TB64_STAMP(k, 1);
+#pragma unroll
+        for (int t = 0; t < NF; t++) epilogue(NF + t, accB[t]);
+        TB64_STAMP(k, 2);
+        // the next tile's halo has landed (only half B's stores may still be in flight)
+        __builtin_amdgcn_s_waitcnt(wait_vm(2 * NF));
+        TB64_STAMP(k, 3);
         barrier();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
 }
 
 __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
@@ -290,7 +435,8 @@ __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
     // the intermediate's pad and leading slots stay zero for the launch
     for (int i = tid; i < 2 * G::MBYTES / 16; i += 256)
         *reinterpret_cast<uint4*>(lds + G::MOFF + i * 16) = uint4{0u, 0u, 0u, 0u};
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (tid < 128) reinterpret_cast<float*>(lds + G::BOFF)[tid] = tid < 64 ? p.b1[tid] : p.b2[tid - 64];
+    __builtin_amdgcn_s_waitcnt(kWaitAll);
     if (wave < 2)
         conv1_role(p, lds, wave, lane, n_items);
     else
