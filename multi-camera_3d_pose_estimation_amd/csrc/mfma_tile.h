@@ -1,6 +1,6 @@
 // Shared device helpers of the 32x32x16-MFMA convolution kernels (tconv.hip,
-// tblock.hip): LDS-DMA, epilogue packing, the permuted-cout A rows
-// and the bank-conflict-free lane -> pixel map of a 32-pixel B fragment.
+// tblock.hip, tblock64.hip): LDS-DMA, epilogue packing, the permuted-cout A rows
+// and the bank-conflict-free lane -> pixel maps of a 32-pixel B fragment.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -70,6 +70,28 @@ __device__ __forceinline__ int frag_pixel(int f, int r32) {
     } else {
         return f * 32 + r32;
     }
+}
+
+// 8x4 pixel blocks (images of W % 4 == 0 at a row pitch RS = 2 mod 4, e.g. W + 2 slots with
+// a zero pad on each side): lane r32 -> (row, col) of the block, block b = r32 / 4 of 4 lanes;
+// lane group {0-3,12-15,20-27} (b = 0, 3, 5, 6) takes rows 0, 2, 4, 6 and {4-11,16-19,28-31}
+// (b = 1, 2, 4, 7) rows 1, 3, 5, 7.  Row i starts at residue i * RS mod 16 = multiples of 4
+// (even rows) and of 4 plus 2 (odd rows), distinct within a group, so every tap's 16 slots
+// per group are distinct mod 16 — conflict-free ds_read_b128 with any constant tap offset.
+// grp = the lane group, pos = rank within it (0-15): 2 x 16 blocks use (grp, pos).
+__device__ __forceinline__ int lane_grp(int r32) { return (0x96 >> (r32 >> 2)) & 1; }
+__device__ __forceinline__ int lane_pos(int r32) { return 4 * (r32 >> 3) + (r32 & 3); }
+__device__ __forceinline__ int blk_row(int r32) { return 2 * (r32 >> 3) + lane_grp(r32); }
+__device__ __forceinline__ int blk_col(int r32) { return r32 & 3; }
+
+// Tile pixel (row-major [crop][row][col]) of fragment f on 8x4 blocks: per crop TH/8 x W/4
+// blocks, row-block-major.
+template <int W, int TH, int NB>
+__device__ __forceinline__ int frag_pixel_blk(int f, int r32) {
+    static_assert(W % 4 == 0 && TH % 8 == 0, "8x4 blocks");
+    constexpr int FC = W / 4, FPC = (TH / 8) * FC;
+    const int nb = f / FPC, rem = f - nb * FPC, rb = rem / FC, cb = rem - rb * FC;
+    return (nb * TH + 8 * rb + blk_row(r32)) * W + 4 * cb + blk_col(r32);
 }
 
 }  // namespace mfma_tile

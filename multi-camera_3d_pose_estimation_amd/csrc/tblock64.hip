@@ -70,14 +70,6 @@ struct B64 {
     static_assert((6 * HSP + 2 * RS + 2) * 16 < 65536 && (6 * HSM + 2 * RS + 2) * 16 < 65536, "ds_read offset range");
 };
 
-// Lane r32 of a half-wave -> pixel of an 8x4 block: block b = r32 / 4 of 4 lanes; the
-// groups {0-3,12-15,20-27} (b = 0, 3, 5, 6) take rows 0, 2, 4, 6 and {4-11,16-19,28-31}
-// (b = 1, 2, 4, 7) rows 1, 3, 5, 7.  grp = the lane group, pos = rank within it (0-15).
-__device__ __forceinline__ int lane_grp(int r32) { return (0x96 >> (r32 >> 2)) & 1; }
-__device__ __forceinline__ int lane_pos(int r32) { return 4 * (r32 >> 3) + (r32 & 3); }
-__device__ __forceinline__ int blk_row(int r32) { return 2 * (r32 >> 3) + lane_grp(r32); }
-__device__ __forceinline__ int blk_col(int r32) { return r32 & 3; }
-
 // Intermediate / output pixel (row r, column x) of fragment t for lane r32; pad = a
 // duplicate lane of conv1's last fragment (reads a real lane's address, never written).
 __device__ __forceinline__ void frag_pixel64(int t, int r32, int& r, int& x, bool& pad) {

@@ -54,7 +54,11 @@ struct TCfg {
     static constexpr int NT = 3;                                 // 32-pixel fragments per wave
     static constexpr int P = NB * TH * W;                        // output pixels per tile
     static constexpr int NCH = CIN / 32;                         // items per tile
-    static constexpr int RS = W + 1, HR = TH + 2;                // halo row pitch (slots), rows
+    // BLK: fragments are 8x4 pixel blocks (frag_pixel_blk) on a row pitch of W + 2 slots (= 2
+    // mod 4): conflict-free B reads where 32-pixel raster fragments wrap rows (W = 12: the
+    // raster map measured 43 % of the LDS cycles in bank conflicts)
+    static constexpr bool BLK = W % 4 == 0 && W % 16 != 0 && TH % 8 == 0 && !(W == 24 && TH == 16 && NB == 1);
+    static constexpr int RS = BLK ? W + 2 : W + 1, HR = TH + 2;  // halo row pitch (slots), rows
     // PM (pixel-major halo): a halo pixel's four 16-B planes are slots 5p .. 5p+3 (5p+4 is a
     // never-read pad), so a DMA instruction reads ~13 pixels x 64 contiguous bytes instead
     // of 64 pixels x 16 B (a quarter of the cache lines); the 80-B pixel pitch keeps 16
@@ -78,6 +82,14 @@ struct TCfg {
                   "ds_read offset range");
     static_assert(STORES + 2 * NT < 64 && PPW < 64, "vmcnt range");
 };
+
+template <bool BLK, int W, int TH, int NB>
+__device__ __forceinline__ int tile_pixel(int f, int r32) {
+    if constexpr (BLK)
+        return frag_pixel_blk<W, TH, NB>(f, r32);
+    else
+        return frag_pixel<W, TH, NB>(f, r32);
+}
 
 struct TParams {
     const uint16_t* x;
@@ -164,7 +176,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     int bv[G::NT], eoff[G::NT], enb[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; t++) {
-        const int pp = frag_pixel<W, TH, NB>(pg * G::NT + t, r32);
+        const int pp = tile_pixel<G::BLK, W, TH, NB>(pg * G::NT + t, r32);
         const int nb = pp / (TH * W), rem = pp - nb * (TH * W);
         const int ty = rem / W, x = rem - (rem / W) * W;
         bv[t] = (h * G::QSTRIDE + (nb * G::HR * G::RS + ty * G::RS + x) * G::PSTRIDE) * 16;
@@ -384,7 +396,7 @@ __global__ __launch_bounds__(512, 1) void tconv_half_kernel(TParams p) {
     int bv[G::NT], eoff[G::NT], enb[G::NT];
 #pragma unroll
     for (int t = 0; t < G::NT; t++) {
-        const int pp = frag_pixel<W, TH, NB>(pg * G::NT + t, r32);
+        const int pp = tile_pixel<G::T::BLK, W, TH, NB>(pg * G::NT + t, r32);
         const int nb = pp / (TH * W), rem = pp - nb * (TH * W);
         const int ty = rem / W, x = rem - (rem / W) * W;
         bv[t] = (h + (nb * G::HR * G::RS + ty * G::RS + x) * 2) * 16;
