@@ -175,10 +175,12 @@ def tri_valu_issue(tri_ms, n_points):
             "frac": floor / tri_ms, "source": "profiles/r01_tri_pmc.json"}
 
 
-def tri_line(ops, syn, dev, s, views, mode, reps=10):
+def tri_line(ops, syn, dev, s, views, mode, reps=10, tolerance=False):
     """One triangulation launch over a resident TRI_T-frame stream (the per-step 256-frame
     launch is latency-bound and says nothing about the kernel).  HIP events on the launch
-    stream; the stream is ~2.4-4x the Infinity Cache, so every launch streams from HBM."""
+    stream; the stream is ~2.4-4x the Infinity Cache, so every launch streams from HBM.
+    tolerance=True: the throughput solver (MVP_TRI_TOLERANCE, <= 1e-4 world units against
+    the exact-rounding path; its fallback launch is inside the timed region)."""
     cams = syn.make_rig(views, seed=1)
     cd = torch.tensor(ops.pack_cameras(syn.reference_camera_params(cams)), device=dev)
     k = torch.tensor(syn.make_kpts_2d(syn.make_poses(2000, seed=2), cams, seed=3), device=dev)
@@ -186,11 +188,11 @@ def tri_line(ops, syn, dev, s, views, mode, reps=10):
     ci = list(range(views)) if mode == ops.TRI_ALL_VIEWS else [0, 1]
     out = torch.empty((TRI_T, 17, 3), dtype=torch.float32, device=dev)
     for _ in range(2):
-        ops.triangulate(k, cd, ci, mode=mode, out=out)
+        ops.triangulate(k, cd, ci, mode=mode, out=out, tolerance=tolerance)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
     for _ in range(reps):
-        ops.triangulate(k, cd, ci, mode=mode, out=out)
+        ops.triangulate(k, cd, ci, mode=mode, out=out, tolerance=tolerance)
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
@@ -450,9 +452,18 @@ def main():
     if rank == 0:
         del frames
         torch.cuda.empty_cache()
-        tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
-        tri["kernel"] = "triangulate_reference_kernel"
-        tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17)
+        if V == 2:
+            tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE, tolerance=True)
+            tri["kernel"] = "triangulate_tol2_kernel (+ triangulate_tol2_fallback_kernel)"
+            tri["solver"] = "tolerance (MVP_TRI_TOLERANCE): the pipeline's default"
+            compat = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
+            compat["kernel"] = "triangulate_reference_kernel"
+            compat["valu_issue"] = tri_valu_issue(compat["avg_launch_ms"], TRI_T * 17)
+            tri["reference_compat"] = compat
+        else:
+            tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
+            tri["kernel"] = "triangulate_reference_kernel"
+            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17)
         extra["roofline_triangulate"] = tri
         if not args.no_extra:
             t4 = tri_line(ops, syn, dev, s, 4, ops.TRI_ALL_VIEWS)

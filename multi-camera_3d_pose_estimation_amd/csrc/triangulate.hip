@@ -26,6 +26,10 @@
 #include "mvp_common.h"
 
 #include <cfloat>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 namespace {
 
@@ -420,7 +424,9 @@ __device__ __forceinline__ double rcp_nr(double b) {
     return __builtin_fma(r, e, r);
 }
 
-// Both views of a point: (u, v) pixels -> undistorted pixels (P = K), OpenCV's iteration.
+// Both views of a point: (u, v) pixels -> undistorted pixels (P = K), OpenCV's iteration:
+// the first NF32 of the 5 in f32, the rest in fp64.
+template <int NF32>
 __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const float (&v)[2],
                                                    const double* __restrict__ c0, const double* __restrict__ c1,
                                                    const CamFast& f0, const CamFast& f1, const CamTol& t0,
@@ -439,7 +445,7 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
     f2v x = X0, y = Y0;
     bool neg0 = false, neg1 = false;
 #pragma unroll
-    for (int j = 0; j < 3; j++) {
+    for (int j = 0; j < NF32; j++) {
         const f2v r2 = __builtin_elementwise_fma(x, x, y * y);
         const f2v den = __builtin_elementwise_fma(__builtin_elementwise_fma(__builtin_elementwise_fma(K4, r2, K1), r2, K0),
                                                   r2, one);
@@ -457,7 +463,7 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
     double xd[2] = {(double)x.x, (double)x.y}, yd[2] = {(double)y.x, (double)y.y};
     bool neg[2] = {neg0, neg1};
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
+    for (int j = NF32; j < 5; j++) {
 #pragma unroll
         for (int q = 0; q < 2; q++) {
             const double* c = cc[q];
@@ -679,9 +685,49 @@ __global__ __launch_bounds__(kBlock) void triangulate_all_views_kernel(
 // MVP_TRI_REFERENCE | MVP_TRI_TOLERANCE with camera_indices of length 2 (the reference's
 // hard-coded [0, 1]): the top-2 rule reduces to one comparison (np.argsort of two values:
 // [0, 1] unless conf[1] < conf[0], NaN sorts last).
+struct Tol2Sel {
+    int pos0, pos1;
+    float u[2], v[2];
+};
+__device__ __forceinline__ Tol2Sel tol2_select(const float* __restrict__ kp, int V, const CamIdx& ci) {
+    const int ca = ci.v[0], cb = ci.v[1];
+    const float conf_a = kp[2 * V + ca], conf_b = kp[2 * V + cb];
+    // stable ascending argsort of (conf_a, conf_b), NaN last: swapped iff conf_b sorts before conf_a
+    const bool swap = isnan(conf_a) ? !isnan(conf_b) : (conf_b < conf_a);
+    // rows of the lower-confidence camera first; each view's point comes from its column
+    // ci.v[pos] and its parameters from camera key = its position pos in camera_indices
+    Tol2Sel r;
+    r.pos0 = swap ? 1 : 0;
+    r.pos1 = swap ? 0 : 1;
+    const int col0 = ci.v[r.pos0], col1 = ci.v[r.pos1];
+    r.u[0] = kp[col0];
+    r.u[1] = kp[col1];
+    r.v[0] = kp[V + col0];
+    r.v[1] = kp[V + col1];
+    return r;
+}
+
+// Points the tolerance kernel could not certify (the inverse iteration has not provably
+// converged: sigma_4 ~ sigma_3 geometry, Inf input) are re-solved on the exact path by a
+// second, one-workgroup launch, so the exact path's registers (Jacobi on A^T and V^T: the
+// inline fallback held the kernel at 150 VGPRs = 3 waves per SIMD) never limit the
+// occupancy of the throughput kernel.  The tolerance kernel marks such a point's x output
+// with a signalling-NaN sentinel (arithmetic never produces it) and appends its index to a
+// per-stream list (one atomic per wave); past the list's capacity the fallback sweeps the
+// outputs for the sentinel instead.  The fallback resets the list count for the next launch.
+constexpr int kFbCap = 1 << 16;
+constexpr uint32_t kFbSentinel = 0x7FA5A5A5u;
+
+struct FbList {
+    unsigned* count;  // [1]
+    unsigned* idx;    // [kFbCap]
+    int force;        // tests: send every finite point to the fallback (MVPOSE_TRI_FORCE_FALLBACK=1)
+};
+
+template <int NF32>
 __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
-    float* __restrict__ out, double* __restrict__ out4) {
+    float* __restrict__ out, double* __restrict__ out4, FbList fb) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
     __shared__ CamFast sfast[kMaxCams];
     __shared__ CamTol stol[2];
@@ -694,47 +740,109 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     __syncthreads();
     const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
-    const float* __restrict__ kp = kpts + p * 3 * V;
-    const int ca = ci.v[0], cb = ci.v[1];
-    const float conf_a = kp[2 * V + ca], conf_b = kp[2 * V + cb];
-    // stable ascending argsort of (conf_a, conf_b), NaN last: swapped iff conf_b sorts before conf_a
-    const bool swap = isnan(conf_a) ? !isnan(conf_b) : (conf_b < conf_a);
-    // rows of the lower-confidence camera first; each view's point comes from its column
-    // ci.v[pos] and its parameters from camera key = its position pos in camera_indices
-    const int pos0 = swap ? 1 : 0, pos1 = swap ? 0 : 1;
-    const int col0 = ci.v[pos0], col1 = ci.v[pos1];
-    const float u[2] = {kp[col0], kp[col1]}, v[2] = {kp[V + col0], kp[V + col1]};
-    const double* cp[2] = {scam[pos0], scam[pos1]};
-    float ux[2], uy[2];
-    undistort_pair_tol(u, v, cp[0], cp[1], sfast[pos0], sfast[pos1], stol[pos0], stol[pos1], ux, uy);
-    double A[4][4];
+    const Tol2Sel sel = tol2_select(kpts + p * 3 * V, V, ci);
+    const double* cp[2] = {scam[sel.pos0], scam[sel.pos1]};
+    bool ok;
+    if (isnan(sel.u[0]) || isnan(sel.u[1]) || isnan(sel.v[0]) || isnan(sel.v[1])) {
+        // a NaN coordinate makes every entry of its view's rows, hence the whole SVD, NaN on
+        // the exact path: all outputs NaN
+        const double qn = __builtin_nan("");
+        const double nv[4] = {qn, qn, qn, qn};
+        write_result(nv, p, out, out4);
+        ok = true;
+    } else {
+        float ux[2], uy[2];
+        undistort_pair_tol<NF32>(sel.u, sel.v, cp[0], cp[1], sfast[sel.pos0], sfast[sel.pos1], stol[sel.pos0],
+                           stol[sel.pos1], ux, uy);
+        double A[4][4];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-        const double* P = cp[q] + 26;
-        const double x = ux[q], y = uy[q];
+        for (int q = 0; q < 2; q++) {
+            const double* P = cp[q] + 26;
+            const double x = ux[q], y = uy[q];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            A[2 * q][k] = __builtin_fma(x, P[8 + k], -P[0 + k]);
-            A[2 * q + 1][k] = __builtin_fma(y, P[8 + k], -P[4 + k]);
+            for (int k = 0; k < 4; k++) {
+                A[2 * q][k] = __builtin_fma(x, P[8 + k], -P[0 + k]);
+                A[2 * q + 1][k] = __builtin_fma(y, P[8 + k], -P[4 + k]);
+            }
+        }
+        double nv[4];
+        ok = normal_eq_null_vector<4>(A, nv) && !fb.force;
+        if (ok) write_result(nv, p, out, out4);
+        else reinterpret_cast<unsigned*>(out)[3 * p] = kFbSentinel;
+    }
+    // wave-aggregated append of the uncertified points
+    const unsigned long long m = __ballot(!ok);
+    if (m) {
+        const int lane = __lane_id();
+        const int leader = __ffsll((long long)m) - 1;
+        unsigned base = 0;
+        if (lane == leader) base = atomicAdd(fb.count, (unsigned)__popcll(m));
+        base = __shfl(base, leader);
+        if (!ok) {
+            const unsigned slot = base + (unsigned)__popcll(m & ((1ull << lane) - 1));
+            if (slot < (unsigned)kFbCap) fb.idx[slot] = (unsigned)p;
         }
     }
+}
+
+// The exact path (OpenCV undistortion with IEEE divisions, Jacobi SVD) for one point.
+__device__ __noinline__ void tol2_exact_point(const float* __restrict__ kpts, int64_t p, int V,
+                                              const double (*scam)[MVP_CAM_DOUBLES], const CamIdx& ci,
+                                              float* __restrict__ out, double* __restrict__ out4) {
+    const Tol2Sel sel = tol2_select(kpts + p * 3 * V, V, ci);
+    const double* cp[2] = {scam[sel.pos0], scam[sel.pos1]};
+    float e0x, e0y, e1x, e1y;
+    undistort_point(sel.u[0], sel.v[0], cp[0], e0x, e0y);
+    undistort_point(sel.u[1], sel.v[1], cp[1], e1x, e1y);
+    double E[4][4];
+    add_view_rows(E, 0, e0x, e0y, cp[0] + 26);
+    add_view_rows(E, 2, e1x, e1y, cp[1] + 26);
+    double At[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) At[c][r] = E[r][c];
     double nv[4];
-    if (!normal_eq_null_vector<4>(A, nv)) {
-        // not provably converged (or non-finite): the exact path for this point
-        float e0x, e0y, e1x, e1y;
-        undistort_point(u[0], v[0], cp[0], e0x, e0y);
-        undistort_point(u[1], v[1], cp[1], e1x, e1y);
-        double E[4][4];
-        add_view_rows(E, 0, e0x, e0y, cp[0] + 26);
-        add_view_rows(E, 2, e1x, e1y, cp[1] + 26);
-        double At[4][4];
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-#pragma unroll
-            for (int r = 0; r < 4; r++) At[c][r] = E[r][c];
-        jacobi_null_vector<4>(At, nv);
-    }
+    jacobi_null_vector<4>(At, nv);
     write_result(nv, p, out, out4);
+}
+
+// One workgroup: the listed points (or, past the list's capacity, every point whose x
+// output carries the sentinel), then the count back to 0 for the next launch on the stream.
+__global__ __launch_bounds__(kBlock) void triangulate_tol2_fallback_kernel(
+    const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
+    float* __restrict__ out, double* __restrict__ out4, FbList fb) {
+    __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
+    __shared__ CamFast sfast[kMaxCams];
+    load_cams(scam, sfast, cams, n_cams);
+    const unsigned cnt = __atomic_load_n(fb.count, __ATOMIC_RELAXED);
+    if (cnt <= (unsigned)kFbCap) {
+        for (unsigned i = threadIdx.x; i < cnt; i += kBlock) tol2_exact_point(kpts, fb.idx[i], V, scam, ci, out, out4);
+    } else {
+        const unsigned* ob = reinterpret_cast<const unsigned*>(out);
+        for (int64_t p = threadIdx.x; p < n; p += kBlock)
+            if (ob[3 * p] == kFbSentinel) tol2_exact_point(kpts, p, V, scam, ci, out, out4);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *fb.count = 0u;
+}
+
+// The tolerance kernel's fallback list, one per (device, stream), allocated on first use
+// (a stream-captured launch needs one uncaptured call on that stream first).
+FbList tol_fallback_list(hipStream_t s) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, FbList> lists;
+    int dev = 0;
+    MVP_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = lists.find({dev, s});
+    if (it != lists.end()) return it->second;
+    unsigned* buf = nullptr;
+    MVP_HIP(hipMalloc(&buf, (1 + (size_t)kFbCap) * sizeof(unsigned)));
+    MVP_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned), s));
+    const FbList fb{buf, buf + 1, 0};
+    lists[{dev, s}] = fb;
+    return fb;
 }
 
 }  // namespace
@@ -768,10 +876,20 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
     if (mode == MVP_TRI_REFERENCE) {
         MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
                     "n_cam_idx <= n_cams");
-        if (tol && n_cam_idx == 2)
-            hipLaunchKernelGGL(triangulate_tol2_kernel, grid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
-                               out_xyz, out_xyzw);
-        else if (exact)
+        if (tol && n_cam_idx == 2 && n_points < (1LL << 32)) {
+            FbList fb = tol_fallback_list(s);
+            const char* ff = getenv("MVPOSE_TRI_FORCE_FALLBACK");  // tests: exercise the fallback list / sweep
+            fb.force = ff && ff[0] == '1';
+            const char* e = getenv("MVPOSE_TRI_F32");  // A/B: f32 undistortion iterations (3 or 4)
+            if (e && e[0] == '4')
+                hipLaunchKernelGGL(triangulate_tol2_kernel<4>, grid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
+                                   out_xyz, out_xyzw, fb);
+            else
+                hipLaunchKernelGGL(triangulate_tol2_kernel<3>, grid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
+                                   out_xyz, out_xyzw, fb);
+            hipLaunchKernelGGL(triangulate_tol2_fallback_kernel, dim3(1), block, 0, s, kpts, n_points, V, cams,
+                               n_cams, ci, out_xyz, out_xyzw, fb);
+        } else if (exact)
             hipLaunchKernelGGL(triangulate_reference_kernel<kExact>, grid, block, 0, s, kpts, n_points, V, cams,
                                n_cams, ci, n_cam_idx, out_xyz, out_xyzw);
         else

@@ -24,12 +24,19 @@ from .hrnet import N_JOINTS
 class MultiViewPipeline:
     def __init__(self, camera_params, estimator: BatchPoseEstimator | None = None, camera_indices=(0, 1),
                  mode: int = ops.TRI_REFERENCE, device="cuda", detector=None, bbox_thr: float = 0.3,
-                 **estimator_kw):
+                 tri_solver: str = "tolerance", **estimator_kw):
         """camera_params: {camera key: [K, R, T, dist]} (utils.get_params_from_name order),
         keys 0..V-1 as the reference assumes (pose_estimation.py:276-280).
         detector: an mvpose.rtmdet.RTMDetector run on every camera-frame before the crops
         (PoseEstimator.predict, mmpose_pose_estimation.py:234-250: its first person box with
-        score > bbox_thr, else the whole image), or None (whole-image crops)."""
+        score > bbox_thr, else the whole image), or None (whole-image crops).
+        tri_solver: "tolerance" (default: MVP_TRI_TOLERANCE, <= 1e-4 world units against
+        OpenCV's rounding sequence, bit-identical on almost every point) or "reference_compat"
+        (OpenCV 4.9's fp64 rounding sequence, QR + inverse iteration with the Jacobi
+        restatement where that has not converged)."""
+        if tri_solver not in ("tolerance", "reference_compat"):
+            raise ValueError(f"tri_solver {tri_solver!r}: 'tolerance' or 'reference_compat'")
+        self.tri_solver = tri_solver
         self.detector = detector
         self.bbox_thr = bbox_thr
         self._best = None
@@ -72,7 +79,7 @@ class MultiViewPipeline:
         else:
             out.pop("moments_done", None)
         out["kpts_3d"] = ops.triangulate(out["kpts_2d"], self.cams, self.camera_indices, mode=self.mode,
-                                         out=out.get("kpts_3d"))
+                                         out=out.get("kpts_3d"), tolerance=self.tri_solver == "tolerance")
         return out
 
     def detect(self, flat: torch.Tensor) -> torch.Tensor:

@@ -248,3 +248,25 @@ def test_tolerance_mode_full_size(ops):
     print(f"noise-free 10k: max |tol - pose| {err.max():.3g}, max |tol - exact| {np.abs(tol0 - ex0).max():.3g}")
     np.testing.assert_allclose(tol0, ex0, rtol=0, atol=ATOL)
     np.testing.assert_allclose(tol0, poses[:10_000], rtol=0, atol=2e-2)
+
+
+@pytest.mark.parametrize("frames", [1000, 6000])
+def test_tolerance_mode_fallback_list_and_sweep(ops, frames, monkeypatch):
+    """The tolerance kernel's out-of-line fallback: with every point forced onto it the result
+    is the exact path's, bit for bit — through the per-stream list (1,000 frames = 17 k points)
+    and, past the list's 65,536 entries, through the sentinel sweep (6,000 frames = 102 k
+    points); the next unforced launch on the same stream starts from an empty list."""
+    cams = syn.make_rig(2, seed=81)
+    k = syn.make_kpts_2d(syn.make_poses(frames, seed=82), cams, seed=83, noise_px=1.0)
+    k[3, 2, 0, 0] = np.nan
+    cp = syn.reference_camera_params(cams)
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    kd = torch.tensor(np.ascontiguousarray(k), device="cuda")
+    ex, exw = ops.triangulate(kd, cams_d, [0, 1], exact=True, return_xyzw=True)
+    monkeypatch.setenv("MVPOSE_TRI_FORCE_FALLBACK", "1")
+    fo, fow = ops.triangulate(kd, cams_d, [0, 1], tolerance=True, return_xyzw=True)
+    monkeypatch.delenv("MVPOSE_TRI_FORCE_FALLBACK")
+    np.testing.assert_array_equal(fo.cpu().numpy(), ex.cpu().numpy())
+    np.testing.assert_array_equal(fow.cpu().numpy(), exw.cpu().numpy())
+    tol = ops.triangulate(kd, cams_d, [0, 1], tolerance=True).cpu().numpy()
+    np.testing.assert_allclose(tol, ex.cpu().numpy(), rtol=0, atol=ATOL, equal_nan=True)
