@@ -539,12 +539,14 @@ __device__ __forceinline__ bool normal_eq_null_vector(const double (&A)[M][4], d
     // units, so its e₄ component is ~1/350) and λ₄/λ₃ reaches ~2e-5 on the synthetic rigs:
     // three fixed steps left a third of the points unconverged.  Iterate to a geometric
     // convergence test instead (remaining error ≈ step · step / previous step <= 1e-13).
-    double prev = 1.0;
-    for (int it = 0; it < 8; it++) {
+    // Branch-free per lane: every lane takes the same steps (a converged lane stays
+    // converged), two unconditionally, more only while some lane of the wave is still
+    // contracting — the per-lane early exits compiled to ~40 register copies per step.
+    auto step = [&](double& dd) {
         double y[4] = {x[0], x[1], x[2], x[3]};
         solve(y);
         const double is = rsqrt_fast(y[0] * y[0] + y[1] * y[1] + y[2] * y[2] + y[3] * y[3]);
-        double dd = 0;
+        dd = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             y[q] *= is;  // M⁻¹ is positive definite (up to the pivot clamp): no sign flip
@@ -552,15 +554,26 @@ __device__ __forceinline__ bool normal_eq_null_vector(const double (&A)[M][4], d
             dd += e * e;
             x[q] = y[q];
         }
-        if (dd <= 1e-26 || (dd <= 1e-16 && dd * dd <= 1e-26 * prev)) {
-#pragma unroll
-            for (int q = 0; q < 4; q++) nv[q] = x[q];
-            return true;
-        }
-        if (it >= 2 && !(dd < 0.25 * prev)) return false;  // not contracting (or NaN)
+    };
+    auto converged = [](double dd, double prev) { return dd <= 1e-26 || (dd <= 1e-16 && dd * dd <= 1e-26 * prev); };
+    double d0, d1;
+    step(d0);
+    step(d1);
+    bool ok = converged(d1, d0) || converged(d0, 1.0);
+    bool failed = false;
+    double prev = d1;
+#pragma unroll 1
+    for (int it = 2; it < 8 && __builtin_amdgcn_ballot_w64(!ok && !failed) != 0; it++) {
+        double dd;
+        step(dd);
+        const bool now = converged(dd, prev);
+        failed = failed || (!ok && !now && !(dd < 0.25 * prev));  // not contracting (or NaN)
+        ok = ok || now;
         prev = dd;
     }
-    return false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) nv[q] = x[q];
+    return ok && !failed;
 }
 
 // Solver stages.  kExact: the restatement for every lane (OpenCV undistortion
@@ -753,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     } else {
         float ux[2], uy[2];
         undistort_pair_tol<NF32>(sel.u, sel.v, cp[0], cp[1], sfast[sel.pos0], sfast[sel.pos1], stol[sel.pos0],
-                           stol[sel.pos1], ux, uy);
+                                 stol[sel.pos1], ux, uy);
         double A[4][4];
 #pragma unroll
         for (int q = 0; q < 2; q++) {

@@ -1,5 +1,6 @@
 """One triangulation workload for counter collection: V=2 reference mode,
-T frames (default 100k, BASELINE config 4 stream), fast solver, `reps` launches.
+T frames (default 100k, BASELINE config 4 stream), `reps` launches of the default solver
+(or the tolerance solver with MVPOSE_TRI_ONCE_TOL=1).
 
     python tools/tri_once.py [T] [reps]
 """
@@ -22,6 +23,7 @@ kd = torch.tensor(k, device="cuda")
 cd = torch.tensor(ops.pack_cameras(syn.reference_camera_params(cams)), device="cuda")
 out = torch.empty((T, 17, 3), device="cuda")
 for _ in range(reps):
-    ops.triangulate(kd, cd, [0, 1], mode=ops.TRI_REFERENCE, out=out)
+    ops.triangulate(kd, cd, [0, 1], mode=ops.TRI_REFERENCE, out=out,
+                    tolerance=os.environ.get("MVPOSE_TRI_ONCE_TOL") == "1")
 torch.cuda.synchronize()
 print("tri_once done", T, reps)
