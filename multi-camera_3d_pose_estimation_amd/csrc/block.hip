@@ -295,7 +295,8 @@ void launch_basic_block_c32(const uint16_t* x, const uint16_t* w1, const float* 
                             const float* b2, uint16_t* y, int N, int H, int W, hipStream_t s) {
     MVP_REQUIRE(basic_block_c32_supported(H, W), "basic block: unsupported plane %dx%d", H, W);
     if (N == 0) return;
-    if (launch_tblock32(x, w1, b1, w2, b2, y, N, H, W, s)) return;  // 32x32x16 version (tblock.hip)
+    if (launch_tblock32s(x, w1, b1, w2, b2, y, N, H, W, s)) return;  // streaming version (tblock32s.hip)
+    if (launch_tblock32(x, w1, b1, w2, b2, y, N, H, W, s)) return;   // tile version (tblock.hip)
     using C = BlockCfg<48>;
     static bool attr = false;
     if (!attr) {

@@ -138,6 +138,8 @@ const uint16_t* conv_zero_region();
 bool basic_block_c32_supported(int H, int W);
 // 32x32x16 version of the fused block (tblock.hip) for W = 48, H % 16 == 0; false when
 // not applicable (or MVPOSE_NO_TBLOCK=1).  Not bit-identical to the separate convs.
+bool launch_tblock32s(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
+                      uint16_t* y, int N, int H, int W, hipStream_t s);
 bool launch_tblock32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2, const float* b2,
                      uint16_t* y, int N, int H, int W, hipStream_t s);
 void launch_basic_block_c32(const uint16_t* x, const uint16_t* w1, const float* b1, const uint16_t* w2,

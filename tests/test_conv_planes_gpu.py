@@ -111,6 +111,35 @@ def test_tblock64_bitwise_equals_two_tconv_launches(n, monkeypatch):
     assert arena_b < arena_a
 
 
+@pytest.mark.parametrize("n", [1, 5, 37, 301, 700])
+def test_tblock32s_bitwise_equals_tile_kernel(n, monkeypatch):
+    """The streaming 32-channel BasicBlock (tblock32s.hip: whole crops per workgroup, input rows
+    through a 30-row LDS ring, warp-specialised conv1 / conv2) reproduces the tile kernel
+    (tblock.hip) bit for bit — same MFMA sequence per accumulator, same epilogues.  n = 1, 5,
+    37: fewer crops than CUs (one crop per workgroup, unused CUs); 301, 700: ragged
+    multi-crop ranges, so the ring wraps across crop boundaries."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    _set_mode(monkeypatch, "tconv")
+    spec, xi, yo, _ = hrnet.basic_block_spec(32, 64, 48, seed=17, n_blocks=2)
+    gen = torch.Generator().manual_seed(18)
+    x = torch.randn((n, 64, 48, 32), generator=gen).bfloat16().cuda()
+    outs = []
+    for off in ("1", "0"):
+        monkeypatch.setenv("MVPOSE_NO_TBLOCK32S", off)
+        g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+        out = torch.full_like(x, float("nan"))
+        g.run(x, out)
+        torch.cuda.synchronize()
+        outs.append(out)
+        g.close()
+    a, b = outs
+    d = (a.float() - b.float()).abs()
+    print(f"tblock32s n={n}: max |stream - tile| {d.max().item():.3g}, identical {(d == 0).float().mean().item():.6f}")
+    assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("mode", ["wsconv", "tconv"])
 @pytest.mark.parametrize("c,h,w", [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)])
 def test_batch_positions(c, h, w, mode, monkeypatch):

@@ -1,0 +1,110 @@
+// Phase timeline of tblock32s_kernel from s_memtime stamps (a TB32S_STAMPS build of the
+// kernel source; not part of libmvpose).  Build here, run on the GPU box:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include -o tools/s32_stamps tools/s32_stamps.hip
+//   ./tools/s32_stamps [N]
+#define TB32S_STAMPS 1
+#include "../multi-camera_3d_pose_estimation_amd/csrc/tblock32s.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+namespace mvp {
+void set_error(const char*, ...) {}
+[[noreturn]] void fail(int, const char* fmt, ...) {
+    va_list a;
+    va_start(a, fmt);
+    vfprintf(stderr, fmt, a);
+    va_end(a);
+    fprintf(stderr, "\n");
+    exit(1);
+}
+const uint16_t* conv_zero_region() {
+    static uint16_t* z = nullptr;
+    if (!z) {
+        MVP_HIP(hipMalloc(&z, 65536));
+        MVP_HIP(hipMemset(z, 0, 65536));
+    }
+    return z;
+}
+}  // namespace mvp
+
+static uint16_t bf16(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t)((u + 0x7FFF + ((u >> 16) & 1)) >> 16);
+}
+
+int main(int argc, char** argv) {
+    using G = mvp::S32;
+    const int N = argc > 1 ? atoi(argv[1]) : 1024;
+    std::mt19937 rng(1);
+    std::normal_distribution<float> nd(0.f, 1.f);
+    const size_t nx = (size_t)N * 64 * 48 * 32, nw = 32 * 9 * 32;
+    std::vector<uint16_t> hx(nx), hw(2 * nw);
+    std::vector<float> hb(64);
+    for (auto& v : hx) v = bf16(nd(rng));
+    for (auto& v : hw) v = bf16(nd(rng) * 0.05f);
+    for (auto& v : hb) v = nd(rng) * 0.1f;
+    uint16_t *x, *y, *w;
+    float* b;
+    unsigned long long* st;
+    int cus = 0;
+    MVP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int grid = std::min(N, cus);
+    const size_t nst = (size_t)grid * 8 * 16 * 4;
+    MVP_HIP(hipMalloc(&x, nx * 2));
+    MVP_HIP(hipMalloc(&y, nx * 2));
+    MVP_HIP(hipMalloc(&w, 2 * nw * 2));
+    MVP_HIP(hipMalloc(&b, 64 * 4));
+    MVP_HIP(hipMalloc(&st, nst * 8));
+    MVP_HIP(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+    MVP_HIP(hipMemcpy(w, hw.data(), 2 * nw * 2, hipMemcpyHostToDevice));
+    MVP_HIP(hipMemcpy(b, hb.data(), 64 * 4, hipMemcpyHostToDevice));
+    MVP_HIP(hipMemset(st, 0, nst * 8));
+    MVP_HIP(hipFuncSetAttribute((const void*)mvp::tblock32s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    mvp::S32Params p{x, w, b, w + nw, b + 32, y, mvp::conv_zero_region(), N, st};
+    hipEvent_t e0, e1;
+    MVP_HIP(hipEventCreate(&e0));
+    MVP_HIP(hipEventCreate(&e1));
+    for (int i = 0; i < 3; i++) hipLaunchKernelGGL(mvp::tblock32s_kernel, dim3(grid), dim3(512), G::LDS, 0, p);
+    MVP_HIP(hipEventRecord(e0));
+    const int reps = 10;
+    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(mvp::tblock32s_kernel, dim3(grid), dim3(512), G::LDS, 0, p);
+    MVP_HIP(hipEventRecord(e1));
+    MVP_HIP(hipEventSynchronize(e1));
+    float ms = 0;
+    MVP_HIP(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned long long> h(nst);
+    MVP_HIP(hipMemcpy(h.data(), st, nst * 8, hipMemcpyDeviceToHost));
+    printf("N=%d grid=%d: %.1f us per launch (stamped build)\n", N, grid, ms * 1000 / reps);
+    auto at = [&](int blk, int wave, int k, int i) { return (long long)h[((blk * 8 + wave) * 16 + k) * 4 + i]; };
+    std::vector<long long> c1_mfma, c1_epi, c1_bar, c2_mfma, c2_epi, c2_dma, c2_bar, phase;
+    for (int blk = 0; blk < grid; blk++)
+        for (int k = 2; k < 14; k++) {
+            for (int wv = 0; wv < 4; wv++) {
+                c1_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
+                c1_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
+                c1_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 2));
+            }
+            phase.push_back(at(blk, 0, k + 1, 0) - at(blk, 0, k, 0));
+            for (int wv = 4; wv < 8; wv++) {
+                c2_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
+                c2_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
+                c2_dma.push_back(at(blk, wv, k, 3) - at(blk, wv, k, 2));
+                c2_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 3));
+            }
+        }
+    auto med = [](std::vector<long long> v) {
+        std::sort(v.begin(), v.end());
+        return v.empty() ? 0LL : v[v.size() / 2];
+    };
+    printf("phase %lld ticks\n", med(phase));
+    printf("conv1: mfma loop %lld, epilogue %lld, barrier wait %lld\n", med(c1_mfma), med(c1_epi), med(c1_bar));
+    printf("conv2: dma burst %lld, prev epilogue %lld, setup+mfma %lld, dma wait+barrier %lld\n", med(c2_mfma),
+           med(c2_epi), med(c2_dma), med(c2_bar));
+    printf("ideal per SIMD: (4 + 3) x 18 x 32 = %d cycles\n", 7 * 18 * 32);
+    return 0;
+}
