@@ -14,11 +14,12 @@ from collections import defaultdict
 
 GROUPS = {"backbone": ("conv_mfma_kernel", "stem_kernel", "stem_mfma_kernel", "fuse_sum_kernel", "conv1x1_kernel",
                        "conv1x1_pair_kernel", "basic_block", "wsconv", "tconv_kernel", "tblock32_kernel",
-                       "s2conv_kernel", "stem2_kernel", "trans1_kernel", "head1x1_kernel"),
+                       "tblock32s_kernel", "tblock64_kernel", "s2conv_kernel", "stem2_kernel", "trans1_kernel",
+                       "head1x1_kernel", "head_fuse_kernel"),
           "moments": ("moments_kernel",),
           "preprocess": ("preprocess_kernel",), "decode": ("decode_kernel",),
-          "triangulate": ("triangulate_reference_kernel",
-                          "triangulate_all_views_kernel")}
+          "triangulate": ("triangulate_reference_kernel", "triangulate_all_views_kernel",
+                          "triangulate_tol2_kernel")}
 
 
 def load(path, counter):
