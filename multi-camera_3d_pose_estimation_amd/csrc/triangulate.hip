@@ -799,7 +799,7 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
 }
 
 // The exact path (OpenCV undistortion with IEEE divisions, Jacobi SVD) for one point.
-__device__ __noinline__ void tol2_exact_point(const float* __restrict__ kpts, int64_t p, int V,
+__device__ __forceinline__ void tol2_exact_point(const float* __restrict__ kpts, int64_t p, int V,
                                               const double (*scam)[MVP_CAM_DOUBLES], const CamIdx& ci,
                                               float* __restrict__ out, double* __restrict__ out4) {
     const Tol2Sel sel = tol2_select(kpts + p * 3 * V, V, ci);
@@ -827,8 +827,9 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_fallback_kernel(
     float* __restrict__ out, double* __restrict__ out4, FbList fb) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
     __shared__ CamFast sfast[kMaxCams];
-    load_cams(scam, sfast, cams, n_cams);
     const unsigned cnt = __atomic_load_n(fb.count, __ATOMIC_RELAXED);
+    if (cnt == 0) return;  // the usual case: nothing to re-solve, the count is already 0
+    load_cams(scam, sfast, cams, n_cams);
     if (cnt <= (unsigned)kFbCap) {
         for (unsigned i = threadIdx.x; i < cnt; i += kBlock) tol2_exact_point(kpts, fb.idx[i], V, scam, ci, out, out4);
     } else {
