@@ -315,206 +315,6 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// Half-item variant for the resident-weight planes: an item is 16 input channels (two
-// 8-channel planes, pixel pitch 2 slots) and the ring has 4 slots, so an item's DMA is
-// issued 3 items (1.5 full 32-channel items of MFMAs) before its use instead of 1, in less
-// LDS than the 2-slot ring of 32-channel pixel-major items.  K order (16-channel half,
-// tap) differs from tconv_kernel's (chunk, tap, half): equal to f32 summation-order rounding.
-template <int CIN, int H, int W, int TH, int NB>
-struct THCfg {
-    using T = TCfg<CIN, H, W, TH, NB, true>;
-    static constexpr int NW = T::NW, NT = T::NT, BM = T::BM, MG = T::MG, RS = T::RS, HR = T::HR;
-    static constexpr int HS = T::HS, WT = T::WT, NCH = T::NCH;
-    static constexpr int NI = CIN / 16;                          // half items per tile
-    static constexpr int HT = 2 * HS;                            // halo slots per half item
-    static constexpr int PPW = (HT + 64 * NW - 1) / (64 * NW);   // DMA pieces per wave per half item
-    static constexpr int BUF = PPW * NW * 1024, NBUF = 4, D = NBUF - 1;
-    static constexpr int WPPW = (NCH * WT + 64 * NW - 1) / (64 * NW);
-    static constexpr int WOFF = NBUF * BUF;
-    static constexpr int LDS = WOFF + WPPW * NW * 1024;
-    static constexpr int ST = 2 * NT;                            // stores (and residual loads) per wave per tile
-    static_assert(NI >= D + 1, "vmcnt bookkeeping assumes at most one tile end among the last D items");
-    static_assert(2 * PPW + 2 * ST < 64, "vmcnt range");
-};
-
-template <int CIN, int H, int W, int TH, int NB, bool RES>
-__global__ __launch_bounds__(512, 1) void tconv_half_kernel(TParams p) {
-    using G = THCfg<CIN, H, W, TH, NB>;
-    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int mg = wave % G::MG, pg = wave / G::MG;
-    if ((int)blockIdx.x >= p.n_tiles) return;
-    constexpr int tiles_h = H / TH;
-
-    auto wsrc_off = [&](int ws) {
-        const int tq = ws / G::BM, co = ws - (ws / G::BM) * G::BM;
-        const int cs = (co & ~31) | row_cout(co & 31);
-        return (cs * 9 + (tq >> 2)) * CIN + (tq & 3) * 8;
-    };
-    // per-lane DMA geometry: slot s = 2 * halo pixel + plane
-    int pk[G::PPW], po[G::PPW];
-#pragma unroll
-    for (int j = 0; j < G::PPW; j++) {
-        const int s = (j * G::NW + wave) * 64 + lane;
-        int kind = 0, off = 0, nb = 0, hy = 0;
-        if (s < G::HT) {
-            const int q = s & 1, hs = s >> 1;
-            if (hs > 0) {
-                const int t = hs - 1;
-                nb = t / (G::HR * G::RS);
-                const int rr = t - nb * (G::HR * G::RS);
-                hy = rr / G::RS;
-                const int hx = rr - hy * G::RS;
-                if (hx < W) {
-                    kind = 1;
-                    off = ((nb * H + hy - 1) * W + hx) * CIN + q * 8;
-                }
-            }
-        }
-        pk[j] = (kind << 28) | (nb << 8) | hy;
-        po[j] = off;
-    }
-    const uint16_t* zl = p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8;
-    auto tile_pos = [&](int tile, int& n0, int& ho0) {
-        n0 = (tile / tiles_h) * NB;
-        ho0 = (tile - (tile / tiles_h) * tiles_h) * TH;
-    };
-    auto issue = [&](int item, int buf) {
-        const int tile = blockIdx.x + (item / G::NI) * gridDim.x, half = item % G::NI;
-        int n0, ho0;
-        tile_pos(tile, n0, ho0);
-        const uint16_t* xb = p.x + ((long)(n0 * H + ho0) * W) * CIN + half * 16;
-        uint8_t* dst = lds + buf * G::BUF;
-#pragma unroll
-        for (int j = 0; j < G::PPW; j++) {
-            const int g = pk[j], kind = g >> 28, nb = (g >> 8) & 255, hy = g & 255;
-            const bool in = kind == 1 && (unsigned)(ho0 + hy - 1) < (unsigned)H && n0 + nb < p.N;
-            glds16(in ? xb + po[j] : zl, dst + (j * G::NW + wave) * 1024);
-        }
-    };
-    int bv[G::NT], eoff[G::NT], enb[G::NT];
-#pragma unroll
-    for (int t = 0; t < G::NT; t++) {
-        const int pp = tile_pixel<G::T::BLK, W, TH, NB>(pg * G::NT + t, r32);
-        const int nb = pp / (TH * W), rem = pp - nb * (TH * W);
-        const int ty = rem / W, x = rem - (rem / W) * W;
-        bv[t] = (h + (nb * G::HR * G::RS + ty * G::RS + x) * 2) * 16;
-        eoff[t] = (nb * H + ty) * W + x;
-        enb[t] = nb;
-    }
-    const int av = G::WOFF + (h * G::BM + mg * 32 + r32) * 16;
-    const int n_items = ((p.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1) * G::NI;
-    f32x16 bias_init;
-    {
-        const float* bp = p.bias + mg * 32 + 16 * h;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const float4 b4 = *reinterpret_cast<const float4*>(bp + 4 * j);
-            bias_init[4 * j] = b4.x;
-            bias_init[4 * j + 1] = b4.y;
-            bias_init[4 * j + 2] = b4.z;
-            bias_init[4 * j + 3] = b4.w;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < G::WPPW; j++) {
-        const int s = (j * G::NW + wave) * 64 + lane;
-        const int chunk = s / G::WT;
-        const uint16_t* src = s < G::NCH * G::WT ? p.w + chunk * 32 + wsrc_off(s - chunk * G::WT) : zl;
-        glds16(src, lds + G::WOFF + (j * G::NW + wave) * 1024);
-    }
-    // prologue: items 0 .. D-1 (past the end: the last item again, into a slot never read)
-#pragma unroll
-    for (int j = 0; j < G::D; j++) issue(min(j, n_items - 1), j);
-    f32x16 acc[G::NT];
-    for (int k = 0; k < n_items; k++) {
-        const int buf = k & (G::NBUF - 1), half = k % G::NI;
-        const bool first = half == 0, last = half == G::NI - 1;
-        // item k's pieces have landed.  Younger than them: items k+1, k+2's DMA, and the
-        // stores (+ residual loads) of a tile that ended among items k-3 .. k-1
-        if (k == 0)
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // + the resident weights
-        else if (k < G::NI || half == G::D)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::PPW) : "memory");
-        else if (half == 0 || half == 1)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::PPW + (RES ? 2 : 1) * G::ST) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::PPW + G::ST) : "memory");
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        const int tile = blockIdx.x + (k / G::NI) * gridDim.x;
-        int n0, ho0;
-        tile_pos(tile, n0, ho0);
-        const int cob = mg * 32 + 16 * h;
-        if (first) {
-#pragma unroll
-            for (int t = 0; t < G::NT; t++) acc[t] = bias_init;
-        }
-        uint4 rv[G::NT][2];
-        const long pix0 = (long)(n0 * H + ho0) * W;
-        if (RES && last) {
-#pragma unroll
-            for (int t = 0; t < G::NT; t++) {
-                const bool ok = n0 + enb[t] < p.N;
-                const uint16_t* rs = ok ? p.res + (pix0 + eoff[t]) * p.Cout + cob : p.zero + lane * 16;
-                rv[t][0] = *reinterpret_cast<const uint4*>(rs);
-                rv[t][1] = *reinterpret_cast<const uint4*>(rs + 8);
-            }
-        }
-        asm volatile("" ::: "memory");
-        issue(min(k + G::D, n_items - 1), (k + G::D) & (G::NBUF - 1));
-        asm volatile("" ::: "memory");
-        int bva[G::NT];
-#pragma unroll
-        for (int t = 0; t < G::NT; t++) bva[t] = bv[t] + buf * G::BUF;
-        const int ava = av + (half >> 1) * G::WT * 16 + (half & 1) * 2 * G::BM * 16;
-        bf16x8 fa[2], fb[2][G::NT];
-        auto load = [&](int tap, bf16x8& a, bf16x8 (&b)[G::NT]) {
-            const int dy = tap / 3, dx = tap % 3;
-            a = *reinterpret_cast<const bf16x8*>(lds + ava + tap * 4 * G::BM * 16);
-#pragma unroll
-            for (int t = 0; t < G::NT; t++)
-                b[t] = *reinterpret_cast<const bf16x8*>(lds + bva[t] + (dy * G::RS + dx) * 2 * 16);
-        };
-        load(0, fa[0], fb[0]);
-#pragma unroll
-        for (int tap = 0; tap < 9; tap++) {
-            const int cur = tap & 1;
-            if (tap + 1 < 9) load(tap + 1, fa[cur ^ 1], fb[cur ^ 1]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int t = 0; t < G::NT; t++)
-                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur], fb[cur][t], acc[t], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (last) {
-            if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
-#pragma unroll
-            for (int t = 0; t < G::NT; t++) {
-                const bool ok = n0 + enb[t] < p.N;
-                uint16_t* yrow = ok ? p.y + (pix0 + eoff[t]) * p.Cout + cob : p.sink + lane * 16;
-                uint32_t o[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++) {
-                    float v0 = acc[t][2 * e], v1 = acc[t][2 * e + 1];
-                    if (RES) {
-                        const uint4 rr = rv[t][e >> 2];
-                        const uint32_t u = (e & 3) == 0 ? rr.x : (e & 3) == 1 ? rr.y : (e & 3) == 2 ? rr.z : rr.w;
-                        v0 += lo_bf16(u);
-                        v1 += hi_bf16(u);
-                    }
-                    o[e] = pack_bf16x2(relu1(v0), relu1(v1));
-                }
-                *reinterpret_cast<uint4*>(yrow) = uint4{o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<uint4*>(yrow + 8) = uint4{o[4], o[5], o[6], o[7]};
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 int g_t_cus = 0;
 uint16_t* g_t_sink = nullptr;
 
@@ -553,24 +353,6 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
         const char* e = getenv("MVPOSE_TCONV_PM");  // A/B: 0 = plane-major halo everywhere
         return !(e && e[0] == '0');
     }();
-    if constexpr (WRES && BM == 64) {
-        static const bool half_env = [] {
-            const char* e = getenv("MVPOSE_TCONV_HALF");  // A/B: 1 = 16-channel items, 4-slot ring
-            return e && e[0] == '1';
-        }();
-        if (half_env) {
-            using GH = THCfg<CIN, H, W, TH, NB>;
-            static_assert(GH::LDS <= 160 * 1024, "LDS budget");
-            auto kh = c.res ? tconv_half_kernel<CIN, H, W, TH, NB, true> : tconv_half_kernel<CIN, H, W, TH, NB, false>;
-            static bool attr_h[2] = {false, false};
-            if (!attr_h[c.res ? 1 : 0]) {
-                MVP_HIP(hipFuncSetAttribute((const void*)kh, hipFuncAttributeMaxDynamicSharedMemorySize, GH::LDS));
-                attr_h[c.res ? 1 : 0] = true;
-            }
-            hipLaunchKernelGGL(kh, dim3(std::min(p.n_tiles, g_t_cus)), dim3(GH::NW * 64), GH::LDS, s, p);
-            return;
-        }
-    }
     constexpr bool PM_OK = TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
     if constexpr (PM_OK) {
         if (pm_env) {
