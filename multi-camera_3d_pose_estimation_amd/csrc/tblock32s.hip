@@ -333,8 +333,14 @@ __device__ __forceinline__ void conv2_role(const S32Params& p, uint8_t* lds, int
             if ((o[0] ^ o[3] ^ o[5]) == 0x12345678u)
 #endif
             {
+#ifdef TB32S_NT_STORE  // A/B: non-temporal output stores
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(u32x4{o[0], o[1], o[2], o[3]}, reinterpret_cast<u32x4*>(yp));
+                __builtin_nontemporal_store(u32x4{o[4], o[5], o[6], o[7]}, reinterpret_cast<u32x4*>(yp + 8));
+#else
                 *reinterpret_cast<uint4*>(yp) = uint4{o[0], o[1], o[2], o[3]};
                 *reinterpret_cast<uint4*>(yp + 8) = uint4{o[4], o[5], o[6], o[7]};
+#endif
             }
         }
     };

@@ -424,6 +424,14 @@ __device__ __forceinline__ double rcp_nr(double b) {
     return __builtin_fma(r, e, r);
 }
 
+// r = 1/b to ~11 ulp: v_rcp_f64 (~2^-24) + one Newton step (profiles/r03p_rcp_probe.log).
+// For the undistortion's fp64 steps, whose outputs are rounded to f32: 11 ulp of fp64 is
+// ~1e-15 relative, four orders below the f32 rounding they feed.
+__device__ __forceinline__ double rcp_nr1(double b) {
+    const double r = __builtin_amdgcn_rcp(b);
+    return __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+}
+
 // Both views of a point: (u, v) pixels -> undistorted pixels (P = K), OpenCV's iteration:
 // the first NF32 of the 5 in f32, the rest in fp64.
 template <int NF32>
@@ -469,7 +477,7 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
             const double* c = cc[q];
             const double k0 = c[9], k1 = c[10], k2 = c[11], k3 = c[12], k4 = c[13];
             const double r2 = xd[q] * xd[q] + yd[q] * yd[q];
-            const double ic = rcp_nr(1 + ((k4 * r2 + k1) * r2 + k0) * r2);
+            const double ic = rcp_nr1(1 + ((k4 * r2 + k1) * r2 + k0) * r2);
             neg[q] = neg[q] || ic < 0;
             const double dX = 2 * k2 * xd[q] * yd[q] + k3 * (r2 + 2 * xd[q] * xd[q]);
             const double dY = k2 * (r2 + 2 * yd[q] * yd[q]) + 2 * k3 * xd[q] * yd[q];
@@ -481,7 +489,7 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
     for (int q = 0; q < 2; q++) {
         const double* c = cc[q];
         const double xx = neg[q] ? x0[q] : xd[q], yy = neg[q] ? y0[q] : yd[q];
-        const double ww = rcp_nr(c[6] * xx + c[7] * yy + c[8]);
+        const double ww = rcp_nr1(c[6] * xx + c[7] * yy + c[8]);
         ox[q] = (float)((c[0] * xx + c[1] * yy + c[2]) * ww);
         oy[q] = (float)((c[3] * xx + c[4] * yy + c[5]) * ww);
     }
