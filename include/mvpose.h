@@ -340,6 +340,20 @@ int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, in
                    float* final_traj, float* best_traj, float* batch_costs, float* iter_means, int* iters,
                    void* stream);
 
+/* Joint trajectory + extrinsic refinement: sgd_optimize(extrinsic_optimization_IDs=ids,
+ * optimize_trajectory=True) (pose_refinement.py:894-1096 with :931-954 — the listed cameras'
+ * R (3x3 matrix, the reference's default learnable form) and T are leaf tensors in the same
+ * Adam optimizer as the trajectory, ahead of it, and in the same clip_grad_norm_).  As
+ * mvp_sgd_refine, plus learn_cam_host [n_learn] (host) camera slots (0 <= slot < V, distinct,
+ * n_learn <= 2) whose R, T receive the likelihood gradient (dcost/dR_ij = dcost/dP_i X_j,
+ * dcost/dT_i = dcost/dP_i, P = R X + T) and their own Adam state.  cams_final / cams_best
+ * [M][n_learn][12] f32 (R row-major | T; best = NaN if never improved) are device pointers;
+ * the cams records themselves are not modified. */
+int mvp_sgd_refine_cams(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J,
+                        const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p, float* workspace,
+                        float* final_traj, float* best_traj, float* batch_costs, float* iter_means, int* iters,
+                        const int* learn_cam_host, int n_learn, float* cams_final, float* cams_best, void* stream);
+
 /* project_points_torch (pose_refinement.py:94-179): pts [n][3] f32 -> uv [n][2] f32 for one camera
  * record (R as a 3x3 matrix). */
 /* Extrinsic-from-samples refinement (sgd_optimize(extrinsic_optimization_IDs=[id],

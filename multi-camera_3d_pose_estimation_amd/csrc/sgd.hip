@@ -33,6 +33,8 @@ namespace {
 constexpr int kMaxSgdCams = 16;
 constexpr int kMaxSeg = 32;
 constexpr int kMaxJ = 64;
+constexpr int kMaxLearn = 2;   // learnable cameras (joint trajectory + extrinsic branch)
+constexpr int kCamGrad = 12;   // dR (9, row-major) + dT (3) per learnable camera
 
 struct SgdArgs {
     const float* gauss;
@@ -50,6 +52,10 @@ struct SgdArgs {
     int B, stride, n_win;
     int traj_in_lds;
     mvp_sgd_params p;
+    int n_learn;               // joint branch: cameras whose R, T are learnable (0 = trajectory only)
+    int learn[kMaxLearn];
+    float* cams_final;         // [M][n_learn][12]
+    float* cams_best;          // [M][n_learn][12]
 };
 
 struct Proj {
@@ -102,7 +108,7 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
 
 // d(u,v)/dX transposed applied to (gu, gv): the adjoint of project().
 __device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const Proj& o, bool ign, float gu,
-                                                float gv, float& g0, float& g1, float& g2) {
+                                                float gv, float& g0, float& g1, float& g2, float (&dP)[3]) {
     const float* K = c;
     const float* R = c + 9;
     const float* d = c + 21;
@@ -124,6 +130,9 @@ __device__ __forceinline__ void project_adjoint(const float* __restrict__ c, con
     // x = P0/P2, y = P1/P2, P = R·X + T
     const float iP2 = 1.f / o.P2;
     const float a = gx * iP2, b = gy * iP2, cz = -(gx * o.x + gy * o.y) * iP2;
+    dP[0] = a;  // d/dP of the camera-frame point (the learnable extrinsics' chain)
+    dP[1] = b;
+    dP[2] = cz;
     g0 = R[0] * a + R[3] * b + R[6] * cz;
     g1 = R[1] * a + R[4] * b + R[7] * cz;
     g2 = R[2] * a + R[5] * b + R[8] * cz;
@@ -159,8 +168,11 @@ __device__ __forceinline__ float quad_cost(const Target& g, float d0, float d1) 
 
 constexpr int kU = 4;   // points per thread in flight (independent loads issued together)
 
-template <int BS, int NV>
-__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[8]) {
+constexpr int kRedCols = 2 * kCamGrad;  // widest block reduction: both learnable cameras' gradients
+
+template <int BS, int NV, int NC>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NC]) {
+    static_assert(NV <= NC, "block_sum width");
 #pragma unroll
     for (int i = 0; i < NV; i++)
 #pragma unroll
@@ -182,13 +194,16 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[8]) {
 
 __device__ __forceinline__ bool finite(float x) { return !(isnan(x) || isinf(x)); }
 
-template <int BS>
+template <int BS, bool LEARN>
 __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     extern __shared__ float lds_traj[];
     __shared__ float cam_s[kMaxSgdCams * MVP_SGD_CAM_FLOATS];
     __shared__ int seg_s[kMaxSeg * 2];
     __shared__ float seglen_s[kMaxSeg];
-    __shared__ double red_s[BS / 64][8];
+    __shared__ double red_s[BS / 64][kRedCols];
+    __shared__ int learn_slot[kMaxSgdCams];            // camera -> learnable index, -1 = fixed
+    __shared__ float cstate[kMaxLearn * 2 * kCamGrad];  // Adam m | v of the learnable R, T
+    __shared__ float cgrad[kMaxLearn * kCamGrad];       // the window's reduced camera gradient
 
     const int m = blockIdx.x, tid = threadIdx.x;
     const int T = a.T, V = a.V, J = a.J, B = a.B, NS = a.n_seg;
@@ -211,6 +226,14 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     float* best = a.best_traj + (size_t)m * n3;
 
     for (int i = tid; i < V * MVP_SGD_CAM_FLOATS; i += BS) cam_s[i] = a.cams[i];
+    const int NL = LEARN ? a.n_learn : 0;  // LEARN = false: the trajectory-only kernel, unchanged
+    for (int c = tid; c < V; c += BS) {
+        int sl = -1;
+        for (int l = 0; l < NL; l++)
+            if (a.learn[l] == c) sl = l;
+        learn_slot[c] = sl;
+    }
+    for (int i = tid; i < kMaxLearn * 2 * kCamGrad; i += BS) cstate[i] = 0.f;
     for (int i = tid; i < NS; i += BS) {
         seg_s[2 * i] = a.seg[2 * i];
         seg_s[2 * i + 1] = a.seg[2 * i + 1];
@@ -258,6 +281,10 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
             const int nq = B * J;
             // ---- pass A: forward costs
             double acc[6] = {0, 0, 0, 0, 0, 0};   // lsum, lcnt, ssum, scnt, ab, bb
+            float cg0[LEARN ? kCamGrad : 1], cg1[LEARN ? kCamGrad : 1];  // learnable cameras 0, 1: dR, dT
+            if constexpr (LEARN)
+#pragma unroll
+                for (int k = 0; k < kCamGrad; k++) cg0[k] = cg1[k] = 0.f;
             // likelihood value AND its (not yet 1/n-scaled) gradient: one projection per
             // (point, camera) per step; the scale needs the global finite count.
             for (int q0 = tid; q0 < nq; q0 += kU * BS) {
@@ -294,8 +321,23 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                         const float s01 = g.a01 + g.a10;
                         const float gu = 0.5f * (2.f * g.a00 * d0 + s01 * d1);
                         const float gv = 0.5f * (s01 * d0 + 2.f * g.a11 * d1);
-                        float h0, h1, h2;
-                        project_adjoint(cam, o, ign, gu, gv, h0, h1, h2);
+                        float h0, h1, h2, dP[3];
+                        project_adjoint(cam, o, ign, gu, gv, h0, h1, h2, dP);
+                        if constexpr (LEARN) {
+                            const int ls = learn_slot[c];
+                            auto add_cam = [&](float (&cg)[kCamGrad]) {  // dP/dR_ij = X_j, dP/dT_i = 1
+#pragma unroll
+                                for (int i = 0; i < 3; i++) {
+#pragma unroll
+                                    for (int jj = 0; jj < 3; jj++) cg[3 * i + jj] += dP[i] * xs[u][jj];
+                                    cg[9 + i] += dP[i];
+                                }
+                            };
+                            if (ls == 0)
+                                add_cam(cg0);
+                            else if (ls == 1)
+                                add_cam(cg1);
+                        }
                         g0 += h0;
                         g1 += h1;
                         g2 += h2;
@@ -337,6 +379,21 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                     acc[5] += (double)len * len;
                 }
             block_sum<BS>(acc, red_s);
+            if constexpr (LEARN) {  // the learnable cameras' gradient sums
+                double cgd[kRedCols];
+#pragma unroll
+                for (int k = 0; k < kCamGrad; k++) {
+                    cgd[k] = cg0[k];
+                    cgd[kCamGrad + k] = cg1[k];
+                }
+                block_sum<BS>(cgd, red_s);
+                const double sc = acc[1] > 0 ? 1.0 / acc[1] : 0.0;  // the likelihood's 1/n, as lscale
+                if (tid == 0)
+#pragma unroll
+                    for (int k = 0; k < kRedCols; k++)
+                        if (k < NL * kCamGrad) cgrad[k] = (float)(cgd[k] * sc);
+                __syncthreads();
+            }
             const float L = (float)(acc[0] / acc[1]);
             const float S = lam_s * (float)(acc[2] / acc[3]);
             const float mu = (float)acc[4] / (float)acc[5];
@@ -397,7 +454,20 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                     acc2[1] += (double)rr * rr;
                 }
             block_sum<BS>(acc2, red_s);
-            const float gnorm = (float)sqrt(acc2[0]);
+            float gnorm = (float)sqrt(acc2[0]);
+            if (NL > 0) {
+                // clip_grad_norm_ over [R_0, T_0, (R_1, T_1,) trajectory]: per-tensor norms, then
+                // the norm of the norms
+                double tot = (double)gnorm * gnorm;
+                for (int l = 0; l < NL; l++) {
+                    double r2 = 0.0, t2 = 0.0;
+                    for (int k = 0; k < 9; k++) r2 += (double)cgrad[l * kCamGrad + k] * cgrad[l * kCamGrad + k];
+                    for (int k = 9; k < kCamGrad; k++) t2 += (double)cgrad[l * kCamGrad + k] * cgrad[l * kCamGrad + k];
+                    const float nr = (float)sqrt(r2), nt = (float)sqrt(t2);
+                    tot += (double)nr * nr + (double)nt * nt;
+                }
+                gnorm = (float)sqrt(tot);
+            }
             const float coef = fminf((float)a.p.max_grad_norm / (gnorm + 1e-6f), 1.f);
             const float Bc = lam_b * (float)acc2[1] / (float)aa;
 
@@ -408,6 +478,19 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
             const float nstep = (float)(-(a.p.lr / bc1));
             const float bc2s = (float)sqrt(bc2);
             const int wlo = t0 * J * 3, whi = (t0 + B) * J * 3;
+            if (tid < NL * kCamGrad) {  // the learnable R, T: same single-tensor Adam step
+                const int l = tid / kCamGrad, k = tid - l * kCamGrad;
+                float* prm = cam_s + a.learn[l] * MVP_SGD_CAM_FLOATS + (k < 9 ? 9 + k : 18 + (k - 9));
+                const float g = cgrad[tid] * coef;
+                float mv = cstate[tid];
+                mv = (w1 < 0.5f) ? mv + w1 * (g - mv) : g - (g - mv) * (1.f - w1);
+                float vv = cstate[NL * kCamGrad + tid] * b2;
+                vv = vv + w2 * g * g;
+                cstate[tid] = mv;
+                cstate[NL * kCamGrad + tid] = vv;
+                const float denom = sqrtf(vv) / bc2s + eps;
+                *prm = *prm + nstep * mv / denom;
+            }
             for (int e = tid; e < n3; e += BS) {
                 const float g = (e >= wlo && e < whi) ? gb[e - wlo] * coef : 0.f;
                 float mv = mo[e];
@@ -449,6 +532,11 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
         if (mean[0] < best_total - (float)a.p.tolerance) {
             best_total = mean[0];
             for (int e = tid; e < n3; e += BS) best[e] = X[e];
+            if (tid < NL * kCamGrad) {
+                const int l = tid / kCamGrad, k = tid - l * kCamGrad;
+                a.cams_best[((size_t)m * NL + l) * kCamGrad + k] =
+                    cam_s[a.learn[l] * MVP_SGD_CAM_FLOATS + (k < 9 ? 9 + k : 18 + (k - 9))];
+            }
             no_imp = 0;
         } else {
             no_imp++;
@@ -458,6 +546,11 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     }
     float* fin = a.final_traj + (size_t)m * n3;
     for (int e = tid; e < n3; e += BS) fin[e] = X[e];
+    if (tid < NL * kCamGrad) {
+        const int l = tid / kCamGrad, k = tid - l * kCamGrad;
+        a.cams_final[((size_t)m * NL + l) * kCamGrad + k] =
+            cam_s[a.learn[l] * MVP_SGD_CAM_FLOATS + (k < 9 ? 9 + k : 18 + (k - 9))];
+    }
     if (tid == 0) a.iters[m] = it;
 }
 
@@ -628,11 +721,11 @@ extern "C" int mvp_sgd_workspace_floats(int M, int T, int V, int J, int64_t* out
     MVP_ABI_END
 }
 
-extern "C" int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J,
-                              const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p,
-                              float* workspace, float* final_traj, float* best_traj, float* batch_costs,
-                              float* iter_means, int* iters, void* stream) {
-    MVP_ABI_BEGIN
+namespace {
+void sgd_launch(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J, const int* seg,
+                const float* seg_len, int n_seg, const mvp_sgd_params* p, float* workspace, float* final_traj,
+                float* best_traj, float* batch_costs, float* iter_means, int* iters, const int* learn, int n_learn,
+                float* cams_final, float* cams_best, void* stream) {
     MVP_REQUIRE(p && gauss && traj0 && cams && workspace && final_traj && best_traj && batch_costs && iter_means &&
                     iters,
                 "mvp_sgd_refine: null pointer");
@@ -669,21 +762,58 @@ extern "C" int mvp_sgd_refine(const float* gauss, const float* traj0, const floa
     const int t_win = (T / a.B) * a.B;
     a.n_win = (t_win - a.B) / a.stride + 1;
     a.p = *p;
+    MVP_REQUIRE(n_learn >= 0 && n_learn <= kMaxLearn, "mvp_sgd_refine_cams: n_learn=%d outside [0, %d]", n_learn,
+                kMaxLearn);
+    MVP_REQUIRE(n_learn == 0 || (learn && cams_final && cams_best), "mvp_sgd_refine_cams: null pointer");
+    a.n_learn = n_learn;
+    for (int l = 0; l < kMaxLearn; l++) a.learn[l] = l < n_learn ? learn[l] : -1;
+    for (int l = 0; l < n_learn; l++) {
+        MVP_REQUIRE(learn[l] >= 0 && learn[l] < V, "mvp_sgd_refine_cams: camera slot %d outside [0, V=%d)", learn[l], V);
+        for (int q = 0; q < l; q++)
+            MVP_REQUIRE(learn[q] != learn[l], "mvp_sgd_refine_cams: camera slot %d listed twice", learn[l]);
+    }
+    a.cams_final = cams_final;
+    a.cams_best = cams_best;
     const size_t traj_bytes = (size_t)T * J * 3 * sizeof(float);
     constexpr size_t kLdsBudget = 120 * 1024;
     a.traj_in_lds = traj_bytes <= kLdsBudget;
     const size_t lds = a.traj_in_lds ? traj_bytes : 0;
     hipStream_t s = (hipStream_t)stream;
-    if (T * J > 1024) {
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (n_learn > 0) {  // joint branch: one kernel width (the camera gradient's registers)
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdsBudget));
-        hipLaunchKernelGGL(sgd_kernel<512>, dim3(M), dim3(512), lds, s, a);
+        hipLaunchKernelGGL((sgd_kernel<256, true>), dim3(M), dim3(256), lds, s, a);
+    } else if (T * J > 1024) {
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<512, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)kLdsBudget));
+        hipLaunchKernelGGL((sgd_kernel<512, false>), dim3(M), dim3(512), lds, s, a);
     } else {
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdsBudget));
-        hipLaunchKernelGGL(sgd_kernel<256>, dim3(M), dim3(256), lds, s, a);
+        hipLaunchKernelGGL((sgd_kernel<256, false>), dim3(M), dim3(256), lds, s, a);
     }
     MVP_HIP(hipGetLastError());
+}
+}  // namespace
+
+extern "C" int mvp_sgd_refine(const float* gauss, const float* traj0, const float* cams, int M, int T, int V, int J,
+                              const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p,
+                              float* workspace, float* final_traj, float* best_traj, float* batch_costs,
+                              float* iter_means, int* iters, void* stream) {
+    MVP_ABI_BEGIN
+    sgd_launch(gauss, traj0, cams, M, T, V, J, seg, seg_len, n_seg, p, workspace, final_traj, best_traj, batch_costs,
+               iter_means, iters, nullptr, 0, nullptr, nullptr, stream);
+    MVP_ABI_END
+}
+
+extern "C" int mvp_sgd_refine_cams(const float* gauss, const float* traj0, const float* cams, int M, int T, int V,
+                                   int J, const int* seg, const float* seg_len, int n_seg, const mvp_sgd_params* p,
+                                   float* workspace, float* final_traj, float* best_traj, float* batch_costs,
+                                   float* iter_means, int* iters, const int* learn_cam_host, int n_learn,
+                                   float* cams_final, float* cams_best, void* stream) {
+    MVP_ABI_BEGIN
+    sgd_launch(gauss, traj0, cams, M, T, V, J, seg, seg_len, n_seg, p, workspace, final_traj, best_traj, batch_costs,
+               iter_means, iters, learn_cam_host, n_learn, cams_final, cams_best, stream);
     MVP_ABI_END
 }
 

@@ -18,8 +18,13 @@ Host mirror of the reference's refinement API (pose_refinement.py):
   HIP launch (mvp_extrinsic_sample_grad); the 12 learnable numbers, Adam and
   clip_grad_norm_ stay torch CPU tensors exactly as in the reference.
 
-Scope: the NN trajectory parameterisation (``use_NN``), ``randomize_params`` and
-joint trajectory + extrinsic optimisation raise NotImplementedError.
+* Joint trajectory + extrinsic optimisation (``sgd_optimize(extrinsic_optimization_IDs=ids,
+  optimize_trajectory=True)``, :931-954 + :894-1096): the listed cameras' R (3x3) and T
+  learn inside the same single-launch optimisation (mvp_sgd_refine_cams: their likelihood
+  gradient, their own Adam state, one clip_grad_norm_ over [R, T, ..., trajectory]).
+
+Scope: the NN trajectory parameterisation (``use_NN``) and ``randomize_params`` raise
+NotImplementedError.
 """
 from __future__ import annotations
 
@@ -191,11 +196,14 @@ def extrinsic_sample_grad(samples, targets, cam, n_samples, ignore_distortions=F
 def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=None, lr=0.001, betas=(0.9, 0.999),
                         lambda_smooth=1.0, lambda_body_length=1.0, patience=100, tolerance=1e-5, max_iter=1000,
                         batch_size=None, ignore_distortions=False, own_camera_gaussians=False, max_grad_norm=1.0,
-                        adam_eps=1e-8, device=None):
+                        adam_eps=1e-8, device=None, learn_cams=None):
     """M trajectories in one launch.  gaussians (M,T,V,J,6), initial_trajectories (M,T,J,3)
     (already time-sliced), cameras = V x (K, R, T, dist).  Returns device tensors:
     best (M,T,J,3) (NaN rows if never improved), final, batch_costs (M,max_iter+1,n_win,4),
-    iter_means (M,max_iter+1,4), iters (M,)."""
+    iter_means (M,max_iter+1,4), iters (M,).
+    learn_cams: camera slots (<= 2) whose R (3x3) and T are learned jointly with the trajectory
+    (mvp_sgd_refine_cams); adds cams_final / cams_best (M, n_learn, 12) = [R row-major | T]
+    (best NaN if never improved)."""
     dev = _device(device)
     G = torch.as_tensor(gaussians).to(device=dev, dtype=torch.float32).contiguous()
     X0 = torch.as_tensor(initial_trajectories).to(device=dev, dtype=torch.float32).contiguous()
@@ -236,10 +244,21 @@ def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=N
     batch_costs = torch.zeros((M, n_it, n_win, N_COSTS), dtype=torch.float32, device=dev)
     iter_means = torch.zeros((M, n_it, N_COSTS), dtype=torch.float32, device=dev)
     iters = torch.zeros(M, dtype=torch.int32, device=dev)
-    call("mvp_sgd_refine", _ptr(G), _ptr(X0), _ptr(cams), M, T, V, J, _ptr(seg), _ptr(seg_len), n_seg,
-         ctypes.byref(p), _ptr(ws), _ptr(final), _ptr(best), _ptr(batch_costs), _ptr(iter_means), _ptr(iters),
-         _stream(dev))
-    return {"best": best, "final": final, "batch_costs": batch_costs, "iter_means": iter_means, "iters": iters}
+    out = {"best": best, "final": final, "batch_costs": batch_costs, "iter_means": iter_means, "iters": iters}
+    if learn_cams:
+        nl = len(learn_cams)
+        slots = (ctypes.c_int * nl)(*[int(c) for c in learn_cams])
+        cf = torch.empty((M, nl, 12), dtype=torch.float32, device=dev)
+        cb = torch.full((M, nl, 12), float("nan"), dtype=torch.float32, device=dev)
+        call("mvp_sgd_refine_cams", _ptr(G), _ptr(X0), _ptr(cams), M, T, V, J, _ptr(seg), _ptr(seg_len), n_seg,
+             ctypes.byref(p), _ptr(ws), _ptr(final), _ptr(best), _ptr(batch_costs), _ptr(iter_means), _ptr(iters),
+             slots, nl, _ptr(cf), _ptr(cb), _stream(dev))
+        out["cams_final"], out["cams_best"] = cf, cb
+    else:
+        call("mvp_sgd_refine", _ptr(G), _ptr(X0), _ptr(cams), M, T, V, J, _ptr(seg), _ptr(seg_len), n_seg,
+             ctypes.byref(p), _ptr(ws), _ptr(final), _ptr(best), _ptr(batch_costs), _ptr(iter_means), _ptr(iters),
+             _stream(dev))
+    return out
 
 
 class Optimized_3d_Pose_Estimation:
@@ -295,10 +314,33 @@ class Optimized_3d_Pose_Estimation:
                                        lambda_body_length, patience, tolerance, max_iter, print_frequency,
                                        batch_size, N_sample_points, ignore_distortions, reset_camera_params,
                                        time_interval)
-        if extrinsic_optimization_IDs:
-            raise NotImplementedError("joint trajectory + extrinsic optimisation is not part of the GPU path")
         if self.n_dims != 3:
             raise NotImplementedError("3D trajectories only")
+        ext_ids = list(extrinsic_optimization_IDs or [])
+        learn = []
+        if ext_ids:
+            # joint trajectory + extrinsic optimisation (:931-954): per listed camera the initial R
+            # becomes axis-angle (used only by reset_camera_params), zero R / T entries of the
+            # working copy become random.random()/1e6 (one draw each, the reference's order), and
+            # R (3x3) and T join the trajectory in one Adam / clip_grad_norm_
+            if len(ext_ids) > 2:
+                raise NotImplementedError("at most 2 learnable cameras in the joint optimisation")
+            if reset_camera_params:
+                self.decomposed_cam_params = {k: [c.clone().detach() for c in v]
+                                              for k, v in self.decomposed_cam_params_initial.items()}
+            for ID in ext_ids:
+                if ID not in self.camera_IDs:
+                    raise ValueError(f"extrinsic camera {ID!r} is not in camera_IDs {self.camera_IDs}")
+                self.decomposed_cam_params_initial[ID][1] = rotation_conversion(
+                    self.decomposed_cam_params_initial[ID][1], to_vector=True)
+                Rp, Tp = self.decomposed_cam_params[ID][1], self.decomposed_cam_params[ID][2]
+                if tuple(Rp.shape) != (3, 3):
+                    raise NotImplementedError("joint optimisation learns R as a 3x3 matrix (the reference's "
+                                              "decomposed parameters); an axis-angle R is not supported")
+                with torch.no_grad():
+                    Rp[Rp == 0] = random.random() / 10 ** 6
+                    Tp[Tp == 0] = random.random() / 10 ** 6
+                learn.append(self.camera_IDs.index(ID))
         a, b = time_interval
         G = self.gaussians[a:b]
         X0 = self.initial_trajectory[a:b]
@@ -311,13 +353,25 @@ class Optimized_3d_Pose_Estimation:
                                 lambda_smooth=lambda_smooth, lambda_body_length=lambda_body_length,
                                 patience=patience, tolerance=tolerance, max_iter=max_iter, batch_size=B,
                                 ignore_distortions=ignore_distortions, own_camera_gaussians=own_camera_gaussians,
-                                device=self.device)
+                                device=self.device, learn_cams=learn)
         iters = int(r["iters"][0].item())
         best = r["best"][0].cpu()
         self.trajectory = r["final"][0].cpu()
         self.best_trajectory = None if torch.isnan(best).any() else best
+        best_cams = {}
+        if learn:
+            cf, cb = r["cams_final"][0].cpu(), r["cams_best"][0].cpu()
+            for li, ID in enumerate(ext_ids):
+                prm = self.decomposed_cam_params[ID]
+                best_cams[ID] = (cb[li, :9].reshape(3, 3).clone(), cb[li, 9:].reshape(prm[2].shape).clone())
+                prm[1] = cf[li, :9].reshape(3, 3).clone()
+                prm[2] = cf[li, 9:].reshape(prm[2].shape).clone()
         if self.best_trajectory is not None:
-            self.best_decomposed_cam_params = {k: [p.clone() for p in v] for k, v in self.decomposed_cam_params.items()}
+            self.best_decomposed_cam_params = {k: [p.detach().clone() for p in v]
+                                               for k, v in self.decomposed_cam_params.items()}
+            for ID, (bR, bT) in best_cams.items():
+                self.best_decomposed_cam_params[ID][1] = bR
+                self.best_decomposed_cam_params[ID][2] = bT
         names = ["total_cost", "likelihood_cost"]
         if lambda_smooth > 0:
             names.append("smoothness_cost")

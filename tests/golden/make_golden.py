@@ -285,6 +285,58 @@ def gen_sgd_extrinsic(pr):
         cv2.undistortPoints = und
 
 
+JOINT_CASES = [
+    # name, seed, learnable IDs, (rvec perturbation, T offset) per learnable ID, kwargs
+    ("sgd_joint_c2", 91, [2], [([0.015, -0.02, 0.01], [4.0, -3.0, 2.0])],
+     dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100, max_iter=10, batch_size=None)),
+    # camera 0 is R = I, T = 0: zero entries become random.random()/1e6 (:939-940); two learnable
+    # cameras, overlapping windows, early stop
+    ("sgd_joint_c01", 92, [0, 1], [None, ([-0.01, 0.02, 0.0], [-3.0, 2.0, 5.0])],
+     dict(lr=0.02, lambda_smooth=1e-3, lambda_body_length=0.5, patience=3, max_iter=30, batch_size=8,
+          tolerance=1e-2)),
+]
+
+
+def gen_sgd_joint(pr):
+    """sgd_optimize(extrinsic_optimization_IDs=ids, optimize_trajectory=True)
+    (pose_refinement.py:894-1096 with :931-954): trajectory + the listed cameras' R (3x3) and T
+    in one Adam / clip_grad_norm_."""
+    import random
+    for name, seed, ids, perts, kw in JOINT_CASES:
+        T = 16
+        cams, gauss, init = sgd_inputs(3, T, seed)
+        params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+        for ID, pert in zip(ids, perts):
+            if pert is not None:
+                params[ID][1] = _rotation(pert[0]) @ params[ID][1]
+                params[ID][2] = params[ID][2] + np.array(pert[1]).reshape(3, 1)
+            else:
+                params[ID][1] = np.eye(3)
+                params[ID][2] = np.zeros((3, 1))
+        R0 = np.stack([p[1] for p in params.values()])
+        T0 = np.stack([p[2] for p in params.values()])
+        random.seed(seed + 1)
+        torch.manual_seed(0)
+        opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                              body_lengths=dict(MY_LENGTHS))
+        full_kw = dict(print_frequency=10 ** 9, extrinsic_optimization_IDs=list(ids), optimize_trajectory=True)
+        full_kw.update(kw)
+        opt.sgd_optimize(**full_kw)
+        hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
+        best = opt.best_decomposed_cam_params
+        fin = opt.decomposed_cam_params
+        _save(f"{name}.npz", gauss=gauss, init=init, K=np.stack([c["K"] for c in cams]), R=R0, T=T0,
+              dist=np.stack([c["dist"] for c in cams]), ext_ids=np.array(ids),
+              best=opt.best_trajectory.numpy(), final=opt.trajectory.detach().numpy(),
+              best_R=np.stack([best[i][1].detach().numpy() for i in ids]),
+              best_T=np.stack([best[i][2].detach().numpy() for i in ids]),
+              final_R=np.stack([fin[i][1].detach().numpy() for i in ids]),
+              final_T=np.stack([fin[i][2].detach().numpy() for i in ids]),
+              kw_names=np.array(list(kw.keys())),
+              kw_vals=np.array([np.nan if v is None else float(v) for v in kw.values()]),
+              seeds=np.array([seed, seed + 1, 0]), **{"hist_" + k: v for k, v in hist.items()})
+
+
 def gen_interp(pr):
     """pose_refinement.linear_interpolation (pose_refinement.py:15-84) on a noisy
     kpts_3d-like sequence with spikes, a NaN frame and constant stretches."""
@@ -302,7 +354,7 @@ def gen_interp(pr):
     _save("interp.npz", points=pts, seeds=np.array([seed]), **outs)
 
 
-GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "sgd_extrinsic", "interp")
+GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "sgd_extrinsic", "sgd_joint", "interp")
 
 
 def main():
@@ -315,7 +367,8 @@ def main():
     gens = {"dlt": lambda: gen_dlt(ref_utils), "pose3d": lambda: gen_pose3d(pose_estimation),
             "moments": lambda: gen_moments(PoseEstimator), "project": lambda: gen_project(pr),
             "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr),
-            "sgd_extrinsic": lambda: gen_sgd_extrinsic(pr), "interp": lambda: gen_interp(pr)}
+            "sgd_extrinsic": lambda: gen_sgd_extrinsic(pr), "sgd_joint": lambda: gen_sgd_joint(pr),
+            "interp": lambda: gen_interp(pr)}
     for name in GENERATORS:
         if name in only:
             gens[name]()

@@ -191,5 +191,5 @@ def test_extrinsic_argument_errors():
     with pytest.raises(ValueError):      # 8 frames, batch 3: the reference's einsum fails here
         _opt(z).sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=False, GT_camera_IDs=[0, 1],
                              batch_size=3)
-    with pytest.raises(NotImplementedError):
-        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=True)
+    with pytest.raises(NotImplementedError):   # the joint branch learns at most 2 cameras
+        _opt(z).sgd_optimize(extrinsic_optimization_IDs=[0, 1, 2], optimize_trajectory=True)

@@ -1,0 +1,97 @@
+"""GPU parity of the joint trajectory + extrinsic refinement
+(sgd_optimize(extrinsic_optimization_IDs=ids, optimize_trajectory=True), reference
+pose_refinement.py:894-1096 with :931-954) against golden runs of the reference itself
+(tests/golden/make_golden.py gen_sgd_joint):
+
+* sgd_joint_c2: camera 2 (perturbed R, T) learned with the trajectory, one window;
+* sgd_joint_c01: cameras 0 (R = I, T = 0: every zero entry becomes random.random()/1e6,
+  :939-940, with the golden's random seed) and 1 learned together, 8-frame windows.
+
+The cameras' R (3x3 matrix) and T ride the trajectory's single-launch optimisation
+(mvp_sgd_refine_cams): their likelihood gradient, their own Adam state, one
+clip_grad_norm_ over [R, T, ..., trajectory].  Tolerances as the trajectory branch
+(test_sgd_gpu.py: f32 gradients summed in a different order than torch's autograd), with
+R / T bounds ~3x the measured deviations (printed).
+"""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from test_oracle_sgd import sgd_cams, sgd_kwargs
+
+pytestmark = pytest.mark.gpu
+SGD_ATOL = 1e-4
+HIST_RTOL = 1e-4
+R_ATOL, T_ATOL = 2e-6, 1e-4  # measured 4.6e-7 and 1.2e-7 (T ~ 3e2 has an f32 ulp of 3e-5)
+
+with open(os.path.join(GOLDEN, "body_part_lengths.json")) as _f:
+    MY_LENGTHS = json.load(_f)["my_lengths"]
+
+
+@pytest.fixture(scope="module")
+def refine():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import refine as _refine
+    return _refine
+
+
+@pytest.mark.parametrize("case", ["sgd_joint_c2", "sgd_joint_c01"])
+def test_joint_matches_reference_golden(refine, case):
+    d = np.load(os.path.join(GOLDEN, case + ".npz"))
+    ids = [int(i) for i in d["ext_ids"]]
+    cams = {i: c for i, c in enumerate(sgd_cams(d))}
+    random.seed(int(d["seeds"][1]))
+    opt = refine.Optimized_3d_Pose_Estimation(d["gauss"], d["init"], decomposed_cam_params_initial=cams,
+                                              body_lengths=dict(MY_LENGTHS))
+    opt.sgd_optimize(print_frequency=10 ** 9, extrinsic_optimization_IDs=ids, optimize_trajectory=True,
+                     **sgd_kwargs(d))
+    dx_best = np.abs(opt.best_trajectory.numpy() - d["best"]).max()
+    dx_fin = np.abs(opt.trajectory.numpy() - d["final"]).max()
+    fin_R = np.stack([opt.decomposed_cam_params[i][1].numpy() for i in ids])
+    fin_T = np.stack([opt.decomposed_cam_params[i][2].numpy() for i in ids])
+    best_R = np.stack([opt.best_decomposed_cam_params[i][1].numpy() for i in ids])
+    best_T = np.stack([opt.best_decomposed_cam_params[i][2].numpy() for i in ids])
+    print(f"{case}: |d traj| best {dx_best:.3g} final {dx_fin:.3g}; |d R| final {np.abs(fin_R - d['final_R']).max():.3g} "
+          f"best {np.abs(best_R - d['best_R']).max():.3g}; |d T| final {np.abs(fin_T - d['final_T']).max():.3g} "
+          f"best {np.abs(best_T - d['best_T']).max():.3g}")
+    np.testing.assert_allclose(opt.best_trajectory.numpy(), d["best"], rtol=0, atol=SGD_ATOL)
+    np.testing.assert_allclose(opt.trajectory.numpy(), d["final"], rtol=0, atol=SGD_ATOL)
+    np.testing.assert_allclose(fin_R, d["final_R"], rtol=0, atol=R_ATOL)
+    np.testing.assert_allclose(best_R, d["best_R"], rtol=0, atol=R_ATOL)
+    np.testing.assert_allclose(fin_T, d["final_T"], rtol=0, atol=T_ATOL)
+    np.testing.assert_allclose(best_T, d["best_T"], rtol=0, atol=T_ATOL)
+    for k, v in opt.all_costs_total.items():
+        ref = d["hist_" + k]
+        assert len(v) == len(ref), k
+        np.testing.assert_allclose(np.array(v, np.float64), ref, rtol=HIST_RTOL, atol=1e-7, err_msg=k)
+    # the learnable cameras actually moved; the others are untouched
+    assert np.abs(fin_R - d["R"][ids]).max() > 1e-3
+    for i in range(len(cams)):
+        if i not in ids:
+            np.testing.assert_array_equal(opt.decomposed_cam_params[i][1].numpy(),
+                                          np.asarray(d["R"][i], np.float32))
+
+
+def test_joint_without_learnable_cameras_is_the_trajectory_kernel(refine):
+    """extrinsic_optimization_IDs=[] with optimize_trajectory=True runs the trajectory-only
+    kernel (bit-identical results to an explicit trajectory run)."""
+    d = np.load(os.path.join(GOLDEN, "sgd_joint_c2.npz"))
+    outs = []
+    for ids in ([], None):
+        cams = {i: c for i, c in enumerate(sgd_cams(d))}
+        opt = refine.Optimized_3d_Pose_Estimation(d["gauss"], d["init"], decomposed_cam_params_initial=cams,
+                                                  body_lengths=dict(MY_LENGTHS))
+        kw = sgd_kwargs(d)
+        kw["max_iter"] = 3
+        if ids is None:
+            opt.sgd_optimize(print_frequency=10 ** 9, **kw)
+        else:
+            opt.sgd_optimize(print_frequency=10 ** 9, extrinsic_optimization_IDs=ids, optimize_trajectory=True, **kw)
+        outs.append(opt.trajectory.numpy())
+    np.testing.assert_array_equal(outs[0], outs[1])
