@@ -73,6 +73,7 @@ SIGNATURES = {
     "mvp_sgd_workspace_floats": (c_int, [c_int, c_int, c_int, c_int, P(c_int64)]),
     # mvp_sgd_params struct pointer declared in mvpose/refine.py
     "mvp_sgd_refine": (c_int, None),
+    "mvp_sgd_refine_cams": (c_int, None),
     "mvp_extrinsic_sample_grad": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_int, c_void_p,
                                           c_void_p]),
     "mvp_extrinsic_adam_step": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_double, c_double, c_double, c_double,
