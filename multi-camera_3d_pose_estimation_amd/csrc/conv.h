@@ -29,6 +29,9 @@ struct ConvLaunch {
     // Cout).  relu == 2 selects SiLU (x * sigmoid(x)) applied BEFORE the residual add
     // (CSPNeXtBlock: conv2(conv1(x)) + x); ReLU (1) is applied after it.
     int x_stride = 0, y_stride = 0, r_stride = 0;
+    // w re-laid as tconv16's weight image (tconv16_pack_weights) when the graph made one: the
+    // 128/256-channel branch planes then run tconv16.hip (nullptr: tconv.hip)
+    const uint16_t* w_img = nullptr;
 };
 
 void launch_conv(const ConvLaunch& c, hipStream_t s);
@@ -78,6 +81,13 @@ bool launch_wsconv(const ConvLaunch& c, hipStream_t s);
 // 64 ch @ 32x24 and 64x48, 128 ch @ 16x12, 256 ch @ 8x6 (ReLU epilogue).  false
 // when the conv is not one of those (or MVPOSE_NO_TCONV=1).
 bool launch_tconv(const ConvLaunch& c, hipStream_t s);
+// 128-cout-tile version for 128 ch @ 16x12 and 256 ch @ 8x6 (tconv16.hip), tried first by
+// launch_tconv; false otherwise (no weight image, or MVPOSE_TCONV16=0).
+bool launch_tconv16(const ConvLaunch& c, hipStream_t s);
+// Elements of the weight image of a conv tconv16 serves (0: not one of its planes), and the
+// packing launch (w [cout][3][3][cin] -> img, same element count).
+long tconv16_image_elems(int cin, int cout, int h, int w, int ks, int stride);
+void tconv16_pack_weights(const uint16_t* w, uint16_t* img, int cin, int cout, hipStream_t s);
 
 // 3x3/s2 conv on a polyphase halo, 16-channel items (s2conv.hip): transitions 2/3
 // and the downsampling fuse-layer convs of HRNet-W32 with >= 64 couts (no residual).

@@ -35,6 +35,7 @@ struct Graph {
     std::vector<std::vector<int>> sib;  // 3x3/s2 conv whose (absorbed) 3x3/s2 siblings on its input run in its launch
     std::vector<uint16_t*> sib_w;       // their cout-concatenated weights [128][3][3][cin] (owned)
     std::vector<float*> sib_b;          // and biases [128] (owned)
+    std::vector<uint16_t*> t16_w;       // tconv16 weight image of a 128/256-ch branch-plane conv (owned)
     std::vector<int> head_src;          // heatmap head that also runs the (absorbed) fuse op head_src[k] (-1: none)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
@@ -285,6 +286,7 @@ void sib_fuse(Graph& g, bool enable) {
     const int no = (int)g.ops.size();
     g.sib.assign(no, {});
     g.sib_w.assign(no, nullptr);
+    g.t16_w.assign(no, nullptr);
     g.sib_b.assign(no, nullptr);
     if (!enable) return;
     auto plain_s2 = [&](int k) {
@@ -402,7 +404,33 @@ void cat_fill(Graph& g) {
     }
 }
 
+// Weight images of the convs tconv16.hip serves (alloc at create, refilled with the blobs).
+long t16_elems(const Graph& g, int k) {
+    const mvp_op_desc& op = g.ops[k];
+    if (op.kind != MVP_OP_CONV || g.absorbed[k] || g.cat_src[k] >= 0 || g.pair_tail[k] >= 0 || !op.relu ||
+        g.tensors[op.out].dtype == MVP_DT_F32_NCHW)
+        return 0;
+    const mvp_tensor_desc& x = g.tensors[op.in[0]];
+    return tconv16_image_elems(op.cin, op.cout, x.h, x.w, op.ks, op.stride);
+}
+
+void t16_alloc(Graph& g) {
+    for (int k = 0; k < (int)g.ops.size(); k++) {
+        const long n = t16_elems(g, k);
+        if (n > 0) MVP_HIP(hipMalloc(&g.t16_w[k], (size_t)n * sizeof(uint16_t)));
+    }
+}
+
+void t16_fill(Graph& g) {
+    for (int k = 0; k < (int)g.ops.size(); k++)
+        if (g.t16_w[k]) tconv16_pack_weights(g.wb + g.ops[k].w_off, g.t16_w[k], g.ops[k].cin, g.ops[k].cout, nullptr);
+    MVP_HIP(hipDeviceSynchronize());
+}
+
 void cat_free(Graph& g) {
+    for (uint16_t* p : g.t16_w)
+        if (p) (void)hipFree(p);
+    g.t16_w.clear();
     for (uint16_t* p : g.cat_w)
         if (p) (void)hipFree(p);
     for (float* p : g.cat_b)
@@ -597,6 +625,8 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         mvp::sib_alloc(*g);
         mvp::cat_fill(*g);
         mvp::sib_fill(*g);
+        mvp::t16_alloc(*g);
+        mvp::t16_fill(*g);
         mvp::plan(*g);
         if (g->arena_bytes > 0) {
             hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
@@ -708,6 +738,7 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             c.ks = op.ks;
             c.stride = op.stride;
             c.relu = op.relu;
+            c.w_img = g->t16_w[k];
             if (g->cat_src[k] >= 0) {  // cat-fused: [in[0], absorbed op's input] x [W | W_absorbed]
                 const mvp_op_desc& a = g->ops[g->cat_src[k]];
                 c.x2 = (const uint16_t*)ptr(a.in[0]);
@@ -764,6 +795,7 @@ extern "C" int mvp_graph_refresh_weights(void* handle) {
     MVP_HIP(hipDeviceSynchronize());
     mvp::cat_fill(*g);
     mvp::sib_fill(*g);
+    mvp::t16_fill(*g);
     MVP_HIP(hipDeviceSynchronize());
     MVP_ABI_END
 }

@@ -389,6 +389,7 @@ bool launch_tconv(const ConvLaunch& c, hipStream_t s) {
         launch_t<64, 64, 48, 8, 1, true>(c, s);
         return true;
     }
+    if (launch_tconv16(c, s)) return true;  // 128 ch @ 16x12, 256 ch @ 8x6: 128-cout tiles
     // 128 ch @ 16x12 (streamed weights, two crops per tile): level with wsconv on the
     // plane-major halo (87.9 vs 86.2 us/conv at 1024 crops); with the pixel-major halo (the
     // ring slot fills the 160 KiB exactly) same-box A/B 10,207 -> 10,479 frames/s, backbone

@@ -21,6 +21,8 @@ MODES = {
     "generic": dict(_OFF),
     "wsconv": dict(_OFF, MVPOSE_NO_WSCONV="0"),
     "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0"),
+    # tconv.hip's 64-cout tiles on the 128- and 256-channel planes (tconv16.hip by default)
+    "tconv64": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0", MVPOSE_TCONV16="0"),
 }
 
 
@@ -49,6 +51,8 @@ def _set_mode(monkeypatch, mode):
         monkeypatch.setenv(k, v)
     monkeypatch.setenv("MVPOSE_WSCONV64", "1")
     monkeypatch.setenv("MVPOSE_TCONV128", "1")
+    if mode != "tconv64":
+        monkeypatch.delenv("MVPOSE_TCONV16", raising=False)
 
 
 def _run(c, h, w, n, n_blocks, seed, monkeypatch, mode):
@@ -140,7 +144,7 @@ def test_tblock32s_bitwise_equals_tile_kernel(n, monkeypatch):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", ["wsconv", "tconv"])
+@pytest.mark.parametrize("mode", ["wsconv", "tconv", "tconv64"])
 @pytest.mark.parametrize("c,h,w", [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)])
 def test_batch_positions(c, h, w, mode, monkeypatch):
     """A crop's output must not depend on its batch position or the batch size
