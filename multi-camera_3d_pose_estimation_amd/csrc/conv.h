@@ -30,7 +30,8 @@ struct ConvLaunch {
     // (CSPNeXtBlock: conv2(conv1(x)) + x); ReLU (1) is applied after it.
     int x_stride = 0, y_stride = 0, r_stride = 0;
     // w re-laid as tconv16's weight image (tconv16_pack_weights) when the graph made one: the
-    // 128/256-channel branch planes then run tconv16.hip (nullptr: tconv.hip)
+    // 128/256-channel branch planes then run tconv16.hip (nullptr: tconv.hip), and s2conv's
+    // streamed-weight planes read it instead of w
     const uint16_t* w_img = nullptr;
 };
 

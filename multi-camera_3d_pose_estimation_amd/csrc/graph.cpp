@@ -407,8 +407,9 @@ void cat_fill(Graph& g) {
 // Weight images of the convs tconv16.hip serves (alloc at create, refilled with the blobs).
 long t16_elems(const Graph& g, int k) {
     const mvp_op_desc& op = g.ops[k];
-    if (op.kind != MVP_OP_CONV || g.absorbed[k] || g.cat_src[k] >= 0 || g.pair_tail[k] >= 0 || !op.relu ||
-        g.tensors[op.out].dtype == MVP_DT_F32_NCHW)
+    if (op.kind != MVP_OP_CONV || g.absorbed[k] || g.cat_src[k] >= 0 || g.pair_tail[k] >= 0 ||
+        (op.stride == 1 && !op.relu) || g.tensors[op.out].dtype == MVP_DT_F32_NCHW || !g.sib[k].empty() ||
+        g.twin[k] >= 0 || g.stem_head[k] >= 0)
         return 0;
     const mvp_tensor_desc& x = g.tensors[op.in[0]];
     return tconv16_image_elems(op.cin, op.cout, x.h, x.w, op.ks, op.stride);

@@ -86,6 +86,7 @@ struct SParams {
     uint16_t* y1;
     uint16_t* y2;
     int c1, c2, relu1, relu2;
+    int img;  // w is the slot-order weight image (tconv16_pack_weights, BM = 128): 1 KB contiguous per DMA piece
 };
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM, bool PM>
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
             }
         } else if (!WRES && s < G::HT + G::WT) {
             kind = 2;
-            off = wsrc_off(s - G::HT);
+            off = p.img ? (s - G::HT) * 8 : wsrc_off(s - G::HT);
         }
         pk[j] = (kind << 28) | (nb << 8) | hy;
         po[j] = off;
@@ -145,7 +146,8 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
         int n0, ho0, cb;
         tile_of(tile, n0, ho0, cb);
         const uint16_t* xb = p.x + ((long)(n0 * H + 2 * ho0) * W) * CIN + slice * 16;
-        const uint16_t* wb = p.w + (long)cb * BM * 9 * CIN + slice * 16;
+        const uint16_t* wb =
+            p.img ? p.w + (long)(cb * G::NCH + slice) * G::WT * 8 : p.w + (long)cb * BM * 9 * CIN + slice * 16;
         uint8_t* dst = lds + buf * G::BUF;
 #pragma unroll
         for (int j = 0; j < G::PPW; j++) {
@@ -322,8 +324,11 @@ void launch_s(const ConvLaunch& c, hipStream_t s) {
     MVP_REQUIRE(c.Cin == CIN && c.H == H && c.W == W, "s2conv: plane mismatch");
     const long tiles = (long)((c.N + NB - 1) / NB) * (G::HO / TH) * (c.Cout / BM);
     MVP_REQUIRE(tiles < (1L << 30), "s2conv: too many tiles");
-    SParams p{c.x, c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles, c.Cout / BM, c.relu,
-              nullptr, nullptr, 0, 0, 0, 0};
+    // streamed weights from the graph's weight image when it made one (BM = 128 layout)
+    const char* ei = getenv("MVPOSE_S2_IMG");  // A/B: 0 = gather the weights from w
+    const bool img = !WRES && BM == 128 && c.w_img != nullptr && !(ei && ei[0] == '0');
+    SParams p{c.x, img ? c.w_img : c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles,
+              c.Cout / BM, c.relu, nullptr, nullptr, 0, 0, 0, 0, img ? 1 : 0};
     launch_sp<CIN, H, W, TH, NB, WRES, BM>(p, s);
 }
 
@@ -360,7 +365,7 @@ void launch_s2conv_multi(const S2Multi& m, hipStream_t s) {
     const long tiles = (long)m.N * (G::HO / 8);
     SParams p{m.x, m.w, m.bias, m.y[0], conv_zero_region(), g_s_sink, m.N, m.cout[0], (int)tiles, 1, m.relu[0],
               m.n_out > 1 ? m.y[1] : nullptr, m.n_out > 2 ? m.y[2] : nullptr, m.n_out > 1 ? m.cout[1] : 0,
-              m.n_out > 2 ? m.cout[2] : 0, m.n_out > 1 ? m.relu[1] : 0, m.n_out > 2 ? m.relu[2] : 0};
+              m.n_out > 2 ? m.cout[2] : 0, m.n_out > 1 ? m.relu[1] : 0, m.n_out > 2 ? m.relu[2] : 0, 0};
     if (tiles == 0) return;
     launch_sp<32, 64, 48, 8, 1, true, 128>(p, s);
     MVP_HIP(hipGetLastError());

@@ -361,7 +361,12 @@ bool t16_plane(int cin, int cout, int h, int w) {
 }  // namespace
 
 long tconv16_image_elems(int cin, int cout, int h, int w, int ks, int stride) {
-    return (ks == 3 && stride == 1 && t16_plane(cin, cout, h, w)) ? (long)cout * 9 * cin : 0;
+    // stride 1: this file's planes; stride 2: s2conv.hip's streamed-weight planes (same
+    // [tap][plane][128 couts] item image: transition2 / 3 and the fuse-layer chains' last convs)
+    const bool s1 = stride == 1 && t16_plane(cin, cout, h, w);
+    const bool s2 = stride == 2 && ((h == 32 && w == 24 && cout == 128 && cin == 64) ||
+                                    (h == 16 && w == 12 && cout % 128 == 0 && (cin == 32 || cin == 64 || cin == 128)));
+    return (ks == 3 && (s1 || s2)) ? (long)cout * 9 * cin : 0;
 }
 
 void tconv16_pack_weights(const uint16_t* w, uint16_t* img, int cin, int cout, hipStream_t s) {
