@@ -338,6 +338,10 @@ struct GParams {
     long M;                // n * Ho * Wo
     int cin, N, npad, xs, ys, rs, act, n_nb;
     int H, W, Ho, Wo;
+    // GEMM kernel: w re-laid by det_pack_gemm_weights (per 32-channel K step, every cout's
+    // four swizzled 16-B chunks in LDS slot order: a weight DMA instruction reads 1 KB
+    // contiguous instead of 16 rows x 64 B); nullptr: gather from w
+    const uint16_t* wimg = nullptr;
 };
 
 // s_waitcnt vmcnt(n') for the largest level n' <= n (wave-uniform n): at most n' of this
@@ -419,11 +423,14 @@ det_conv_gemm_kernel(GParams p) {
     // (advanced by 32 channels per K step), and each pixel's image base (the tap moves it)
     constexpr int ARW = (A_R64 + NWV - 1) / NWV;
     const uint16_t* asrc[ARW];
+    const int wstep = p.wimg ? p.npad * 32 : 32;  // elements between K steps of a weight row
 #pragma unroll
     for (int j = 0; j < ARW; j++) {
         const int sl = (wave + j * NWV) * 64 + lane;
         const int co = sl >> 2, kg = (sl & 3) ^ swz(co);
-        asrc[j] = (co0 + co < p.npad) ? p.w + (size_t)(co0 + co) * K + kg * 8 : nullptr;
+        asrc[j] = (co0 + co >= p.npad) ? nullptr
+                  : p.wimg             ? p.wimg + ((size_t)co0 * 4 + sl) * 8
+                                       : p.w + (size_t)(co0 + co) * K + kg * 8;
     }
     const uint16_t* bimg[BR];
 #pragma unroll
@@ -438,7 +445,7 @@ det_conv_gemm_kernel(GParams p) {
         for (int j = 0; j < ARW; j++) {
             const int r = wave + j * NWV;
             if (r < A_R64) {  // wave-uniform
-                const void* src = (live && asrc[j]) ? (const void*)(asrc[j] + k0)
+                const void* src = (live && asrc[j]) ? (const void*)(asrc[j] + (size_t)q * wstep)
                                                     : (const void*)(p.zero + ((r * 64 + lane) & 1023) * 8);
                 glds16_det(src, base + r * 64 * 16);
             }
@@ -1036,9 +1043,27 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
     MVP_HIP(hipGetLastError());
 }
 
+__global__ __launch_bounds__(256) void det_pack_gemm_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ img,
+                                                          int npad, int K) {
+    const long n = (long)npad * K / 8;  // 16-B slots
+    for (long d = blockIdx.x * 256L + threadIdx.x; d < n; d += (long)gridDim.x * 256) {
+        const long qc = d >> 2;  // (K step, cout)
+        const int c = (int)(d & 3), co = (int)(qc % npad), q = (int)(qc / npad);
+        const int kg = c ^ ((-(co >> 2)) & 3);  // the GEMM kernel's swz(co): co0 is a multiple of 16
+        *reinterpret_cast<uint4*>(img + d * 8) =
+            *reinterpret_cast<const uint4*>(w + (size_t)co * K + (size_t)q * 32 + kg * 8);
+    }
+}
+
+void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hipStream_t s) {
+    MVP_REQUIRE(npad % 32 == 0 && K % 32 == 0, "det_pack_gemm_weights: npad %d, K %d", npad, K);
+    hipLaunchKernelGGL(det_pack_gemm_kernel, dim3(512), dim3(256), 0, s, w, img, npad, K);
+    MVP_HIP(hipGetLastError());
+}
+
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s) {
+                          hipStream_t s, const uint16_t* wimg) {
     MVP_REQUIRE(cin % 32 == 0 && N % 4 == 0 && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
                 "det conv: cin=%d cout=%d strides %d/%d", cin, N, xs, ys);
     MVP_REQUIRE((ks == 1 && stride == 1) || (ks == 3 && (stride == 1 || stride == 2)), "det conv: ks %d stride %d", ks,
@@ -1056,7 +1081,7 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
                    : npad % 64 == 0                   ? 64
                                                       : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
-              (npad + bn - 1) / bn, H, W, Ho, Wo};
+              (npad + bn - 1) / bn, H, W, Ho, Wo, wimg};
     // halo-tile kernel for the 32-channel 3x3/s1 convs: 14.03 -> 13.77 ms per 64 frames
     // (same-box tools/det_ab.sh); MVPOSE_DET_HALO=0 keeps the im2col GEMM for them
     static const bool halo_env = [] {

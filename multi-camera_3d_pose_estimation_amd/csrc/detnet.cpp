@@ -24,7 +24,18 @@ struct DetNet {
     int64_t arena_bytes = 0;
     char* arena = nullptr;
     float* ca_scratch = nullptr;
+    std::vector<uint16_t*> wimg;  // per conv op: the GEMM kernel's weight image (owned)
 };
+
+void free_det(DetNet& g) {
+    if (g.arena) (void)hipFree(g.arena);
+    if (g.ca_scratch) (void)hipFree(g.ca_scratch);
+    for (uint16_t* p : g.wimg)
+        if (p) (void)hipFree(p);
+    g.arena = nullptr;
+    g.ca_scratch = nullptr;
+    g.wimg.clear();
+}
 
 int64_t per_image_bytes(const mvp_tensor_desc& t) { return (int64_t)t.h * t.w * t.c * 2; }
 
@@ -206,8 +217,18 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
             mvp::fail(MVP_ERR_NOMEM, "mvp_det_create: arena of %lld bytes: %s", (long long)g->arena_bytes,
                       hipGetErrorString(e));
         MVP_HIP(hipMalloc(&g->ca_scratch, (size_t)max_batch * 17 * g->max_ca * sizeof(float)));  // launch_det_ca scratch
+        // conv weight images for the GEMM kernel (the blobs are not rewritten after create)
+        g->wimg.assign(g->ops.size(), nullptr);
+        for (size_t k = 0; k < g->ops.size(); k++) {
+            const mvp_det_op& op = g->ops[k];
+            if (op.kind != MVP_DET_CONV) continue;
+            const int npad = mvp::det_cout_pad(op.out.c), K = op.ks * op.ks * op.in.c;
+            MVP_HIP(hipMalloc(&g->wimg[k], (size_t)npad * K * sizeof(uint16_t)));
+            mvp::det_pack_gemm_weights(w_dev + op.w_off, g->wimg[k], npad, K, nullptr);
+        }
+        MVP_HIP(hipDeviceSynchronize());
     } catch (...) {
-        if (g->arena) (void)hipFree(g->arena);
+        mvp::free_det(*g);
         delete g;
         throw;
     }
@@ -229,6 +250,8 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
     auto T = [&](int t) -> const mvp_tensor_desc& { return g->tensors[t]; };
     static const float kMean[3] = {103.53f, 116.28f, 123.675f};
     static const float kStd[3] = {57.375f, 57.12f, 58.395f};
+    const char* ewi = getenv("MVPOSE_DET_WIMG");  // A/B: 0 = gather the GEMM weights from the blob
+    const bool wimg_on = !(ewi && ewi[0] == '0');
     if (begin == 0) launch_det_letterbox(frames, n, h, w, g->size, kMean, kStd, base(g->input), s);
     for (int k = begin; k < end; k++) {
         const mvp_det_op& op = g->ops[k];
@@ -241,7 +264,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
                                      op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
                                      vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                     op.act, s);
+                                     op.act, s, wimg_on ? g->wimg[k] : nullptr);
                 break;
             }
             case MVP_DET_DW: {
@@ -338,8 +361,7 @@ extern "C" int mvp_det_destroy(void* handle) {
     MVP_ABI_BEGIN
     DetNet* g = static_cast<DetNet*>(handle);
     if (g) {
-        if (g->arena) (void)hipFree(g->arena);
-        if (g->ca_scratch) (void)hipFree(g->ca_scratch);
+        mvp::free_det(*g);
         delete g;
     }
     MVP_ABI_END
