@@ -130,7 +130,11 @@ void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uin
 // shapes (or MVPOSE_NO_TRANSFUSE=1).
 bool trans1_supported(int H, int W, int C, int cout0, int cout1);
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
-                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s);
+                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s,
+                   const uint16_t* wimg = nullptr);
+X
+constexpr long kTrans1ImageElems = 16L * 9 * 2 * 96 * 8;
+void trans1_pack_weights(const uint16_t* wb, int64_t w0_off, int64_t w1_off, uint16_t* img, hipStream_t s);
 
 // HRModule fuse: out = relu( sum_i up_i(in_i) ), nearest upsample factor up_i
 // (1, 2, 4, 8); all tensors bf16 NHWC with C channels, out at resolution H x W.

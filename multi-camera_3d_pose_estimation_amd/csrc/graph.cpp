@@ -36,6 +36,7 @@ struct Graph {
     std::vector<uint16_t*> sib_w;       // their cout-concatenated weights [128][3][3][cin] (owned)
     std::vector<float*> sib_b;          // and biases [128] (owned)
     std::vector<uint16_t*> t16_w;       // tconv16 weight image of a 128/256-ch branch-plane conv (owned)
+    std::vector<uint16_t*> tr_w;        // trans1 weight image of a twin-fused transition (owned)
     std::vector<int> head_src;          // heatmap head that also runs the (absorbed) fuse op head_src[k] (-1: none)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
@@ -287,6 +288,7 @@ void sib_fuse(Graph& g, bool enable) {
     g.sib.assign(no, {});
     g.sib_w.assign(no, nullptr);
     g.t16_w.assign(no, nullptr);
+    g.tr_w.assign(no, nullptr);
     g.sib_b.assign(no, nullptr);
     if (!enable) return;
     auto plain_s2 = [&](int k) {
@@ -419,19 +421,25 @@ void t16_alloc(Graph& g) {
     for (int k = 0; k < (int)g.ops.size(); k++) {
         const long n = t16_elems(g, k);
         if (n > 0) MVP_HIP(hipMalloc(&g.t16_w[k], (size_t)n * sizeof(uint16_t)));
+        if (g.twin[k] >= 0 && !g.absorbed[k]) MVP_HIP(hipMalloc(&g.tr_w[k], (size_t)kTrans1ImageElems * sizeof(uint16_t)));
     }
 }
 
 void t16_fill(Graph& g) {
-    for (int k = 0; k < (int)g.ops.size(); k++)
+    for (int k = 0; k < (int)g.ops.size(); k++) {
         if (g.t16_w[k]) tconv16_pack_weights(g.wb + g.ops[k].w_off, g.t16_w[k], g.ops[k].cin, g.ops[k].cout, nullptr);
+        if (g.tr_w[k]) trans1_pack_weights(g.wb, g.ops[k].w_off, g.ops[g.twin[k]].w_off, g.tr_w[k], nullptr);
+    }
     MVP_HIP(hipDeviceSynchronize());
 }
 
 void cat_free(Graph& g) {
     for (uint16_t* p : g.t16_w)
         if (p) (void)hipFree(p);
+    for (uint16_t* p : g.tr_w)
+        if (p) (void)hipFree(p);
     g.t16_w.clear();
+    g.tr_w.clear();
     for (uint16_t* p : g.cat_w)
         if (p) (void)hipFree(p);
     for (float* p : g.cat_b)
@@ -676,7 +684,7 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         if (g->twin[k] >= 0) {  // transition1: this 3x3/s1 conv and its 3x3/s2 sibling, one pass
             const mvp_op_desc& b = g->ops[g->twin[k]];
             mvp::launch_trans1((const uint16_t*)ptr(op.in[0]), g->wb, op.w_off, g->fb + op.b_off, b.w_off,
-                               g->fb + b.b_off, (uint16_t*)ptr(op.out), (uint16_t*)ptr(b.out), nb, s);
+                               g->fb + b.b_off, (uint16_t*)ptr(op.out), (uint16_t*)ptr(b.out), nb, s, g->tr_w[k]);
             return;
         }
         if (!g->sib[k].empty()) {  // this 3x3/s2 conv and its siblings on the same input

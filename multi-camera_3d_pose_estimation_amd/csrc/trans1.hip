@@ -70,6 +70,9 @@ struct TrParams {
     uint16_t* y1;        // [N][32][24][64]
     const uint16_t* zero;
     int N, n_tiles;
+    // the weight slots of every 16-channel chunk in LDS order (trans1_pack_weights): 1 KB
+    // contiguous per weight DMA instruction instead of 64 scattered rows; nullptr: gather from wb
+    const uint16_t* wimg;
 };
 
 template <bool PM>
@@ -101,6 +104,9 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
                     off = (yy * G::W + xx) * G::C + q * 8;
                 }
             }
+        } else if (s < G::ITEM && p.wimg) {
+            kind = 2;
+            off = (s - G::WA) * 8;
         } else if (s < G::WB) {
             const int ws = s - G::WA, row = ws & 31, tq = ws >> 5;  // tq = tap * 2 + q
             kind = 2;
@@ -118,11 +124,12 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
         const int n = tile / tiles_h, r0 = (tile - n * tiles_h) * G::TH;
         const uint16_t* xb = p.x + ((long)n * G::H + r0 - 1) * G::W * G::C + chunk * 16;
         uint8_t* dst = lds + buf * G::BUF;
+        const uint16_t* wbase = p.wimg ? p.wimg + chunk * (G::ITEM - G::WA) * 8 : p.wb + chunk * 16;
 #pragma unroll
         for (int j = 0; j < G::PPW; j++) {
             const int kind = pk[j] >> 8, hy = pk[j] & 255;
             const bool in = kind == 1 && (unsigned)(r0 - 1 + hy) < (unsigned)G::H;
-            const uint16_t* src = kind == 2 ? p.wb + (po[j] + chunk * 16) : in ? xb + po[j] : zl;
+            const uint16_t* src = kind == 2 ? wbase + po[j] : in ? xb + po[j] : zl;
             glds16(src, dst + (j * G::NW + wave) * 1024);
         }
     };
@@ -244,8 +251,33 @@ bool trans1_supported(int H, int W, int C, int cout0, int cout1) {
     return H == T1C<true>::H && W == T1C<true>::W && C == T1C<true>::C && cout0 == 32 && cout1 == 64;
 }
 
+// Weight image: per 16-channel chunk, t0's [tap][q][32 permuted couts] then t1's [tap][q][64]
+// (the kernel's slots WA .. ITEM), 1,728 x 16 B; same element count as w0 + w1.
+__global__ __launch_bounds__(256) void trans1_pack_kernel(const uint16_t* __restrict__ wb, int w0_off, int w1_off,
+                                                          uint16_t* __restrict__ img) {
+    constexpr int C = 256, NCH = C / 16, S0 = 9 * 2 * 32, SI = S0 + 9 * 2 * 64;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < NCH * SI; i += gridDim.x * 256) {
+        const int chunk = i / SI, ws = i - chunk * SI;
+        const uint16_t* src;
+        if (ws < S0) {
+            const int row = ws & 31, tq = ws >> 5;
+            src = wb + w0_off + (row_cout(row) * 9 + (tq >> 1)) * C + (tq & 1) * 8;
+        } else {
+            const int w = ws - S0, row = w & 63, tq = w >> 6;
+            src = wb + w1_off + (((row & ~31) | row_cout(row & 31)) * 9 + (tq >> 1)) * C + (tq & 1) * 8;
+        }
+        *reinterpret_cast<uint4*>(img + (long)i * 8) = *reinterpret_cast<const uint4*>(src + chunk * 16);
+    }
+}
+
+void trans1_pack_weights(const uint16_t* wb, int64_t w0_off, int64_t w1_off, uint16_t* img, hipStream_t s) {
+    static_assert(T1C<true>::ITEM - T1C<true>::WA == 9 * 2 * 96, "image item");
+    hipLaunchKernelGGL(trans1_pack_kernel, dim3(108), dim3(256), 0, s, wb, (int)w0_off, (int)w1_off, img);
+    MVP_HIP(hipGetLastError());
+}
+
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
-                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s) {
+                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s, const uint16_t* wimg) {
     MVP_REQUIRE(w0_off >= 0 && w1_off >= 0 && w0_off + 32 * 9 * 256 < (1LL << 31) && w1_off + 64 * 9 * 256 < (1LL << 31),
                 "trans1: weight offsets exceed 32 bits");
     if (N == 0) return;
@@ -264,7 +296,9 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     }
     const long tiles = (long)N * (T1C<true>::H / T1C<true>::TH);
     MVP_REQUIRE(tiles * T1C<true>::NCH < (1L << 30), "trans1: too many tiles");
-    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles};
+    const char* ei = getenv("MVPOSE_TRANS1_IMG");  // A/B: 0 = gather the weights from the blob
+    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles,
+               (ei && ei[0] == '0') ? nullptr : wimg};
     const int grid = (int)std::min<long>(tiles, g_tr_cus);
     static const bool pm = [] {
         const char* e = getenv("MVPOSE_TRANS1_PM");  // A/B: 0 = plane-major halo
