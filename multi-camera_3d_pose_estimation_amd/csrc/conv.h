@@ -132,7 +132,7 @@ bool trans1_supported(int H, int W, int C, int cout0, int cout1);
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
                    const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s,
                    const uint16_t* wimg = nullptr);
-X
+// trans1's weight image (9 x 2 x 96 16-B slots per 16-channel chunk, 221,184 elements)
 constexpr long kTrans1ImageElems = 16L * 9 * 2 * 96 * 8;
 void trans1_pack_weights(const uint16_t* wb, int64_t w0_off, int64_t w1_off, uint16_t* img, hipStream_t s);
 
