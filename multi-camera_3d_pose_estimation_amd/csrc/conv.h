@@ -73,10 +73,6 @@ struct PairLaunch {
 bool conv1x1_pair_supported(int cin_total, int cmid, int cout2);
 void launch_conv1x1_pair(const PairLaunch& p, hipStream_t s);
 
-// Weight-stationary 3x3/s1 conv for the Cin == Cout branch planes (wsconv.hip):
-// 64 ch at 32x24 and 128 ch at 16x12.  false when the conv is not one of those
-// (or MVPOSE_NO_WSCONV=1).
-bool launch_wsconv(const ConvLaunch& c, hipStream_t s);
 
 // Lean 3x3/s1 conv on 32x32x16 MFMAs for 384-pixel x 64-cout tiles (tconv.hip):
 // 64 ch @ 32x24 and 64x48, 128 ch @ 16x12, 256 ch @ 8x6 (ReLU epilogue).  false

@@ -877,7 +877,7 @@ void launch_conv_impl(const ConvLaunch& c, hipStream_t s, bool generic_only) {
         MVP_HIP(hipGetLastError());
         return;
     }
-    if (launch_head1x1(c, s) || launch_conv1x1_direct(c, s) || launch_tconv(c, s) || launch_wsconv(c, s) ||
+    if (launch_head1x1(c, s) || launch_conv1x1_direct(c, s) || launch_tconv(c, s) ||
         launch_s2conv(c, s)) {
         MVP_HIP(hipGetLastError());
         return;

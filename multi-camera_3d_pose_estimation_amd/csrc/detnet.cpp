@@ -250,8 +250,6 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
     auto T = [&](int t) -> const mvp_tensor_desc& { return g->tensors[t]; };
     static const float kMean[3] = {103.53f, 116.28f, 123.675f};
     static const float kStd[3] = {57.375f, 57.12f, 58.395f};
-    const char* ewi = getenv("MVPOSE_DET_WIMG");  // A/B: 0 = gather the GEMM weights from the blob
-    const bool wimg_on = !(ewi && ewi[0] == '0');
     if (begin == 0) launch_det_letterbox(frames, n, h, w, g->size, kMean, kStd, base(g->input), s);
     for (int k = begin; k < end; k++) {
         const mvp_det_op& op = g->ops[k];
@@ -264,7 +262,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
                                      op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
                                      vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                     op.act, s, wimg_on ? g->wimg[k] : nullptr);
+                                     op.act, s, g->wimg[k]);
                 break;
             }
             case MVP_DET_DW: {

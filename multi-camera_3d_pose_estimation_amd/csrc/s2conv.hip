@@ -325,8 +325,7 @@ void launch_s(const ConvLaunch& c, hipStream_t s) {
     const long tiles = (long)((c.N + NB - 1) / NB) * (G::HO / TH) * (c.Cout / BM);
     MVP_REQUIRE(tiles < (1L << 30), "s2conv: too many tiles");
     // streamed weights from the graph's weight image when it made one (BM = 128 layout)
-    const char* ei = getenv("MVPOSE_S2_IMG");  // A/B: 0 = gather the weights from w
-    const bool img = !WRES && BM == 128 && c.w_img != nullptr && !(ei && ei[0] == '0');
+    const bool img = !WRES && BM == 128 && c.w_img != nullptr;
     SParams p{c.x, img ? c.w_img : c.w, c.bias, c.y, conv_zero_region(), g_s_sink, c.N, c.Cout, (int)tiles,
               c.Cout / BM, c.relu, nullptr, nullptr, 0, 0, 0, 0, img ? 1 : 0};
     launch_sp<CIN, H, W, TH, NB, WRES, BM>(p, s);

@@ -390,12 +390,10 @@ bool launch_tconv(const ConvLaunch& c, hipStream_t s) {
         return true;
     }
     if (launch_tconv16(c, s)) return true;  // 128 ch @ 16x12, 256 ch @ 8x6: 128-cout tiles
-    // 128 ch @ 16x12 (streamed weights, two crops per tile): level with wsconv on the
-    // plane-major halo (87.9 vs 86.2 us/conv at 1024 crops); with the pixel-major halo (the
-    // ring slot fills the 160 KiB exactly) same-box A/B 10,207 -> 10,479 frames/s, backbone
-    // 24.69 -> 23.82 ms.  MVPOSE_TCONV128=0 hands the plane back to wsconv.
-    const char* e128 = getenv("MVPOSE_TCONV128");
-    if (c.Cin == 128 && c.H == 16 && c.W == 12 && !(e128 && e128[0] == '0')) {
+    // 128 ch @ 16x12 without a weight image (streamed weights, two crops per tile; the
+    // weight-stationary wsconv.hip it replaced in round 2 measured 86.2 us/conv against this
+    // kernel's 87.9 on the plane-major halo, 10,207 -> 10,479 frames/s with the pixel-major one)
+    if (c.Cin == 128 && c.H == 16 && c.W == 12) {
         launch_t<128, 16, 12, 16, 2, false>(c, s);
         return true;
     }

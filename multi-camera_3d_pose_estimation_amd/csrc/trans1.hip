@@ -296,9 +296,7 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     }
     const long tiles = (long)N * (T1C<true>::H / T1C<true>::TH);
     MVP_REQUIRE(tiles * T1C<true>::NCH < (1L << 30), "trans1: too many tiles");
-    const char* ei = getenv("MVPOSE_TRANS1_IMG");  // A/B: 0 = gather the weights from the blob
-    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles,
-               (ei && ei[0] == '0') ? nullptr : wimg};
+    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles, wimg};
     const int grid = (int)std::min<long>(tiles, g_tr_cus);
     static const bool pm = [] {
         const char* e = getenv("MVPOSE_TRANS1_PM");  // A/B: 0 = plane-major halo

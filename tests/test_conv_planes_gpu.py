@@ -2,8 +2,8 @@
 restatement that rounds to bf16 at the same tensor boundaries as the device
 graph (bf16 weights and activations, f32 bias and accumulation).  Every conv
 kernel family that serves a plane is checked: the generic conv_mfma_kernel
-(conv.hip; block.hip for the fused 32-channel block), the weight-stationary
-wsconv.hip and the 32x32x16 tconv.hip.  They sum K in different orders, so each
+(conv.hip; block.hip for the fused 32-channel block), the 32x32x16 tconv.hip and
+tconv16.hip.  They sum K in different orders, so each
 is compared against the reference with a tolerance, not bit for bit:
   relative L2 error <= 4e-3, and |dev - ref| <= 3 bf16 ulps of max|ref|."""
 import numpy as np
@@ -14,12 +14,11 @@ pytestmark = pytest.mark.gpu
 
 PLANES = [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]
 # environment per kernel family: the 32-channel plane runs the fused block,
-# basic_block_c32_kernel ("generic", "wsconv") or tblock ("tconv"); the 64-channel plane at
+# basic_block_c32_kernel ("generic") or tblock ("tconv"); the 64-channel plane at
 # 32x24 runs tblock64 in "tconv" mode
-_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_WSCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
+_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
 MODES = {
     "generic": dict(_OFF),
-    "wsconv": dict(_OFF, MVPOSE_NO_WSCONV="0"),
     "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0"),
     # tconv.hip's 64-cout tiles on the 128- and 256-channel planes (tconv16.hip by default)
     "tconv64": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0", MVPOSE_TCONV16="0"),
@@ -49,8 +48,6 @@ def _reference(sd, x, n_blocks):
 def _set_mode(monkeypatch, mode):
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
-    monkeypatch.setenv("MVPOSE_WSCONV64", "1")
-    monkeypatch.setenv("MVPOSE_TCONV128", "1")
     if mode != "tconv64":
         monkeypatch.delenv("MVPOSE_TCONV16", raising=False)
 
@@ -144,7 +141,7 @@ def test_tblock32s_bitwise_equals_tile_kernel(n, monkeypatch):
     assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode", ["wsconv", "tconv", "tconv64"])
+@pytest.mark.parametrize("mode", ["generic", "tconv", "tconv64"])
 @pytest.mark.parametrize("c,h,w", [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)])
 def test_batch_positions(c, h, w, mode, monkeypatch):
     """A crop's output must not depend on its batch position or the batch size

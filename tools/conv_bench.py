@@ -1,5 +1,5 @@
 """Per-plane BasicBlock timing (two 3x3 convs + residual) at the bench batch, per
-conv kernel family (generic conv_mfma_kernel, wsconv, tconv).  HIP events on
+conv kernel family (generic conv_mfma_kernel, tconv / tconv16).  HIP events on
 torch's stream.
   python tools/conv_bench.py [batch] [reps]"""
 import os
@@ -13,11 +13,8 @@ from mvpose import hrnet  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_WSCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
-MODES = {"generic": dict(_OFF), "wsconv": dict(_OFF, MVPOSE_NO_WSCONV="0"),
-         "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0")}
-os.environ["MVPOSE_WSCONV64"] = "1"
-os.environ["MVPOSE_TCONV128"] = "1"
+_OFF = {"MVPOSE_NO_TCONV": "1", "MVPOSE_NO_TBLOCK": "1"}
+MODES = {"generic": dict(_OFF), "tconv": dict(_OFF, MVPOSE_NO_TCONV="0", MVPOSE_NO_TBLOCK="0")}
 for c, h, w in [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6), (64, 64, 48)]:
     for mode, env in MODES.items():
         os.environ.update(env)

@@ -1,12 +1,11 @@
 """Run one BasicBlock plane a few times (for rocprofv3 counter passes).
-  python tools/conv_one.py C H W [ws 0|1] [batch] [reps]"""
+  python tools/conv_one.py C H W [unused] [batch] [reps]"""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd"))
 c, h, w = (int(v) for v in sys.argv[1:4])
-os.environ["MVPOSE_NO_WSCONV"] = "0" if (len(sys.argv) <= 4 or sys.argv[4] == "1") else "1"
 n = int(sys.argv[5]) if len(sys.argv) > 5 else 1024
 reps = int(sys.argv[6]) if len(sys.argv) > 6 else 3
 import torch  # noqa: E402
