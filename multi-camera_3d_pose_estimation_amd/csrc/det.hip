@@ -1071,29 +1071,16 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const int pad = ks / 2;
     const int Ho = (H + 2 * pad - ks) / stride + 1, Wo = (W + 2 * pad - ks) / stride + 1;
     const int npad = det_cout_pad(N);
-    static const int bn_max = [] {
-        const char* e = getenv("MVPOSE_DET_BN");  // tuning: the widest cout tile (192 default; 96: more workgroups per CU)
-        return e ? atoi(e) : 192;
-    }();
-    const int bn = npad % 192 == 0 && bn_max >= 192   ? 192
-                   : npad % 128 == 0 && bn_max >= 128 ? 128
-                   : npad % 96 == 0 && bn_max >= 96   ? 96
-                   : npad % 64 == 0                   ? 64
-                                                      : 32;
+    // cout tile: the widest of 192 / 128 / 96 / 64 dividing the padded couts.  Measured
+    // alternatives, all slower on RTMDet-m (profiles/r03detcfg.txt, 128 frames, same box):
+    // 128-cout tiles 27.2-27.5 vs 25.9 ms, 256-pixel tiles of 8 waves 27.7, of 4 waves 32.6,
+    // a 4-slot ring level; removed with their environment switches in round 3.
+    const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo, wimg};
-    // halo-tile kernel for the 32-channel 3x3/s1 convs: 14.03 -> 13.77 ms per 64 frames
-    // (same-box tools/det_ab.sh); MVPOSE_DET_HALO=0 keeps the im2col GEMM for them
-    static const bool halo_env = [] {
-        const char* e = getenv("MVPOSE_DET_HALO");
-        return !(e && e[0] == '0');
-    }();
-    static const bool halo64 = [] {
-        // also the 64-channel convs (2 chunk phases): 13.90 -> 13.86 ms per 64 frames; =0 disables
-        const char* e = getenv("MVPOSE_DET_HALO64");
-        return !(e && e[0] == '0');
-    }();
-    if (halo_env && ks == 3 && stride == 1 && (cin == 32 || (cin == 64 && halo64)) && npad <= 64) {
+    // halo-tile kernel for the 32- and 64-channel 3x3/s1 convs (<= 64 couts): 14.03 -> 13.77
+    // and 13.90 -> 13.86 ms per 64 frames against the im2col GEMM (same-box tools/det_ab.sh)
+    if (ks == 3 && stride == 1 && (cin == 32 || cin == 64) && npad <= 64) {
         const long tiles = (long)n * ((H + 1) / 2) * ((W + 63) / 64);
         MVP_REQUIRE(tiles < (1L << 31), "det conv: grid too large");
         if (tiles == 0) return;
@@ -1108,56 +1095,23 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
         MVP_HIP(hipGetLastError());
         return;
     }
-    static const int cps = [] {
-        const char* e = getenv("MVPOSE_DET_CPS");  // tuning: K chunks per barrier (1: 3-slot ring, 2: 2-slot)
-        return e && atoi(e) == 2 ? 2 : 1;
-    }();
-    static const int pw_env = [] {
-        const char* e = getenv("MVPOSE_DET_PW");  // tuning: 4 = 256-pixel tiles (8 waves) for >= 96 couts
-        return e && atoi(e) == 4 ? 4 : 2;
-    }();
-    const int pw = bn >= 96 ? pw_env : 2;
-    static const int fp = [] {
-        const char* e = getenv("MVPOSE_DET_FP");  // tuning: 8 = 256-pixel tiles of 4 waves (128 px each)
-        return e && atoi(e) == 8 ? 8 : 4;
-    }();
-    const int px = fp == 8 && bn >= 96 ? 256 : 64 * pw;
-    static const int ring = [] {
-        // tuning: LDS ring slots (2: three workgroups per CU; 4: three K steps in flight)
-        const char* e = getenv("MVPOSE_DET_RING");
-        return e ? atoi(e) : 3;
-    }();
-    const long blocks = (p.M + px - 1) / px * p.n_nb;
+    constexpr int kPx = 128;  // pixels per tile: 2 pixel waves x 4 fragments of 16
+    const long blocks = (p.M + kPx - 1) / kPx * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
-    const dim3 g((unsigned)blocks), t(128 * pw);
-#define MVP_DET_CONV_LAUNCH(BN, KS, S)                                                           \
-    do {                                                                                        \
-        if (px == 256 && pw == 2)                                                               \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3, 1, 8>), g, t, 0, s, p);  \
-        else if (pw == 4)                                                                       \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 4, 3, 1>), g, t, 0, s, p);     \
-        else if (ring == 2)                                                                     \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 1>), g, t, 0, s, p);     \
-        else if (ring == 4)                                                                     \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 4, 1>), g, t, 0, s, p);     \
-        else if (cps == 2)                                                                      \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 2, 2>), g, t, 0, s, p);     \
-        else                                                                                    \
-            hipLaunchKernelGGL((det_conv_gemm_kernel<BN, KS, S, 2, 3, 1>), g, t, 0, s, p);     \
-    } while (0)
-#define MVP_DET_CONV_BN(KS, S)              \
-    do {                                    \
-        if (bn == 192)                      \
-            MVP_DET_CONV_LAUNCH(192, KS, S); \
-        else if (bn == 128)                 \
-            MVP_DET_CONV_LAUNCH(128, KS, S); \
-        else if (bn == 96)                  \
-            MVP_DET_CONV_LAUNCH(96, KS, S);  \
-        else if (bn == 64)                  \
-            MVP_DET_CONV_LAUNCH(64, KS, S);  \
-        else                                \
-            MVP_DET_CONV_LAUNCH(32, KS, S);  \
+    const dim3 g((unsigned)blocks), t(256);
+#define MVP_DET_CONV_BN(KS, S)                                                                         \
+    do {                                                                                              \
+        if (bn == 192)                                                                                \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<192, KS, S, 2, 3, 1>), g, t, 0, s, p);          \
+        else if (bn == 128)                                                                           \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<128, KS, S, 2, 3, 1>), g, t, 0, s, p);          \
+        else if (bn == 96)                                                                            \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<96, KS, S, 2, 3, 1>), g, t, 0, s, p);           \
+        else if (bn == 64)                                                                            \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<64, KS, S, 2, 3, 1>), g, t, 0, s, p);           \
+        else                                                                                          \
+            hipLaunchKernelGGL((det_conv_gemm_kernel<32, KS, S, 2, 3, 1>), g, t, 0, s, p);           \
     } while (0)
     if (ks == 1)
         MVP_DET_CONV_BN(1, 1);
@@ -1166,7 +1120,6 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     else
         MVP_DET_CONV_BN(3, 2);
 #undef MVP_DET_CONV_BN
-#undef MVP_DET_CONV_LAUNCH
     MVP_HIP(hipGetLastError());
 }
 
