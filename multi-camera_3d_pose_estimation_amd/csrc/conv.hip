@@ -497,17 +497,6 @@ void launch_cfg(const ConvParams& p0, hipStream_t s) {
         }
     }
     MVP_REQUIRE(best > 0, "conv: LDS %d B over budget", C::lds_bytes(p.wmode, n_chunks, 2));
-    static const int force = [] {
-        const char* e = getenv("MVPOSE_CONV_RING");  // tuning experiments only
-        return e ? atoi(e) : 0;
-    }();
-    if (force >= 2 && force <= 4 && C::lds_bytes(p.wmode, n_chunks, force) <= kLdsMax && force != best) {
-        best = force;
-        best_lds = C::lds_bytes(p.wmode, n_chunks, force);
-        best_bpc = force == 2   ? blocks_per_cu<KS, S, BM, TH, TW, NB, 2, NW>(best_lds)
-                   : force == 3 ? blocks_per_cu<KS, S, BM, TH, TW, NB, 3, NW>(best_lds)
-                                : blocks_per_cu<KS, S, BM, TH, TW, NB, 4, NW>(best_lds);
-    }
     if (best == 2)
         launch_ring<KS, S, BM, TH, TW, NB, 2, NW>(p, best_lds, best_bpc, s);
     else if (best == 3)
@@ -522,11 +511,6 @@ template <int KS, int S, int TH, int TW, int NB, int NW>
 void launch_tile(const ConvParams& p, hipStream_t s) {
     const int n_chunks = p.Cin / 32;
     if (p.Cout_pad == 32) return launch_cfg<KS, S, 32, TH, TW, NB, NW>(p, s);
-    static const bool bm64 = [] {
-        const char* e = getenv("MVPOSE_CONV_BM64");  // tuning experiments: streamed 64-cout tiles
-        return e && e[0] == '1';
-    }();
-    if (bm64) return launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
     if (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
         return launch_cfg<KS, S, 64, TH, TW, NB, NW>(p, s);
     if (ConvCfg<KS, S, 32, TH, TW, NB, NW>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
@@ -540,10 +524,6 @@ void launch_tile(const ConvParams& p, hipStream_t s) {
 // workgroup of two waves per SIMD sharing the resident weights.
 template <int KS, int S, int TH, int TW, int NB, int TH8, int TW8, int NB8>
 void launch_tile2(const ConvParams& p, hipStream_t s) {
-    static const int nw_env = [] {
-        const char* e = getenv("MVPOSE_CONV_WAVES");  // tuning experiments only: 4 or 8
-        return e ? atoi(e) : 0;
-    }();
     const int n_chunks = p.Cin / 32;
     const int bm = p.Cout_pad == 32                                                               ? 32
                    : (n_chunks == 1 || ConvCfg<KS, S, 64, TH, TW, NB>::lds_bytes(WM_RESIDENT, n_chunks, 2) <= kLdsMax)
@@ -552,7 +532,7 @@ void launch_tile2(const ConvParams& p, hipStream_t s) {
                                                                                                     : 64;
     const int blocks4 = bm == 32 ? lds_blocks<KS, S, 32, TH, TW, NB, 4>(n_chunks)
                                  : lds_blocks<KS, S, 64, TH, TW, NB, 4>(n_chunks);
-    const bool eight = nw_env == 8 || (nw_env != 4 && blocks4 < 2);
+    const bool eight = blocks4 < 2;
     if (eight)
         launch_tile<KS, S, TH8, TW8, NB8, 8>(p, s);
     else
@@ -571,18 +551,8 @@ void launch_plane(const ConvParams& p, hipStream_t s) {
             launch_tile2<KS, S, 16, 12, 1, 16, 12, 2>(p, s);
         else if (p.Wo == 6 && p.Ho == 8)
             launch_tile2<KS, S, 8, 6, 4, 8, 6, 8>(p, s);
-        else {
-            static const int t3 = [] {
-                const char* e = getenv("MVPOSE_DET_TILE3");  // tuning experiments (detector planes)
-                return e ? atoi(e) : 0;
-            }();
-            if (t3 == 8)
-                launch_tile<KS, S, 8, 16, 1, 8>(p, s);
-            else if (t3 == 2)
-                launch_tile2<KS, S, 4, 16, 1, 8, 16, 1>(p, s);
-            else
-                launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
-        }
+        else
+            launch_tile<KS, S, 4, 16, 1, 4>(p, s);  // generic masked tiling
     } else {
         const char* e = getenv("MVPOSE_S2_TILE");  // tuning experiments only
         const int v = e ? atoi(e) : 0;  // 7: the pre-sweep 4-wave default
@@ -758,43 +728,9 @@ struct FuseParams {
     int H, W, C, lgc, relu;
 };
 
-__global__ __launch_bounds__(256) void fuse_sum_kernel(FuseParams p) {
-    const int i = blockIdx.x * 256 + threadIdx.x;  // (pixel, chunk) within crop n
-    const int n = blockIdx.y;
-    const int hw = p.H * p.W;
-    if (i >= (hw << p.lgc)) return;
-    const int ch = i & ((1 << p.lgc) - 1);
-    const int pix = i >> p.lgc;
-    const int h = (int)((unsigned)pix / (unsigned)p.W), w = pix - h * p.W;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < p.n_in; k++) {
-        const int lg = p.lg[k];
-        const int hs = p.H >> lg, ws = p.W >> lg;
-        const long src = ((long)n * hs * ws + (h >> lg) * ws + (w >> lg)) * p.C + ch * 8;
-        const uint4 v = *reinterpret_cast<const uint4*>(p.in[k] + src);
-        acc[0] += bf16_to_f32(v.x & 0xffff);
-        acc[1] += bf16_to_f32(v.x >> 16);
-        acc[2] += bf16_to_f32(v.y & 0xffff);
-        acc[3] += bf16_to_f32(v.y >> 16);
-        acc[4] += bf16_to_f32(v.z & 0xffff);
-        acc[5] += bf16_to_f32(v.z >> 16);
-        acc[6] += bf16_to_f32(v.w & 0xffff);
-        acc[7] += bf16_to_f32(v.w >> 16);
-    }
-    if (p.relu)
-#pragma unroll
-        for (int q = 0; q < 8; q++) acc[q] = fmaxf(acc[q], 0.f);
-    uint4 o;
-    o.x = (uint32_t)f32_to_bf16(acc[0]) | ((uint32_t)f32_to_bf16(acc[1]) << 16);
-    o.y = (uint32_t)f32_to_bf16(acc[2]) | ((uint32_t)f32_to_bf16(acc[3]) << 16);
-    o.z = (uint32_t)f32_to_bf16(acc[4]) | ((uint32_t)f32_to_bf16(acc[5]) << 16);
-    o.w = (uint32_t)f32_to_bf16(acc[6]) | ((uint32_t)f32_to_bf16(acc[7]) << 16);
-    *reinterpret_cast<uint4*>(p.out + ((long)n * hw + pix) * p.C + ch * 8) = o;
-}
-
-// the same with the input count a template parameter: all NI 16-B loads issue before the
-// first sum (the runtime-count loop waited for each load in turn); sums in input order, so
-// bit-identical to fuse_sum_kernel
+// out = relu(sum_k up(in_k)) per 16-B chunk, the input count a template parameter: all NI
+// 16-B loads issue before the first sum (a runtime-count loop waited for each load in turn:
+// +0.45 % frames/s, round 2); sums in input order
 template <int NI>
 __global__ __launch_bounds__(256) void fuse_sum_n_kernel(FuseParams p) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -951,13 +887,7 @@ void launch_fuse_sum(const uint16_t* const* in, const int* up, int n_in, uint16_
     MVP_REQUIRE(per < (1L << 30) && N < 65536, "fuse: plane too large");
     if (per == 0 || N == 0) return;
     const dim3 g((unsigned)((per + 255) / 256), (unsigned)N);
-    static const bool loop = [] {
-        const char* e = getenv("MVPOSE_FUSE_LOOP");  // A/B: 1 = the runtime-count loop kernel
-        return e && e[0] == '1';
-    }();
-    if (loop)
-        hipLaunchKernelGGL(fuse_sum_kernel, g, dim3(256), 0, s, p);
-    else if (n_in == 1)
+    if (n_in == 1)
         hipLaunchKernelGGL(fuse_sum_n_kernel<1>, g, dim3(256), 0, s, p);
     else if (n_in == 2)
         hipLaunchKernelGGL(fuse_sum_n_kernel<2>, g, dim3(256), 0, s, p);

@@ -573,23 +573,16 @@ void launch_conv1x1_pair(const PairLaunch& c, hipStream_t s) {
         const long grid = std::min<long>((long)g_cus1 * pc, (units + kPairThreads / 64 - 1) / (kPairThreads / 64));
         hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(kPairThreads), lds, s, p);
     };
-    // look-ahead depth (MVPOSE_PAIR_LA, diagnostics): units in flight per wave
-    static int la = -1;
-    if (la < 0) {
-        const char* e = getenv("MVPOSE_PAIR_LA");
-        la = e ? atoi(e) : 0;
-    }
+    // look-ahead depth (units in flight per wave) as measured best per join: 64-ch 1 (1,496 vs
+    // 1,575 us per join graph with 2), the cat-fused 128-ch join 3
     MVP_REQUIRE(c.res || c.x2, "conv1x1_pair: a join without residual must be cat-fused");
     if (cin == 64) {
         MVP_REQUIRE(c.res != nullptr, "conv1x1_pair: 64-ch join needs its residual");
-        if (la == 2) go(conv1x1_pair_kernel<2, true, 2>, 2);
-        else go(conv1x1_pair_kernel<2, true, 1>, 2);  // 1496 vs 1575 us per join graph (LA 2)
+        go(conv1x1_pair_kernel<2, true, 1>, 2);
     } else if (c.res) {
         go(conv1x1_pair_kernel<4, true, 1>, 4);
     } else {
-        if (la == 1) go(conv1x1_pair_kernel<4, false, 1>, 4);
-        else if (la == 2) go(conv1x1_pair_kernel<4, false, 2>, 4);
-        else go(conv1x1_pair_kernel<4, false, 3>, 4);
+        go(conv1x1_pair_kernel<4, false, 3>, 4);
     }
     MVP_HIP(hipGetLastError());
 }

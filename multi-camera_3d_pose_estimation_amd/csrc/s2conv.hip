@@ -281,14 +281,6 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
 int g_s_cus = 0;
 uint16_t* g_s_sink = nullptr;
 
-bool s2_pm() {
-    static const bool pm = [] {
-        const char* e = getenv("MVPOSE_S2_PM");  // A/B: 0 = plane-major halo (PM measured +0.7 % frames/s)
-        return !(e && e[0] == '0');
-    }();
-    return pm;
-}
-
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM, bool PM>
 void launch_sp_pm(SParams p, hipStream_t s) {
     using G = SCfg<CIN, H, W, TH, NB, WRES, BM, PM>;
@@ -302,12 +294,10 @@ void launch_sp_pm(SParams p, hipStream_t s) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(G::NT_THREADS), G::LDS, s, p);
 }
 
+// the pixel-major halo (+0.7 % frames/s over plane-major, round 2)
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>
 void launch_sp(SParams p, hipStream_t s) {
-    if (s2_pm())
-        launch_sp_pm<CIN, H, W, TH, NB, WRES, BM, true>(p, s);
-    else
-        launch_sp_pm<CIN, H, W, TH, NB, WRES, BM, false>(p, s);
+    launch_sp_pm<CIN, H, W, TH, NB, WRES, BM, true>(p, s);
 }
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, int BM>

@@ -348,25 +348,13 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
     const char* dg = getenv("MVPOSE_TCONV_DIAG");
     TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM,
               dg ? atoi(dg) : 0};
-    // pixel-major halo wherever its 25 % larger ring slot still fits the LDS
-    static const bool pm_env = [] {
-        const char* e = getenv("MVPOSE_TCONV_PM");  // A/B: 0 = plane-major halo everywhere
-        return !(e && e[0] == '0');
-    }();
-    constexpr bool PM_OK = TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
-    if constexpr (PM_OK) {
-        if (pm_env) {
-            if (c.res)
-                launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM, true>(p, s);
-            else
-                launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM, true>(p, s);
-            return;
-        }
-    }
+    // pixel-major halo wherever its 25 % larger ring slot still fits the LDS (+2.4-2.9 %
+    // frames/s on the 64- and 256-ch planes, round 2), plane-major otherwise
+    constexpr bool PM = TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;
     if (c.res)
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM, false>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, true, BM, PM>(p, s);
     else
-        launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM, false>(p, s);
+        launch_t_kernel<CIN, H, W, TH, NB, WRES, false, BM, PM>(p, s);
 }
 
 }  // namespace

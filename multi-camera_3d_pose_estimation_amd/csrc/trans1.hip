@@ -285,8 +285,6 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     if (!attr) {
         MVP_HIP(hipFuncSetAttribute((const void*)trans1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     T1C<true>::LDS));
-        MVP_HIP(hipFuncSetAttribute((const void*)trans1_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    T1C<false>::LDS));
         attr = true;
     }
     if (g_tr_cus == 0) {
@@ -298,14 +296,8 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     MVP_REQUIRE(tiles * T1C<true>::NCH < (1L << 30), "trans1: too many tiles");
     TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles, wimg};
     const int grid = (int)std::min<long>(tiles, g_tr_cus);
-    static const bool pm = [] {
-        const char* e = getenv("MVPOSE_TRANS1_PM");  // A/B: 0 = plane-major halo
-        return !(e && e[0] == '0');
-    }();
-    if (pm)
-        hipLaunchKernelGGL(trans1_kernel<true>, dim3(grid), dim3(T1C<true>::NTH), T1C<true>::LDS, s, p);
-    else
-        hipLaunchKernelGGL(trans1_kernel<false>, dim3(grid), dim3(T1C<false>::NTH), T1C<false>::LDS, s, p);
+    // pixel-major halo (+0.4 % frames/s over plane-major, round 2)
+    hipLaunchKernelGGL(trans1_kernel<true>, dim3(grid), dim3(T1C<true>::NTH), T1C<true>::LDS, s, p);
     MVP_HIP(hipGetLastError());
 }
 
