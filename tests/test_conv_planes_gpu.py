@@ -141,6 +141,24 @@ def test_tblock32s_bitwise_equals_tile_kernel(n, monkeypatch):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("c,h,w,n", [(128, 16, 12, 1), (128, 16, 12, 1100), (256, 8, 6, 5), (256, 8, 6, 2100)])
+def test_tconv16_tile_ranges_vs_reference(c, h, w, n, monkeypatch):
+    """tconv16.hip at batch sizes the 37-crop test does not reach: one crop (a single tile,
+    seven empty XCD slots of its group of 8), and batches whose tiles outnumber the CUs so
+    that each workgroup loops over several tiles (2100 crops of the 256-ch plane: its two
+    128-cout blocks on a fixed cout block per workgroup, XCD-major tile order)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    got, ref = _run(c, h, w, n, 1, 21, monkeypatch, "tconv")
+    assert torch.isfinite(got).all()
+    rel = (torch.linalg.vector_norm(got - ref) / torch.linalg.vector_norm(ref)).item()
+    mx = (got - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    print(f"tconv16 C={c} {h}x{w} n={n}: rel L2 {rel:.2e}, max abs {mx:.3e} (max|ref| {scale:.2f})")
+    assert rel <= 4e-3
+    assert mx <= 3 * scale * 2.0 ** -8
+
+
 @pytest.mark.parametrize("mode", ["generic", "tconv", "tconv64"])
 @pytest.mark.parametrize("c,h,w", [(32, 64, 48), (64, 32, 24), (128, 16, 12), (256, 8, 6)])
 def test_batch_positions(c, h, w, mode, monkeypatch):
