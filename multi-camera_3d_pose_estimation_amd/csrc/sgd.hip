@@ -112,8 +112,10 @@ __device__ __forceinline__ void project_adjoint(const float* __restrict__ c, con
     const float* K = c;
     const float* R = c + 9;
     const float* d = c + 21;
-    // (u, v) = (h0, h1) / h2, h = K·[xd, yd, 1]
-    const float ih2 = 1.f / o.h2;
+    // (u, v) = (h0, h1) / h2, h = K·[xd, yd, 1].  The adjoint's reciprocals are v_rcp_f32
+    // (1 ulp): only the forward value needs torch's correctly rounded divisions, the gradient
+    // already differs from autograd's by f32 summation order (an IEEE 1/x is ~10 VALU ops)
+    const float ih2 = __builtin_amdgcn_rcpf(o.h2);
     const float gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
     const float gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
     float gx = gxd, gy = gyd;
@@ -128,7 +130,7 @@ __device__ __forceinline__ void project_adjoint(const float* __restrict__ c, con
         gy = dxy * gxd + dyy * gyd;
     }
     // x = P0/P2, y = P1/P2, P = R·X + T
-    const float iP2 = 1.f / o.P2;
+    const float iP2 = __builtin_amdgcn_rcpf(o.P2);
     const float a = gx * iP2, b = gy * iP2, cz = -(gx * o.x + gy * o.y) * iP2;
     dP[0] = a;  // d/dP of the camera-frame point (the learnable extrinsics' chain)
     dP[1] = b;
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(kExtBlock) void extrinsic_grad_kernel(const float* 
             gx = dxx * gxd + dxy * gyd;
             gy = dxy * gxd + dyy * gyd;
         }
-        const float iP2 = 1.f / o.P2;
+        const float iP2 = __builtin_amdgcn_rcpf(o.P2);
         const float gp[3] = {gx * iP2, gy * iP2, -(gx * o.x + gy * o.y) * iP2};
         const float xs[3] = {X0, X1, X2};
         acc[0] += val;
