@@ -206,7 +206,9 @@ int mvp_graph_forward(void* handle, const void* input_dev, int batch, void* outp
 int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);
 /* The weight blobs passed to mvp_graph_create were rewritten in place (e.g. an RCCL
  * broadcast from rank 0 after every rank built its graph): re-derive every weight
- * the graph copied out of them at create time (cat-fused 1x1 weights / biases).
+ * the graph copied out of them at create time (cat-fused 1x1 weights / biases, the
+ * sibling-fused 3x3/s2 weights, and the slot-order weight images of the 128/256-channel
+ * branch planes, the streamed-weight 3x3/s2 convs and transition1).
  * Blocking (device-synchronising). */
 int mvp_graph_refresh_weights(void* handle);
 int mvp_graph_destroy(void* handle);
