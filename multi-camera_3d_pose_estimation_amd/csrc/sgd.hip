@@ -66,6 +66,16 @@ struct Proj {
     float xd, yd;
 };
 
+// a / b for finite normal operands: one v_rcp_f32 and a Markstein correction step
+// (q = a·r, e = a − q·b, q + e·r): the correctly rounded quotient except in rare
+// double-rounding cases (≤ 1 ulp), 4 VALU operations against ~10 for the IEEE sequence
+__device__ __forceinline__ float div_fast(float a, float b) {
+    const float r = __builtin_amdgcn_rcpf(b);
+    const float q = a * r;
+    const float e = __builtin_fmaf(-q, b, a);
+    return __builtin_fmaf(e, r, q);
+}
+
 // project_points_torch (pose_refinement.py:118-177) for one point, torch op order.
 __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, float X1, float X2, bool ign) {
     const float* K = c;
@@ -77,8 +87,8 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
     const float P1 = X0 * R[3] + X1 * R[4] + X2 * R[5] + T[1];
     const float P2 = X0 * R[6] + X1 * R[7] + X2 * R[8] + T[2];
     o.P2 = P2;
-    o.x = P0 / P2;
-    o.y = P1 / P2;
+    o.x = div_fast(P0, P2);
+    o.y = div_fast(P1, P2);
     if (!ign) {
         const float x = o.x, y = o.y;
         const float r2 = x * x + y * y;
@@ -101,8 +111,8 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
     const float h1 = o.xd * K[3] + o.yd * K[4] + K[5];
     const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
     o.h2 = h2;
-    o.u = h0 / h2;
-    o.v = h1 / h2;
+    o.u = div_fast(h0, h2);
+    o.v = div_fast(h1, h2);
     return o;
 }
 
