@@ -340,7 +340,7 @@ def ingest_line(est, V, n_frames=512, batch=128):
                     "moments on the compute stream (2D stage only, serial moments)"}
 
 
-def detector_line(dev, est, cams_params, V, batch=128, reps=5):
+def detector_line(dev, est, cams_params, V, batch=None, reps=5):
     """the person detector the reference runs on every camera-frame
     (RTMDet-m, mmpose_pose_estimation.py:234-250), alone (letterbox -> graph -> per-frame
     selection, HIP events on the launch stream) and in front of the 2D->3D pipeline
@@ -349,6 +349,10 @@ def detector_line(dev, est, cams_params, V, batch=128, reps=5):
     camera-frame (38.94 GMAC)."""
     from mvpose.pipeline import MultiViewPipeline
     from mvpose.rtmdet import RTMDetector
+    # one detector forward per process() call: the whole step's camera-frames (512; 9.4 GiB of
+    # activation arena).  tools/det_bench.py: 4,980 camera-frames/s at 128 per forward, 5,160 at
+    # 256, 5,220 at 512 — the last round of workgroups of each conv fills more of the GPU
+    batch = batch or est.max_frames
     det = RTMDetector(seed=0, max_batch=batch, device=dev)
     g = torch.Generator(device=dev).manual_seed(99)
     fr = torch.randint(0, 256, (batch, 720, 1280, 3), dtype=torch.uint8, device=dev, generator=g)
@@ -366,7 +370,7 @@ def detector_line(dev, est, cams_params, V, batch=128, reps=5):
     tf = flops / (ms * 1e-3) / 1e12
     pipe = MultiViewPipeline(cams_params, estimator=est, device=dev, detector=det)
     # the pipeline at the headline batch (est.max_frames camera-frames: 256 2-cam frames, the
-    # detector in max_batch chunks); the same 128 frames tiled, a fresh generator for the rest
+    # detector in max_batch chunks)
     n_pipe = est.max_frames
     fr_p = fr.repeat((n_pipe + batch - 1) // batch, 1, 1, 1)[:n_pipe]
     fr2 = fr_p.reshape(n_pipe // V, V, 720, 1280, 3)
