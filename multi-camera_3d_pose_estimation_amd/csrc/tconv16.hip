@@ -168,7 +168,9 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
             const int g = pk[j], kind = g >> 29, nb = (g >> 24) & 31, hy = (g >> 19) & 31, off = g & 0x7ffff;
             const bool in = kind == 1 && (unsigned)(ho0 + hy - 1) < (unsigned)H && n0 + nb < p.N;
             const uint16_t* src = kind == 2 ? wb + off : in ? xb + off : zl;
-            glds16(src, dst + (j * G::NW + wave) * 1024);
+            // pieces wholly past the item's slots (6 of 64 on the 128-ch plane) are not issued
+            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::HT + G::WT)
+                glds16(src, dst + (j * G::NW + wave) * 1024);
         }
     };
 
@@ -267,7 +269,9 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
         }
 
         if (last && do_st) {
-            if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
+            // the residual loads precede this item's DMA pieces (PPW, or PPW - 1 on the waves whose
+            // last piece is past the item): wait for all but PPW - 1 of them
+            if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW - 1) : "memory");
 #pragma unroll
             for (int a = 0; a < G::NA; a++)
 #pragma unroll
