@@ -154,7 +154,9 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
             const int g = pk[j], kind = g >> 28, nb = (g >> 8) & 255, hy = g & 255;
             const bool in = kind == 1 && (unsigned)(2 * ho0 + hy - 1) < (unsigned)H && n0 + nb < p.N;
             const uint16_t* src = (!WRES && kind == 2) ? wb + po[j] : in ? xb + po[j] : zl;
-            glds16(src, dst + (j * G::NW + wave) * 1024);
+            // pieces wholly past the item's slots are not issued (the 128->256 plane: 4 of 72)
+            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::ITEM_SLOTS)
+                glds16(src, dst + (j * G::NW + wave) * 1024);
         }
     };
 

@@ -130,7 +130,9 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
             const int kind = pk[j] >> 8, hy = pk[j] & 255;
             const bool in = kind == 1 && (unsigned)(r0 - 1 + hy) < (unsigned)G::H;
             const uint16_t* src = kind == 2 ? wbase + po[j] : in ? xb + po[j] : zl;
-            glds16(src, dst + (j * G::NW + wave) * 1024);
+            // pieces wholly past the item's slots are not issued (3 of 72)
+            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::ITEM)
+                glds16(src, dst + (j * G::NW + wave) * 1024);
         }
     };
 
