@@ -31,6 +31,7 @@ TRI_T = 1_000_000           # frames per triangulation-roofline launch: 612 MB (
                             # per launch, well past the 256 MiB Infinity Cache -> an HBM measurement
 SGD_V, SGD_T, SGD_M = 8, 400, 256   # BASELINE config 5 (V=8, T=400); M trajectories per launch
 SGD_ITERS = 40
+SGD_BENCH_ATOL = 2e-4      # cm, final trajectory vs the reference after 40 Adam iterations
 # FP32 FLOP per (frame, camera, joint) projection + likelihood forward + adjoint in sgd_kernel
 # (csrc/sgd.hip project / quad_cost / project_adjoint, distortion on, counted by hand: DESIGN.md
 # §4) and per trajectory coordinate (stencil + segment adjoints + Adam)
@@ -211,20 +212,16 @@ def sgd_line(dev):
     (pose_refinement.py:894-1096), SGD_M trajectories per launch (one workgroup each), a fixed
     SGD_ITERS iterations (early stop disabled).  Outside the timed region of the headline."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from mvpose import refine, synthetic as syn
-    rng = np.random.default_rng(5)
-    cams = syn.make_rig(SGD_V, seed=5)
-    poses = syn.make_poses(SGD_T, seed=6)
-    g = np.zeros((SGD_T, SGD_V, 17, 6))
-    for v, c in enumerate(cams):
-        g[:, v, :, 0:2] = syn.project(poses, c) + rng.normal(0, 2.0, (SGD_T, 17, 2))
-        g[:, v, :, 2] = g[:, v, :, 5] = 9.0
-    x0 = (poses + rng.normal(0, 3.0, poses.shape)).astype(np.float32)
+    from mvpose import refine
+    from sgd_problem import BENCH_C5_ITERS, BENCH_C5_KW, bench_c5_inputs, inputs_digest
+    cams, g, x0 = bench_c5_inputs(SGD_V, SGD_T)
+    ref = np.load(os.path.join(ROOT, "tests", "golden", "bench_sgd_c5.npz"))
+    assert str(ref["digest"]) == inputs_digest(cams, g, x0), "bench SGD problem drifted from its golden"
+    assert BENCH_C5_ITERS == SGD_ITERS
     with open(os.path.join(ROOT, "tests", "golden", "body_part_lengths.json")) as f:
         lengths = json.load(f)["my_lengths"]
     camlist = [[c["K"], c["R"], c["T"], c["dist"]] for c in cams]
-    kw = dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=10 ** 9, tolerance=1e-5,
-              max_iter=SGD_ITERS - 1, body_lengths=dict(lengths), device=dev)
+    kw = dict(BENCH_C5_KW, body_lengths=dict(lengths), device=dev)
     res = {}
     for M in (1, SGD_M):
         G = torch.tensor(np.broadcast_to(g, (M,) + g.shape).copy(), device=dev)
@@ -237,11 +234,18 @@ def sgd_line(dev):
         e1.record(s)
         torch.cuda.synchronize()
         assert int(r["iters"].min()) == SGD_ITERS, r["iters"]
+        # parity against the reference's own run of this problem (tests/golden/bench_sgd_c5.npz,
+        # pose_refinement.sgd_optimize): every trajectory of the launch within SGD_BENCH_ATOL cm
+        dev_max = float((r["final"] - torch.tensor(ref["final"], device=dev)).abs().max())
+        assert dev_max <= SGD_BENCH_ATOL, (M, dev_max)
         res[M] = e0.elapsed_time(e1) / SGD_ITERS
+        res[f"dev{M}"] = dev_max
     flop_iter = SGD_T * 17 * (SGD_V * SGD_FLOP_PER_PROJ + 3 * SGD_FLOP_PER_COORD)
     tf = flop_iter * SGD_M / (res[SGD_M] * 1e-3) / 1e12
     return {"workload": f"BASELINE config 5: V={SGD_V}, T={SGD_T}, one window, {SGD_ITERS} Adam iterations, "
                         f"lr 0.01, lambda_s 1e-6, lambda_b 1 (early stop off)",
+            "parity": {"max_abs_cm_vs_reference": max(res["dev1"], res[f"dev{SGD_M}"]), "atol_cm": SGD_BENCH_ATOL,
+                       "reference": "tests/golden/bench_sgd_c5.npz (pose_refinement.sgd_optimize, same problem)"},
             "ms_per_iter_1traj": res[1], "ms_per_iter_M": res[SGD_M], "M": SGD_M,
             "trajectory_iterations_per_s": SGD_M / (res[SGD_M] * 1e-3),
             "roofline": {"bound": "fp32 valu", "achieved": tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",

@@ -86,6 +86,21 @@ int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double
                     float* out_xyz_dev, double* out_xyzw_dev, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * mvp_triangulate_points_f64 — replaces utils.triangulate_points (utils.py:1277-1336)
+ * called with float64 keypoints, as the extrinsic branch does on its Gaussian samples
+ * (pose_refinement.py:811): OpenCV keeps CV_64F through undistortPoints, triangulatePoints
+ * and convertPointsFromHomogeneous, so nothing is rounded to f32.
+ *
+ * kpts_dev : [n_points][2 views][2] float64 (the reference's (n_pts, 2, 2) layout).
+ * cams_dev : [2][MVP_CAM_DOUBLES] float64, camera 1 then camera 2; P (slots 26..37) as the
+ *            caller computed it (the reference's np.dot in the parameters' own dtype).
+ * out_xyz_dev  : [n_points][3] float64.  out_xyzw_dev: optional [n_points][4] float64.
+ * Exact JacobiSVDImpl_ restatement for every point.
+ * ------------------------------------------------------------------------- */
+int mvp_triangulate_points_f64(const double* kpts_dev, int64_t n_points, const double* cams_dev,
+                               double* out_xyz_dev, double* out_xyzw_dev, void* stream);
+
+/* ---------------------------------------------------------------------------
  * 2D stage around the backbone (replaces, per camera frame, what
  * PoseEstimator.predict gets from mmpose at mmpose_pose_estimation.py:253-267).
  *

@@ -42,14 +42,15 @@ struct CamIdx {
 
 // cvUndistortPointsInternal (OpenCV 4.9), R = I, P = K, 5 iterations, 5 coefficients.
 // The k4..k6 / thin-prism terms are zero and contribute exact zeros; they are
-// omitted (sign-of-zero differences cannot change the f32 result).
-__device__ __forceinline__ void undistort_point(float uf, float vf, const double* __restrict__ c,
-                                                float& ox, float& oy) {
+// omitted (sign-of-zero differences cannot change the result).  OpenCV computes in
+// double and stores into the source's depth: undistort_point rounds to f32 (CV_32FC2
+// keypoints, the pipeline), undistort_point_f64 keeps the double (CV_64FC2).
+__device__ __forceinline__ void undistort_point_f64(double u, double v, const double* __restrict__ c,
+                                                    double& ox, double& oy) {
     const double fx = c[0], fy = c[4];
     const double ifx = 1. / fx, ify = 1. / fy;
     const double cx = c[2], cy = c[5];
     const double k0 = c[9], k1 = c[10], k2 = c[11], k3 = c[12], k4 = c[13];
-    const double u = uf, v = vf;
     double x = (u - cx) * ifx;
     double y = (v - cy) * ify;
     const double x0 = x, y0 = y;
@@ -70,8 +71,16 @@ __device__ __forceinline__ void undistort_point(float uf, float vf, const double
     double xx = c[0] * x + c[1] * y + c[2];
     double yy = c[3] * x + c[4] * y + c[5];
     double ww = 1. / (c[6] * x + c[7] * y + c[8]);
-    ox = (float)(xx * ww);
-    oy = (float)(yy * ww);
+    ox = xx * ww;
+    oy = yy * ww;
+}
+
+__device__ __forceinline__ void undistort_point(float uf, float vf, const double* __restrict__ c,
+                                                float& ox, float& oy) {
+    double x, y;
+    undistort_point_f64(uf, vf, c, x, y);
+    ox = (float)x;
+    oy = (float)y;
 }
 
 // 1/b with the arithmetic of the compiler's IEEE fp64 division (v_div_scale,
@@ -373,9 +382,8 @@ __device__ __forceinline__ void write_result(const double (&nv)[4], int64_t p, f
     }
 }
 
-__device__ __forceinline__ void add_view_rows(double (*A)[4], int r, float ux, float uy,
+__device__ __forceinline__ void add_view_rows(double (*A)[4], int r, double x, double y,
                                               const double* __restrict__ P) {
-    const double x = ux, y = uy;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         A[r][k] = x * P[8 + k] - P[0 + k];
@@ -839,7 +847,10 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_fallback_kernel(
     if (cnt == 0) return;  // the usual case: nothing to re-solve, the count is already 0
     load_cams(scam, sfast, cams, n_cams);
     if (cnt <= (unsigned)kFbCap) {
-        for (unsigned i = threadIdx.x; i < cnt; i += kBlock) tol2_exact_point(kpts, fb.idx[i], V, scam, ci, out, out4);
+        for (unsigned i = threadIdx.x; i < cnt; i += kBlock) {
+            const unsigned p = fb.idx[i];
+            if ((int64_t)p < n) tol2_exact_point(kpts, p, V, scam, ci, out, out4);  // never write past this call's n
+        }
     } else {
         const unsigned* ob = reinterpret_cast<const unsigned*>(out);
         for (int64_t p = threadIdx.x; p < n; p += kBlock)
@@ -849,11 +860,60 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_fallback_kernel(
     if (threadIdx.x == 0) *fb.count = 0u;
 }
 
+// utils.triangulate_points (utils.py:1277-1336) on float64 keypoints, as the extrinsic
+// branch calls it on its Gaussian samples (pose_refinement.py:811): cv.undistortPoints keeps
+// CV_64F (no f32 rounding of the undistorted points), cv.triangulatePoints builds the same
+// fp64 A and writes a CV_64F points4D, cv.convertPointsFromHomogeneous divides in double
+// (scale = w != 0 ? 1./w : 1.).  kpts: (n, 2 views, 2) [point][view][x, y]; cams: the two
+// views' records (camera 1 first).  Exact Jacobi restatement for every point.
+__global__ __launch_bounds__(kBlock) void triangulate_pairs_f64_kernel(const double* __restrict__ kpts, int64_t n,
+                                                                       const double* __restrict__ cams,
+                                                                       double* __restrict__ out,
+                                                                       double* __restrict__ out4) {
+    __shared__ double scam[2][MVP_CAM_DOUBLES];
+    for (int i = threadIdx.x; i < 2 * MVP_CAM_DOUBLES; i += blockDim.x) scam[i / MVP_CAM_DOUBLES][i % MVP_CAM_DOUBLES] = cams[i];
+    __syncthreads();
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const double* k = kpts + 4 * p;
+    double E[4][4];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        double ex, ey;
+        undistort_point_f64(k[2 * q], k[2 * q + 1], scam[q], ex, ey);
+        add_view_rows(E, 2 * q, ex, ey, scam[q] + 26);
+    }
+    double At[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) At[c][r] = E[r][c];
+    double nv[4];
+    jacobi_null_vector<4>(At, nv);
+    const double w = nv[3];
+    const double s = (w != 0.) ? 1. / w : 1.;
+    out[3 * p + 0] = nv[0] * s;
+    out[3 * p + 1] = nv[1] * s;
+    out[3 * p + 2] = nv[2] * s;
+    if (out4) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) out4[4 * p + q] = nv[q];
+    }
+}
+
 // The tolerance kernel's fallback list, one per (device, stream), allocated on first use
-// (a stream-captured launch needs one uncaptured call on that stream first).
-FbList tol_fallback_list(hipStream_t s) {
+// (a stream-captured launch needs one uncaptured call on that stream first).  The list is
+// shared by every call on its stream, so a call holds the list's own mutex from the first
+// launch to the second: two host threads on one stream (PyTorch's default stream is shared)
+// then enqueue tol A, fallback A, tol B, fallback B, never tol A, tol B, fallback A, ...
+struct FbSlot {
+    FbList fb;
+    std::mutex* mu;
+};
+
+FbSlot tol_fallback_list(hipStream_t s) {
     static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, FbList> lists;
+    static std::map<std::pair<int, hipStream_t>, FbSlot> lists;
     int dev = 0;
     MVP_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lock(mu);
@@ -862,9 +922,9 @@ FbList tol_fallback_list(hipStream_t s) {
     unsigned* buf = nullptr;
     MVP_HIP(hipMalloc(&buf, (1 + (size_t)kFbCap) * sizeof(unsigned)));
     MVP_HIP(hipMemsetAsync(buf, 0, sizeof(unsigned), s));
-    const FbList fb{buf, buf + 1, 0};
-    lists[{dev, s}] = fb;
-    return fb;
+    const FbSlot slot{FbList{buf, buf + 1, 0}, new std::mutex};  // lives as long as the process
+    lists[{dev, s}] = slot;
+    return slot;
 }
 
 }  // namespace
@@ -899,7 +959,9 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
         MVP_REQUIRE(n_cam_idx <= n_cams, "mvp_triangulate: reference mode keys params by position: need "
                     "n_cam_idx <= n_cams");
         if (tol && n_cam_idx == 2 && n_points < (1LL << 32)) {
-            FbList fb = tol_fallback_list(s);
+            const FbSlot slot = tol_fallback_list(s);
+            std::lock_guard<std::mutex> call_lock(*slot.mu);
+            FbList fb = slot.fb;
             const char* ff = getenv("MVPOSE_TRI_FORCE_FALLBACK");  // tests: exercise the fallback list / sweep
             fb.force = ff && ff[0] == '1';
             const char* e = getenv("MVPOSE_TRI_F32");  // A/B: f32 undistortion iterations (3 or 4)
@@ -940,6 +1002,20 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
     } else {
         mvp::fail(MVP_ERR_ARG, "mvp_triangulate: unknown mode %d", mode);
     }
+    MVP_HIP(hipGetLastError());
+    MVP_ABI_END
+}
+
+extern "C" int mvp_triangulate_points_f64(const double* kpts_2d, int64_t n_points, const double* cams,
+                                          double* out_xyz, double* out_xyzw, void* stream) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(n_points >= 0, "mvp_triangulate_points_f64: n_points < 0");
+    if (n_points == 0) return MVP_OK;
+    MVP_REQUIRE(kpts_2d && cams && out_xyz, "mvp_triangulate_points_f64: null device pointer");
+    const int64_t blocks = (n_points + kBlock - 1) / kBlock;
+    MVP_REQUIRE(blocks < (1LL << 31), "mvp_triangulate_points_f64: too many points");
+    hipLaunchKernelGGL(triangulate_pairs_f64_kernel, dim3((unsigned)blocks), dim3(kBlock), 0,
+                       reinterpret_cast<hipStream_t>(stream), kpts_2d, n_points, cams, out_xyz, out_xyzw);
     MVP_HIP(hipGetLastError());
     MVP_ABI_END
 }

@@ -40,6 +40,7 @@ SIGNATURES = {
     "mvp_camera_pack": (c_int, [P(c_double), P(c_double), P(c_double), P(c_double), P(c_double)]),
     "mvp_triangulate": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, P(c_int), c_int, c_int,
                                 c_void_p, c_void_p, c_void_p]),
+    "mvp_triangulate_points_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mvp_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, P(c_float), P(c_float),
                                c_int, c_int, c_void_p, c_void_p]),
     "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,

@@ -43,7 +43,10 @@ def _require(t: torch.Tensor, dtype, name: str):
 
 def pack_camera(K, R, T, dist) -> np.ndarray:
     """One MVP_CAM_DOUBLES record: [K | dist | R | T | P | pad] with
-    P = np.dot(K, hstack(R, T)) exactly as reference utils.py:1318-1319."""
+    P = np.dot(K, hstack(R, T)) exactly as reference utils.py:1318-1319 — in the parameters'
+    own dtype (float32 camera tensors give the reference a float32 P, e.g. the extrinsic
+    branch's decomposed parameters, pose_refinement.py:808-811), stored as float64."""
+    P = np.dot(np.asarray(K), np.hstack((np.asarray(R), np.asarray(T).reshape(-1, 1))))
     K = np.asarray(K, dtype=np.float64).reshape(3, 3)
     R = np.asarray(R, dtype=np.float64).reshape(3, 3)
     T = np.asarray(T, dtype=np.float64).reshape(3, 1)
@@ -57,7 +60,7 @@ def pack_camera(K, R, T, dist) -> np.ndarray:
     rec[9:14] = d
     rec[14:23] = R.ravel()
     rec[23:26] = T.ravel()
-    rec[26:38] = np.dot(K, np.hstack((R, T))).ravel()
+    rec[26:38] = np.asarray(P, dtype=np.float64).ravel()
     return rec
 
 
@@ -106,4 +109,23 @@ def triangulate(kpts: torch.Tensor, cams: torch.Tensor, cam_idx: Sequence[int] =
     ci = (ctypes.c_int * len(cam_idx))(*[int(c) for c in cam_idx])
     call("mvp_triangulate", _ptr(kpts), n, V, _ptr(cams), cams.shape[0], ci, len(cam_idx), int(mode),
          _ptr(out), _ptr(xyzw) if xyzw is not None else None, _stream(kpts.device))
+    return (out, xyzw) if return_xyzw else out
+
+
+def triangulate_points_f64(kpts: torch.Tensor, cams: torch.Tensor, return_xyzw: bool = False):
+    """utils.triangulate_points on float64 keypoints (mvp_triangulate_points_f64): kpts
+    (..., 2, 2) float64 [view][x, y] on GPU, cams (2, 40) float64 (camera 1, camera 2) ->
+    (..., 3) float64, OpenCV's CV_64F semantics end to end."""
+    _require(kpts, torch.float64, "kpts")
+    _require(cams, torch.float64, "cams")
+    if kpts.dim() < 2 or tuple(kpts.shape[-2:]) != (2, 2):
+        raise ValueError(f"kpts must be (..., 2, 2), got {tuple(kpts.shape)}")
+    if tuple(cams.shape) != (2, CAM_DOUBLES):
+        raise ValueError(f"cams must be (2, {CAM_DOUBLES}), got {tuple(cams.shape)}")
+    lead = tuple(kpts.shape[:-2])
+    n = int(np.prod(lead)) if lead else 1
+    out = torch.empty(lead + (3,), dtype=torch.float64, device=kpts.device)
+    xyzw = torch.empty(lead + (4,), dtype=torch.float64, device=kpts.device) if return_xyzw else None
+    call("mvp_triangulate_points_f64", _ptr(kpts), n, _ptr(cams), _ptr(out),
+         _ptr(xyzw) if xyzw is not None else None, _stream(kpts.device))
     return (out, xyzw) if return_xyzw else out

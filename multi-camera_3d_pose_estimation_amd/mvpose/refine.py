@@ -476,16 +476,14 @@ class Optimized_3d_Pose_Estimation:
         samples = self.sample_gaussians(G, GT, N)                    # (T, J, N, 2, 2) f64
         self.samples = samples
         J = G.shape[2]
-        # construct_sample_cost: triangulate every sample with the GT pair (utils.triangulate_points)
-        kt = np.empty((T * J * N, 3, 2), np.float32)
-        flat = samples.reshape(-1, 2, 2)
-        kt[:, 0, :] = flat[:, :, 0]
-        kt[:, 1, :] = flat[:, :, 1]
-        kt[:, 2, :] = 1.0
+        # construct_sample_cost (:808-812): utils.triangulate_points on the float64 samples with the
+        # GT pair's float32 parameters — OpenCV keeps CV_64F throughout (mvp_triangulate_points_f64;
+        # P = np.dot in float32 as the reference computes it), then .to(float32)
         p1, p2 = self.decomposed_cam_params[GT[0]], self.decomposed_cam_params[GT[1]]
         pair = ops.pack_cameras([[p.detach().numpy() for p in (p1[0], p1[1], p1[2], p1[3])],
                                  [p.detach().numpy() for p in (p2[0], p2[1], p2[2], p2[3])]])
-        samples_3d = ops.triangulate(torch.from_numpy(kt).to(dev), torch.from_numpy(pair).to(dev), [0, 1])
+        kd = torch.from_numpy(np.ascontiguousarray(samples.reshape(-1, 2, 2))).to(dev)
+        samples_3d = ops.triangulate_points_f64(kd, torch.from_numpy(pair).to(dev)).to(torch.float32)
         samples_3d = samples_3d.reshape(T, J, N, 3).contiguous()
         self.samples_3d = samples_3d
         # targets: camera index 2's means (:802, hard-coded) with camera 0's Σ⁻¹ (quirk F5, :663)

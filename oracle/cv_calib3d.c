@@ -88,6 +88,19 @@ void orc_undistort_points_f32(const float* src, int64_t n, const double* K, cons
     }
 }
 
+/* CV_64FC2 keypoints: cvUndistortPointsInternal stores the doubles unrounded
+ * (the extrinsic branch's Gaussian samples, pose_refinement.py:811). */
+void orc_undistort_points_f64(const double* src, int64_t n, const double* K, const double* dist,
+                              int ndist, double* dst)
+{
+    double A[3][3], k[14];
+    memset(k, 0, sizeof(k));
+    for (int i = 0; i < 9; i++) A[i / 3][i % 3] = K[i];
+    for (int i = 0; i < ndist && i < 14; i++) k[i] = dist[i];
+    for (int64_t i = 0; i < n; i++)
+        undistort_one(src[2 * i], src[2 * i + 1], A, k, 5, &dst[2 * i], &dst[2 * i + 1]);
+}
+
 /* ---- lapack.cpp JacobiSVDImpl_<double>, Vt only ------------------------- */
 /* At: n rows of length m (row stride m), i.e. At = Aᵀ for A (m x n).  Vt: n x n. */
 void orc_jacobi_svd(double* At, int m, int n, double* Wout, double* Vt)
@@ -183,6 +196,42 @@ void orc_triangulate_nview(const double* Ps, int nv, const float* xs, int64_t n,
             out4[k * n + i] = (float)Vt[12 + k];
             if (out4_f64) out4_f64[k * n + i] = Vt[12 + k];
         }
+    }
+}
+
+/* icvTriangulatePoints with CV_64F points: the same fp64 A from double x, y; points4D is
+ * CV_64F (the points' type), so the null vector is stored unrounded. */
+void orc_triangulate_nview_f64(const double* Ps, int nv, const double* xs, int64_t n, double* out4)
+{
+    double At[4 * 32], Vt[16];
+    const int m = 2 * nv;
+    for (int64_t i = 0; i < n; i++) {
+        double A[32][4];
+        for (int j = 0; j < nv; j++) {
+            const double* P = Ps + 12 * j;
+            double x = xs[(j * n + i) * 2 + 0];
+            double y = xs[(j * n + i) * 2 + 1];
+            for (int k = 0; k < 4; k++) {
+                A[j * 2 + 0][k] = x * P[8 + k] - P[0 + k];
+                A[j * 2 + 1][k] = y * P[8 + k] - P[4 + k];
+            }
+        }
+        for (int c = 0; c < 4; c++)
+            for (int r = 0; r < m; r++) At[c * m + r] = A[r][c];
+        orc_jacobi_svd(At, m, 4, NULL, Vt);
+        for (int k = 0; k < 4; k++) out4[k * n + i] = Vt[12 + k];
+    }
+}
+
+/* ---- fundam.cpp convertPointsFromHomogeneous, f64, 4 -> 3 (scale = w != 0 ? 1./w : 1.) */
+void orc_from_homogeneous_f64(const double* in, int64_t n, double* out)
+{
+    for (int64_t i = 0; i < n; i++) {
+        double w = in[4 * i + 3];
+        double scale = w != 0. ? 1. / w : 1.;
+        out[3 * i + 0] = in[4 * i + 0] * scale;
+        out[3 * i + 1] = in[4 * i + 1] * scale;
+        out[3 * i + 2] = in[4 * i + 2] * scale;
     }
 }
 

@@ -41,6 +41,9 @@ def _load():
     lib.orc_jacobi_svd.argtypes = [f64p, ctypes.c_int, ctypes.c_int, f64p, f64p]
     lib.orc_triangulate_nview.argtypes = [f64p, ctypes.c_int, f32p, ctypes.c_int64, f32p, f64p]
     lib.orc_from_homogeneous_f32.argtypes = [f32p, ctypes.c_int64, f32p]
+    lib.orc_undistort_points_f64.argtypes = [f64p, ctypes.c_int64, f64p, f64p, ctypes.c_int, f64p]
+    lib.orc_triangulate_nview_f64.argtypes = [f64p, ctypes.c_int, f64p, ctypes.c_int64, f64p]
+    lib.orc_from_homogeneous_f64.argtypes = [f64p, ctypes.c_int64, f64p]
     _lib = lib
     return lib
 
@@ -54,10 +57,12 @@ def _p(a, t):
 # --------------------------------------------------------------------------
 def undistort_points(src, cameraMatrix, distCoeffs, R=None, P=None):
     """cv2.undistortPoints(src, K, dist, R=None, P=K) for the case the reference
-    uses (utils.py:1314-1315).  src: (N,1,2) float32.  Returns (N,1,2) float32."""
+    uses (utils.py:1314-1315).  src: (N,1,2) float32 (the pipeline's keypoints) or float64
+    (the extrinsic branch's samples, pose_refinement.py:811); returns the same dtype (OpenCV
+    writes into the source's depth)."""
     lib = _load()
     src = np.asarray(src)
-    assert src.dtype == np.float32, "reference feeds float32 keypoints"
+    assert src.dtype in (np.float32, np.float64), "reference feeds float32 or float64 keypoints"
     assert R is None, "reference passes R=None"
     K = np.ascontiguousarray(np.asarray(cameraMatrix, dtype=np.float64).reshape(3, 3))
     if P is not None:
@@ -67,13 +72,17 @@ def undistort_points(src, cameraMatrix, distCoeffs, R=None, P=None):
     d = np.ascontiguousarray(np.asarray(distCoeffs, dtype=np.float64).ravel())
     pts = np.ascontiguousarray(src.reshape(-1, 2))
     out = np.empty_like(pts)
+    if src.dtype == np.float64:
+        lib.orc_undistort_points_f64(_p(pts, ctypes.c_double), pts.shape[0], _p(K, ctypes.c_double),
+                                     _p(d, ctypes.c_double), int(d.size), _p(out, ctypes.c_double))
+        return out.reshape(src.shape)
     lib.orc_undistort_points_f32(_p(pts, ctypes.c_float), pts.shape[0], _p(K, ctypes.c_double),
                                  _p(d, ctypes.c_double), int(d.size), _p(out, ctypes.c_float))
     return out.reshape(src.shape)
 
 
 def triangulate_points_cv(P1, P2, x1, x2, return_f64=False):
-    """cv2.triangulatePoints(P1, P2, x1 (2,N), x2 (2,N)) -> (4,N) in x1's dtype (f32)."""
+    """cv2.triangulatePoints(P1, P2, x1 (2,N), x2 (2,N)) -> (4,N) in x1's dtype (f32 or f64)."""
     return triangulate_nview_cv([P1, P2], [x1, x2], return_f64=return_f64)
 
 
@@ -82,8 +91,14 @@ def triangulate_nview_cv(Ps, xs, return_f64=False):
     nv = len(Ps)
     Ps = np.ascontiguousarray(np.stack([np.asarray(P, dtype=np.float64).reshape(3, 4) for P in Ps]))
     xs = [np.asarray(x) for x in xs]
-    assert all(x.dtype == np.float32 for x in xs)
     n = xs[0].shape[1]
+    if all(x.dtype == np.float64 for x in xs):
+        X = np.ascontiguousarray(np.stack([x.T for x in xs]))  # (nv, n, 2)
+        out64 = np.empty((4, n), np.float64)
+        lib.orc_triangulate_nview_f64(_p(Ps, ctypes.c_double), nv, _p(X, ctypes.c_double), n,
+                                      _p(out64, ctypes.c_double))
+        return out64
+    assert all(x.dtype == np.float32 for x in xs)
     X = np.ascontiguousarray(np.stack([x.T for x in xs]).astype(np.float32))  # (nv, n, 2)
     out = np.empty((4, n), np.float32)
     out64 = np.empty((4, n), np.float64)
@@ -93,8 +108,13 @@ def triangulate_nview_cv(Ps, xs, return_f64=False):
 
 
 def convert_points_from_homogeneous(src):
-    """cv2.convertPointsFromHomogeneous on (N,4) float32 -> (N,1,3) float32."""
+    """cv2.convertPointsFromHomogeneous on (N,4) float32 -> (N,1,3) float32 (float64 -> float64)."""
     lib = _load()
+    if np.asarray(src).dtype == np.float64:
+        src = np.ascontiguousarray(np.asarray(src).reshape(-1, 4))
+        out = np.empty((src.shape[0], 3), np.float64)
+        lib.orc_from_homogeneous_f64(_p(src, ctypes.c_double), src.shape[0], _p(out, ctypes.c_double))
+        return out.reshape(-1, 1, 3)
     src = np.ascontiguousarray(np.asarray(src, dtype=np.float32).reshape(-1, 4))
     out = np.empty((src.shape[0], 3), np.float32)
     lib.orc_from_homogeneous_f32(_p(src, ctypes.c_float), src.shape[0], _p(out, ctypes.c_float))
@@ -117,10 +137,11 @@ def jacobi_svd(A):
 # Reference orchestration restated
 # --------------------------------------------------------------------------
 def projection_matrix(K, R, T):
-    """P = K [R|T] exactly as utils.py:1318-1319 computes it (np.dot, fp64)."""
-    K = np.asarray(K, dtype=np.float64)
-    R = np.asarray(R, dtype=np.float64)
-    T = np.asarray(T, dtype=np.float64)
+    """P = K [R|T] exactly as utils.py:1318-1319 computes it: np.dot in the parameters' own
+    dtype (fp64 calibration files; float32 torch parameters in the extrinsic branch)."""
+    K = np.asarray(K)
+    R = np.asarray(R)
+    T = np.asarray(T)
     return np.dot(K, np.hstack((R, T.reshape(-1, 1))))
 
 

@@ -30,6 +30,8 @@ sys.path.insert(0, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd"))
 from mvpose import synthetic as syn  # noqa: E402
 from oracle import cv_ref  # noqa: E402
 from oracle import heatmap_ref  # noqa: E402
+sys.path.insert(0, os.path.dirname(HERE))
+from sgd_problem import BENCH_C5_KW, bench_c5_inputs, inputs_digest, sgd_inputs  # noqa: E402
 
 REF = "/root/reference"
 
@@ -167,26 +169,6 @@ MY_LENGTHS = {  # reference examples/body_part_lengths.yaml:my_lengths (key orde
 }
 
 
-def sgd_inputs(V, T, seed):
-    """Synthetic heatmaps_2d (T,V,17,6) f64 Gaussians + kpts_3d (T,17,3) f32 init."""
-    rng = np.random.default_rng(seed)
-    cams = syn.make_rig(V, seed=seed)
-    poses = syn.make_poses(T, seed=seed + 1)
-    gauss = np.zeros((T, V, 17, 6))
-    for v, c in enumerate(cams):
-        uv = syn.project(poses, c) + rng.normal(0, 2.0, (T, 17, 2))
-        sx = rng.uniform(2.0, 6.0, (T, 17))
-        sy = rng.uniform(2.0, 6.0, (T, 17))
-        rho = rng.uniform(-0.4, 0.4, (T, 17))
-        gauss[:, v, :, 0:2] = uv
-        gauss[:, v, :, 2] = sx * sx
-        gauss[:, v, :, 3] = rho * sx * sy
-        gauss[:, v, :, 4] = rho * sx * sy
-        gauss[:, v, :, 5] = sy * sy
-    init = (poses + rng.normal(0, 3.0, poses.shape)).astype(np.float32)
-    return cams, gauss, init
-
-
 def gen_sgd(pr):
     """Optimized_3d_Pose_Estimation.sgd_optimize (pose_refinement.py:894-1096),
     trajectory-only path, as the CLI drives it (pose_refinement.py:1210-1214)."""
@@ -220,6 +202,54 @@ def gen_sgd(pr):
               seeds=np.array([seed]), **{"hist_" + k: v for k, v in hist.items()})
 
 
+C5_CASES = [
+    # BASELINE config 5 (V=8, T=400): T*J = 399*17 > 1024 runs sgd_kernel<512, false> (csrc/sgd.hip).
+    # name, seed, kwargs
+    ("sgd_V8_T400", 65, dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100, max_iter=8,
+                             batch_size=None)),
+    ("sgd_V8_T400_b100", 66, dict(lr=0.01, lambda_smooth=1e-3, lambda_body_length=0.5, patience=100,
+                                  max_iter=8, batch_size=100)),
+    ("sgd_V8_T400_stop", 67, dict(lr=0.05, lambda_smooth=1e-6, lambda_body_length=1.0, patience=3,
+                                  max_iter=400, batch_size=None, tolerance=1.0)),
+]
+
+
+def gen_sgd_c5(pr):
+    """sgd_optimize at BASELINE config 5's size (pose_refinement.py:894-1096): one window,
+    overlapping windows of 100 frames, and an early stop.  The 2.6 MB inputs are rebuilt by
+    the tests from the seed (tests/sgd_problem.py) and checked against the stored digest."""
+    for name, seed, kw in C5_CASES:
+        cams, gauss, init = sgd_inputs(8, 400, seed)
+        params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+        torch.manual_seed(0)
+        opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                              body_lengths=dict(MY_LENGTHS))
+        full_kw = dict(print_frequency=10 ** 9)
+        full_kw.update(kw)
+        opt.sgd_optimize(**full_kw)
+        hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
+        print(name, "history length", len(hist["total_cost"]))
+        _save(f"{name}.npz", V=np.array([8]), T=np.array([400]), digest=np.array(inputs_digest(cams, gauss, init)),
+              best=opt.best_trajectory.numpy(), final=opt.trajectory.detach().numpy(),
+              kw_names=np.array(list(kw.keys())), kw_vals=np.array([np.nan if v is None else float(v)
+                                                                  for v in kw.values()]),
+              seeds=np.array([seed]), **{"hist_" + k: v for k, v in hist.items()})
+
+
+def gen_bench_sgd(pr):
+    """The bench's config-5 SGD line (bench.py::sgd_line, 40 Adam iterations on all 400 rows:
+    time_interval [0, None]) run by the reference; the bench asserts its final trajectory
+    against this."""
+    cams, gauss, init = bench_c5_inputs()
+    params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+    torch.manual_seed(0)
+    opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                          body_lengths=dict(MY_LENGTHS))
+    opt.sgd_optimize(print_frequency=10 ** 9, time_interval=[0, None], batch_size=None, **BENCH_C5_KW)
+    _save("bench_sgd_c5.npz", digest=np.array(inputs_digest(cams, gauss, init)),
+          final=opt.trajectory.detach().numpy(), n_hist=np.array([len(opt.all_costs_total["total_cost"])]))
+
+
 def _rotation(rvec):
     th = np.linalg.norm(rvec)
     k = np.asarray(rvec) / th
@@ -241,48 +271,42 @@ EXTRINSIC_CASES = [
 
 def gen_sgd_extrinsic(pr):
     """sgd_optimize(extrinsic_optimization_IDs=[id], optimize_trajectory=False,
-    GT_camera_IDs=[a, b]) (pose_refinement.py:684-706, :800-831, :894-1096).  The stub
-    cv2.undistortPoints gets the float64 samples cast to float32 (the oracle restates the
-    float32-keypoint path the pipeline uses; real cv2 would keep float64 here)."""
+    GT_camera_IDs=[a, b]) (pose_refinement.py:684-706, :800-831, :894-1096).  The float64
+    samples go through the stub cv2 in float64, as real cv2 keeps CV_64F (the oracle's
+    float64 undistortPoints / triangulatePoints / convertPointsFromHomogeneous)."""
     import random
-    cv2 = sys.modules["cv2"]
-    und = cv2.undistortPoints
-    cv2.undistortPoints = lambda src, *a, **k: und(np.asarray(src, np.float32), *a, **k)
-    try:
-        for name, seed, ext_id, gt, pert, kw in EXTRINSIC_CASES:
-            kw = dict(kw)
-            T = 9        # time_interval [0, -1] keeps 8 rows: batch_size 4 -> windows [0,4) [2,6) [4,8)
-            cams, gauss, init = sgd_inputs(3, T, seed)
-            params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
-            if pert is not None:
-                params[ext_id][1] = _rotation(pert[0]) @ params[ext_id][1]
-                params[ext_id][2] = params[ext_id][2] + np.array(pert[1]).reshape(3, 1)
-            R0 = np.stack([p[1] for p in params.values()])
-            T0 = np.stack([p[2] for p in params.values()])
-            np.random.seed(seed)
-            random.seed(seed + 1)
-            torch.manual_seed(0)
-            n_samples = kw.pop("N_sample_points")   # sgd_optimize's own N_sample_points is unused (:684)
-            opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
-                                                  body_lengths=dict(MY_LENGTHS), N_sample_points=n_samples)
-            full_kw = dict(print_frequency=10 ** 9, extrinsic_optimization_IDs=[ext_id], optimize_trajectory=False,
-                           GT_camera_IDs=gt)
-            full_kw.update(kw)
-            opt.sgd_optimize(**full_kw)
-            hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
-            best = opt.best_decomposed_cam_params[ext_id]
-            fin = opt.decomposed_cam_params[ext_id]
-            _save(f"{name}.npz", gauss=gauss, init=init, K=np.stack([c["K"] for c in cams]), R=R0, T=T0,
-                  dist=np.stack([c["dist"] for c in cams]), ext_id=np.array([ext_id]), gt_ids=np.array(gt),
-                  n_samples=np.array([n_samples]),
-                  samples=opt.samples, samples_3d=opt.samples_3d.numpy(),
-                  best_R=best[1].detach().numpy(), best_T=best[2].detach().numpy(),
-                  final_R=fin[1].detach().numpy(), final_T=fin[2].detach().numpy(),
-                  kw_names=np.array(list(kw.keys())),
-                  kw_vals=np.array([np.nan if v is None else float(v) for v in kw.values()]),
-                  seeds=np.array([seed, seed + 1, 0]), **{"hist_" + k: v for k, v in hist.items()})
-    finally:
-        cv2.undistortPoints = und
+    for name, seed, ext_id, gt, pert, kw in EXTRINSIC_CASES:
+        kw = dict(kw)
+        T = 9        # time_interval [0, -1] keeps 8 rows: batch_size 4 -> windows [0,4) [2,6) [4,8)
+        cams, gauss, init = sgd_inputs(3, T, seed)
+        params = {i: [c["K"].copy(), c["R"].copy(), c["T"].copy(), c["dist"].copy()] for i, c in enumerate(cams)}
+        if pert is not None:
+            params[ext_id][1] = _rotation(pert[0]) @ params[ext_id][1]
+            params[ext_id][2] = params[ext_id][2] + np.array(pert[1]).reshape(3, 1)
+        R0 = np.stack([p[1] for p in params.values()])
+        T0 = np.stack([p[2] for p in params.values()])
+        np.random.seed(seed)
+        random.seed(seed + 1)
+        torch.manual_seed(0)
+        n_samples = kw.pop("N_sample_points")   # sgd_optimize's own N_sample_points is unused (:684)
+        opt = pr.Optimized_3d_Pose_Estimation(torch.tensor(gauss), init, decomposed_cam_params_initial=params,
+                                              body_lengths=dict(MY_LENGTHS), N_sample_points=n_samples)
+        full_kw = dict(print_frequency=10 ** 9, extrinsic_optimization_IDs=[ext_id], optimize_trajectory=False,
+                       GT_camera_IDs=gt)
+        full_kw.update(kw)
+        opt.sgd_optimize(**full_kw)
+        hist = {k: np.array([float(x) for x in v], np.float64) for k, v in opt.all_costs_total.items()}
+        best = opt.best_decomposed_cam_params[ext_id]
+        fin = opt.decomposed_cam_params[ext_id]
+        _save(f"{name}.npz", gauss=gauss, init=init, K=np.stack([c["K"] for c in cams]), R=R0, T=T0,
+              dist=np.stack([c["dist"] for c in cams]), ext_id=np.array([ext_id]), gt_ids=np.array(gt),
+              n_samples=np.array([n_samples]),
+              samples=opt.samples, samples_3d=opt.samples_3d.numpy(),
+              best_R=best[1].detach().numpy(), best_T=best[2].detach().numpy(),
+              final_R=fin[1].detach().numpy(), final_T=fin[2].detach().numpy(),
+              kw_names=np.array(list(kw.keys())),
+              kw_vals=np.array([np.nan if v is None else float(v) for v in kw.values()]),
+              seeds=np.array([seed, seed + 1, 0]), **{"hist_" + k: v for k, v in hist.items()})
 
 
 JOINT_CASES = [
@@ -354,7 +378,8 @@ def gen_interp(pr):
     _save("interp.npz", points=pts, seeds=np.array([seed]), **outs)
 
 
-GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "sgd_extrinsic", "sgd_joint", "interp")
+GENERATORS = ("dlt", "pose3d", "moments", "project", "bodylen", "sgd", "sgd_c5", "bench_sgd", "sgd_extrinsic", "sgd_joint",
+              "interp")
 
 
 def main():
@@ -366,7 +391,8 @@ def main():
     from mmpose_pose_estimation import PoseEstimator  # noqa: E402
     gens = {"dlt": lambda: gen_dlt(ref_utils), "pose3d": lambda: gen_pose3d(pose_estimation),
             "moments": lambda: gen_moments(PoseEstimator), "project": lambda: gen_project(pr),
-            "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr),
+            "bodylen": lambda: gen_bodylen(ref_utils), "sgd": lambda: gen_sgd(pr), "sgd_c5": lambda: gen_sgd_c5(pr),
+            "bench_sgd": lambda: gen_bench_sgd(pr),
             "sgd_extrinsic": lambda: gen_sgd_extrinsic(pr), "sgd_joint": lambda: gen_sgd_joint(pr),
             "interp": lambda: gen_interp(pr)}
     for name in GENERATORS:

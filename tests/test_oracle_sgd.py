@@ -76,3 +76,27 @@ def test_linear_interpolation_matches_reference(case, kw):
     from oracle import interp_ref
     d = np.load(os.path.join(GOLDEN, "interp.npz"))
     np.testing.assert_array_equal(interp_ref.linear_interpolation(d["points"], **kw), d["out_" + case])
+
+
+C5_CASES = ["sgd_V8_T400", "sgd_V8_T400_b100", "sgd_V8_T400_stop"]
+
+
+def c5_problem(d):
+    """Rebuild a config-5 golden's inputs from its seed and check them against the digest the
+    generator recorded (the 2.6 MB inputs are not stored)."""
+    from sgd_problem import inputs_digest, sgd_inputs
+    cams, gauss, init = sgd_inputs(int(d["V"][0]), int(d["T"][0]), int(d["seeds"][0]))
+    assert inputs_digest(cams, gauss, init) == str(d["digest"]), "synthetic problem generator drifted"
+    return [[c["K"], c["R"], c["T"], c["dist"]] for c in cams], gauss, init
+
+
+@pytest.mark.parametrize("case", C5_CASES)
+def test_sgd_config5_matches_reference(case):
+    """BASELINE config 5 (V=8, T=400): one window, windows of 100, early stop (317 iterations)."""
+    d = np.load(os.path.join(GOLDEN, case + ".npz"))
+    cams, gauss, init = c5_problem(d)
+    r = sgd_ref.refine(gauss, init, cams, body_lengths=dict(MY_LENGTHS), **sgd_kwargs(d))
+    np.testing.assert_array_equal(r.best_trajectory.numpy(), d["best"])
+    np.testing.assert_array_equal(r.trajectory.numpy(), d["final"])
+    for k, v in r.all_costs_total.items():
+        np.testing.assert_array_equal(np.array([float(x) for x in v]), d["hist_" + k])

@@ -5,11 +5,11 @@ optimize_trajectory=False, GT_camera_IDs=[a, b]), reference pose_refinement.py:6
 
 * the Gaussian samples: the reference's np.random.multivariate_normal loop on the global
   RNG — bit-identical (CPU, no kernel);
-* the triangulated samples (mvp_triangulate on the float32-cast samples; the golden's stub
-  cv2 does the same cast) — within 1e-3 cm: P = K[R|T] is fp64 here and float32 np.dot in
-  the reference.  PARITY UNPINNED for this leg: real cv2 keeps the float64 samples in float64
-  through undistortPoints / triangulatePoints, so the goldens restate the float32-keypoint
-  path the pipeline uses, not the reference's exact numbers (DESIGN §5);
+* the triangulated samples: utils.triangulate_points on the float64 samples with the GT
+  pair's float32 parameters, CV_64F end to end as real cv2 keeps it (mvp_triangulate_points_f64,
+  P = the reference's float32 np.dot; the golden's stub cv2 is the oracle's float64 OpenCV
+  restatement) — within 1e-4 cm and bit-identical on >= 99 % of coordinates (the exact Jacobi
+  path; cv2's numerics themselves are the restatement's, unpinned as everywhere);
 * one mvp_extrinsic_sample_grad pass vs a torch fp32 autograd restatement of
   construct_sample_cost's cost() — cost rtol 1e-5, gradient rtol 1e-4;
 * the whole optimisation: the shared cost / running-mean history (F6), final and best
@@ -137,7 +137,9 @@ def test_extrinsic_optimisation_matches_reference(name, device_adam):
         pytest.skip("no GPU")
     z, kw = _load(name)
     opt, ext = _run_opt(z, kw, device_adam)
-    np.testing.assert_allclose(opt.samples_3d.cpu().numpy(), z["samples_3d"], rtol=0, atol=1e-3)
+    s3 = opt.samples_3d.cpu().numpy()
+    np.testing.assert_allclose(s3, z["samples_3d"], rtol=0, atol=1e-4)
+    assert np.mean(s3 == z["samples_3d"]) >= 0.99
     names = [k[5:] for k in z.files if k.startswith("hist_")]
     assert list(opt.all_costs_total.keys()) == names
     worst = 0.0
@@ -180,6 +182,34 @@ def test_device_adam_matches_host_adam(name):
                                    b.decomposed_cam_params[ext][k].detach().numpy(), rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(a.best_decomposed_cam_params[ext][k].numpy(),
                                    b.best_decomposed_cam_params[ext][k].numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_triangulate_points_f64_dropin_vs_oracle():
+    """utils.triangulate_points with float64 keypoints (mvp_triangulate_points_f64) vs the
+    OpenCV restatement's CV_64F path (undistortPoints / triangulatePoints /
+    convertPointsFromHomogeneous in double), with float64 and with float32 camera parameters
+    (the reference's np.dot P in the parameters' dtype)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import synthetic as syn
+    from mvpose.utils import triangulate_points
+    from oracle import cv_ref
+    cams = syn.make_rig(2, seed=17)
+    k = syn.make_kpts_2d(syn.make_poses(300, seed=18), cams, seed=19, noise_px=1.5)
+    pts = np.stack([k[:, :, :2, 0], k[:, :, :2, 1]], axis=2).astype(np.float64)  # (T, J, view, xy)
+    pts += np.random.default_rng(20).normal(0, 1e-3, pts.shape)                  # off the f32 grid
+    for dt in (np.float64, np.float32):
+        a = [np.asarray(cams[0][n], dt) for n in ("K", "dist", "R", "T")]
+        b = [np.asarray(cams[1][n], dt) for n in ("K", "dist", "R", "T")]
+        got = triangulate_points(pts, *a, *b)
+        ref = cv_ref.triangulate_points(pts, *a, *b)
+        assert got.dtype == np.float64 and ref.dtype == np.float64 and got.shape == ref.shape
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-9)
+        assert np.mean(got == ref) >= 0.99, np.mean(got == ref)
+    # float32 keypoints keep the float32 pipeline path
+    got32 = triangulate_points(pts.astype(np.float32), *a, *b)
+    assert got32.dtype == np.float32
 
 
 def test_extrinsic_argument_errors():

@@ -21,7 +21,7 @@ import torch
 
 from conftest import GOLDEN
 from oracle import sgd_ref
-from test_oracle_sgd import SGD_CASES, sgd_cams, sgd_kwargs
+from test_oracle_sgd import C5_CASES, SGD_CASES, c5_problem, sgd_cams, sgd_kwargs
 
 pytestmark = pytest.mark.gpu
 SGD_ATOL = 1e-4
@@ -68,6 +68,46 @@ def test_sgd_matches_reference_golden(refine, case):
         ref = d["hist_" + k]
         assert len(v) == len(ref), k
         np.testing.assert_allclose(np.array(v, np.float64), ref, rtol=1e-4, atol=1e-7, err_msg=k)
+
+
+@pytest.mark.parametrize("case", C5_CASES)
+def test_sgd_config5_matches_reference_golden(refine, case):
+    """BASELINE config 5 at its own size (V=8, T=400 -> 399 rows after time_interval [0, -1]):
+    T*J = 6,783 > 1024 runs sgd_kernel<512, false> (the bench's kernel), trajectory in LDS.
+    One window (8 iterations), overlapping windows of 100 (7 windows), early stop (64
+    iterations, patience 3)."""
+    from mvpose import refine as _r
+    d = np.load(os.path.join(GOLDEN, case + ".npz"))
+    cams, gauss, init = c5_problem(d)
+    opt = _r.Optimized_3d_Pose_Estimation(gauss, init, decomposed_cam_params_initial=dict(enumerate(cams)),
+                                          body_lengths=dict(MY_LENGTHS))
+    opt.sgd_optimize(print_frequency=10 ** 9, **sgd_kwargs(d))
+    np.testing.assert_allclose(opt.best_trajectory.numpy(), d["best"], rtol=0, atol=SGD_ATOL)
+    np.testing.assert_allclose(opt.trajectory.numpy(), d["final"], rtol=0, atol=SGD_ATOL)
+    for k, v in opt.all_costs_total.items():
+        ref = d["hist_" + k]
+        assert len(v) == len(ref), k
+        np.testing.assert_allclose(np.array(v, np.float64), ref, rtol=1e-4, atol=1e-7, err_msg=k)
+
+
+def test_sgd_long_trajectory_outside_lds_matches_oracle(refine):
+    """T = 700 rows: the trajectory (142 KB) exceeds the kernel's 120 KB LDS budget, so the
+    Adam state and the trajectory live in the global workspace (traj_in_lds == false,
+    csrc/sgd.hip sgd_launch) — against the oracle, windows of 140 and one window."""
+    for V, T, kw in ((2, 701, dict(batch_size=140, lr=0.02, lambda_smooth=1e-3, lambda_body_length=0.5,
+                                     max_iter=4)),
+                     (3, 701, dict(batch_size=None, lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0,
+                                   max_iter=6))):
+        cams, gauss, init = _problem(V, T, seed=300 + V)
+        ref = sgd_ref.refine(gauss, init, cams, body_lengths=dict(MY_LENGTHS), **kw)
+        opt = refine.Optimized_3d_Pose_Estimation(gauss, init, decomposed_cam_params_initial=dict(enumerate(cams)),
+                                                  body_lengths=dict(MY_LENGTHS))
+        opt.sgd_optimize(print_frequency=10 ** 9, **kw)
+        np.testing.assert_allclose(opt.best_trajectory.numpy(), ref.best_trajectory.numpy(), rtol=0, atol=SGD_ATOL)
+        np.testing.assert_allclose(opt.trajectory.numpy(), ref.trajectory.numpy(), rtol=0, atol=SGD_ATOL)
+        for k in ref.all_costs_total:
+            np.testing.assert_allclose(np.array(opt.all_costs_total[k], np.float64),
+                                       np.array([float(x) for x in ref.all_costs_total[k]]), rtol=1e-4, atol=1e-7)
 
 
 def _problem(V, T, seed):

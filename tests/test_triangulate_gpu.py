@@ -270,3 +270,39 @@ def test_tolerance_mode_fallback_list_and_sweep(ops, frames, monkeypatch):
     np.testing.assert_array_equal(fow.cpu().numpy(), exw.cpu().numpy())
     tol = ops.triangulate(kd, cams_d, [0, 1], tolerance=True).cpu().numpy()
     np.testing.assert_allclose(tol, ex.cpu().numpy(), rtol=0, atol=ATOL, equal_nan=True)
+
+
+def test_tolerance_mode_two_host_threads_one_stream(ops, monkeypatch):
+    """Two host threads triangulating different-size batches on the same (default) stream with
+    every point forced onto the fallback list: each call's list launch pair is enqueued under
+    the list's lock, so neither call re-solves the other's indices (A_tol, B_tol,
+    A_fb, B_fb would read B's indices with A's pointers) and both equal the exact path."""
+    import threading
+    cams = syn.make_rig(2, seed=91)
+    cp = syn.reference_camera_params(cams)
+    cams_d = torch.tensor(ops.pack_cameras(cp), device="cuda")
+    ks = [torch.tensor(syn.make_kpts_2d(syn.make_poses(n, seed=92 + n), cams, seed=93, noise_px=1.0), device="cuda")
+          for n in (300, 2000)]
+    exact = [ops.triangulate(k, cams_d, [0, 1], exact=True).cpu().numpy() for k in ks]
+    monkeypatch.setenv("MVPOSE_TRI_FORCE_FALLBACK", "1")
+    outs = [[], []]
+    errs = []
+
+    def work(i):
+        try:
+            torch.cuda.set_device(0)
+            for _ in range(20):
+                outs[i].append(ops.triangulate(ks[i], cams_d, [0, 1], tolerance=True))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    monkeypatch.delenv("MVPOSE_TRI_FORCE_FALLBACK")
+    assert not errs, errs
+    for i in range(2):
+        for o in outs[i]:
+            np.testing.assert_array_equal(o.cpu().numpy(), exact[i])
