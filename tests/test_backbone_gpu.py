@@ -55,6 +55,42 @@ def test_backbone_batch_consistency(models):
     assert torch.equal(full[3], one[0])
 
 
+def test_headline_batch_1024_crops(models):
+    """The bench's forward (1,024 crops, BASELINE config 2): 16 crops at spread positions —
+    first / last, both sides of the 64-, 256- and 512-crop boundaries where the persistent
+    kernels' tile rounds and XCD assignment turn over — equal bit for bit the same crops
+    through a 5-crop forward, and 4 of them are within the fp32 oracle tolerance."""
+    _, ref = models
+    from mvpose import hrnet
+    sd = hrnet.random_state_dict(7)
+    big = hrnet.HRNetBackbone(sd, max_batch=1024)
+    small = hrnet.HRNetBackbone(sd, max_batch=8)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.zeros((1024, 256, 192, 4), dtype=torch.bfloat16, device="cuda")
+    x[..., :3] = torch.randn((1024, 256, 192, 3), generator=g, device="cuda").bfloat16()
+    full = big.forward(x).clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(full).all()
+    idx = [0, 1, 63, 64, 127, 255, 256, 257, 511, 512, 513, 640, 767, 900, 1022, 1023]
+    for i in range(0, len(idx), 4):
+        sel = idx[i:i + 4]
+        # 5-crop batches: the 4 probes plus a filler crop, in a different order
+        b = x[sel[::-1] + [500]].contiguous()
+        out = small.forward(b)
+        torch.cuda.synchronize()
+        for j, k in enumerate(sel[::-1]):
+            assert torch.equal(out[j], full[k]), f"crop {k} differs between the 1024- and 5-crop forwards"
+    probes = [0, 257, 767, 1023]
+    with torch.no_grad():
+        r = ref(x[probes].float()[..., :3].permute(0, 3, 1, 2).contiguous().cpu())
+    o = full[probes].cpu()
+    rel = (torch.linalg.vector_norm(o - r) / torch.linalg.vector_norm(r)).item()
+    cos = torch.nn.functional.cosine_similarity(o.reshape(4, -1), r.reshape(4, -1)).min().item()
+    print(f"1024-crop forward vs fp32 oracle on crops {probes}: rel L2 {rel:.3e}, min cosine {cos:.6f}")
+    assert rel <= 1.5e-2 and cos >= 0.99
+    del big
+
+
 def test_micro_batched_segments_bitwise_equal(models):
     """Segment micro-batching (Infinity-Cache residency) must not change a bit."""
     dev, _ = models

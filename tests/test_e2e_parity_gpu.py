@@ -19,9 +19,10 @@ Asserted per workload (tolerances in LIMITS; measured rates printed and recorded
 * >= decidable_fraction of maps lead their runner-up by > MARGIN of the map's max|h| in
   fp32, and there the argmax agrees on >= DECIDABLE_MIN;
 * where the argmax agrees (and the max's sign, which decides MSRA's -1 marker), the decoded
-  keypoint differs from the oracle's only by the +-0.25-cell MSRA refinement step's sign
-  (|dx|, |dy| in {0, one step, two steps}: sign(h[x+1] - h[x-1]) is itself a near-tie on a
-  symmetric peak), and is bit-exact on >= exact_min of those maps;
+  keypoint equals the oracle's, except by the +-0.25-cell MSRA refinement step (one or two
+  steps) only on an axis where the oracle's own sign(h[x+1] - h[x-1]) is a near-tie
+  (|h[x+1] - h[x-1]| <= MARGIN x max|h|: bf16 cannot decide it), and is bit-exact on
+  >= exact_min of those maps;
 * where both views' x, y are bit-exact and the camera order (ascending score, the
   reference's top-2 rule) agrees, kpts_3d is within 1e-4 world units — on >= k3_min of
   all joints.
@@ -34,15 +35,16 @@ from oracle import cv_ref, heatmap_ref, hrnet_ref
 
 pytestmark = pytest.mark.gpu
 
-T, V = 8, 2
+V = 2
+FRAMES = {"peaked": 128, "random": 32}   # synchronised frames per workload (x V camera-frames)
 MARGIN = 1e-2              # fp32 top-1 lead over top-2, in units of the map's max|h|
 DECIDABLE_MIN = 0.99
 LIMITS = {
-    # measured (r03e, MI355X): peaked argmax 0.989 (269/272), decidable 0.934 with agreement
-    # 1.000, kpts_3d compared on 0.926 of joints; random argmax 0.831, decidable 0.272,
-    # kpts_2d exact 1.000 where the argmax agrees
+    # measured (r03e, MI355X, 8 frames): peaked argmax 0.989 (269/272), decidable 0.934 with
+    # agreement 1.000, kpts_3d compared on 0.926 of joints; random argmax 0.831, decidable
+    # 0.272, kpts_2d exact 1.000 where the argmax agrees, kpts_3d on 78/136 = 0.574 of joints
     "peaked": dict(argmax_min=0.98, decidable_fraction=0.90, exact_min=0.90, k3_min=0.85),
-    "random": dict(argmax_min=0.80, decidable_fraction=0.20, exact_min=0.50, k3_min=0.0),
+    "random": dict(argmax_min=0.80, decidable_fraction=0.20, exact_min=0.50, k3_min=0.45),
 }
 
 
@@ -51,6 +53,7 @@ def runs(request):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet, pipeline, synthetic as syn
+    T = FRAMES[request.param]
     if request.param == "peaked":
         sd = hrnet.peaked_state_dict()
         frames = syn.make_skeleton_frames(T * V, seed=31)[0].reshape(T, V, 720, 1280, 3)
@@ -71,12 +74,15 @@ def runs(request):
     k2 = np.zeros((T, 17, 3, V), np.float32)
     amax = np.zeros((T, V, 17), np.int64)
     oavg = np.zeros((T, V, 17, 64 * 48), np.float32)
-    for t in range(T):
-        for v in range(V):
-            x = torch.from_numpy(heatmap_ref.preprocess(frames[t, v], M))[None]
-            avg, _, _ = hrnet_ref.flip_test_forward(model, x)
-            oavg[t, v] = avg[0].numpy().reshape(17, -1)
-            k, s, idx = heatmap_ref.msra_decode(avg[0].numpy())
+    flat = frames.reshape(T * V, 720, 1280, 3)
+    for c0 in range(0, T * V, 16):        # the oracle network in batches of 16 camera-frames
+        xs = torch.from_numpy(np.stack([heatmap_ref.preprocess(f, M) for f in flat[c0:c0 + 16]]))
+        avg, _, _ = hrnet_ref.flip_test_forward(model, xs)
+        for i in range(avg.shape[0]):
+            t, v = divmod(c0 + i, V)
+            a = avg[i].numpy()
+            oavg[t, v] = a.reshape(17, -1)
+            k, s, idx = heatmap_ref.msra_decode(a)
             k2[t, :, :2, v] = heatmap_ref.keypoints_to_image(k, center, scale)
             k2[t, :, 2, v] = s
             amax[t, v] = idx
@@ -123,12 +129,37 @@ def _agree(runs):
     return same & valid_same
 
 
+def _refinement_near_tie(runs):
+    """(T, 17, 2, V): the oracle's MSRA refinement difference h[x+1] - h[x-1] (x axis) /
+    h[y+1] - h[y-1] (y axis) at its argmax is within MARGIN x max|h| of zero."""
+    o = runs["oavg"].reshape(runs["oavg"].shape[:3] + (64, 48))         # (T, V, 17, H, W)
+    am = runs["amax"]
+    py, px = am // 48, am % 48
+    T = o.shape[0]
+    tie = np.zeros((T, 17, 2, V), bool)
+    for t in range(T):
+        for v in range(V):
+            for j in range(17):
+                h = o[t, v, j]
+                x, y = px[t, v, j], py[t, v, j]
+                lim = MARGIN * np.abs(h).max()
+                if 0 < x < 47:
+                    tie[t, j, 0, v] = abs(float(h[y, x + 1]) - float(h[y, x - 1])) <= lim
+                if 0 < y < 63:
+                    tie[t, j, 1, v] = abs(float(h[y + 1, x]) - float(h[y - 1, x])) <= lim
+    return tie
+
+
 def test_keypoints_where_argmax_agrees(runs):
     g, o = runs["gpu"]["kpts_2d"], runs["k2"]
     agree = _agree(runs)                                                 # (T, 17, V)
     step = np.float32(runs["scale"][0]) / np.float32(192.0)              # one 0.25-cell step in image px
     d = np.abs(g[:, :, :2, :] - o[:, :, :2, :])                          # (T, 17, 2, V)
-    ok = (d == 0) | (np.abs(d - step) <= 1e-3 * step) | (np.abs(d - 2 * step) <= 1e-3 * step)
+    tie = _refinement_near_tie(runs)
+    steps = (np.abs(d - step) <= 1e-3 * step) | (np.abs(d - 2 * step) <= 1e-3 * step)
+    ok = (d == 0) | (steps & tie)
+    print(f"[{runs['name']}] refinement steps off by one/two on {int(((d > 0) & agree[:, :, None, :]).sum())} "
+          f"coordinates, all at oracle near-ties: {bool(ok.transpose(0, 1, 3, 2)[agree].all())}")
     exact = (d == 0).all(axis=2) & agree
     one = ((d > 0) & (d < 1.5 * step)).any(axis=2) & agree
     print(f"[{runs['name']}] kpts_2d bit-exact {exact.mean():.4f} of all, "
