@@ -161,19 +161,38 @@ def cpu_baseline(n_frames, n_frames_1t, views):
     return out
 
 
-def tri_valu_issue(tri_ms, n_points):
-    """The triangulation kernel's real bound: FP64 VALU issue (OpenCV-order fp64
-    undistortion + QR).  From the committed PMC pass (profiles/r01_tri_pmc.json):
-    VALU instructions per launch x 4 cycles (wave64 on a 16-lane SIMD) over 1024
-    SIMDs at 2.4 GHz = the issue floor; frac = floor / measured launch time."""
-    path = os.path.join(ROOT, "profiles", "r01_tri_pmc.json")
+# VALU issue model (MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction issues over 2
+# cycles; fp64 runs at half the f32 rate — 78.6 vs 157.3 TFLOP/s vector peak — so 4 cycles;
+# transcendentals 8 cycles, the guide's 'vector-instruction ISSUE cost' row)
+VALU_CYC, F64_CYC, TRANS_CYC = 2, 4, 8
+N_SIMDS, CLOCK_HZ = 1024, 2.4e9
+
+
+def tri_valu_issue(tri_ms, n_points, pmc_file):
+    """The triangulation kernels' real bound: VALU issue (fp64 undistortion + solver).  From a
+    committed PMC pass of that kernel: per-wave instruction counts by type x their issue cycles
+    (VALU_CYC / F64_CYC / TRANS_CYC) over the 1,024 SIMDs at 2.4 GHz = the issue floor of a
+    launch of n_points; frac = floor / measured launch time."""
+    path = os.path.join(ROOT, "profiles", pmc_file)
     if not os.path.exists(path):
         return None
     pmc = json.load(open(path))
-    scale = n_points / pmc["points_per_launch"]   # VALU instructions scale with the points
-    floor = pmc["valu_issue_floor_ms"] * scale
-    return {"valu_instr_per_launch": pmc["valu_instr_per_launch"] * scale, "issue_floor_ms": floor,
-            "frac": floor / tri_ms, "source": "profiles/r01_tri_pmc.json"}
+    if "per_wave" in pmc:          # r03 format (tools/r03_tri.sh): raw SQ counters per wave
+        w = pmc["per_wave"]
+        f64 = w["SQ_INSTS_VALU_ADD_F64"] + w["SQ_INSTS_VALU_FMA_F64"] + w["SQ_INSTS_VALU_MUL_F64"]
+        trans = w["SQ_INSTS_VALU_TRANS_F64"]
+        valu = w["SQ_INSTS_VALU"]
+    else:                          # r01 format (tools/pmc_tri.sh)
+        f64 = pmc["f64_add_per_wave"] + pmc["f64_fma_per_wave"] + pmc["f64_mul_per_wave"]
+        trans = 0.0
+        valu = pmc["valu_instr_per_wave"]
+    cyc = (valu - f64 - trans) * VALU_CYC + f64 * F64_CYC + trans * TRANS_CYC
+    waves = n_points / 64.0
+    floor = waves * cyc / (N_SIMDS * CLOCK_HZ) * 1e3
+    return {"valu_instr_per_wave": valu, "f64_instr_per_wave": f64, "trans_f64_per_wave": trans,
+            "issue_cycles_per_wave": cyc, "issue_floor_ms": floor, "frac": floor / tri_ms,
+            "model": f"{VALU_CYC} cyc per VALU, {F64_CYC} per fp64, {TRANS_CYC} per fp64 transcendental "
+                     "(SIMD-32, MI355X_MICROARCH.md); 1,024 SIMDs at 2.4 GHz", "source": f"profiles/{pmc_file}"}
 
 
 def tri_line(ops, syn, dev, s, views, mode, reps=10, tolerance=False):
@@ -322,6 +341,79 @@ def extrinsic_line(dev, T=1000, N=100, reps=20):
                                                                     "target per (t, joint) is L2-resident"}}
 
 
+def stage_lines(est, frames, traffic, reps=10):
+    """SURVEY §8(d) lines for the step's small kernels at the headline batch (B·V camera-frames),
+    each launch timed alone with HIP events on the launch stream: preprocess (crop +
+    normalise, original + flipped), decode (flip average + MSRA), moments (revert + means /
+    covariances).  Bytes per launch from the committed PMC pass (2·FETCH_SIZE + WRITE_SIZE,
+    tools/pmc_traffic.py) next to the algorithmic bytes of each kernel's model."""
+    import ctypes
+    from mvpose._lib import call
+    from mvpose.estimator import COCO_FLIP_INDICES, HEATMAP_THR, MEAN, STD
+    from mvpose.hrnet import HEATMAP_HW, INPUT_HW, N_JOINTS
+    dev = est.device
+    n = frames.shape[0]
+    h, w = frames.shape[1:3]
+    s = torch.cuda.current_stream(dev)
+    sp = ctypes.c_void_p(s.cuda_stream)
+    p = (lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None)
+    mean, std = (ctypes.c_float * 3)(*MEAN), (ctypes.c_float * 3)(*STD)
+    flip = (ctypes.c_int * N_JOINTS)(*COCO_FLIP_INDICES)
+    crops, hm = est.crops[: 2 * n], est.heatmaps[: 2 * n]
+    avg = torch.empty((n, N_JOINTS) + HEATMAP_HW, dtype=torch.float32, device=dev)
+    kp = torch.empty((n, N_JOINTS, 2), dtype=torch.float32, device=dev)
+    sc = torch.empty((n, N_JOINTS), dtype=torch.float32, device=dev)
+    gauss = torch.empty((n, N_JOINTS, 6), dtype=torch.float64, device=dev)
+    launches = {
+        "preprocess": lambda: call("mvp_preprocess", p(frames), n, h, w, p(est.crop_minv), INPUT_HW[0], INPUT_HW[1],
+                                   mean, std, int(est.swap_rb), 1, p(crops), sp),
+        "decode": lambda: call("mvp_heatmap_decode", p(hm[:n]), p(hm[n:]), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1],
+                               flip, 1, p(est.center_scale), INPUT_HW[1], INPUT_HW[0], p(avg), p(kp), p(sc), None,
+                               None, 1, sp),
+        "moments": lambda: call("mvp_heatmap_moments", p(avg), n, N_JOINTS, HEATMAP_HW[0], HEATMAP_HW[1],
+                                p(est.revert_minv), h, w, ctypes.c_float(HEATMAP_THR), int(est.separable), None,
+                                p(gauss), sp),
+    }
+    hm_b = N_JOINTS * HEATMAP_HW[0] * HEATMAP_HW[1] * 4          # one f32 heatmap stack per crop
+    crop_b = INPUT_HW[0] * INPUT_HW[1] * 4 * 2                   # one bf16 crop (RGB + pad)
+    algo = {  # algorithmic bytes per camera-frame
+        "preprocess": (2 * crop_b, "writes the original + flipped bf16 crops (786 KB); reads the frame rows the "
+                                   "whole-image warp touches (PMC: ~0.68 MB per camera-frame)"),
+        "decode": (3 * hm_b, "reads both f32 heatmap stacks (2 x 209 KB), writes the flip average (209 KB)"),
+        "moments": (hm_b, "reads the flip-averaged f32 maps (209 KB); the reverted 17x720x1280 map is never formed"),
+    }
+    out = {}
+    for name, fn in launches.items():
+        for _ in range(2):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        pmc = traffic.get(name, {}).get("hbm_bytes_per_launch")
+        per_unit, model = algo[name]
+        gbs = per_unit * n / (ms * 1e-3) / 1e9
+        line = {"kernel": {"preprocess": "preprocess_kernel", "decode": "decode_kernel",
+                           "moments": "moments_kernel"}[name],
+                "camera_frames_per_launch": n, "avg_launch_ms": ms, "launches": reps,
+                "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": gbs / HBM_PEAK_GBS, "bytes_per_camera_frame": per_unit, "bytes_model": model,
+                             "traffic": pmc}}
+        if pmc:
+            line["roofline"]["traffic_GBps"] = pmc / (ms * 1e-3) / 1e9
+        if name == "moments":
+            flop = 20.0 * N_JOINTS * h * w * n   # SURVEY §8(d): ~20 FLOP per (pixel, joint) of the reverted map
+            line["flop_model_TFLOPs"] = flop / (ms * 1e-3) / 1e12
+            line["flop_note"] = ("the per-pixel FLOP model of §8(d) (0.31 GFLOP per camera-frame) over the launch "
+                                 "time; above the FP32 peak because the separable fast path sums whole column "
+                                 "runs in closed form instead of walking the reverted map")
+        out[name] = line
+    return out
+
+
 def ingest_line(est, V, n_frames=512, batch=128):
     """SURVEY §7 "host frame supply": the same 2D stage fed from HOST memory (decoded
     frames in RAM, as the reference holds whole videos, utils.py:849-909) through the
@@ -463,20 +555,23 @@ def main():
     bb_tflops = flops / (bb_ms * 1e-3) / 1e12
     extra = {}
     if rank == 0:
+        traffic_all, _ = committed_traffic()
+        extra["stages"] = stage_lines(est, frames.reshape(B * V, 720, 1280, 3), traffic_all)
         del frames
         torch.cuda.empty_cache()
         if V == 2:
             tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE, tolerance=True)
             tri["kernel"] = "triangulate_tol2_kernel (+ triangulate_tol2_fallback_kernel)"
+            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17, "r03t_tri_tol_pmc.json")
             tri["solver"] = "tolerance (MVP_TRI_TOLERANCE): the pipeline's default"
             compat = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
             compat["kernel"] = "triangulate_reference_kernel"
-            compat["valu_issue"] = tri_valu_issue(compat["avg_launch_ms"], TRI_T * 17)
+            compat["valu_issue"] = tri_valu_issue(compat["avg_launch_ms"], TRI_T * 17, "r01_tri_pmc.json")
             tri["reference_compat"] = compat
         else:
             tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
             tri["kernel"] = "triangulate_reference_kernel"
-            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17)
+            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17, "r01_tri_pmc.json")
         extra["roofline_triangulate"] = tri
         if not args.no_extra:
             t4 = tri_line(ops, syn, dev, s, 4, ops.TRI_ALL_VIEWS)

@@ -68,8 +68,13 @@ struct Proj {
 
 // a / b for finite normal operands: one v_rcp_f32 and a Markstein correction step
 // (q = a·r, e = a − q·b, q + e·r): the correctly rounded quotient except in rare
-// double-rounding cases (≤ 1 ulp), 4 VALU operations against ~10 for the IEEE sequence
+// double-rounding cases (≤ 1 ulp), 4 VALU operations against ~10 for the IEEE sequence.
+// Outside 2^-125 <= |b| <= 2^125, |a| <= 2^125 (a point almost on the camera plane or far
+// off axis) v_rcp_f32 flushes or the product overflows where torch's quotient is finite:
+// those lanes take the IEEE division (a branch no lane of a normal wave enters).
 __device__ __forceinline__ float div_fast(float a, float b) {
+    const float ab = __builtin_fabsf(b);
+    if (__builtin_expect(!(ab >= 0x1p-125f && ab <= 0x1p125f && __builtin_fabsf(a) <= 0x1p125f), 0)) return a / b;
     const float r = __builtin_amdgcn_rcpf(b);
     const float q = a * r;
     const float e = __builtin_fmaf(-q, b, a);

@@ -24,7 +24,11 @@ Host mirror of the reference's refinement API (pose_refinement.py):
   gradient, their own Adam state, one clip_grad_norm_ over [R, T, ..., trajectory]).
 
 Scope: the NN trajectory parameterisation (``use_NN``) and ``randomize_params`` raise
-NotImplementedError.
+NotImplementedError.  A joint call that would learn an axis-angle R raises it too: the
+reference converts each learnable camera's INITIAL R to axis-angle (:935), so a second joint
+call with ``reset_camera_params=True`` restarts from that vector and learns its 3 numbers;
+the kernel learns R as a 3x3 matrix only.  A trajectory-only call after such a reset runs
+(the fixed axis-angle R is converted to its matrix, as project_points_torch does).
 """
 from __future__ import annotations
 
@@ -316,6 +320,9 @@ class Optimized_3d_Pose_Estimation:
                                        time_interval)
         if self.n_dims != 3:
             raise NotImplementedError("3D trajectories only")
+        if reset_camera_params:   # :907-908, on every path (the cameras an earlier call learned are dropped)
+            self.decomposed_cam_params = {k: [c.clone().detach() for c in v]
+                                          for k, v in self.decomposed_cam_params_initial.items()}
         ext_ids = list(extrinsic_optimization_IDs or [])
         learn = []
         if ext_ids:
@@ -325,9 +332,6 @@ class Optimized_3d_Pose_Estimation:
             # R (3x3) and T join the trajectory in one Adam / clip_grad_norm_
             if len(ext_ids) > 2:
                 raise NotImplementedError("at most 2 learnable cameras in the joint optimisation")
-            if reset_camera_params:
-                self.decomposed_cam_params = {k: [c.clone().detach() for c in v]
-                                              for k, v in self.decomposed_cam_params_initial.items()}
             for ID in ext_ids:
                 if ID not in self.camera_IDs:
                     raise ValueError(f"extrinsic camera {ID!r} is not in camera_IDs {self.camera_IDs}")

@@ -95,3 +95,35 @@ def test_joint_without_learnable_cameras_is_the_trajectory_kernel(refine):
             opt.sgd_optimize(print_frequency=10 ** 9, extrinsic_optimization_IDs=ids, optimize_trajectory=True, **kw)
         outs.append(opt.trajectory.numpy())
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_reset_camera_params_on_every_path(refine):
+    """reset_camera_params (:907-908) applies to every sgd_optimize path: after a joint call
+    learned camera 2, a trajectory-only call with reset=True runs on the initial cameras
+    (camera 2's initial R is now the axis-angle vector the joint call stored, :935, used as
+    project_points_torch would: as its rotation matrix) and equals a fresh object's run on
+    those cameras bit for bit; without reset it keeps the learned camera.  A second joint
+    call with reset=True would learn that axis-angle R: the documented gap raises."""
+    d = np.load(os.path.join(GOLDEN, "sgd_joint_c2.npz"))
+    cams = {i: c for i, c in enumerate(sgd_cams(d))}
+    kw = dict(print_frequency=10 ** 9, lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, max_iter=6)
+    random.seed(5)
+    opt = refine.Optimized_3d_Pose_Estimation(d["gauss"], d["init"], decomposed_cam_params_initial=cams,
+                                              body_lengths=dict(MY_LENGTHS))
+    opt.sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=True, **kw)
+    learned_R = opt.decomposed_cam_params[2][1].clone()
+    assert tuple(opt.decomposed_cam_params_initial[2][1].shape) == (3,)   # axis-angle after :935
+    opt.sgd_optimize(reset_camera_params=False, **kw)
+    keep = opt.trajectory.clone()
+    np.testing.assert_array_equal(opt.decomposed_cam_params[2][1].numpy(), learned_R.numpy())
+    opt.sgd_optimize(reset_camera_params=True, **kw)
+    reset = opt.trajectory.clone()
+    assert tuple(opt.decomposed_cam_params[2][1].shape) == (3,)
+    fresh_cams = {i: [c.clone() for c in v] for i, v in opt.decomposed_cam_params_initial.items()}
+    fresh = refine.Optimized_3d_Pose_Estimation(d["gauss"], d["init"], decomposed_cam_params_initial=fresh_cams,
+                                                body_lengths=dict(MY_LENGTHS))
+    fresh.sgd_optimize(**kw)
+    assert torch.equal(reset, fresh.trajectory)
+    assert not torch.equal(keep, reset)
+    with pytest.raises(NotImplementedError):
+        opt.sgd_optimize(extrinsic_optimization_IDs=[2], optimize_trajectory=True, reset_camera_params=True, **kw)
