@@ -66,19 +66,21 @@ struct Proj {
     float xd, yd;
 };
 
-// a / b for finite normal operands: one v_rcp_f32 and a Markstein correction step
-// (q = a·r, e = a − q·b, q + e·r): the correctly rounded quotient except in rare
-// double-rounding cases (≤ 1 ulp), 4 VALU operations against ~10 for the IEEE sequence.
-// Outside 2^-125 <= |b| <= 2^125, |a| <= 2^125 (a point almost on the camera plane or far
-// off axis) v_rcp_f32 flushes or the product overflows where torch's quotient is finite:
-// those lanes take the IEEE division (a branch no lane of a normal wave enters).
-__device__ __forceinline__ float div_fast(float a, float b) {
-    const float ab = __builtin_fabsf(b);
-    if (__builtin_expect(!(ab >= 0x1p-125f && ab <= 0x1p125f && __builtin_fabsf(a) <= 0x1p125f), 0)) return a / b;
+// (a0 / b, a1 / b) for finite normal operands: one v_rcp_f32 and a Markstein correction
+// step per quotient (q = a·r, e = a − q·b, q + e·r): the correctly rounded quotient except in
+// rare double-rounding cases (≤ 1 ulp), 4 VALU operations against ~10 for the IEEE sequence.
+// Range: v_rcp_f32 flushes for |b| < 2^-126 (a point within 1e-38 cm of the camera plane:
+// here NaN; in torch x = P0 / P2 is ~1e30 or more, whose square overflows f32 in the
+// distortion polynomial, so the term is non-finite there too and nan_mean's mask drops it in
+// both — they differ only for a point within ~1e-38 cm of the camera centre itself) and
+// returns 0 for |b| > 2^126 (a depth of 1e38 cm: here 0, in torch a quotient below 1e-38).  A per-lane
+// range guard with an IEEE fallback measured +4.5-8 % per SGD iteration
+// (profiles/r04_sgd_guard_ab.txt) for no observable difference, so there is none.
+__device__ __forceinline__ void div2_fast(float a0, float a1, float b, float& q0, float& q1) {
     const float r = __builtin_amdgcn_rcpf(b);
-    const float q = a * r;
-    const float e = __builtin_fmaf(-q, b, a);
-    return __builtin_fmaf(e, r, q);
+    const float p0 = a0 * r, p1 = a1 * r;
+    q0 = __builtin_fmaf(__builtin_fmaf(-p0, b, a0), r, p0);
+    q1 = __builtin_fmaf(__builtin_fmaf(-p1, b, a1), r, p1);
 }
 
 // project_points_torch (pose_refinement.py:118-177) for one point, torch op order.
@@ -92,8 +94,7 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
     const float P1 = X0 * R[3] + X1 * R[4] + X2 * R[5] + T[1];
     const float P2 = X0 * R[6] + X1 * R[7] + X2 * R[8] + T[2];
     o.P2 = P2;
-    o.x = div_fast(P0, P2);
-    o.y = div_fast(P1, P2);
+    div2_fast(P0, P1, P2, o.x, o.y);
     if (!ign) {
         const float x = o.x, y = o.y;
         const float r2 = x * x + y * y;
@@ -116,8 +117,7 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
     const float h1 = o.xd * K[3] + o.yd * K[4] + K[5];
     const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
     o.h2 = h2;
-    o.u = div_fast(h0, h2);
-    o.v = div_fast(h1, h2);
+    div2_fast(h0, h1, h2, o.u, o.v);
     return o;
 }
 

@@ -17,7 +17,7 @@ argmax can only move where two cells are within that of each other.
 Asserted per workload (tolerances in LIMITS; measured rates printed and recorded in DESIGN §5):
 * argmax agreement >= argmax_min of all (frame, view, joint) heatmaps;
 * >= decidable_fraction of maps lead their runner-up by > MARGIN of the map's max|h| in
-  fp32, and there the argmax agrees on >= DECIDABLE_MIN;
+  fp32, and there the argmax agrees on >= decidable_min;
 * where the argmax agrees (and the max's sign, which decides MSRA's -1 marker), the decoded
   keypoint equals the oracle's, except by the +-0.25-cell MSRA refinement step (one or two
   steps) only on an axis where the oracle's own sign(h[x+1] - h[x-1]) is a near-tie
@@ -38,13 +38,14 @@ pytestmark = pytest.mark.gpu
 V = 2
 FRAMES = {"peaked": 128, "random": 32}   # synchronised frames per workload (x V camera-frames)
 MARGIN = 1e-2              # fp32 top-1 lead over top-2, in units of the map's max|h|
-DECIDABLE_MIN = 0.99
 LIMITS = {
-    # measured (r03e, MI355X, 8 frames): peaked argmax 0.989 (269/272), decidable 0.934 with
-    # agreement 1.000, kpts_3d compared on 0.926 of joints; random argmax 0.831, decidable
-    # 0.272, kpts_2d exact 1.000 where the argmax agrees, kpts_3d on 78/136 = 0.574 of joints
-    "peaked": dict(argmax_min=0.98, decidable_fraction=0.90, exact_min=0.90, k3_min=0.85),
-    "random": dict(argmax_min=0.80, decidable_fraction=0.20, exact_min=0.50, k3_min=0.45),
+    # measured (r04a, MI355X): peaked (128 frames, 4,352 maps) argmax 0.9970, decidable 0.956
+    # with agreement 1.000, kpts_2d bit-exact on 0.9882 of same-argmax maps (51 two-step
+    # coordinates, all at oracle near-ties), kpts_3d compared on 2081/2176 = 0.956 of joints;
+    # random (32 frames, 1,088 maps) argmax 0.838, decidable 0.284 with agreement 0.990,
+    # kpts_2d exact 0.998 where the argmax agrees, kpts_3d on 307/544 = 0.564 of joints
+    "peaked": dict(argmax_min=0.99, decidable_fraction=0.93, decidable_min=0.99, exact_min=0.97, k3_min=0.92),
+    "random": dict(argmax_min=0.80, decidable_fraction=0.20, decidable_min=0.98, exact_min=0.50, k3_min=0.45),
 }
 
 
@@ -101,11 +102,12 @@ def test_argmax_agreement(runs):
 
 def test_argmax_agreement_on_decidable_maps(runs):
     """Where the fp32 oracle's maximum leads its runner-up cell by more than the bf16
-    path's own error, the argmax must agree (>= DECIDABLE_MIN).  The error scale is the
+    path's own error, the argmax must agree (>= the workload's decidable_min).  The error scale is the
     map's magnitude: bf16 heatmaps differ from fp32 by ~1-3 % of max|h| per map (measured,
     tools/e2e_diag.py), so a lead below MARGIN x max|h| is a near-tie that bf16 compute
     (the allowed dtype) cannot resolve.  Many random-weight maps have no peak at all (all
-    cells below zero, the head bias): their argmax is decided by noise in either dtype."""
+    cells below zero, the head bias): their argmax is decided by noise in either dtype.
+    Agreement there must reach the workload's decidable_min."""
     o = runs["oavg"]                                                     # (T, V, 17, HW)
     top2 = -np.sort(-o, axis=-1)[..., :2]
     lead = (top2[..., 0] - top2[..., 1]) / np.abs(o).max(axis=-1)
@@ -116,7 +118,7 @@ def test_argmax_agreement_on_decidable_maps(runs):
               f"{agree[sel].mean() if sel.any() else 1:.4f}")
     sel = lead > MARGIN
     assert sel.sum() >= runs["lim"]["decidable_fraction"] * sel.size, sel.mean()
-    assert agree[sel].mean() >= DECIDABLE_MIN, agree[sel].mean()
+    assert agree[sel].mean() >= runs["lim"]["decidable_min"], agree[sel].mean()
 
 
 def _agree(runs):
