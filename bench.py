@@ -161,10 +161,11 @@ def cpu_baseline(n_frames, n_frames_1t, views):
     return out
 
 
-# VALU issue model (MI355X_MICROARCH.md: SIMD-32, a wave64 VALU instruction issues over 2
-# cycles; fp64 runs at half the f32 rate — 78.6 vs 157.3 TFLOP/s vector peak — so 4 cycles;
-# transcendentals 8 cycles, the guide's 'vector-instruction ISSUE cost' row)
-VALU_CYC, F64_CYC, TRANS_CYC = 2, 4, 8
+# VALU issue model: cycles per wave64 instruction per SIMD, measured on MI355X with every CU
+# busy (tools/fp64_probe.hip, profiles/r04_fp64_probe.txt): v_fma_f64 5.3, v_mul_f64 5.0,
+# v_add_f64 4.6, v_rcp_f64 16.4, v_fma_f32 2.7 (the guide's SIMD-32 model gives 2 for f32 and
+# 4 for fp64 at half rate; the measured costs include the issue overheads at full occupancy)
+VALU_CYC, F64_CYC, TRANS_CYC = 2.67, 5.0, 16.4
 N_SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
@@ -192,7 +193,7 @@ def tri_valu_issue(tri_ms, n_points, pmc_file):
     return {"valu_instr_per_wave": valu, "f64_instr_per_wave": f64, "trans_f64_per_wave": trans,
             "issue_cycles_per_wave": cyc, "issue_floor_ms": floor, "frac": floor / tri_ms,
             "model": f"{VALU_CYC} cyc per VALU, {F64_CYC} per fp64, {TRANS_CYC} per fp64 transcendental "
-                     "(SIMD-32, MI355X_MICROARCH.md); 1,024 SIMDs at 2.4 GHz", "source": f"profiles/{pmc_file}"}
+                     "(measured, profiles/r04_fp64_probe.txt); 1,024 SIMDs at 2.4 GHz", "source": f"profiles/{pmc_file}"}
 
 
 def tri_line(ops, syn, dev, s, views, mode, reps=10, tolerance=False):

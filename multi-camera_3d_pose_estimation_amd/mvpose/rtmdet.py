@@ -190,6 +190,19 @@ def random_state_dict(seed: int = 0, calibrated: bool = True):
     return sd
 
 
+def peaked_state_dict():
+    """random_state_dict(0) with the classification head fitted to a peaked person score on
+    rendered skeleton frames (tools/train_peaked_rtmdet.py: every BN's statistics re-calibrated
+    on those frames, then the cls BN affines and rtm_cls fitted; data/rtmdet_m_peaked.npz holds
+    only those tensors).  Synthetic test weights with one clear best prior per frame, as a
+    trained detector has on a visible person: the detector parity test's workload."""
+    sd = random_state_dict(0)
+    with np.load(os.path.join(DATA_DIR, "rtmdet_m_peaked.npz")) as z:
+        for k in z.files:
+            sd[k] = torch.from_numpy(z[k].astype(np.float32))
+    return sd
+
+
 def fold(sd, name):
     """ConvModule conv (cout, cin/g, k, k) + eval BN -> (w f64 same shape, bias f64 (cout,))."""
     w = sd[name + ".conv.weight"].double().numpy()

@@ -12,7 +12,8 @@ is against oracle/rtmdet_ref.py (parity unpinned against the libraries themselve
 * per-frame selection (best row) exactly the argmax rule on the GPU's candidates;
 * NMS exactly the oracle's post-processing on the GPU's candidates;
 * end to end vs the fp32 oracle: the selected box agrees wherever the fp32 winner leads
-  its runner-up by a margin that bf16 cannot overturn.
+  its runner-up by a margin that bf16 cannot overturn — on the seeded random weights and on
+  the peaked (trained-like) head of rtmdet.peaked_state_dict.
 """
 import ctypes
 
@@ -25,6 +26,8 @@ from mvpose import _lib, rtmdet as D
 from oracle import rtmdet_ref as R
 
 pytestmark = pytest.mark.gpu
+PEAK_BAND = 3.0   # logits below the fp32 selection that count as the frame's peak region
+SAT = 16.6355     # f32 sigmoid(x) == 1.0 above this logit (1 - 2^-24 rounds up)
 
 
 def _frames(n, h, w, seed):
@@ -186,6 +189,76 @@ def test_end_to_end_vs_fp32_oracle(sd, det640):
             agree += int(gi == int(t2.indices[0]))
     print(f"same prior {same}/{n}, decided {decided}, agree {agree}")
     assert agree == decided
+
+
+def test_end_to_end_peaked_vs_fp32_oracle():
+    """The selected prior on a trained-like detector: rtmdet.peaked_state_dict (classification
+    head fitted to one clear best prior per person, tools/train_peaked_rtmdet.py) on skeleton
+    frames the fit never saw.  The fp32 side selects as the reference does: the highest f32
+    score among the priors that survive post-processing (score > score_thr, a box of positive
+    size), the lowest index on ties.  A frame is decidable when no other prior can overturn
+    that under the bf16 path's own logit error on the frame's peak region (max |GPU - fp32|
+    over priors within PEAK_BAND of the selection; bf16 error grows with the logit): each is
+    below the selection by twice that error, or a robustly saturated (score 1.0) tie with a
+    later index.  There the GPU must select the same prior (>= 95 % of those frames), and
+    most frames must be decidable."""
+    from mvpose import synthetic as syn
+    sd = D.peaked_state_dict()
+    m = R.build_model(sd)
+    det = D.RTMDetector(sd, max_batch=8)
+    n = 32
+    frames, _ = syn.make_skeleton_frames(n, seed=77)
+    cands, bests = [], []
+    for i0 in range(0, n, 8):
+        out = det.detect(torch.from_numpy(frames[i0:i0 + 8]).cuda())
+        cands.append(out["cand"].cpu().clone())
+        bests.append(out["best"].cpu().clone())
+    det.close()
+    cand, best = torch.cat(cands), torch.cat(bests).numpy()
+    leads, agree, dmed, errs, decs = [], [], [], [], []
+    for i in range(n):
+        img, sf, _ = R.letterbox(frames[i], 640)
+        with torch.no_grad():
+            cs, bp = m(R.normalize(img))
+        lg = torch.cat([c[0, 0].reshape(-1) for c in cs])
+        dmed.append(float(torch.median((cand[i, :, 5] - lg).abs())))
+        # the reference's selection is the first detection after post-processing: the best
+        # prior among those with score > score_thr and a box of positive size (min_bbox_size 0)
+        sc, bx = R.candidates(cs, bp)
+        bx = bx * torch.tensor([1 / sf[0], 1 / sf[1]] * 2)
+        ok = (sc > R.TEST_CFG["score_thr"]) & (bx[:, 2] - bx[:, 0] > 0) & (bx[:, 3] - bx[:, 1] > 0)
+        # fp32 selection: the highest SCORE (sigmoid, f32) among valid priors, the lowest prior
+        # index on ties (the stable sort) — f32 sigmoids of logits above ~16.64 are exactly 1.0,
+        # so saturated peaks tie and the index decides, in mmdet and on the GPU alike
+        scv = sc.masked_fill(~ok, -1.0)
+        sel = int(torch.nonzero(scv == scv.max())[0])
+        # the bf16 path's logit error where it matters: over the frame's peak region (priors
+        # within PEAK_BAND of the selected logit), the largest |GPU - fp32| logit difference
+        near = lg >= lg[sel] - PEAK_BAND
+        e = float((cand[i, :, 5] - lg).abs()[near].max())
+        errs.append(e)
+        # decidable: every other valid prior is either clearly below the selection (by 2 e), or a
+        # robust saturated tie the index decides (both above SAT + 2 e, the other later)
+        idx = torch.arange(len(lg))
+        other = ok & (idx != sel)
+        below = lg[sel] - lg > 2 * e
+        tie = (lg > SAT + 2 * e) & (lg[sel] > SAT + 2 * e) & (idx > sel)
+        lead = float((lg[sel] - lg[other & ~tie]).min()) if bool((other & ~tie).any()) else float("inf")
+        leads.append(lead)
+        decs.append(bool((below | tie | ~other).all()))
+        agree.append(int(best[i, 5]) == sel)
+        if not agree[-1]:
+            gi = int(best[i, 5])
+            print(f"frame {i}: GPU prior {gi} (fp32 {float(lg[gi]):.3f}, GPU {float(cand[i, gi, 5]):.3f}), fp32 "
+                  f"selection {sel} (fp32 {float(lg[sel]):.3f}, GPU {float(cand[i, sel, 5]):.3f}), lead {lead:.3f}, "
+                  f"peak-region error {e:.3f}, decidable {decs[-1]}")
+    leads, agree, errs, dec = np.array(leads), np.array(agree), np.array(errs), np.array(decs)
+    print(f"peaked detector: median |d logit| per frame {np.median(dmed):.3f} (max {max(dmed):.3f}); peak-region "
+          f"|d logit| median {np.median(errs):.3f} (max {errs.max():.3f}); fp32 top-1 lead median "
+          f"{np.median(leads):.2f}; decidable {dec.sum()}/{n}, agreement there "
+          f"{agree[dec].mean():.3f}; agreement overall {agree.mean():.3f}")
+    assert dec.mean() >= 0.6
+    assert agree[dec].mean() >= 0.95
 
 
 def test_pose_estimator_with_detector(det640):
