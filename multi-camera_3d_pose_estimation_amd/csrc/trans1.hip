@@ -52,9 +52,13 @@ struct T1C {
     static constexpr int F0 = TH * W / 32;                 // t0 fragments per tile (24)
     static constexpr int H1 = TH / 2, W1 = W / 2;          // t1 rows / columns per tile
     static constexpr int F1 = H1 * W1 / 32;                // t1 fragments per tile (6)
-    static constexpr int NF0 = 4, NF1 = 6;                 // fragments per t0 / t1 wave
-    static constexpr int ST1 = 2 * NF1;                    // epilogue stores per t1 wave
-    static_assert(F0 == 6 * NF0 && F1 == NF1, "6 t0 waves x 4 fragments, 2 t1 waves (cout groups)");
+    // waves 0-3 run t0 (6 fragments each), waves 4-7 t1 (one 32-cout group, 3 fragments each):
+    // every SIMD hosts one wave of each role, 54 + 27 MFMAs per item (the former 6 + 2 split
+    // put 90 on two SIMDs and 72 on the others)
+    static constexpr int NF0 = 6, NF1 = 3;                 // fragments per t0 / t1 wave
+    static constexpr int NFM = NF0 > NF1 ? NF0 : NF1;
+    static constexpr int ST1 = 2 * NFM;                    // epilogue stores per wave (at most)
+    static_assert(F0 == 4 * NF0 && F1 == 2 * NF1, "4 t0 waves x 6 fragments, 4 t1 waves (2 cout groups x 3)");
     static_assert(LDS <= 160 * 1024, "LDS budget");
     static_assert(H % TH == 0 && C % 16 == 0, "tiling");
     static_assert(PPW < 48 && ST1 < 48, "vmcnt range");
@@ -83,7 +87,7 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     if ((int)blockIdx.x >= p.n_tiles) return;
     constexpr int tiles_h = G::H / G::TH;
-    const bool is_t1 = wave >= 6;
+    const bool is_t1 = wave >= 4;
     const uint16_t* zl = p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8;
 
     // ---- per-lane DMA geometry of this wave's item pieces (fixed for the launch)
@@ -137,9 +141,9 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
     };
 
     // ---- fragment geometry: t0 waves fragments f = wave * 4 + i, t1 waves f = i (cout group wave - 6)
-    int bv[G::NF1], eo[G::NF1];
+    int bv[G::NFM], eo[G::NFM];
 #pragma unroll
-    for (int i = 0; i < G::NF1; i++) {
+    for (int i = 0; i < G::NFM; i++) {
         if (!is_t1) {
             const int f = (i < G::NF0) ? wave * G::NF0 + i : 0;
             const int pp = frag_pixel<G::W, G::TH, 1>(f, r32);
@@ -147,13 +151,14 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
             bv[i] = (h * G::QS + (ty * G::RS + x) * G::PS) * 16;  // tap (0,0) of (ty, x): pixel 1 + (ty-1+1)*RS + x-1
             eo[i] = ty * G::W + x;
         } else {
-            const int pp = i * 32 + r32;                 // t1: 8 rows x 24 columns, generic order
+            const int fi = i < G::NF1 ? ((wave - 4) >> 1) * G::NF1 + i : 0;
+            const int pp = fi * 32 + r32;                // t1: 8 rows x 24 columns, generic order
             const int ro = pp / G::W1, c = pp - ro * G::W1;
             bv[i] = (h * G::QS + (2 * ro * G::RS + 2 * c) * G::PS) * 16;  // y (2ro-1, 2c-1): pixel 1 + 2ro*RS + 2c - 1
             eo[i] = ro * G::W1 + c;
         }
     }
-    const int mg1 = wave - 6;
+    const int mg1 = (wave - 4) & 1;
     const int av = is_t1 ? (G::WB + h * 64 + mg1 * 32 + r32) * 16 : (G::WA + h * 32 + r32) * 16;
     float* sbias = reinterpret_cast<float*>(lds + 2 * G::BUF);
     if (tid < 32) sbias[tid] = p.b0[tid];
