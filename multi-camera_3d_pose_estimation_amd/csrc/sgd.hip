@@ -183,7 +183,12 @@ __device__ __forceinline__ float quad_cost(const Target& g, float d0, float d1) 
     return 0.5f * ((d0 * g.a00 + d1 * g.a10) * d0 + (d0 * g.a01 + d1 * g.a11) * d1);
 }
 
-constexpr int kU = 4;   // points per thread in flight (independent loads issued together)
+// points per thread in flight (independent loads issued together): 4 in the 256-thread
+// workgroups (one wave per SIMD, ILP hides the latency); 1 in the 1,024-thread config-5 kernel,
+// whose 4 waves per SIMD need <= 128 VGPRs (kU = 4 spills there; kU = 1 and 2 ran level:
+// profiles/r04_sgd_occupancy_ab.txt)
+template <int BS>
+constexpr int points_in_flight() { return BS >= 1024 ? 1 : 4; }
 
 constexpr int kRedCols = 2 * kCamGrad;  // widest block reduction: both learnable cameras' gradients
 
@@ -200,13 +205,17 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NC]) {
 #pragma unroll
         for (int i = 0; i < NV; i++) red[w][i] = v[i];
     __syncthreads();
+    // wave partials added in wave order; the k loop stays rolled, so only NV sums are live
+    // (unrolled, the compiler loaded all BS / 64 x NV partials at once: 96 VGPRs at BS = 1,024)
+    double s[NV];
 #pragma unroll
-    for (int i = 0; i < NV; i++) {
-        double s = 0.0;
+    for (int i = 0; i < NV; i++) s[i] = 0.0;
+#pragma unroll 1
+    for (int k = 0; k < BS / 64; k++)
 #pragma unroll
-        for (int k = 0; k < BS / 64; k++) s += red[k][i];
-        v[i] = s;
-    }
+        for (int i = 0; i < NV; i++) s[i] += red[k][i];
+#pragma unroll
+    for (int i = 0; i < NV; i++) v[i] = s[i];
 }
 
 __device__ __forceinline__ bool finite(float x) { return !(isnan(x) || isinf(x)); }
@@ -222,6 +231,7 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     __shared__ float cstate[kMaxLearn * 2 * kCamGrad];  // Adam m | v of the learnable R, T
     __shared__ float cgrad[kMaxLearn * kCamGrad];       // the window's reduced camera gradient
 
+    constexpr int kU = points_in_flight<BS>();
     const int m = blockIdx.x, tid = threadIdx.x;
     const int T = a.T, V = a.V, J = a.J, B = a.B, NS = a.n_seg;
     const int TJ = T * J, n3 = TJ * 3;
@@ -800,10 +810,10 @@ void sgd_launch(const float* gauss, const float* traj0, const float* cams, int M
         MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdsBudget));
         hipLaunchKernelGGL((sgd_kernel<256, true>), dim3(M), dim3(256), lds, s, a);
-    } else if (T * J > 1024) {
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<512, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    } else if (T * J > 1024) {  // 16 waves: 4 per SIMD (M = 256 config 5: 0.211 -> 0.170 ms per iteration vs 512)
+        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdsBudget));
-        hipLaunchKernelGGL((sgd_kernel<512, false>), dim3(M), dim3(512), lds, s, a);
+        hipLaunchKernelGGL((sgd_kernel<1024, false>), dim3(M), dim3(1024), lds, s, a);
     } else {
         MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)kLdsBudget));

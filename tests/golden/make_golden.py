@@ -203,7 +203,7 @@ def gen_sgd(pr):
 
 
 C5_CASES = [
-    # BASELINE config 5 (V=8, T=400): T*J = 399*17 > 1024 runs sgd_kernel<512, false> (csrc/sgd.hip).
+    # BASELINE config 5 (V=8, T=400): T*J = 399*17 > 1024 runs sgd_kernel<1024, false> (csrc/sgd.hip).
     # name, seed, kwargs
     ("sgd_V8_T400", 65, dict(lr=0.01, lambda_smooth=1e-6, lambda_body_length=1.0, patience=100, max_iter=8,
                              batch_size=None)),

@@ -73,7 +73,7 @@ def test_sgd_matches_reference_golden(refine, case):
 @pytest.mark.parametrize("case", C5_CASES)
 def test_sgd_config5_matches_reference_golden(refine, case):
     """BASELINE config 5 at its own size (V=8, T=400 -> 399 rows after time_interval [0, -1]):
-    T*J = 6,783 > 1024 runs sgd_kernel<512, false> (the bench's kernel), trajectory in LDS.
+    T*J = 6,783 > 1024 runs sgd_kernel<1024, false> (the bench's kernel), trajectory in LDS.
     One window (8 iterations), overlapping windows of 100 (7 windows), early stop (64
     iterations, patience 3)."""
     from mvpose import refine as _r
