@@ -518,16 +518,33 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                 const float denom = sqrtf(vv) / bc2s + eps;
                 *prm = *prm + nstep * mv / denom;
             }
-            for (int e = tid; e < n3; e += BS) {
-                const float g = (e >= wlo && e < whi) ? gb[e - wlo] * coef : 0.f;
-                float mv = mo[e];
-                mv = (w1 < 0.5f) ? mv + w1 * (g - mv) : g - (g - mv) * (1.f - w1);
-                float vv = ve[e] * b2;
-                vv = vv + w2 * g * g;
-                mo[e] = mv;
-                ve[e] = vv;
-                const float denom = sqrtf(vv) / bc2s + eps;
-                X[e] = X[e] + nstep * mv / denom;
+            // kA coordinates per thread per round, every load issued before the first store
+            // (the stores could alias the next coordinate's loads for the compiler)
+            constexpr int kA = 4;
+            for (int e0 = tid; e0 < n3; e0 += kA * BS) {
+                float gg[kA], m0[kA], v0[kA], x0[kA];
+#pragma unroll
+                for (int u = 0; u < kA; u++) {
+                    const int e = min(e0 + u * BS, n3 - 1);
+                    gg[u] = (e >= wlo && e < whi) ? gb[e - wlo] : 0.f;
+                    m0[u] = mo[e];
+                    v0[u] = ve[e];
+                    x0[u] = X[e];
+                }
+#pragma unroll
+                for (int u = 0; u < kA; u++) {
+                    const int e = e0 + u * BS;
+                    if (e >= n3) break;
+                    const float g = (e >= wlo && e < whi) ? gg[u] * coef : 0.f;
+                    float mv = m0[u];
+                    mv = (w1 < 0.5f) ? mv + w1 * (g - mv) : g - (g - mv) * (1.f - w1);
+                    float vv = v0[u] * b2;
+                    vv = vv + w2 * g * g;
+                    mo[e] = mv;
+                    ve[e] = vv;
+                    const float denom = sqrtf(vv) / bc2s + eps;
+                    X[e] = x0[u] + nstep * mv / denom;
+                }
             }
             __syncthreads();
 
