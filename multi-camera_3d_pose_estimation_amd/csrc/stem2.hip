@@ -74,7 +74,7 @@ struct StemParams {
     int N, n_tiles;
 };
 
-__global__ __launch_bounds__(512, 1) void stem2_kernel(StemParams p) {
+__global__ __launch_bounds__(512, 1) void stem2_tile_kernel(StemParams p) {
     using G = S2;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
@@ -277,6 +277,303 @@ __global__ __launch_bounds__(512, 1) void stem2_kernel(StemParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+
+// ------------------------------------------------------------------ streaming version
+// Same arithmetic as stem2_tile_kernel (conv1: 3 k-steps of taps 4s + 2h + j; conv2: 36
+// k-steps (tap, 16-channel quarter) from the bias), hence bit-identical to it, but:
+//  * each workgroup walks whole crops top to bottom in strips of 2 conv2 rows; conv1's rows
+//    go into a 10-row LDS ring (virtual row v = crop * 129 + conv1 row + 1, row -1 = conv2's
+//    zero padding), so no conv1 row is computed twice (the tile kernel recomputed 1 of 5);
+//  * warp-specialised phases, one barrier each: waves 4-7 run conv1 of strip g (4 new rows:
+//    6 of the 12 fragments x one 32-cout group each), waves 0-3 conv2 of strip g-1 (32-pixel
+//    x 32-cout units: two interleaved chains on waves 0-1, one on waves 2-3; the cout group's
+//    36 A fragments resident in 144 VGPRs); in the tile kernel conv1 and conv2 were
+//    barrier-separated and two of the four SIMDs ran half of conv2's units.  Measured
+//    (profiles/r04_stem2_streaming_ab.txt): 6 conv2 + 2 conv1 waves left the conv1 waves
+//    the critical path (their LDS-read latency), 4 + 4 runs 15 % under the tile kernel;
+//  * the input rows of strip g+1 (9 rows, 14 KB) land by LDS-DMA into the second input
+//    buffer under phase g.
+// Ring layout [ring row][image O | E][plane (8 ch)][49 slots]: every conv2 tap is a per-row
+// base register + an immediate below 11 KB.
+struct S2S {
+    static constexpr int H = 256, W = 192, H1 = 128, W1 = 96, H2 = 64, W2 = 48;
+    static constexpr int STRIPS = H2 / 2;              // strips of 2 conv2 rows per crop
+    static constexpr int VR = H1 + 1;                  // virtual conv1 rows per crop (row -1 = zero)
+    static constexpr int NR = 10;                      // ring rows (widest live span: crop boundary)
+    static constexpr int RS = W2 + 1;                  // slots per image row
+    static constexpr int ROWB = 2 * 8 * RS * 16;       // bytes per ring row (O and E, 8 planes)
+    static constexpr int XP = W + 4;                   // staged input row: 2 zero pixels each side
+    static constexpr int XPIECES = XP * 8 / 16;        // 98
+    static constexpr int XROWS = 9;                    // input rows per strip
+    static constexpr int XN = XROWS * XPIECES;         // 882 pieces
+    static constexpr int XINSTR = (XN + 63) / 64;      // 14 wave DMA instructions
+    static constexpr int MOFF = 0;
+    static constexpr int XOFF = MOFF + NR * ROWB;      // 2 input buffers
+    static constexpr int XBYTES = XINSTR * 1024;
+    static constexpr int BOFF = XOFF + 2 * XBYTES;
+    static constexpr int LDS = BOFF + 2 * 64 * 4;
+    static constexpr int F1 = 4 * W1 / 32;             // 12 conv1 fragments per strip
+    static constexpr int F2 = 2 * W2 / 32;             // 3 conv2 fragments per strip
+    static_assert(LDS <= 160 * 1024, "LDS budget");
+    static_assert((6 * RS + 8 * RS) * 16 < 65536, "ds_read offset range (conv2 B)");
+    static_assert(XINSTR <= 2 * 8 - 2, "DMA split: 2 pieces on waves 0-5, 1 on waves 6-7");
+    static_assert(F2 == 3 && F1 == 2 * 2 * 3, "roles: conv2 fragments 0, 1 | 2; conv1 halves of 2 groups of 3");
+};
+
+__global__ __launch_bounds__(512, 1) void stem2_kernel(StemParams p) {
+    using G = S2S;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r32 = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int crop0 = (int)(((long)p.N * b) / nb), crop1 = (int)(((long)p.N * (b + 1)) / nb);
+    const int n_strips = (crop1 - crop0) * G::STRIPS;
+    if (n_strips == 0) return;  // whole workgroup: uniform
+    const uint16_t* zl = p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8;
+
+    // ---- the ring starts zero (O[r][0] = conv1 column -1 stays zero for the launch)
+    for (int i = tid; i < G::NR * G::ROWB / 16; i += 512)
+        *reinterpret_cast<uint4*>(lds + G::MOFF + i * 16) = uint4{0u, 0u, 0u, 0u};
+    float* sbias = reinterpret_cast<float*>(lds + G::BOFF);
+    if (tid < 64) sbias[tid] = p.b1[tid];
+    else if (tid < 128) sbias[tid] = p.b2[tid - 64];
+
+    // ---- input DMA: instruction j of a strip = pieces 64j .. 64j + 63 ([row][piece]);
+    // this wave issues j = wave and wave + 8 (< 14)
+    int xg[2];  // (row + 1) << 8 | piece, 0 = zero piece
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+        const int i = (wave + m * 8) * 64 + lane;
+        const int row = i / G::XPIECES, k = i - row * G::XPIECES;
+        xg[m] = (i < G::XN && k >= 1 && k <= G::W / 2) ? ((row + 1) << 8) | k : 0;
+    }
+    auto issue = [&](int g) {  // strip g's 9 input rows -> buffer g & 1
+        const int n = crop0 + g / G::STRIPS, s = g % G::STRIPS;
+        const uint16_t* xb = p.x + (long)n * G::H * G::W * 4;
+        uint8_t* dst = lds + G::XOFF + (g & 1) * G::XBYTES;
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            const int j = wave + m * 8;
+            if (j < G::XINSTR) {
+                const int gg = xg[m], row = (gg >> 8) - 1, k = gg & 255;
+                const int gr = 8 * s - 1 + row;
+                const bool in = gg != 0 && (unsigned)gr < (unsigned)G::H;
+                glds16(in ? xb + ((long)gr * G::W + 2 * (k - 1)) * 4 : zl, dst + j * 1024);
+            }
+        }
+    };
+    auto ring = [](int v) { return (v % G::NR) * G::ROWB; };
+
+    if (wave < 4) {
+        // ================= conv2 waves: cout group mg2 = wave & 1; waves 0-1 fragments 0 and 1
+        // (two interleaved chains), waves 2-3 fragment 2
+        const int mg2 = wave & 1;
+        bf16x8 wa[36];
+        {
+            const int co = mg2 * 32 + row_cout(r32);
+#pragma unroll
+            for (int st = 0; st < 36; st++) {
+                const int tap = st >> 2, kq = st & 3;
+                wa[st] = *reinterpret_cast<const bf16x8*>(p.w2 + (co * 9 + tap) * 64 + 16 * kq + 8 * h);
+            }
+        }
+        auto run = [&](auto NUc) {
+            constexpr int NU = decltype(NUc)::value;
+            int lr[NU], c[NU];
+#pragma unroll
+            for (int u = 0; u < NU; u++) {
+                const int f2 = NU == 2 ? u : 2;
+                const int pp = frag_pixel<G::W2, 2, 1>(f2, r32);
+                lr[u] = pp / G::W2;
+                c[u] = pp - lr[u] * G::W2;
+            }
+            issue(0);
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            for (int g = 0; g <= n_strips; g++) {
+                if (g + 1 < n_strips) issue(g + 1);
+                asm volatile("" ::: "memory");
+                if (g >= 1) {
+                    const int cl = (g - 1) / G::STRIPS, s = (g - 1) % G::STRIPS;
+                    const int v0 = cl * G::VR + 4 * s;  // conv1 row 4s - 1
+                    int bvd[NU][3];
+#pragma unroll
+                    for (int u = 0; u < NU; u++)
+#pragma unroll
+                        for (int dy = 0; dy < 3; dy++)
+                            bvd[u][dy] = G::MOFF + ring(v0 + 2 * lr[u] + dy) + (h * G::RS + c[u]) * 16;
+                    f32x16 acc[NU];
+                    {
+                        const float4* bb = reinterpret_cast<const float4*>(sbias + 64 + mg2 * 32 + 16 * h);
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const float4 q = bb[j];
+                            acc[0][4 * j] = q.x;
+                            acc[0][4 * j + 1] = q.y;
+                            acc[0][4 * j + 2] = q.z;
+                            acc[0][4 * j + 3] = q.w;
+                        }
+#pragma unroll
+                        for (int u = 1; u < NU; u++) acc[u] = acc[0];
+                    }
+                    constexpr int kPF = NU == 2 ? 4 : 6;
+                    bf16x8 fb[kPF + 1][NU];
+                    auto load = [&](int st) {
+                        const int tap = st >> 2, kq = st & 3, dy = tap / 3, dx = tap % 3;
+#pragma unroll
+                        for (int u = 0; u < NU; u++)
+                            fb[st % (kPF + 1)][u] = *reinterpret_cast<const bf16x8*>(
+                                lds + bvd[u][dy] + (2 * kq * G::RS + (dx == 1 ? 8 * G::RS : dx == 2 ? 1 : 0)) * 16);
+                    };
+#pragma unroll
+                    for (int st = 0; st < kPF; st++) load(st);
+#pragma unroll
+                    for (int st = 0; st < 36; st++) {
+                        if (st + kPF < 36) load(st + kPF);
+                        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                        for (int u = 0; u < NU; u++)
+                            acc[u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[st], fb[st % (kPF + 1)][u], acc[u], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+#pragma unroll
+                    for (int u = 0; u < NU; u++) {
+                        uint32_t o[8];
+#pragma unroll
+                        for (int e = 0; e < 8; e++) o[e] = pack_bf16x2(relu1(acc[u][2 * e]), relu1(acc[u][2 * e + 1]));
+                        uint16_t* yp = p.y + (((long)(crop0 + cl) * G::H2 + 2 * s + lr[u]) * G::W2 + c[u]) * 64 +
+                                       mg2 * 32 + 16 * h;
+                        *reinterpret_cast<uint4*>(yp) = uint4{o[0], o[1], o[2], o[3]};
+                        *reinterpret_cast<uint4*>(yp + 8) = uint4{o[4], o[5], o[6], o[7]};
+                    }
+                    // the next strip's input has landed (the 2 NU stores are younger)
+                    if constexpr (NU == 2)
+                        asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+                    else
+                        asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                }
+                __builtin_amdgcn_s_barrier();
+            }
+        };
+        if (wave < 2)
+            run(std::integral_constant<int, 2>{});
+        else
+            run(std::integral_constant<int, 1>{});
+    } else {
+        // ================= conv1 waves: cout group mg1, fragments 6 half .. 6 half + 5 in 2 groups of 3
+        const int mg1 = wave & 1, half = (wave - 4) >> 1;
+        bf16x8 a1[3];
+        {
+            const int co = mg1 * 32 + row_cout(r32);
+#pragma unroll
+            for (int st = 0; st < 3; st++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) {
+                    const int tap = 4 * st + 2 * h + (j >> 2), ch = j & 3;
+                    a1[st][j] = (__bf16)(tap < 9 ? p.w1[(co * 9 + tap) * 4 + ch] : 0.f);
+                }
+        }
+        int toff[3][2];
+#pragma unroll
+        for (int st = 0; st < 3; st++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const int tap = 4 * st + 2 * h + j;
+                toff[st][j] = tap < 9 ? ((tap / 3) * G::XP + tap % 3) * 8 : -1;
+            }
+        constexpr int NF = G::F1 / 2;
+        int xo[NF], mo[NF], cro[NF];  // staged-input offset, ring slot offset, conv1 row in strip
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            const int pp = frag_pixel<G::W1, 4, 1>(half * NF + f, r32);
+            const int cr = pp / G::W1, cc = pp - cr * G::W1;
+            cro[f] = cr;
+            xo[f] = ((2 * cr) * G::XP + 2 * cc + 1) * 8;
+            const int img = (cc & 1) ? 0 : 1, j = (cc & 1) ? (cc + 1) / 2 : cc / 2;
+            mo[f] = ((img * 8 + mg1 * 4 + 2 * h) * G::RS + j) * 16;
+        }
+        issue(0);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        for (int g = 0; g <= n_strips; g++) {
+            if (g + 1 < n_strips) issue(g + 1);
+            asm volatile("" ::: "memory");
+            if (g < n_strips) {
+                const int cl = g / G::STRIPS, s = g % G::STRIPS;
+                const int v0 = cl * G::VR + 4 * s;
+                const uint8_t* xb = lds + G::XOFF + (g & 1) * G::XBYTES;
+                if (s == 0)  // conv1 row -1: conv2's zero padding
+                    for (int i = (wave - 4) * 64 + lane; i < G::ROWB / 16; i += 256)
+                        *reinterpret_cast<uint4*>(lds + G::MOFF + ring(v0) + i * 16) = uint4{0u, 0u, 0u, 0u};
+                f32x16 bias;
+                {
+                    const float4* bb = reinterpret_cast<const float4*>(sbias + mg1 * 32 + 16 * h);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const float4 q = bb[j];
+                        bias[4 * j] = q.x;
+                        bias[4 * j + 1] = q.y;
+                        bias[4 * j + 2] = q.z;
+                        bias[4 * j + 3] = q.w;
+                    }
+                }
+                // a group's 24 input reads are issued one group ahead (the MFMAs of a 3-step
+                // group cover too little of the LDS latency on their own)
+                uint2 raw[2][3][3][2];
+                auto load_grp = [&](int grp, uint2 (&r)[3][3][2]) {
+#pragma unroll
+                    for (int st = 0; st < 3; st++)
+#pragma unroll
+                        for (int i = 0; i < 3; i++)
+#pragma unroll
+                            for (int j = 0; j < 2; j++)
+                                r[st][i][j] = *reinterpret_cast<const uint2*>(xb + xo[grp * 3 + i] + max(toff[st][j], 0));
+                };
+                load_grp(0, raw[0]);
+#pragma unroll
+                for (int grp = 0; grp < 2; grp++) {
+                    if (grp + 1 < 2) load_grp(grp + 1, raw[(grp + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    f32x16 acc[3];
+#pragma unroll
+                    for (int i = 0; i < 3; i++) acc[i] = bias;
+#pragma unroll
+                    for (int st = 0; st < 3; st++) {
+                        bf16x8 bf[3];
+#pragma unroll
+                        for (int i = 0; i < 3; i++) {
+                            union {
+                                uint2 u[2];
+                                bf16x8 v;
+                            } t;
+#pragma unroll
+                            for (int j = 0; j < 2; j++) t.u[j] = toff[st][j] >= 0 ? raw[grp & 1][st][i][j] : uint2{0u, 0u};
+                            bf[i] = t.v;
+                        }
+#pragma unroll
+                        for (int i = 0; i < 3; i++)
+                            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[st], bf[i], acc[i], 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int i = 0; i < 3; i++) {
+                        const int f = grp * 3 + i;
+                        uint32_t o[8];
+#pragma unroll
+                        for (int e = 0; e < 8; e++) o[e] = pack_bf16x2(relu1(acc[i][2 * e]), relu1(acc[i][2 * e + 1]));
+                        uint8_t* d = lds + G::MOFF + ring(v0 + 1 + cro[f]) + mo[f];
+                        *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
+                        *reinterpret_cast<uint4*>(d + G::RS * 16) = uint4{o[4], o[5], o[6], o[7]};
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+        }
+    }
+}
+
 int g_s2_cus = 0;
 
 }  // namespace
@@ -293,7 +590,7 @@ void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uin
     if (N == 0) return;
     static bool attr = false;
     if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)stem2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S2::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)stem2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, S2S::LDS));
         attr = true;
     }
     if (g_s2_cus == 0) {
@@ -301,11 +598,26 @@ void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uin
         MVP_HIP(hipGetDevice(&dev));
         MVP_HIP(hipDeviceGetAttribute(&g_s2_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    const long tiles = (long)N * (S2::H2 / S2::TR);
-    MVP_REQUIRE(tiles < (1L << 30), "stem2: too many tiles");
-    StemParams p{x, w1, b1, w2, b2, y, conv_zero_region(), N, (int)tiles};
-    const int grid = (int)std::min<long>(tiles, g_s2_cus);
-    hipLaunchKernelGGL(stem2_kernel, dim3(grid), dim3(S2::NTH), S2::LDS, s, p);
+    const char* e = getenv("MVPOSE_STEM2_TILE");  // tests: the tile kernel (bit-identical reference)
+    if (e && e[0] == '1') {
+        static bool attr_t = false;
+        if (!attr_t) {
+            MVP_HIP(hipFuncSetAttribute((const void*)stem2_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        S2::LDS));
+            attr_t = true;
+        }
+        const long tiles = (long)N * (S2::H2 / S2::TR);
+        MVP_REQUIRE(tiles < (1L << 30), "stem2: too many tiles");
+        StemParams p{x, w1, b1, w2, b2, y, conv_zero_region(), N, (int)tiles};
+        const int grid = (int)std::min<long>(tiles, g_s2_cus);
+        hipLaunchKernelGGL(stem2_tile_kernel, dim3(grid), dim3(S2::NTH), S2::LDS, s, p);
+        MVP_HIP(hipGetLastError());
+        return;
+    }
+    MVP_REQUIRE(N < (1 << 24), "stem2: too many crops");
+    StemParams p{x, w1, b1, w2, b2, y, conv_zero_region(), N, 0};
+    const int grid = std::min(N, g_s2_cus);
+    hipLaunchKernelGGL(stem2_kernel, dim3(grid), dim3(512), S2S::LDS, s, p);
     MVP_HIP(hipGetLastError());
 }
 

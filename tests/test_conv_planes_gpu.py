@@ -249,6 +249,33 @@ def test_bottleneck_join(cat, pair, monkeypatch):
     assert (dev - ref).abs().max().item() <= 3 * ulp, ((dev - ref).abs().max().item(), ulp)
 
 
+@pytest.mark.parametrize("n", [1, 5, 13, 300])
+def test_stem2_streaming_bitwise_equals_tile_kernel(n, monkeypatch):
+    """The streaming stem2 kernel (conv1 rows in a ring, warp-specialised conv1 / conv2 waves,
+    one workgroup per crop range) against the tile kernel (MVPOSE_STEM2_TILE=1): same K order
+    and MFMA sequence per output, so bit-identical; n covers one crop per workgroup, ragged
+    ranges and more crops than CUs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    spec, xi, yo, sd = hrnet.stem_spec(seed=33)
+    gen = torch.Generator().manual_seed(34)
+    x = torch.zeros((n, 256, 192, 4))
+    x[..., :3] = torch.randn((n, 256, 192, 3), generator=gen)
+    xb = x.bfloat16().cuda()
+    outs = {}
+    for tile in ("1", "0"):
+        monkeypatch.setenv("MVPOSE_STEM2_TILE", tile)
+        g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+        out = torch.full((n, 64, 48, 64), float("nan"), dtype=torch.bfloat16, device="cuda")
+        g.run(xb, out)
+        torch.cuda.synchronize()
+        g.close()
+        outs[tile] = out.cpu()
+    assert torch.isfinite(outs["0"].float()).all()
+    assert torch.equal(outs["0"].view(torch.int16), outs["1"].view(torch.int16))
+
+
 @pytest.mark.parametrize("fused", [False, True])
 def test_stem_vs_reference(fused, monkeypatch):
     """HRNet stem conv1 (3x3/s2, 4 -> 64) + conv2 (3x3/s2, 64 -> 64): the fused stem2.hip

@@ -7,7 +7,8 @@ rows = defaultdict(lambda: defaultdict(float))
 calls = defaultdict(set)
 for path in sys.argv[1:]:
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].replace("void mvp::(anonymous namespace)::", "").split("(")[0][:44]
+        name = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "").replace("mvp::", "")
+        name = name.split("(")[0][:44]
         rows[name][r["Counter_Name"]] += float(r["Counter_Value"])
         calls[name].add(r["Dispatch_Id"])
 cols = sorted({c for v in rows.values() for c in v})
