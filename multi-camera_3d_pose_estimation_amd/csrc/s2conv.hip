@@ -69,7 +69,7 @@ struct SCfg {
     static_assert(LDS <= 160 * 1024, "LDS budget");
     static_assert((QS + (3 * PH + RS + 1) * PS) * 16 < 65536 && (16 * BM + 2 * BM) * 16 < 65536,
                   "ds_read offset range");
-    static_assert(STORES < 64 && PPW < 64, "vmcnt range");
+    static_assert(STORES < 64 && 2 * PPW < 64, "vmcnt range");
     static_assert(2 * TH + 1 < 256, "row index packing");
 };
 
@@ -108,11 +108,22 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
     };
 
     // ---- per-lane DMA geometry (fixed for the launch)
-    // pk: kind << 28 | nb << 8 | hy (kind 0 zero, 1 halo, 2 weight; hy = input row - 2*ho0 + 1)
-    int pk[G::PPW], po[G::PPW];
+    // pk: kind << 28 | nb << 8 | hy (kind 0 zero, 1 halo, 2 weight; hy = input row - 2*ho0 + 1).
+    // Streamed-weight planes (!WRES): waves 0-3 issue the item pieces of virtual waves vw = wave
+    // and wave + 4 (their SIMD partner), waves 4-7 none: after the item barrier one wave per
+    // SIMD starts its MFMAs at once while the other issues the DMA (tconv16.hip; 4-6 % per
+    // launch, profiles/r04_dma_split_ab.txt).  The resident-weight planes (halo-only items)
+    // measured level to 2 % slower that way, so every wave issues its own pieces there.
+    constexpr bool SPLIT = !WRES;
+    constexpr int NVW = SPLIT ? 2 : 1;
+    const bool dma_wave = !SPLIT || wave < 4;
+    auto vwave = [&](int v) { return SPLIT ? (wave & 3) + 4 * v : wave; };
+    int pk[NVW][G::PPW], po[NVW][G::PPW];
+#pragma unroll
+    for (int v = 0; v < NVW; v++)
 #pragma unroll
     for (int j = 0; j < G::PPW; j++) {
-        const int s = (j * G::NW + wave) * 64 + lane;
+        const int s = (j * G::NW + vwave(v)) * 64 + lane;
         int kind = 0, off = 0, nb = 0, hy = 0;
         if (s < G::HT) {
             const int qh = PM ? s & 1 : s / G::HS, hs = PM ? s >> 1 : s - (s / G::HS) * G::HS;
@@ -130,8 +141,8 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
             kind = 2;
             off = p.img ? (s - G::HT) * 8 : wsrc_off(s - G::HT);
         }
-        pk[j] = (kind << 28) | (nb << 8) | hy;
-        po[j] = off;
+        pk[v][j] = (kind << 28) | (nb << 8) | hy;
+        po[v][j] = off;
     }
     const uint16_t* zl = p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8;
 
@@ -149,14 +160,18 @@ __global__ __launch_bounds__(512, 1) void s2conv_kernel(SParams p) {
         const uint16_t* wb =
             p.img ? p.w + (long)(cb * G::NCH + slice) * G::WT * 8 : p.w + (long)cb * BM * 9 * CIN + slice * 16;
         uint8_t* dst = lds + buf * G::BUF;
+        if (!dma_wave) return;
+#pragma unroll
+        for (int v = 0; v < NVW; v++)
 #pragma unroll
         for (int j = 0; j < G::PPW; j++) {
-            const int g = pk[j], kind = g >> 28, nb = (g >> 8) & 255, hy = g & 255;
+            const int vw = vwave(v);
+            const int g = pk[v][j], kind = g >> 28, nb = (g >> 8) & 255, hy = g & 255;
             const bool in = kind == 1 && (unsigned)(2 * ho0 + hy - 1) < (unsigned)H && n0 + nb < p.N;
-            const uint16_t* src = (!WRES && kind == 2) ? wb + po[j] : in ? xb + po[j] : zl;
+            const uint16_t* src = (!WRES && kind == 2) ? wb + po[v][j] : in ? xb + po[v][j] : zl;
             // pieces wholly past the item's slots are not issued (the 128->256 plane: 4 of 72)
-            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::ITEM_SLOTS)
-                glds16(src, dst + (j * G::NW + wave) * 1024);
+            if (j < G::PPW - 1 || (j * G::NW + vw) * 64 < G::ITEM_SLOTS)
+                glds16(src, dst + (j * G::NW + vw) * 1024);
         }
     };
 

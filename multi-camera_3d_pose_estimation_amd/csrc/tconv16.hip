@@ -58,7 +58,7 @@ struct T16Cfg {
     static_assert(P == PG * NT * 32 && NW % MG == 0, "tile = pixel groups x 3 fragments x 32 pixels");
     static_assert(H % TH == 0 && CIN % 16 == 0, "tiling");
     static_assert(((2 * RS + 2) * 3 + 1) * 16 < 65536 && (18 * BM) * 16 < 65536, "ds_read offset range");
-    static_assert(STORES + 2 * NA * NT < 64 && PPW < 64, "vmcnt range");
+    static_assert(STORES + 2 * NA * NT < 64 && 2 * PPW < 64, "vmcnt range");
     static_assert(LDS <= 160 * 1024, "LDS budget");
     static_assert(NB <= 31 && HR <= 31 && (long)BM * 9 * CIN < (1 << 19) && (long)NB * H * W * CIN < (1 << 19),
                   "DMA geometry packing");
@@ -120,11 +120,19 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
     constexpr int tiles_h = H / TH;
     const bool do_st = !(p.diag & 2);
 
-    // ---- per-lane DMA geometry (fixed for the launch): kind << 29 | nb << 24 | hy << 19 | offset
-    int pk[G::PPW];
+    // ---- per-lane DMA geometry (fixed for the launch): kind << 29 | nb << 24 | hy << 19 | offset.
+    // Waves 0-3 issue the pieces of "virtual waves" vw = wave and wave + 4 (their SIMD partner),
+    // waves 4-7 issue none: after the item barrier one wave per SIMD starts its MFMAs at once
+    // while the other issues the DMA, instead of both issuing before either computes
+    // (4-6 % per launch, profiles/r04_dma_split_ab.txt).
+    const bool dma_wave = wave < 4;
+    int pk[2][G::PPW];
+#pragma unroll
+    for (int v = 0; v < 2; v++)
 #pragma unroll
     for (int j = 0; j < G::PPW; j++) {
-        const int s = (j * G::NW + wave) * 64 + lane;
+        const int vw = (wave & 3) + 4 * v;
+        const int s = (j * G::NW + vw) * 64 + lane;
         int kind = 0, off = 0, nb = 0, hy = 0;
         if (s < G::HT) {
             const int hp = s / 3, q = s - hp * 3;
@@ -143,7 +151,7 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
             kind = 2;
             off = (s - G::HT) * 8;
         }
-        pk[j] = (kind << 29) | (nb << 24) | (hy << 19) | off;
+        pk[v][j] = (kind << 29) | (nb << 24) | (hy << 19) | off;
     }
     const uint16_t* zl = p.zero + ((wave * 64 + lane) & (kZeroSlots16 - 1)) * 8;
 
@@ -163,14 +171,18 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
         const uint16_t* xb = p.x + ((long)(n0 * H + ho0) * W) * CIN + chunk * 16;
         const uint16_t* wb = p.w + (long)(cb * G::NCH + chunk) * G::WT * 8;
         uint8_t* dst = lds + buf * G::BUF;
+        if (!dma_wave) return;
+#pragma unroll
+        for (int v = 0; v < 2; v++)
 #pragma unroll
         for (int j = 0; j < G::PPW; j++) {
-            const int g = pk[j], kind = g >> 29, nb = (g >> 24) & 31, hy = (g >> 19) & 31, off = g & 0x7ffff;
+            const int vw = (wave & 3) + 4 * v;
+            const int g = pk[v][j], kind = g >> 29, nb = (g >> 24) & 31, hy = (g >> 19) & 31, off = g & 0x7ffff;
             const bool in = kind == 1 && (unsigned)(ho0 + hy - 1) < (unsigned)H && n0 + nb < p.N;
             const uint16_t* src = kind == 2 ? wb + off : in ? xb + off : zl;
             // pieces wholly past the item's slots (6 of 64 on the 128-ch plane) are not issued
-            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::HT + G::WT)
-                glds16(src, dst + (j * G::NW + wave) * 1024);
+            if (j < G::PPW - 1 || (j * G::NW + vw) * 64 < G::HT + G::WT)
+                glds16(src, dst + (j * G::NW + vw) * 1024);
         }
     };
 
@@ -271,7 +283,12 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
         if (last && do_st) {
             // the residual loads precede this item's DMA pieces (PPW, or PPW - 1 on the waves whose
             // last piece is past the item): wait for all but PPW - 1 of them
-            if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW - 1) : "memory");
+            if (RES) {
+                if (dma_wave)
+                    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::PPW - 2) : "memory");
+                else
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
 #pragma unroll
             for (int a = 0; a < G::NA; a++)
 #pragma unroll

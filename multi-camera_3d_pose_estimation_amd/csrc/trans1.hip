@@ -61,7 +61,7 @@ struct T1C {
     static_assert(F0 == 4 * NF0 && F1 == 2 * NF1, "4 t0 waves x 6 fragments, 4 t1 waves (2 cout groups x 3)");
     static_assert(LDS <= 160 * 1024, "LDS budget");
     static_assert(H % TH == 0 && C % 16 == 0, "tiling");
-    static_assert(PPW < 48 && ST1 < 48, "vmcnt range");
+    static_assert(2 * PPW < 48 && ST1 < 48, "vmcnt range");
 };
 
 struct TrParams {
@@ -93,10 +93,16 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
     // ---- per-lane DMA geometry of this wave's item pieces (fixed for the launch)
     // kind 1 halo: po = element offset from the tile's (crop, row -1, col 0) + chunk, hy = halo row;
     // kind 2: weight element offset in the blob (t0 or t1 slice; + chunk * 16 at issue time)
-    int pk[G::PPW], po[G::PPW];
+    // the t1 waves (4-7, half the MFMAs of a t0 wave) issue the item pieces of virtual waves
+    // vw = wave & 3 and (wave & 3) + 4, the t0 waves none: after the item barrier the t0 wave of
+    // each SIMD starts its MFMAs at once (tconv16.hip; 836 -> 811 us, profiles/r04_dma_split_ab.txt)
+    const bool dma_wave = wave >= 4;
+    int pk[2][G::PPW], po[2][G::PPW];
+#pragma unroll
+    for (int v = 0; v < 2; v++)
 #pragma unroll
     for (int j = 0; j < G::PPW; j++) {
-        const int s = (j * G::NW + wave) * 64 + lane;
+        const int s = (j * G::NW + (wave & 3) + 4 * v) * 64 + lane;
         int kind = 0, off = 0, hy = 0;
         if (s < G::WA) {
             const int q = PM ? s % 3 : s / G::HS, hs = PM ? s / 3 : s - q * G::HS;
@@ -120,8 +126,8 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
             kind = 2;
             off = p.w1_off + (((row & ~31) | row_cout(row & 31)) * 9 + (tq >> 1)) * G::C + (tq & 1) * 8;
         }
-        pk[j] = (kind << 8) | hy;
-        po[j] = off;
+        pk[v][j] = (kind << 8) | hy;
+        po[v][j] = off;
     }
     auto issue = [&](int item, int buf) {
         const int tile = blockIdx.x + (item / G::NCH) * gridDim.x, chunk = item % G::NCH;
@@ -129,14 +135,18 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
         const uint16_t* xb = p.x + ((long)n * G::H + r0 - 1) * G::W * G::C + chunk * 16;
         uint8_t* dst = lds + buf * G::BUF;
         const uint16_t* wbase = p.wimg ? p.wimg + chunk * (G::ITEM - G::WA) * 8 : p.wb + chunk * 16;
+        if (!dma_wave) return;
+#pragma unroll
+        for (int v = 0; v < 2; v++)
 #pragma unroll
         for (int j = 0; j < G::PPW; j++) {
-            const int kind = pk[j] >> 8, hy = pk[j] & 255;
+            const int vw = (wave & 3) + 4 * v;
+            const int kind = pk[v][j] >> 8, hy = pk[v][j] & 255;
             const bool in = kind == 1 && (unsigned)(r0 - 1 + hy) < (unsigned)G::H;
-            const uint16_t* src = kind == 2 ? wbase + po[j] : in ? xb + po[j] : zl;
+            const uint16_t* src = kind == 2 ? wbase + po[v][j] : in ? xb + po[v][j] : zl;
             // pieces wholly past the item's slots are not issued (3 of 72)
-            if (j < G::PPW - 1 || (j * G::NW + wave) * 64 < G::ITEM)
-                glds16(src, dst + (j * G::NW + wave) * 1024);
+            if (j < G::PPW - 1 || (j * G::NW + vw) * 64 < G::ITEM)
+                glds16(src, dst + (j * G::NW + vw) * 1024);
         }
     };
 
