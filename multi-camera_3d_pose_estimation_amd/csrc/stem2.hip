@@ -316,7 +316,7 @@ struct S2S {
     static constexpr int F2 = 2 * W2 / 32;             // 3 conv2 fragments per strip
     static_assert(LDS <= 160 * 1024, "LDS budget");
     static_assert((6 * RS + 8 * RS) * 16 < 65536, "ds_read offset range (conv2 B)");
-    static_assert(XINSTR <= 2 * 8 - 2, "DMA split: 2 pieces on waves 0-5, 1 on waves 6-7");
+    static_assert(XINSTR <= 4 * 4, "DMA: the 4 conv1 waves, up to 4 pieces each");
     static_assert(F2 == 3 && F1 == 2 * 2 * 3, "roles: conv2 fragments 0, 1 | 2; conv1 halves of 2 groups of 3");
 };
 
@@ -338,12 +338,15 @@ __global__ __launch_bounds__(512, 1) void stem2_kernel(StemParams p) {
     if (tid < 64) sbias[tid] = p.b1[tid];
     else if (tid < 128) sbias[tid] = p.b2[tid - 64];
 
-    // ---- input DMA: instruction j of a strip = pieces 64j .. 64j + 63 ([row][piece]);
-    // this wave issues j = wave and wave + 8 (< 14)
-    int xg[2];  // (row + 1) << 8 | piece, 0 = zero piece
+    // ---- input DMA: instruction j of a strip = pieces 64j .. 64j + 63 ([row][piece]); the
+    // conv1 waves issue all 14 (wave w: j = (w & 3) + 4m), the conv2 waves none, so each SIMD's
+    // conv2 wave starts its MFMAs at once (same box: 425 -> 337 us; split over all 8 waves as
+    // before, or all on the conv2 waves: 364 -- profiles/r04_dma_split_ab.txt)
+    const bool dma_wave = wave >= 4;
+    int xg[4];  // (row + 1) << 8 | piece, 0 = zero piece
 #pragma unroll
-    for (int m = 0; m < 2; m++) {
-        const int i = (wave + m * 8) * 64 + lane;
+    for (int m = 0; m < 4; m++) {
+        const int i = ((wave & 3) + m * 4) * 64 + lane;
         const int row = i / G::XPIECES, k = i - row * G::XPIECES;
         xg[m] = (i < G::XN && k >= 1 && k <= G::W / 2) ? ((row + 1) << 8) | k : 0;
     }
@@ -351,9 +354,10 @@ __global__ __launch_bounds__(512, 1) void stem2_kernel(StemParams p) {
         const int n = crop0 + g / G::STRIPS, s = g % G::STRIPS;
         const uint16_t* xb = p.x + (long)n * G::H * G::W * 4;
         uint8_t* dst = lds + G::XOFF + (g & 1) * G::XBYTES;
+        if (!dma_wave) return;
 #pragma unroll
-        for (int m = 0; m < 2; m++) {
-            const int j = wave + m * 8;
+        for (int m = 0; m < 4; m++) {
+            const int j = (wave & 3) + m * 4;
             if (j < G::XINSTR) {
                 const int gg = xg[m], row = (gg >> 8) - 1, k = gg & 255;
                 const int gr = 8 * s - 1 + row;

@@ -189,9 +189,11 @@ __device__ __forceinline__ void dma_strip_rows(const S32Params& p, uint8_t* lds,
 #define TB32S_PF2 3
 #endif
 // Row DMAs of the next strip: the conv2 waves issue rows [0, kDmaSplit) of its load, the
-// conv1 waves the rest (each a burst at the start of its phase; VMEM issue is the conv2
-// waves' bottleneck: ~250 ticks per row DMA, ~300 per output store)
-constexpr int kDmaSplit = 4;
+// conv1 waves the rest (each a burst at the start of its phase).  All 12 on the conv2 waves:
+// each SIMD's conv1 wave starts its MFMAs at once instead of both waves of the SIMD issuing
+// DMA first (round 4, same box: 131.8 -> 121.5 us per block; all on the conv1 waves 141.2;
+// the former 4 / 8 split 131.8 -- profiles/r04_dma_split_ab.txt)
+constexpr int kDmaSplit = 12;
 
 // conv1 waves (j = 0..3): fragments j, j+4, j+8, j+12 of the strip's 10 intermediate rows.
 __device__ __forceinline__ void conv1_role(const S32Params& p, uint8_t* lds, int j, int lane, int n_strips, int crop0,
