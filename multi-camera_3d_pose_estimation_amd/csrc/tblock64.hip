@@ -4,8 +4,11 @@
 // the block moves its 100 MB (1,024 crops) input twice and writes the intermediate once;
 // fused, HBM sees the input (with a 4-row halo per 8 output rows) and the output only.
 //
-// One workgroup of 4 waves (one per SIMD) per CU, persistent over tiles of 8 output rows
-// of one crop.  The waves specialise:
+// One workgroup of 4 waves (one per SIMD) per CU, persistent over a contiguous range of
+// crops, each crop's 4 tiles of 8 output rows top to bottom (round 4: tiles 1-3 of a crop copy
+// their first two intermediate rows from the previous tile instead of recomputing them, 8 -> 6
+// conv1 fragments; 120 -> 114.5 us per block, profiles/r04_tblock64_rowreuse_ab.txt).  The
+// waves specialise:
 //   waves 0, 1  conv1 for output rows -1 .. 8 (10 rows: conv2's halo), cout group 0 / 1
 //               -> the intermediate (bias, ReLU, bf16; rows outside the image = 0 = conv2's
 //               zero padding) in LDS;
@@ -187,32 +190,46 @@ __device__ __forceinline__ void static_for(F&& f) {
 #endif
 constexpr int kPF = TB64_PF;
 
-// conv1 waves: tile k's 10 intermediate rows from input ring slot k & 1 into intermediate
-// buffer k & 1, then the phase barrier.  n_items + 2 barriers, as the conv2 waves.
-// Fragments 0-3 are half A, 4-7 half B; half A's epilogues at steps 40, 47, 54, 61.
-__device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items) {
+// conv1 waves: tile k's intermediate rows from input ring slot k & 1 into intermediate
+// buffer k & 1, then the phase barrier.  n_items + 2 barriers, as the conv2 waves.  A
+// workgroup walks its crops' 4 tiles top to bottom, so tile k's intermediate rows 0-1
+// (output rows ho0 - 1, ho0) are tile k-1's rows 8-9: for s > 0 they are copied from the
+// other buffer and only rows 2-9 are computed (6 fragments of 8x4 blocks, 3 per half); the
+// first tile of a crop computes all 10 rows (8 fragments, rows 0-7 as blocks, 8-9 as 2x16).
+// Same MFMA sequence per output row either way: bit-identical.
+// Fragments 0 .. NF-1 are half A, NF .. 2NF-1 half B; half A's epilogues at steps 40 + 7j.
+__device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items,
+                                           int crop0) {
     using G = B64;
-    constexpr int H = G::H, TH = G::TH, RS = G::RS, NF = G::F1 / 2;
+    constexpr int H = G::H, TH = G::TH, RS = G::RS;
     const int h = lane >> 5, r32 = lane & 31;
     bf16x8 wa[G::KS];
     load_weights(p.w1, cg, r32, h, wa);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
-    // fragment t, lane r32: intermediate pixel (r, x) (frag_pixel64); its input tap (0, 0) is
-    // halo pixel (r, x - 1) = slot r * RS + x, and it lands in intermediate slot r * RS + x + 1
-    int bv1[G::F1], mw[G::F1];
+    // fragment t, lane r32: intermediate pixel (r, x); its input tap (0, 0) is halo pixel
+    // (r, x - 1) = slot r * RS + x, and it lands in intermediate slot r * RS + x + 1.
+    // Full set (first tile of a crop): frag_pixel64; shifted set (s > 0): 8x4 blocks at rows 2-9.
+    int bvf[G::F1], mwf[G::F1], rf[G::F1], bvs[6], mws[6], rs6[6];
 #pragma unroll
     for (int t = 0; t < G::F1; t++) {
         int r, x;
         bool pad;
         frag_pixel64(t, r32, r, x, pad);
-        bv1[t] = (h * G::HSP + r * RS + x) * 16;
-        mw[t] = pad ? -1 : G::MOFF + ((4 * cg + 2 * h) * G::HSM + r * RS + x + 1) * 16;
+        bvf[t] = (h * G::HSP + r * RS + x) * 16;
+        mwf[t] = pad ? -1 : G::MOFF + ((4 * cg + 2 * h) * G::HSM + r * RS + x + 1) * 16;
+        rf[t] = r;
     }
-    barrier();  // prologue: tile 0's halo and the zeroed intermediate
-    for (int k = 0; k < n_items; k++) {
-        TB64_STAMP(k, 0);
-        const int tile = blockIdx.x + k * gridDim.x;
-        const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * TH;
+#pragma unroll
+    for (int t = 0; t < 6; t++) {
+        const int r = 2 + blk_row(r32), x = 4 * t + blk_col(r32);
+        bvs[t] = (h * G::HSP + r * RS + x) * 16;
+        mws[t] = G::MOFF + ((4 * cg + 2 * h) * G::HSM + r * RS + x + 1) * 16;
+        rs6[t] = r;
+    }
+    auto tile_body = [&](auto nf_tag, const int (&bv1)[2 * decltype(nf_tag)::value],
+                         const int (&mw)[2 * decltype(nf_tag)::value], const int (&rr)[2 * decltype(nf_tag)::value],
+                         int k, int ho0) {
+        constexpr int NF = decltype(nf_tag)::value;
         f32x16 accA[NF], accB[NF];
         accA[0] = bias_acc(lds, 0, cg, h);
 #pragma unroll
@@ -231,11 +248,8 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
         };
         auto epilogue = [&](int t, const f32x16& a) {
             if (mw[t] < 0) return;
-            int r, x;
-            bool pad;
-            frag_pixel64(t, r32, r, x, pad);
             // rows outside the image are conv2's zero padding
-            const bool live = (unsigned)(ho0 - 1 + r) < (unsigned)H;
+            const bool live = (unsigned)(ho0 - 1 + rr[t]) < (unsigned)H;
             uint32_t o[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) o[e] = live ? pack_bf16x2(relu1(a[2 * e]), relu1(a[2 * e + 1])) : 0u;
@@ -261,6 +275,24 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
         TB64_STAMP(k, 1);
 #pragma unroll
         for (int t = 0; t < NF; t++) epilogue(NF + t, accB[t]);
+    };
+    barrier();  // prologue: tile 0's halo and the zeroed intermediate
+    for (int k = 0; k < n_items; k++) {
+        TB64_STAMP(k, 0);
+        const int s = k % G::TILES_H, ho0 = s * TH;
+        if (s == 0) {
+            tile_body(std::integral_constant<int, G::F1 / 2>{}, bvf, mwf, rf, k, ho0);
+        } else {
+            // rows 0-1 = the previous tile's rows 8-9 (this wave's 4 planes, pads included)
+            const int mo = (k & 1) * G::MBYTES, mp = ((k - 1) & 1) * G::MBYTES;
+            for (int i = lane; i < 4 * 2 * RS; i += 64) {
+                const int q = 4 * cg + i / (2 * RS), rem = i % (2 * RS), r = rem / RS, xs = rem - r * RS;
+                const int so = G::MOFF + (q * G::HSM + r * RS + xs) * 16;
+                *reinterpret_cast<uint4*>(lds + so + mo) =
+                    *reinterpret_cast<const uint4*>(lds + so + mp + 8 * RS * 16);
+            }
+            tile_body(std::integral_constant<int, 3>{}, bvs, mws, rs6, k, ho0);
+        }
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
         TB64_STAMP(k, 2);
         barrier();
@@ -280,10 +312,9 @@ struct HaloSrc {
     int ho0, buf;
     bool valid;
 };
-__device__ __forceinline__ HaloSrc halo_src(const TB64Params& p, int k, int buf, bool valid) {
+__device__ __forceinline__ HaloSrc halo_src(const TB64Params& p, int crop0, int k, int buf, bool valid) {
     using G = B64;
-    const int tile = blockIdx.x + k * gridDim.x;
-    const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * G::TH;
+    const int n = crop0 + k / G::TILES_H, ho0 = (k % G::TILES_H) * G::TH;
     return HaloSrc{p.x + ((long)n * G::H + ho0) * G::W * 64, ho0, buf, valid};
 }
 __device__ __forceinline__ const uint16_t* halo_block(const HaloSrc& hs, int lane, const uint16_t* zl, int b) {
@@ -315,7 +346,7 @@ static_assert(kDmaStep0 + kDmaStride * (B64::XPPW - 1) < 72, "DMA pieces fit the
 // conv2 waves: in phase k, the halo DMA of tile k+1 and conv2 of tile k-1 from intermediate
 // buffer (k-1) & 1 + bias + residual (from the input ring) + ReLU -> y.
 __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items,
-                                           const uint16_t* zl) {
+                                           const uint16_t* zl, int crop0) {
     using G = B64;
     constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS, NF = G::F2 / 2;
     const int h = lane >> 5, r32 = lane & 31, dw = cg;
@@ -328,17 +359,16 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
     const int er = blk_row(r32), ex = blk_col(r32);
 #pragma unroll
     for (int t = 0; t < G::F2; t++) bv2[t] = G::MOFF + (h * G::HSM + er * RS + 4 * t + ex) * 16;
-    issue_halo(halo_src(p, 0, 0, true), lds, dw, lane, zl);
+    issue_halo(halo_src(p, crop0, 0, 0, true), lds, dw, lane, zl);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // prologue
-    issue_halo(halo_src(p, 1, 1, n_items > 1), lds, dw, lane, zl);
+    issue_halo(halo_src(p, crop0, 1, 1, n_items > 1), lds, dw, lane, zl);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // phase 0: conv1 of tile 0 only
     for (int k = 1; k <= n_items; k++) {
         TB64_STAMP(k, 0);
         const int kp = k - 1;
-        const int tile = blockIdx.x + kp * gridDim.x;
-        const int n = tile / G::TILES_H, ho0 = (tile - n * G::TILES_H) * TH;
+        const int n = crop0 + kp / G::TILES_H, ho0 = (kp % G::TILES_H) * TH;
         const long pix0 = ((long)n * H + ho0) * W;
         f32x16 accA[NF], accB[NF];
         accA[0] = bias_acc(lds, 1, cg, h);
@@ -359,7 +389,7 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
         for (int t = 1; t < NF; t++) accA[t] = accA[0];
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
         __builtin_amdgcn_sched_barrier(0);
-        const HaloSrc hn = halo_src(p, k + 1, (k + 1) & 1, k + 1 < n_items);
+        const HaloSrc hn = halo_src(p, crop0, k + 1, (k + 1) & 1, k + 1 < n_items);
         const uint16_t* blk = nullptr;
         const int mo = (kp & 1) * G::MBYTES;
         bf16x8 fb[kPF + 1][NF];
@@ -422,17 +452,20 @@ __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    if ((int)blockIdx.x >= p.n_tiles) return;
-    const int n_items = (p.n_tiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1;
+    // this workgroup's crops: a balanced contiguous range, walked tile by tile top to bottom
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int crop0 = (int)(((long)p.N * b) / nb), crop1 = (int)(((long)p.N * (b + 1)) / nb);
+    const int n_items = (crop1 - crop0) * G::TILES_H;
+    if (n_items == 0) return;  // whole workgroup: uniform
     // the intermediate's pad and leading slots stay zero for the launch
     for (int i = tid; i < 2 * G::MBYTES / 16; i += 256)
         *reinterpret_cast<uint4*>(lds + G::MOFF + i * 16) = uint4{0u, 0u, 0u, 0u};
     if (tid < 128) reinterpret_cast<float*>(lds + G::BOFF)[tid] = tid < 64 ? p.b1[tid] : p.b2[tid - 64];
     __builtin_amdgcn_s_waitcnt(kWaitAll);
     if (wave < 2)
-        conv1_role(p, lds, wave, lane, n_items);
+        conv1_role(p, lds, wave, lane, n_items, crop0);
     else
-        conv2_role(p, lds, wave - 2, lane, n_items, p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8);
+        conv2_role(p, lds, wave - 2, lane, n_items, p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8, crop0);
 }
 
 int g_tb64_cus = 0;
@@ -462,7 +495,7 @@ void launch_tblock64(const uint16_t* x, const uint16_t* w1, const float* b1, con
     const long tiles = (long)N * G::TILES_H;
     MVP_REQUIRE(tiles < (1L << 30), "tblock64: too many tiles");
     TB64Params p{x, w1, b1, w2, b2, y, conv_zero_region(), N, (int)tiles};
-    const int grid = (int)std::min<long>(tiles, g_tb64_cus);
+    const int grid = std::min(N, g_tb64_cus);  // contiguous crop ranges (conv1 reuses rows across a crop's tiles)
     hipLaunchKernelGGL(tblock64_kernel, dim3(grid), dim3(256), G::LDS, s, p);
     MVP_HIP(hipGetLastError());
 }

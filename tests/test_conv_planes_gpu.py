@@ -82,12 +82,13 @@ def test_basic_block_vs_reference(c, h, w, monkeypatch):
         assert mx <= 3 * scale * 2.0 ** -8
 
 
-@pytest.mark.parametrize("n", [37, 301])
+@pytest.mark.parametrize("n", [1, 5, 37, 301])
 def test_tblock64_bitwise_equals_two_tconv_launches(n, monkeypatch):
     """The fused 64-channel BasicBlock (tblock64.hip: warp-specialised conv1 / conv2 waves,
-    the intermediate only in LDS) reproduces the two separate tconv launches bit for bit —
-    same MFMA sequence per accumulator, same epilogues.  n = 37: fewer tiles than CUs (one per
-    workgroup); n = 301: the persistent loop with its ring / intermediate double buffers."""
+    the intermediate only in LDS, a crop's tiles walked top to bottom with intermediate rows
+    0-1 of tiles 1-3 copied from the previous tile) reproduces the two separate tconv launches
+    bit for bit — same MFMA sequence per accumulator, same epilogues.  n = 1, 5, 37: one crop
+    per workgroup; n = 301: more crops than CUs (ragged 1-2 crops per workgroup)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet
