@@ -195,7 +195,12 @@ __device__ __forceinline__ void dma_strip_rows(const S32Params& p, uint8_t* lds,
 // the former 4 / 8 split 131.8 -- profiles/r04_dma_split_ab.txt)
 constexpr int kDmaSplit = 12;
 
-// conv1 waves (j = 0..3): fragments j, j+4, j+8, j+12 of the strip's 10 intermediate rows.
+// conv1 waves (j = 0..3).  The first strip of a crop: fragments j, j+4, j+8, j+12 of the
+// strip's 10 intermediate rows (image rows 8s - 1 .. 8s + 8; one pad fragment).  Later strips:
+// rows 0-1 are the previous strip's rows 8-9, copied from the other intermediate buffer (wave j
+// copies plane j), and only rows 2-9 are computed: fragments 3 + j, 7 + j, 11 + j (12 instead of
+// 15 + 1 pad; 54 instead of 72 MFMAs per wave).  Same MFMA sequence per row: bit-identical.
+// (Round 4: 123.0 -> 114.8 us per block same-box, profiles/r04_tblock64_rowreuse_ab.txt.)
 __device__ __forceinline__ void conv1_role(const S32Params& p, uint8_t* lds, int j, int lane, int n_strips, int crop0,
                                            const uint16_t* zl) {
     using G = S32;
@@ -205,8 +210,9 @@ __device__ __forceinline__ void conv1_role(const S32Params& p, uint8_t* lds, int
     bf16x8 wa[G::KS];
     load_weights(p.w1, r32, h, wa);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
-    int pi[NF], px[NF];
-    bool pad[NF];
+    // full set (first strip of a crop): NF fragments, the last a pad on wave 3; reuse set: 3
+    int pi[NF], px[NF], pir[3], pxr[3];
+    bool pad[NF], padr[3] = {false, false, false};
 #pragma unroll
     for (int t = 0; t < NF; t++) {
         int f = j + 4 * t;
@@ -216,6 +222,76 @@ __device__ __forceinline__ void conv1_role(const S32Params& p, uint8_t* lds, int
         pi[t] = pp / G::W;
         px[t] = pp - pi[t] * G::W;
     }
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        const int pp = frag_pixel<G::W, G::MR, 1>(3 + j + 4 * t, r32);
+        pir[t] = pp / G::W;
+        pxr[t] = pp - pir[t] * G::W;
+    }
+    // one strip's conv1: NA fragments in half A, NB in half B (half A's epilogues run in the
+    // shadow of half B's MFMAs; only half B's is exposed)
+    auto strip_body = [&](auto na_tag, auto nb_tag, const int* fpi, const int* fpx, const bool* fpad, int k,
+                          const Strip& st) {
+        constexpr int NA = decltype(na_tag)::value, NB = decltype(nb_tag)::value, NT = NA + NB;
+        constexpr int NM = NA > NB ? NA : NB;
+        const int v0 = st.cl * G::VR + 8 * st.s;  // virtual row of intermediate row 0's tap row 0
+        int bv[NT][3];
+#pragma unroll
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int dy = 0; dy < 3; dy++)
+                bv[t][dy] = h * G::PL + (ring_row(v0 + fpi[t] + dy) * RS + fpx[t]) * 16;
+        constexpr int NS = (NB > 0 ? 2 : 1) * G::KS;
+        f32x16 accA[NA], accB[NB > 0 ? NB : 1];
+        accA[0] = bias_acc(lds, 0, h);
+#pragma unroll
+        for (int t = 1; t < NA; t++) accA[t] = accA[0];
+#pragma unroll
+        for (int t = 0; t < NB; t++) accB[t] = accA[0];
+        uint8_t* mb = lds + G::MOFF + (k & 1) * G::MBYTES;
+        auto epilogue = [&](int t, const f32x16& a) {
+            if (fpad[t]) return;
+            // intermediate row pi = image row 8s - 1 + pi: rows outside are conv2's zero padding
+            const bool live = (unsigned)(8 * st.s - 1 + fpi[t]) < (unsigned)G::H;
+            uint32_t o[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) o[e] = live ? pack_bf16x2(relu1(a[2 * e]), relu1(a[2 * e + 1])) : 0u;
+            uint8_t* d = mb + (2 * h * G::MPL / 16 + 1 + fpi[t] * RS + fpx[t]) * 16;
+            *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(d + G::MPL) = uint4{o[4], o[5], o[6], o[7]};
+        };
+        bf16x8 fb[kPF + 1][NM];
+        auto load = [&](auto Gs) {
+            constexpr int g = Gs, s = g % G::KS, hb = g / G::KS, t0 = hb * NA, nt = hb ? NB : NA;
+            constexpr int tap = s >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
+#pragma unroll
+            for (int t = 0; t < nt; t++)
+                fb[g % (kPF + 1)][t] =
+                    *reinterpret_cast<const bf16x8*>(lds + bv[t0 + t][dy] + (2 * ks * (G::PL / 16) + dx) * 16);
+        };
+        static_for<0, kPF>(load);
+        static_for<0, NS>([&](auto Gs) {
+            constexpr int g = Gs, s = g % G::KS;
+            if constexpr (g + kPF < NS) load(std::integral_constant<int, g + kPF>{});
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g < G::KS) {
+#pragma unroll
+                for (int t = 0; t < NA; t++)
+                    accA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accA[t], 0, 0, 0);
+            } else {
+#pragma unroll
+                for (int t = 0; t < NB; t++)
+                    accB[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accB[t], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g >= G::KS + 3 && (g - G::KS - 3) % 6 == 0 && (g - G::KS - 3) / 6 < NA)
+                epilogue((g - G::KS - 3) / 6, accA[(g - G::KS - 3) / 6]);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        S32_STAMP(k, 1);
+#pragma unroll
+        for (int t = 0; t < NB; t++) epilogue(NA + t, accB[t]);
+    };
     barrier();  // prologue: strip 0's rows, zeroed images, biases
     for (int k = 0; k <= n_strips; k++) {
         S32_STAMP(k, 0);
@@ -223,64 +299,17 @@ __device__ __forceinline__ void conv1_role(const S32Params& p, uint8_t* lds, int
         if (k + 1 < n_strips) dma_strip_rows(p, lds, crop0, k + 1, kDmaSplit, 12, j, lane, zl);
         if (k < n_strips) {
             const Strip st = strip_of(k);
-            const int v0 = st.cl * G::VR + 8 * st.s;  // virtual row of intermediate row 0's tap row 0
-            int bv[NF][3];
-#pragma unroll
-            for (int t = 0; t < NF; t++)
-#pragma unroll
-                for (int dy = 0; dy < 3; dy++)
-                    bv[t][dy] = h * G::PL + (ring_row(v0 + pi[t] + dy) * RS + px[t]) * 16;
-            // two halves of NF/2 fragments in one 36-step schedule: half A's epilogues (ReLU,
-            // bf16, intermediate stores) run in the shadow of half B's MFMAs; only half B's
-            // is exposed (the whole epilogue after the loop measured ~2.0k ticks per phase)
-            constexpr int NH = NF / 2, NS = 2 * G::KS;
-            f32x16 accA[NH], accB[NH];
-            accA[0] = bias_acc(lds, 0, h);
-#pragma unroll
-            for (int t = 1; t < NH; t++) accA[t] = accA[0];
-#pragma unroll
-            for (int t = 0; t < NH; t++) accB[t] = accA[0];
-            uint8_t* mb = lds + G::MOFF + (k & 1) * G::MBYTES;
-            auto epilogue = [&](int t, const f32x16& a) {
-                if (pad[t]) return;
-                // intermediate row pi = image row 8s - 1 + pi: rows outside are conv2's zero padding
-                const bool live = (unsigned)(8 * st.s - 1 + pi[t]) < (unsigned)G::H;
-                uint32_t o[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++) o[e] = live ? pack_bf16x2(relu1(a[2 * e]), relu1(a[2 * e + 1])) : 0u;
-                uint8_t* d = mb + (2 * h * G::MPL / 16 + 1 + pi[t] * RS + px[t]) * 16;
-                *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<uint4*>(d + G::MPL) = uint4{o[4], o[5], o[6], o[7]};
-            };
-            bf16x8 fb[kPF + 1][NH];
-            auto load = [&](auto Gs) {
-                constexpr int g = Gs, s = g % G::KS, t0 = (g / G::KS) * NH;
-                constexpr int tap = s >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
-#pragma unroll
-                for (int t = 0; t < NH; t++)
-                    fb[g % (kPF + 1)][t] =
-                        *reinterpret_cast<const bf16x8*>(lds + bv[t0 + t][dy] + (2 * ks * (G::PL / 16) + dx) * 16);
-            };
-            static_for<0, kPF>(load);
-            static_for<0, NS>([&](auto Gs) {
-                constexpr int g = Gs, s = g % G::KS;
-                if constexpr (g + kPF < NS) load(std::integral_constant<int, g + kPF>{});
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < NH; t++) {
-                    if constexpr (g < G::KS)
-                        accA[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accA[t], 0, 0, 0);
-                    else
-                        accB[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[s], fb[g % (kPF + 1)][t], accB[t], 0, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (g >= G::KS + 3 && (g - G::KS - 3) % 6 == 0 && (g - G::KS - 3) / 6 < NH)
-                    epilogue((g - G::KS - 3) / 6, accA[(g - G::KS - 3) / 6]);
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            S32_STAMP(k, 1);
-#pragma unroll
-            for (int t = 0; t < NH; t++) epilogue(NH + t, accB[t]);
+            if (st.s == 0) {
+                strip_body(std::integral_constant<int, NF / 2>{}, std::integral_constant<int, NF / 2>{}, pi, px, pad, k,
+                           st);
+            } else {
+                // rows 0-1 = the previous strip's rows 8-9 (plane j, pad slots included)
+                const uint8_t* mp = lds + G::MOFF + ((k - 1) & 1) * G::MBYTES + j * G::MPL + 16;
+                uint8_t* mc = lds + G::MOFF + (k & 1) * G::MBYTES + j * G::MPL + 16;
+                for (int i = lane; i < 2 * RS; i += 64)
+                    *reinterpret_cast<uint4*>(mc + i * 16) = *reinterpret_cast<const uint4*>(mp + (8 * RS + i) * 16);
+                strip_body(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, pir, pxr, padr, k, st);
+            }
             __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
             S32_STAMP(k, 2);
         }
