@@ -189,11 +189,13 @@ __device__ __forceinline__ void dma_strip_rows(const S32Params& p, uint8_t* lds,
 #define TB32S_PF2 3
 #endif
 // Row DMAs of the next strip: the conv2 waves issue rows [0, kDmaSplit) of its load, the
-// conv1 waves the rest (each a burst at the start of its phase).  All 12 on the conv2 waves:
-// each SIMD's conv1 wave starts its MFMAs at once instead of both waves of the SIMD issuing
-// DMA first (round 4, same box: 131.8 -> 121.5 us per block; all on the conv1 waves 141.2;
-// the former 4 / 8 split 131.8 -- profiles/r04_dma_split_ab.txt)
-constexpr int kDmaSplit = 12;
+// conv1 waves the rest (each a burst at the start of its phase).  8: a strip's 8 new rows all
+// on the conv2 waves, so each SIMD's conv1 wave starts its MFMAs at once instead of both waves
+// of the SIMD issuing DMA first; only the 12-row load of a crop's first strip gives its last 4
+// rows to the conv1 waves (round 4, same box: the former 4 / 8 split 131.8 us per block, all on
+// the conv1 waves 141.2, all 12 on the conv2 waves 121.5; with conv1's row reuse, 12: 116.5,
+// 8: 112.4 -- profiles/r04_dma_split_ab.txt)
+constexpr int kDmaSplit = 8;
 
 // conv1 waves (j = 0..3).  The first strip of a crop: fragments j, j+4, j+8, j+12 of the
 // strip's 10 intermediate rows (image rows 8s - 1 .. 8s + 8; one pad fragment).  Later strips:
