@@ -33,6 +33,7 @@ namespace {
 constexpr int kMaxSgdCams = 16;
 constexpr int kMaxSeg = 32;
 constexpr int kMaxJ = 64;
+constexpr int kMaxJointSeg = 6;  // segments per joint listed for pass B (more: the full segment loop)
 constexpr int kMaxLearn = 2;   // learnable cameras (joint trajectory + extrinsic branch)
 constexpr int kCamGrad = 12;   // dR (9, row-major) + dT (3) per learnable camera
 
@@ -226,6 +227,9 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     __shared__ float cam_s[kMaxSgdCams * MVP_SGD_CAM_FLOATS];
     __shared__ int seg_s[kMaxSeg * 2];
     __shared__ float seglen_s[kMaxSeg];
+    __shared__ int jseg[kMaxJ][kMaxJointSeg];  // per joint: the segments touching it, in segment order
+    __shared__ int jseg_n[kMaxJ];
+    __shared__ int jseg_over;
     __shared__ double red_s[BS / 64][kRedCols];
     __shared__ int learn_slot[kMaxSgdCams];            // camera -> learnable index, -1 = fixed
     __shared__ float cstate[kMaxLearn * 2 * kCamGrad];  // Adam m | v of the learnable R, T
@@ -265,6 +269,18 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
         seg_s[2 * i] = a.seg[2 * i];
         seg_s[2 * i + 1] = a.seg[2 * i + 1];
         seglen_s[i] = a.seg_len[i];
+    }
+    if (tid == 0) jseg_over = 0;
+    __syncthreads();
+    for (int j = tid; j < J; j += BS) {
+        int c = 0;
+        for (int sg = 0; sg < NS; sg++)
+            if (a.seg[2 * sg] == j || a.seg[2 * sg + 1] == j) {
+                if (c < kMaxJointSeg) jseg[j][c] = sg;
+                c++;
+            }
+        jseg_n[j] = c;
+        if (c > kMaxJointSeg) jseg_over = 1;
     }
     for (int r = tid; r < T * Vg * J; r += BS) {
         const int j = r % J, tc = r / J, c = tc % Vg, t = tc / Vg;
@@ -448,8 +464,12 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                         g2 += coef * ((xa[2] - xb[2]) - (xb[2] - xc[2]));
                     }
                 }
-                if (use_b)
-                    for (int s = 0; s < NS; s++) {
+                if (use_b) {
+                    // the segments touching joint j, in segment order (the same additions as the
+                    // loop over all NS segments, which stays for a joint in more than kMaxJointSeg)
+                    const int nsj = jseg_over ? NS : jseg_n[j];
+                    for (int m = 0; m < nsj; m++) {
+                        const int s = jseg_over ? m : jseg[j][m];
                         const int ja = seg_s[2 * s], jb = seg_s[2 * s + 1];
                         if (ja != j && jb != j) continue;
                         const float* xa = X + 3 * (t * J + ja);
@@ -465,6 +485,7 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                         g1 += dl * e1;
                         g2 += dl * e2;
                     }
+                }
                 gb[3 * q + 0] = g0;
                 gb[3 * q + 1] = g1;
                 gb[3 * q + 2] = g2;
