@@ -1,6 +1,7 @@
 // Internal (not part of the C-ABI): convolution / fuse launchers used by the
 // HRNet graph runtime (hrnet.cpp).
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -116,6 +117,16 @@ void launch_stem(const uint16_t* x, const float* w, const float* bias, uint16_t*
 // 64 -> 64, w2 bf16 [64][3][3][64]), both BN-folded with ReLU, in one launch; conv1's
 // output never leaves LDS.  x [N][256][192][4] -> y [N][64][48][64].  stem2_supported is
 // false for other shapes (or MVPOSE_NO_STEMFUSE=1).
+// Crop-streaming kernels (tblock32s, tblock64's row reuse, streaming stem2) give each workgroup
+// a contiguous crop range: worth it only when every CU gets at least one crop; below that the
+// caller takes the per-tile kernel, which spreads N * tiles-per-crop items over every CU.
+// (Measured, profiles/r04_crop_ranges_ab.txt: the tile kernels win 22 % at 40 crops and 1.8 % at
+// 160; at 400 crops -- ragged 1-2 crops per CU -- the crop ranges still win, row reuse included.)
+inline bool crop_ranges_balanced(int N, int cus) {
+    const char* e = getenv("MVPOSE_CROP_STREAM");  // tests: 1 = the crop-streaming kernels at any batch
+    if (e && e[0] == '1') return true;
+    return N >= cus;
+}
 bool stem2_supported(int H, int W, int cin2, int cout2);
 void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uint16_t* w2, const float* b2,
                   uint16_t* y, int N, int H, int W, hipStream_t s);

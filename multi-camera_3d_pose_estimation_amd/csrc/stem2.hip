@@ -603,7 +603,7 @@ void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uin
         MVP_HIP(hipDeviceGetAttribute(&g_s2_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     const char* e = getenv("MVPOSE_STEM2_TILE");  // tests: the tile kernel (bit-identical reference)
-    if (e && e[0] == '1') {
+    if ((e && e[0] == '1') || !crop_ranges_balanced(N, g_s2_cus)) {  // + small / ragged batches
         static bool attr_t = false;
         if (!attr_t) {
             MVP_HIP(hipFuncSetAttribute((const void*)stem2_tile_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

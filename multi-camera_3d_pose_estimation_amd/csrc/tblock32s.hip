@@ -485,6 +485,7 @@ bool launch_tblock32s(const uint16_t* x, const uint16_t* w1, const float* b1, co
         MVP_HIP(hipGetDevice(&dev));
         MVP_HIP(hipDeviceGetAttribute(&g_s32_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
+    if (!crop_ranges_balanced(N, g_s32_cus)) return false;  // small / ragged batch: the tile kernel
     MVP_REQUIRE(N < (1 << 24), "tblock32s: too many crops");
     S32Params p{x, w1, b1, w2, b2, y, conv_zero_region(), N};
     const int grid = std::min(N, g_s32_cus);

@@ -190,6 +190,22 @@ __device__ __forceinline__ void static_for(F&& f) {
 #endif
 constexpr int kPF = TB64_PF;
 
+// Tile k of this workgroup: crop and strip.  ST (strided, small batches): tile
+// blockIdx.x + k * gridDim.x, conv1 computing every row; else a contiguous crop range.
+// A template parameter so the crop-range kernel's code is unchanged by the strided mode.
+template <bool ST>
+__device__ __forceinline__ void tile_of64(int crop0, int k, int& n, int& s) {
+    using G = B64;
+    if (ST) {
+        const int t = (int)blockIdx.x + k * (int)gridDim.x;
+        n = t / G::TILES_H;
+        s = t - n * G::TILES_H;
+    } else {
+        n = crop0 + k / G::TILES_H;
+        s = k % G::TILES_H;
+    }
+}
+
 // conv1 waves: tile k's intermediate rows from input ring slot k & 1 into intermediate
 // buffer k & 1, then the phase barrier.  n_items + 2 barriers, as the conv2 waves.  A
 // workgroup walks its crops' 4 tiles top to bottom, so tile k's intermediate rows 0-1
@@ -198,6 +214,7 @@ constexpr int kPF = TB64_PF;
 // first tile of a crop computes all 10 rows (8 fragments, rows 0-7 as blocks, 8-9 as 2x16).
 // Same MFMA sequence per output row either way: bit-identical.
 // Fragments 0 .. NF-1 are half A, NF .. 2NF-1 half B; half A's epilogues at steps 40 + 7j.
+template <bool ST>
 __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items,
                                            int crop0) {
     using G = B64;
@@ -279,8 +296,10 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
     barrier();  // prologue: tile 0's halo and the zeroed intermediate
     for (int k = 0; k < n_items; k++) {
         TB64_STAMP(k, 0);
-        const int s = k % G::TILES_H, ho0 = s * TH;
-        if (s == 0) {
+        int n_, s;
+        tile_of64<ST>(crop0, k, n_, s);
+        const int ho0 = s * TH;
+        if (s == 0 || ST) {  // strided tiles: no previous tile of the crop in the other buffer
             tile_body(std::integral_constant<int, G::F1 / 2>{}, bvf, mwf, rf, k, ho0);
         } else {
             // rows 0-1 = the previous tile's rows 8-9 (this wave's 4 planes, pads included)
@@ -312,9 +331,12 @@ struct HaloSrc {
     int ho0, buf;
     bool valid;
 };
+template <bool ST>
 __device__ __forceinline__ HaloSrc halo_src(const TB64Params& p, int crop0, int k, int buf, bool valid) {
     using G = B64;
-    const int n = crop0 + k / G::TILES_H, ho0 = (k % G::TILES_H) * G::TH;
+    int n, s;
+    tile_of64<ST>(crop0, k, n, s);
+    const int ho0 = s * G::TH;
     return HaloSrc{p.x + ((long)n * G::H + ho0) * G::W * 64, ho0, buf, valid};
 }
 __device__ __forceinline__ const uint16_t* halo_block(const HaloSrc& hs, int lane, const uint16_t* zl, int b) {
@@ -345,6 +367,7 @@ static_assert(kDmaStep0 + kDmaStride * (B64::XPPW - 1) < 72, "DMA pieces fit the
 
 // conv2 waves: in phase k, the halo DMA of tile k+1 and conv2 of tile k-1 from intermediate
 // buffer (k-1) & 1 + bias + residual (from the input ring) + ReLU -> y.
+template <bool ST>
 __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, int cg, int lane, int n_items,
                                            const uint16_t* zl, int crop0) {
     using G = B64;
@@ -359,16 +382,18 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
     const int er = blk_row(r32), ex = blk_col(r32);
 #pragma unroll
     for (int t = 0; t < G::F2; t++) bv2[t] = G::MOFF + (h * G::HSM + er * RS + 4 * t + ex) * 16;
-    issue_halo(halo_src(p, crop0, 0, 0, true), lds, dw, lane, zl);
+    issue_halo(halo_src<ST>(p, crop0, 0, 0, true), lds, dw, lane, zl);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // prologue
-    issue_halo(halo_src(p, crop0, 1, 1, n_items > 1), lds, dw, lane, zl);
+    issue_halo(halo_src<ST>(p, crop0, 1, 1, n_items > 1), lds, dw, lane, zl);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // phase 0: conv1 of tile 0 only
     for (int k = 1; k <= n_items; k++) {
         TB64_STAMP(k, 0);
         const int kp = k - 1;
-        const int n = crop0 + kp / G::TILES_H, ho0 = (kp % G::TILES_H) * TH;
+        int n, sp;
+        tile_of64<ST>(crop0, kp, n, sp);
+        const int ho0 = sp * TH;
         const long pix0 = ((long)n * H + ho0) * W;
         f32x16 accA[NF], accB[NF];
         accA[0] = bias_acc(lds, 1, cg, h);
@@ -389,7 +414,7 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
         for (int t = 1; t < NF; t++) accA[t] = accA[0];
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
         __builtin_amdgcn_sched_barrier(0);
-        const HaloSrc hn = halo_src(p, crop0, k + 1, (k + 1) & 1, k + 1 < n_items);
+        const HaloSrc hn = halo_src<ST>(p, crop0, k + 1, (k + 1) & 1, k + 1 < n_items);
         const uint16_t* blk = nullptr;
         const int mo = (kp & 1) * G::MBYTES;
         bf16x8 fb[kPF + 1][NF];
@@ -447,6 +472,7 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
 }
 
+template <bool ST>
 __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
     using G = B64;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
@@ -455,7 +481,7 @@ __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
     // this workgroup's crops: a balanced contiguous range, walked tile by tile top to bottom
     const int nb = gridDim.x, b = blockIdx.x;
     const int crop0 = (int)(((long)p.N * b) / nb), crop1 = (int)(((long)p.N * (b + 1)) / nb);
-    const int n_items = (crop1 - crop0) * G::TILES_H;
+    const int n_items = ST ? (b < p.n_tiles ? (p.n_tiles - 1 - b) / nb + 1 : 0) : (crop1 - crop0) * G::TILES_H;
     if (n_items == 0) return;  // whole workgroup: uniform
     // the intermediate's pad and leading slots stay zero for the launch
     for (int i = tid; i < 2 * G::MBYTES / 16; i += 256)
@@ -463,9 +489,9 @@ __global__ __launch_bounds__(256, 1) void tblock64_kernel(TB64Params p) {
     if (tid < 128) reinterpret_cast<float*>(lds + G::BOFF)[tid] = tid < 64 ? p.b1[tid] : p.b2[tid - 64];
     __builtin_amdgcn_s_waitcnt(kWaitAll);
     if (wave < 2)
-        conv1_role(p, lds, wave, lane, n_items, crop0);
+        conv1_role<ST>(p, lds, wave, lane, n_items, crop0);
     else
-        conv2_role(p, lds, wave - 2, lane, n_items, p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8, crop0);
+        conv2_role<ST>(p, lds, wave - 2, lane, n_items, p.zero + ((wave * 64 + lane) & (kZeroSlots - 1)) * 8, crop0);
 }
 
 int g_tb64_cus = 0;
@@ -484,7 +510,8 @@ void launch_tblock64(const uint16_t* x, const uint16_t* w1, const float* b1, con
     if (N == 0) return;
     static bool attr = false;
     if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)tblock64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)tblock64_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)tblock64_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
         attr = true;
     }
     if (g_tb64_cus == 0) {
@@ -494,9 +521,13 @@ void launch_tblock64(const uint16_t* x, const uint16_t* w1, const float* b1, con
     }
     const long tiles = (long)N * G::TILES_H;
     MVP_REQUIRE(tiles < (1L << 30), "tblock64: too many tiles");
+    // contiguous crop ranges (conv1 reuses rows across a crop's tiles) from one crop per CU;
+    // smaller batches: tiles strided over every CU, every tile computing all 10 rows
     TB64Params p{x, w1, b1, w2, b2, y, conv_zero_region(), N, (int)tiles};
-    const int grid = std::min(N, g_tb64_cus);  // contiguous crop ranges (conv1 reuses rows across a crop's tiles)
-    hipLaunchKernelGGL(tblock64_kernel, dim3(grid), dim3(256), G::LDS, s, p);
+    if (crop_ranges_balanced(N, g_tb64_cus))
+        hipLaunchKernelGGL(tblock64_kernel<false>, dim3(std::min(N, g_tb64_cus)), dim3(256), G::LDS, s, p);
+    else
+        hipLaunchKernelGGL(tblock64_kernel<true>, dim3((int)std::min<long>(tiles, g_tb64_cus)), dim3(256), G::LDS, s, p);
     MVP_HIP(hipGetLastError());
 }
 

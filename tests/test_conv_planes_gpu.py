@@ -82,17 +82,22 @@ def test_basic_block_vs_reference(c, h, w, monkeypatch):
         assert mx <= 3 * scale * 2.0 ** -8
 
 
+@pytest.mark.parametrize("stream", ["1", "0"])
 @pytest.mark.parametrize("n", [1, 5, 37, 301])
-def test_tblock64_bitwise_equals_two_tconv_launches(n, monkeypatch):
+def test_tblock64_bitwise_equals_two_tconv_launches(n, stream, monkeypatch):
     """The fused 64-channel BasicBlock (tblock64.hip: warp-specialised conv1 / conv2 waves,
     the intermediate only in LDS, a crop's tiles walked top to bottom with intermediate rows
     0-1 of tiles 1-3 copied from the previous tile) reproduces the two separate tconv launches
     bit for bit — same MFMA sequence per accumulator, same epilogues.  n = 1, 5, 37: one crop
-    per workgroup; n = 301: more crops than CUs (ragged 1-2 crops per workgroup)."""
+    per workgroup; n = 301: more crops than CUs (ragged 1-2 crops per workgroup).
+    stream = "1" forces the crop-contiguous ranges at every batch; "0" leaves the launcher's
+    rule (conv.h crop_ranges_balanced), which below one crop per CU (n = 1, 5, 37) picks the
+    strided mode: one tile per workgroup slot, no row reuse."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet
     _set_mode(monkeypatch, "tconv")
+    monkeypatch.setenv("MVPOSE_CROP_STREAM", stream)
     spec, xi, yo, _ = hrnet.basic_block_spec(64, 32, 24, seed=13, n_blocks=2)
     gen = torch.Generator().manual_seed(14)
     x = torch.randn((n, 32, 24, 64), generator=gen).bfloat16().cuda()
@@ -124,6 +129,8 @@ def test_tblock32s_bitwise_equals_tile_kernel(n, monkeypatch):
         pytest.skip("no GPU")
     from mvpose import hrnet
     _set_mode(monkeypatch, "tconv")
+    # Force the streaming kernel at these unbalanced batches (the launcher would pick the tile kernel).
+    monkeypatch.setenv("MVPOSE_CROP_STREAM", "1")
     spec, xi, yo, _ = hrnet.basic_block_spec(32, 64, 48, seed=17, n_blocks=2)
     gen = torch.Generator().manual_seed(18)
     x = torch.randn((n, 64, 48, 32), generator=gen).bfloat16().cuda()
@@ -259,6 +266,8 @@ def test_stem2_streaming_bitwise_equals_tile_kernel(n, monkeypatch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from mvpose import hrnet
+    # Force the streaming kernel at these unbalanced batches (the launcher would pick the tile kernel).
+    monkeypatch.setenv("MVPOSE_CROP_STREAM", "1")
     spec, xi, yo, sd = hrnet.stem_spec(seed=33)
     gen = torch.Generator().manual_seed(34)
     x = torch.zeros((n, 256, 192, 4))

@@ -64,15 +64,15 @@ int main(int argc, char** argv) {
     MVP_HIP(hipMemcpy(w, hw.data(), 2 * nw * 2, hipMemcpyHostToDevice));
     MVP_HIP(hipMemcpy(b, hb.data(), 128 * 4, hipMemcpyHostToDevice));
     MVP_HIP(hipMemset(st, 0, nst * 8));
-    MVP_HIP(hipFuncSetAttribute((const void*)mvp::tblock64_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    MVP_HIP(hipFuncSetAttribute((const void*)mvp::tblock64_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
     mvp::TB64Params p{x, w, b, w + nw, b + 64, y, mvp::conv_zero_region(), N, tiles, st};
     hipEvent_t e0, e1;
     MVP_HIP(hipEventCreate(&e0));
     MVP_HIP(hipEventCreate(&e1));
-    for (int i = 0; i < 3; i++) hipLaunchKernelGGL(mvp::tblock64_kernel, dim3(grid), dim3(256), G::LDS, 0, p);
+    for (int i = 0; i < 3; i++) hipLaunchKernelGGL(mvp::tblock64_kernel<false>, dim3(grid), dim3(256), G::LDS, 0, p);
     MVP_HIP(hipEventRecord(e0));
     const int reps = 10;
-    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(mvp::tblock64_kernel, dim3(grid), dim3(256), G::LDS, 0, p);
+    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(mvp::tblock64_kernel<false>, dim3(grid), dim3(256), G::LDS, 0, p);
     MVP_HIP(hipEventRecord(e1));
     MVP_HIP(hipEventSynchronize(e1));
     float ms = 0;
