@@ -17,6 +17,10 @@
 #include "det.h"
 #include "mvp_common.h"
 
+#ifndef DET_HALO_TR
+#define DET_HALO_TR 4  // output rows per halo tile (2, 4 or 8)
+#endif
+
 namespace mvp {
 namespace {
 
@@ -551,9 +555,13 @@ det_conv_gemm_kernel(GParams p) {
 // workgroup then runs its 9 K-steps without another barrier (3 workgroups per CU hide the
 // DMA).  One chunk: K order (tap, channel) as the GEMM kernel, identical sums; two chunks
 // (64 channels, one DMA + compute phase each): chunk-major K order, equal to f32 rounding.
-template <int BN, int NCK>  // NCK 32-channel input chunks, one DMA + compute phase each
-__global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
-    constexpr int TR = 2, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;  // halo pixels
+// TR output rows per tile (2 or 4): wave (wp, wc) computes rows wp, wp + 2, ... of cout half
+// wc.  4 rows spread each tile's weight DMA over twice the pixels (62.5 KB of LDS, 2
+// workgroups per CU, against 54 KB and 3 for 2 rows); the K order per output is the same.
+template <int BN, int NCK, int TR = 2>  // NCK 32-channel input chunks, one DMA + compute phase each
+__global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GParams p) {
+    constexpr int TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;  // halo pixels
+    constexpr int NRW = TR / 2;                                // output rows per wave
     constexpr int A_SLOTS = 9 * 4 * BN, A_R64 = A_SLOTS / 64;
     constexpr int B_R64 = (HP * 4 + 63) / 64;
     constexpr int WCT = BN / 32;
@@ -569,11 +577,13 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
     const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
     const int kg = lane >> 4, r16 = lane & 15;
     const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
-    f32x4 acc[4][WCT];
+    f32x4 acc[NRW][4][WCT];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
+    for (int rw = 0; rw < NRW; rw++)
 #pragma unroll
-        for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < WCT; c++) acc[rw][i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int q = 0; q < NCK; q++) {
     if (q > 0) __builtin_amdgcn_s_barrier();  // every wave is done with chunk q-1's images
     // weights: slot s of tap tp = tp * 4BN + 4co + (kg ^ swz(co))
@@ -598,25 +608,31 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
 #pragma unroll
     for (int tp = 0; tp < 9; tp++) {
         const int dy = tp / 3, dx = tp % 3;
-        bf16x8 a[WCT], b[4];
+        bf16x8 a[WCT], b[NRW][4];
 #pragma unroll
         for (int c = 0; c < WCT; c++)
             a[c] = *reinterpret_cast<const bf16x8*>(lds + tp * 4 * BN * 16 + (wc * (BN / 2) + c * 16) * 64 + soff);
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int hp = (wp + dy) * HW_ + i * 16 + r16 + dx;
-            b[i] = *reinterpret_cast<const bf16x8*>(lds + A_SLOTS * 16 + hp * 64 + ((kg ^ swz(hp)) * 16));
-        }
+        for (int rw = 0; rw < NRW; rw++)
 #pragma unroll
-        for (int i = 0; i < 4; i++)
+            for (int i = 0; i < 4; i++) {
+                const int hp = (wp + 2 * rw + dy) * HW_ + i * 16 + r16 + dx;
+                b[rw][i] = *reinterpret_cast<const bf16x8*>(lds + A_SLOTS * 16 + hp * 64 + ((kg ^ swz(hp)) * 16));
+            }
 #pragma unroll
-            for (int c = 0; c < WCT; c++)
-                acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+        for (int rw = 0; rw < NRW; rw++)
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < WCT; c++)
+                    acc[rw][i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[rw][i], acc[rw][i][c], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
-    const int ho = ho0 + wp;
-    if (ho >= p.H) return;
+#pragma unroll
+    for (int rw = 0; rw < NRW; rw++) {
+    const int ho = ho0 + wp + 2 * rw;
+    if (ho >= p.H) break;
 #pragma unroll
     for (int c = 0; c < WCT; c++) {
         const int co = wc * (BN / 2) + c * 16 + kg * 4;
@@ -627,7 +643,8 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
             const int wo = wo0 + i * 16 + r16;
             if (wo >= p.W) continue;
             const long m = ((long)n * p.H + ho) * p.W + wo;
-            float v[4] = {acc[i][c][0] + bb.x, acc[i][c][1] + bb.y, acc[i][c][2] + bb.z, acc[i][c][3] + bb.w};
+            const f32x4 ac = acc[rw][i][c];
+            float v[4] = {ac[0] + bb.x, ac[1] + bb.y, ac[2] + bb.z, ac[3] + bb.w};
             if (p.act == 2)
 #pragma unroll
                 for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
@@ -641,6 +658,7 @@ __global__ __launch_bounds__(256, 3) void det_conv_halo_kernel(GParams p) {
             *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
                 uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
         }
+    }
     }
 }
 
@@ -1081,17 +1099,23 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     // halo-tile kernel for the 32- and 64-channel 3x3/s1 convs (<= 64 couts): 14.03 -> 13.77
     // and 13.90 -> 13.86 ms per 64 frames against the im2col GEMM (same-box tools/det_ab.sh)
     if (ks == 3 && stride == 1 && (cin == 32 || cin == 64) && npad <= 64) {
-        const long tiles = (long)n * ((H + 1) / 2) * ((W + 63) / 64);
+        const char* e = getenv("MVPOSE_DET_HALO_ROWS");  // tests: 2 = the 2-row tiles
+        const int tr = (e && e[0] == '2') ? 2 : DET_HALO_TR;
+        const long tiles = (long)n * ((H + tr - 1) / tr) * ((W + 63) / 64);
         MVP_REQUIRE(tiles < (1L << 31), "det conv: grid too large");
         if (tiles == 0) return;
-        if (cin == 64 && npad == 64)
-            hipLaunchKernelGGL((det_conv_halo_kernel<64, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
-        else if (cin == 64)
-            hipLaunchKernelGGL((det_conv_halo_kernel<32, 2>), dim3((unsigned)tiles), dim3(256), 0, s, p);
-        else if (npad == 64)
-            hipLaunchKernelGGL((det_conv_halo_kernel<64, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
-        else
-            hipLaunchKernelGGL((det_conv_halo_kernel<32, 1>), dim3((unsigned)tiles), dim3(256), 0, s, p);
+        auto go = [&](auto kern) { hipLaunchKernelGGL(kern, dim3((unsigned)tiles), dim3(256), 0, s, p); };
+        if (tr == 2) {
+            if (cin == 64 && npad == 64) go(det_conv_halo_kernel<64, 2, 2>);
+            else if (cin == 64) go(det_conv_halo_kernel<32, 2, 2>);
+            else if (npad == 64) go(det_conv_halo_kernel<64, 1, 2>);
+            else go(det_conv_halo_kernel<32, 1, 2>);
+        } else {
+            if (cin == 64 && npad == 64) go(det_conv_halo_kernel<64, 2, DET_HALO_TR>);
+            else if (cin == 64) go(det_conv_halo_kernel<32, 2, DET_HALO_TR>);
+            else if (npad == 64) go(det_conv_halo_kernel<64, 1, DET_HALO_TR>);
+            else go(det_conv_halo_kernel<32, 1, DET_HALO_TR>);
+        }
         MVP_HIP(hipGetLastError());
         return;
     }

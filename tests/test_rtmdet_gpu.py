@@ -107,6 +107,28 @@ def test_layer_by_layer(sd, size, n):
     det.close()
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_halo_rows_bitwise(sd, size, n, monkeypatch):
+    """The 3x3/s1 convs with <= 64 channels on 4-row halo tiles (det_conv_halo_kernel<BN,
+    NCK, 4>, the default) against the 2-row tiles (MVPOSE_DET_HALO_ROWS=2): each output's K
+    order and epilogue are the same, so every tensor of the forward and the candidates are
+    bit-identical."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=7)).cuda()
+    outs = []
+    for rows in ("2", "4"):
+        monkeypatch.setenv("MVPOSE_DET_HALO_ROWS", rows)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        det.run_ops(frames, 0, len(det.spec.ops))
+        torch.cuda.synchronize()
+        ts = [det.tensor(t, n).cpu() for t in range(len(det.spec.tensors))]
+        outs.append((ts, det.cand[:n].cpu()))
+        det.close()
+    (ta, ca), (tb, cb) = outs
+    for t, (x, y) in enumerate(zip(ta, tb)):
+        assert torch.equal(x.view(torch.int16), y.view(torch.int16)), (size, t)
+    assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
+
+
 def test_select_is_argmax_of_candidates(det640):
     fr = torch.from_numpy(_frames(3, 720, 1280, seed=11)).cuda()
     out = det640.detect(fr)
