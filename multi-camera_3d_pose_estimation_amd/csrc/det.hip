@@ -706,20 +706,35 @@ __global__ __launch_bounds__(256) void ca_pool_kernel(CaParams p) {
     }
 }
 
-__global__ __launch_bounds__(256) void ca_fc_kernel(CaParams p) {
+// One 64-lane workgroup per (image, 64 output channels): the C-long dot products keep their
+// k order (one fmaf chain per output), with the weights loaded kCaBatch rows at a time ahead
+// of the chain; one workgroup per image with one load per fmaf ran ~95 us per call at 128
+// images (a load latency per k, half the CUs idle).
+constexpr int kCaBatch = 8;
+
+__global__ __launch_bounds__(64) void ca_fc_kernel(CaParams p) {
     extern __shared__ float mean[];  // [C]
-    const int n = blockIdx.x, tid = threadIdx.x;
-    for (int c = tid; c < p.C; c += 256) {
+    const int n = blockIdx.y, tid = threadIdx.x;
+    for (int c = tid; c < p.C; c += 64) {
         float sum = 0.f;
         for (int i = 0; i < kCaSplit; i++) sum += p.part[((size_t)n * kCaSplit + i) * p.C + c];
         mean[c] = sum / (float)p.HW;
     }
     __syncthreads();
-    for (int c = tid; c < p.C; c += 256) {
-        float a = p.b[c];
-        for (int k = 0; k < p.C; k++) a = fmaf(p.wt[(size_t)k * p.C + c], mean[k], a);
-        p.s[(size_t)n * p.C + c] = fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
+    const int c = blockIdx.x * 64 + tid;
+    if (c >= p.C) return;
+    float a = p.b[c];
+    const float* wc = p.wt + c;
+    int k = 0;
+    for (; k + kCaBatch <= p.C; k += kCaBatch) {
+        float w[kCaBatch];
+#pragma unroll
+        for (int j = 0; j < kCaBatch; j++) w[j] = wc[(size_t)(k + j) * p.C];
+#pragma unroll
+        for (int j = 0; j < kCaBatch; j++) a = fmaf(w[j], mean[k + j], a);
     }
+    for (; k < p.C; k++) a = fmaf(wc[(size_t)k * p.C], mean[k], a);
+    p.s[(size_t)n * p.C + c] = fminf(fmaxf(a + 3.f, 0.f), 6.f) / 6.f;
 }
 
 __global__ __launch_bounds__(256) void ca_scale_kernel(uint16_t* x, const float* s, int HW, int C, int xs) {
@@ -1159,7 +1174,8 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
     CaParams p{x, wt, b, part, sc, HW, C, xs};
     hipLaunchKernelGGL(ca_pool_kernel, dim3(kCaSplit, (unsigned)n), dim3(256), lds, s, p);
     MVP_HIP(hipGetLastError());
-    hipLaunchKernelGGL(ca_fc_kernel, dim3((unsigned)n), dim3(256), (size_t)C * sizeof(float), s, p);
+    hipLaunchKernelGGL(ca_fc_kernel, dim3((unsigned)((C + 63) / 64), (unsigned)n), dim3(64), (size_t)C * sizeof(float),
+                       s, p);
     MVP_HIP(hipGetLastError());
     const long work = (long)HW * (C / 8);
     hipLaunchKernelGGL(ca_scale_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, sc, HW,
