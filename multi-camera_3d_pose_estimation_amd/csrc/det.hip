@@ -850,6 +850,61 @@ __global__ __launch_bounds__(256) void det_head_kernel(HeadParams p) {
     out[5] = a[0];
 }
 
+// The same head with the features staged through LDS: a pixel's [cls | reg] channels sit
+// xs elements apart, so one lane per pixel made every 16-B load instruction touch 64 rows
+// (2.3 TB/s).  Here the workgroup's 256 pixels x 32 + 32 channels arrive as 64-B runs per
+// pixel (coalesced), then each lane runs the same fmaf chains in the same k order.
+constexpr int kHeadKC = 32;  // channels of cls and of reg per staging step
+
+__global__ __launch_bounds__(256) void det_head_staged_kernel(HeadParams p) {
+#pragma clang fp contract(off)  // box arithmetic rounded op by op, as mmdet's torch ops
+    extern __shared__ float swh[];  // [5][F], then the pixel block [256][9] uint4
+    uint4* sx = reinterpret_cast<uint4*>(swh + ((5 * p.F + 3) & ~3));
+    const int n = blockIdx.y, tid = threadIdx.x;
+    for (int i = tid; i < 5 * p.F; i += 256) swh[i] = p.w[i];
+    const int HW = p.H * p.W, px0 = blockIdx.x * 256;
+    const uint16_t* xb = p.x + (size_t)n * HW * p.xs;
+    float a[5] = {p.b[0], p.b[1], p.b[2], p.b[3], p.b[4]};
+    for (int kc = 0; kc < p.F; kc += kHeadKC) {
+        __syncthreads();  // the previous step's block is consumed (and the weights are in)
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int i = tid + 256 * j, pl = i >> 3, q = i & 7;
+            const int pg = min(px0 + pl, HW - 1);
+            const int ch = q < 4 ? kc + 8 * q : p.F + kc + 8 * (q - 4);
+            sx[pl * 9 + q] = *reinterpret_cast<const uint4*>(xb + (size_t)pg * p.xs + ch);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int sq = 0; sq < kHeadKC / 8; sq++) {
+            const int k = kc + 8 * sq;
+            float c[8], r[8];
+            unpack8(sx[tid * 9 + sq], c);
+            unpack8(sx[tid * 9 + 4 + sq], r);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                a[0] = fmaf(swh[k + j], c[j], a[0]);
+#pragma unroll
+                for (int o = 1; o < 5; o++) a[o] = fmaf(swh[o * p.F + k + j], r[j], a[o]);
+            }
+        }
+    }
+    const int px = px0 + tid;
+    if (px >= HW) return;
+    const int yy = px / p.W, xx = px - yy * p.W;
+    const float s = (float)p.stride;
+    const float pxf = (float)xx * s, pyf = (float)yy * s;
+    const float d0 = expf(a[1]) * s, d1 = expf(a[2]) * s, d2 = expf(a[3]) * s, d3 = expf(a[4]) * s;
+    const float lim = (float)p.size;
+    float* out = p.cand + ((size_t)n * p.n_priors + p.prior0 + px) * 6;
+    out[0] = 1.f / (1.f + expf(-a[0]));
+    out[1] = fminf(fmaxf(pxf - d0, 0.f), lim);
+    out[2] = fminf(fmaxf(pyf - d1, 0.f), lim);
+    out[3] = fminf(fmaxf(pxf + d2, 0.f), lim);
+    out[4] = fminf(fmaxf(pyf + d3, 0.f), lim);
+    out[5] = a[0];
+}
+
 // ------------------------------------------------------------------ per-frame argmax
 // The reference keeps the first detection after mmdet's NMS = the highest-scoring prior
 // that passed score_thr and the min-size filter (NMS never removes the top box).  Ties go
@@ -1206,8 +1261,13 @@ void launch_det_head(const uint16_t* x, int xs, int F, const float* w, const flo
     MVP_REQUIRE(F % 8 == 0 && xs >= 2 * F && prior0 + H * W <= n_priors, "det head: shape");
     HeadParams p{x, w, b, cand, H, W, F, xs, stride, size, n_priors, prior0};
     if (n == 0) return;
-    hipLaunchKernelGGL(det_head_kernel, dim3((unsigned)((H * W + 255) / 256), (unsigned)n), dim3(256),
-                       (size_t)5 * F * sizeof(float), s, p);
+    const dim3 grid((unsigned)((H * W + 255) / 256), (unsigned)n);
+    const char* e = getenv("MVPOSE_DET_HEAD_DIRECT");  // tests: 1 = one lane per pixel from HBM
+    if (F % kHeadKC == 0 && !(e && e[0] == '1'))
+        hipLaunchKernelGGL(det_head_staged_kernel, grid, dim3(256),
+                           (size_t)((5 * F + 3) & ~3) * sizeof(float) + 256 * 9 * sizeof(uint4), s, p);
+    else
+        hipLaunchKernelGGL(det_head_kernel, grid, dim3(256), (size_t)5 * F * sizeof(float), s, p);
     MVP_HIP(hipGetLastError());
 }
 

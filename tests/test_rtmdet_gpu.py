@@ -129,6 +129,25 @@ def test_halo_rows_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_head_staged_bitwise(sd, size, n, monkeypatch):
+    """The head predictions with the [cls | reg] features staged through LDS
+    (det_head_staged_kernel, the default) against one lane per pixel reading HBM directly
+    (MVPOSE_DET_HEAD_DIRECT=1): same fmaf chains in the same k order, bit-identical
+    candidates."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=8)).cuda()
+    cands = []
+    for direct in ("1", "0"):
+        monkeypatch.setenv("MVPOSE_DET_HEAD_DIRECT", direct)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        det.run_ops(frames, 0, len(det.spec.ops))
+        torch.cuda.synchronize()
+        cands.append(det.cand[:n].cpu())
+        det.close()
+    assert torch.isfinite(cands[1]).all()
+    assert torch.equal(cands[0].view(torch.int32), cands[1].view(torch.int32))
+
+
 def test_select_is_argmax_of_candidates(det640):
     fr = torch.from_numpy(_frames(3, 720, 1280, seed=11)).cuda()
     out = det640.detect(fr)
