@@ -757,31 +757,41 @@ __global__ __launch_bounds__(256) void ca_scale_kernel(uint16_t* x, const float*
 // workgroup per (image, 8-channel group) keeps the plane in LDS and applies the 5x5 max
 // three times, writing each result into its slice.
 __global__ __launch_bounds__(256) void spp_kernel(uint16_t* buf, int H, int W, int C, int xs) {
-    extern __shared__ uint4 pl[];  // two planes [H*W] of 8 channels
+    extern __shared__ uint4 pl[];  // three planes [H*W] of 8 channels: input, row maxima, output
     const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, HW = H * W;
     uint16_t* base = buf + (size_t)n * HW * xs + cg * 8;
     uint4* a = pl;
-    uint4* b = pl + HW;
+    uint4* r = pl + HW;
+    uint4* b = pl + 2 * HW;
     for (int i = tid; i < HW; i += 256) a[i] = *reinterpret_cast<const uint4*>(base + (size_t)i * xs);
+    // the 5x5 max as a 5-wide row max, then a 5-tall column max of those (max is exact and
+    // order-free; every value is bf16, so the packed row maxima are exact too)
     for (int k = 1; k <= 3; k++) {
         __syncthreads();
         for (int i = tid; i < HW; i += 256) {
             const int y = i / W, x = i - y * W;
             float m[8];
             for (int c = 0; c < 8; c++) m[c] = -__builtin_inff();
-            for (int dy = -2; dy <= 2; dy++) {
-                const int yy = y + dy;
-                if (yy < 0 || yy >= H) continue;
-                for (int dx = -2; dx <= 2; dx++) {
-                    const int xx = x + dx;
-                    if (xx < 0 || xx >= W) continue;
-                    float v[8];
-                    unpack8(a[yy * W + xx], v);
+            for (int xx = max(x - 2, 0); xx <= min(x + 2, W - 1); xx++) {
+                float v[8];
+                unpack8(a[y * W + xx], v);
 #pragma unroll
-                    for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
-                }
+                for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
             }
-            const uint4 o = pack8(m);  // exact: every value is already bf16
+            r[i] = pack8(m);
+        }
+        __syncthreads();
+        for (int i = tid; i < HW; i += 256) {
+            const int y = i / W, x = i - y * W;
+            float m[8];
+            for (int c = 0; c < 8; c++) m[c] = -__builtin_inff();
+            for (int yy = max(y - 2, 0); yy <= min(y + 2, H - 1); yy++) {
+                float v[8];
+                unpack8(r[yy * W + x], v);
+#pragma unroll
+                for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
+            }
+            const uint4 o = pack8(m);
             b[i] = o;
             *reinterpret_cast<uint4*>(base + (size_t)i * xs + k * C) = o;
         }
@@ -1240,7 +1250,7 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
 
 void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s) {
     MVP_REQUIRE(C % 8 == 0 && xs >= 4 * C && xs % 8 == 0, "spp: C=%d stride=%d", C, xs);
-    const size_t lds = (size_t)2 * H * W * sizeof(uint4);
+    const size_t lds = (size_t)3 * H * W * sizeof(uint4);
     MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large", H, W);
     if (n == 0) return;
     hipLaunchKernelGGL(spp_kernel, dim3((unsigned)(C / 8), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
