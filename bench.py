@@ -69,16 +69,19 @@ def spawn_ranks(n):
     return subprocess.call(cmd)
 
 
+# The committed PMC traffic pass the roofline lines cite (tools/pmc_traffic.py): named explicitly —
+# a newest-file rule picked r04zz_ over r04zz2_ by lexicographic order in round 4.
+TRAFFIC_FILE = "profiles/r04zz2_traffic.json"
+
+
 def committed_traffic():
-    """HBM bytes per launch from the newest committed PMC pass (profiles/rNN_traffic.json,
-    tools/pmc_traffic.py: 2*FETCH_SIZE + WRITE_SIZE, gfx950-corrected) — PMC counters cannot be
-    read from inside a normal run."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
-    if not files:
+    """HBM bytes per launch from the committed PMC pass TRAFFIC_FILE (2*FETCH_SIZE + WRITE_SIZE,
+    gfx950-corrected) — PMC counters cannot be read from inside a normal run."""
+    path = os.path.join(ROOT, TRAFFIC_FILE)
+    if not os.path.exists(path):
         return {}, None
-    with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
+    with open(path) as f:
+        return json.load(f), TRAFFIC_FILE
 
 
 def setup_dist(args):
@@ -161,39 +164,31 @@ def cpu_baseline(n_frames, n_frames_1t, views):
     return out
 
 
-# VALU issue model: cycles per wave64 instruction per SIMD, measured on MI355X with every CU
-# busy (tools/fp64_probe.hip, profiles/r04_fp64_probe.txt): v_fma_f64 5.3, v_mul_f64 5.0,
-# v_add_f64 4.6, v_rcp_f64 16.4, v_fma_f32 2.7 (the guide's SIMD-32 model gives 2 for f32 and
-# 4 for fp64 at half rate; the measured costs include the issue overheads at full occupancy)
-VALU_CYC, F64_CYC, TRANS_CYC = 2.67, 5.0, 16.4
-N_SIMDS, CLOCK_HZ = 1024, 2.4e9
+# Triangulation's real bound is VALU issue (fp64 undistortion + solver), read from a committed PMC
+# pass of the same kernel (tools/tri_pmc_json.py): valu_busy = SQ_ACTIVE_INST_VALU x 4 cycles per
+# SIMD over GRBM_GUI_ACTIVE / 8 cycles per XCD, at the clock the chip held in that pass
+# (GRBM_GUI_ACTIVE / 8 / dispatch duration).  The issue floor at that clock is the busy cycles'
+# share of the launch: floor_ms = valu_busy x the pass's duration.
+TRI_TOL_PMC = "r05_tri_tol_pmc.json"
+TRI_REF_PMC = "r05_tri_ref_pmc.json"
 
 
-def tri_valu_issue(tri_ms, n_points, pmc_file):
-    """The triangulation kernels' real bound: VALU issue (fp64 undistortion + solver).  From a
-    committed PMC pass of that kernel: per-wave instruction counts by type x their issue cycles
-    (VALU_CYC / F64_CYC / TRANS_CYC) over the 1,024 SIMDs at 2.4 GHz = the issue floor of a
-    launch of n_points; frac = floor / measured launch time."""
+def tri_valu_issue(tri_ms, pmc_file):
     path = os.path.join(ROOT, "profiles", pmc_file)
     if not os.path.exists(path):
         return None
     pmc = json.load(open(path))
-    if "per_wave" in pmc:          # r03 format (tools/r03_tri.sh): raw SQ counters per wave
-        w = pmc["per_wave"]
-        f64 = w["SQ_INSTS_VALU_ADD_F64"] + w["SQ_INSTS_VALU_FMA_F64"] + w["SQ_INSTS_VALU_MUL_F64"]
-        trans = w["SQ_INSTS_VALU_TRANS_F64"]
-        valu = w["SQ_INSTS_VALU"]
-    else:                          # r01 format (tools/pmc_tri.sh)
-        f64 = pmc["f64_add_per_wave"] + pmc["f64_fma_per_wave"] + pmc["f64_mul_per_wave"]
-        trans = 0.0
-        valu = pmc["valu_instr_per_wave"]
-    cyc = (valu - f64 - trans) * VALU_CYC + f64 * F64_CYC + trans * TRANS_CYC
-    waves = n_points / 64.0
-    floor = waves * cyc / (N_SIMDS * CLOCK_HZ) * 1e3
-    return {"valu_instr_per_wave": valu, "f64_instr_per_wave": f64, "trans_f64_per_wave": trans,
-            "issue_cycles_per_wave": cyc, "issue_floor_ms": floor, "frac": floor / tri_ms,
-            "model": f"{VALU_CYC} cyc per VALU, {F64_CYC} per fp64, {TRANS_CYC} per fp64 transcendental "
-                     "(measured, profiles/r04_fp64_probe.txt); 1,024 SIMDs at 2.4 GHz", "source": f"profiles/{pmc_file}"}
+    if "valu_busy" not in pmc:
+        return None
+    w = pmc.get("per_wave", {})
+    f64 = sum(w.get(k, 0.0) for k in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64"))
+    return {"frac": pmc["valu_busy"], "clock_GHz": pmc.get("clock_GHz_median"),
+            "pmc_launch_ms": pmc.get("duration_ms_median"), "bench_launch_ms": tri_ms,
+            "valu_instr_per_wave": w.get("SQ_INSTS_VALU"), "f64_instr_per_wave": f64,
+            "trans_f64_per_wave": w.get("SQ_INSTS_VALU_TRANS_F64"),
+            "model": "frac = SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs / (GRBM_GUI_ACTIVE / 8): the SIMDs' VALU-issue "
+                     "share of the kernel's cycles, at the clock GRBM_GUI_ACTIVE / 8 / duration (MI355X_MICROARCH.md "
+                     "DVFS give-back)", "source": f"profiles/{pmc_file}"}
 
 
 def tri_line(ops, syn, dev, s, views, mode, reps=10, tolerance=False):
@@ -563,16 +558,16 @@ def main():
         if V == 2:
             tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE, tolerance=True)
             tri["kernel"] = "triangulate_tol2_kernel (+ triangulate_tol2_fallback_kernel)"
-            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17, "r03t_tri_tol_pmc.json")
+            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_TOL_PMC)
             tri["solver"] = "tolerance (MVP_TRI_TOLERANCE): the pipeline's default"
             compat = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
             compat["kernel"] = "triangulate_reference_kernel"
-            compat["valu_issue"] = tri_valu_issue(compat["avg_launch_ms"], TRI_T * 17, "r01_tri_pmc.json")
+            compat["valu_issue"] = tri_valu_issue(compat["avg_launch_ms"], TRI_REF_PMC)
             tri["reference_compat"] = compat
         else:
             tri = tri_line(ops, syn, dev, s, V, ops.TRI_REFERENCE)
             tri["kernel"] = "triangulate_reference_kernel"
-            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_T * 17, "r01_tri_pmc.json")
+            tri["valu_issue"] = tri_valu_issue(tri["avg_launch_ms"], TRI_REF_PMC)
         extra["roofline_triangulate"] = tri
         if not args.no_extra:
             t4 = tri_line(ops, syn, dev, s, 4, ops.TRI_ALL_VIEWS)

@@ -73,17 +73,23 @@ int mvp_camera_pack(const double* K_host, const double* dist5_host, const double
 #define MVP_TRI_REFERENCE 0
 #define MVP_TRI_ALL_VIEWS 1
 /* OR-ed into mode: solve every point with the exact JacobiSVDImpl_ restatement
- * (default: QR + inverse iteration, Jacobi only where that has not converged). */
+ * (default: QR + inverse iteration, Jacobi where that has not converged or its f32
+ * outputs are not certified equal to Jacobi's: the same float32 bits either way). */
 #define MVP_TRI_EXACT_JACOBI 0x10
-/* OR-ed into mode: throughput solver validated to <= 1e-4 world units against the exact
- * path (mixed f32/fp64 undistortion, normal-equation inverse iteration; the exact path for
- * any point that has not provably converged).  Reference mode with 2 listed cameras; other
- * cases run the default solver. */
+/* OR-ed into mode: throughput solver whose float32 outputs are certified bit-identical to the
+ * exact path's (mixed f32/fp64 undistortion, normal-equation inverse iteration; a point whose
+ * f32 roundings cannot be proven equal is re-solved on the exact path by a second launch).
+ * Reference mode with 2 listed cameras; other cases run the default solver.  With
+ * out_xyzw_dev != NULL every point takes the exact path (the float64 vectors are diagnostics). */
 #define MVP_TRI_TOLERANCE 0x20
 
 int mvp_triangulate(const float* kpts_dev, int64_t n_points, int V, const double* cams_dev,
                     int n_cams, const int* cam_idx_host, int n_cam_idx, int mode,
                     float* out_xyz_dev, double* out_xyzw_dev, void* stream);
+
+/* Points the MVP_TRI_TOLERANCE solver re-solved on the exact path on this stream so far
+ * (observability; synchronises the stream).  No reference counterpart. */
+int mvp_triangulate_fallback_total(void* stream, unsigned long long* out_total_host);
 
 /* ---------------------------------------------------------------------------
  * mvp_triangulate_points_f64 — replaces utils.triangulate_points (utils.py:1277-1336)

@@ -596,8 +596,6 @@ bool launch_conv1x1_wide(const ConvLaunch& c, hipStream_t s) {
     if (c.ks != 1 || c.stride != 1 || c.out_f32_nchw || c.Cout != 256 || !c.relu) return false;
     if (!(cin == 64 || (cin == 128 && c.x2 && c.c1 == 64))) return false;
     if (cin == 64 && !c.res) return false;
-    const char* e = getenv("MVPOSE_NO_WIDE1X1");  // diagnostics/tests: conv1x1_kernel instead
-    if (e && e[0] == '1') return false;
     const long n_pix = (long)c.N * c.H * c.W;
     if (n_pix == 0) return true;
     PPair p{c.x, c.x2, 64, cin == 128 ? 64 : 0, 2, c.w, c.bias, c.res, c.y, nullptr, nullptr,
@@ -674,11 +672,6 @@ bool launch_conv1x1_direct(const ConvLaunch& c, hipStream_t s) {
     if (launch_conv1x1_wide(c, s)) return true;
     const int bm = conv_cout_pad(c.Cout) % 128 == 0 && c.Cin <= 64 ? 128 : conv_cout_pad(c.Cout) % 64 == 0 ? 64 : 32;
     if (c.Cout % (bm / 4) != 0) return false;  // lane groups own bm/4 consecutive couts
-    static const bool disabled = [] {
-        const char* e = getenv("MVPOSE_NO_1X1");  // diagnostics: use the generic conv kernel
-        return e && e[0] == '1';
-    }();
-    if (disabled && !c.x2) return false;
     const int cout_pad = conv_cout_pad(c.Cout);
     const int kch = c.Cin / 32;
     P1x1 p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), (long)c.N * c.H * c.W, c.Cout, c.relu,

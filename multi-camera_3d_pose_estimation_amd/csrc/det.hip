@@ -247,71 +247,6 @@ __global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
     if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(a1);
 }
 
-// Variant (MVPOSE_DET_DW=1): weights staged in LDS (wave-uniform broadcast reads), loop over
-// the kernel rows outside so each tap row's 40 weights are read once per lane.
-template <int G>
-__global__ __launch_bounds__(G * 64) void dw5b_kernel(DwParams p) {
-    __shared__ uint4 sh[G][kDwHH * kDwHW];
-    __shared__ float4 sw[G][25][2];
-    const int n_groups = p.C / (8 * G);
-    const int grp = blockIdx.x % n_groups;
-    const int t2 = blockIdx.x / n_groups;
-    const int tw = t2 % p.tiles_w, th = t2 / p.tiles_w;
-    const int n = blockIdx.y;
-    const int h0 = th * kDwTH - 2, w0 = tw * kDwTW - 2;
-    const int tid = threadIdx.x;
-    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs + grp * 8 * G;
-    for (int i = tid; i < kDwHH * kDwHW * G; i += G * 64) {
-        const int pix = i / G, q = i - pix * G;
-        const int r = pix / kDwHW, c = pix - r * kDwHW;
-        const int hi = h0 + r, wi = w0 + c;
-        sh[q][pix] = (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                         ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + q * 8)
-                         : uint4{0u, 0u, 0u, 0u};
-    }
-    for (int i = tid; i < G * 50; i += G * 64)
-        (&sw[0][0][0])[i] = reinterpret_cast<const float4*>(p.w + (size_t)grp * G * 200)[i];
-    __syncthreads();
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-    const int col = lane & 15, rp = lane >> 4;
-    const int chunk = grp * G + wave;
-    float a0[8], a1[8];
-#pragma unroll
-    for (int c = 0; c < 8; c++) a0[c] = a1[c] = 0.f;
-#pragma unroll
-    for (int kh = 0; kh < 5; kh++) {
-        float w[5][8];
-#pragma unroll
-        for (int kw = 0; kw < 5; kw++) {
-            const float4 u = sw[wave][kh * 5 + kw][0], v = sw[wave][kh * 5 + kw][1];
-            w[kw][0] = u.x, w[kw][1] = u.y, w[kw][2] = u.z, w[kw][3] = u.w;
-            w[kw][4] = v.x, w[kw][5] = v.y, w[kw][6] = v.z, w[kw][7] = v.w;
-        }
-#pragma unroll
-        for (int o = 0; o < 2; o++) {
-#pragma unroll
-            for (int kw = 0; kw < 5; kw++) {
-                float v[8];
-                unpack8(sh[wave][(2 * rp + o + kh) * kDwHW + col + kw], v);
-                float* acc = o ? a1 : a0;
-#pragma unroll
-                for (int c = 0; c < 8; c++) acc[c] = fmaf(v[c], w[kw][c], acc[c]);
-            }
-        }
-    }
-    const int ho = th * kDwTH + 2 * rp, wo = tw * kDwTW + col;
-    if (wo >= p.W) return;
-    const float* bc = p.b + chunk * 8;
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-        a0[c] = act_f(a0[c] + bc[c], p.act);
-        a1[c] = act_f(a1[c] + bc[c], p.act);
-    }
-    uint16_t* yb = p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + chunk * 8;
-    if (ho < p.H) *reinterpret_cast<uint4*>(yb) = pack8(a0);
-    if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(a1);
-}
-
 // ------------------------------------------------------------------ conv = GEMM
 // Every detector conv is a GEMM over the flat output-pixel index m = (n, ho, wo):
 //   Y[m][cout] = sum_k X~[m][k] W[cout][k],  k = (tap, cin) (weights [cout][kh][kw][cin]),
@@ -1126,15 +1061,7 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
     const long blocks = (long)p.tiles_w * ((H + kDwTH - 1) / kDwTH) * (C / (8 * G));
     if (n == 0 || blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
-    static const bool variant = [] {
-        const char* e = getenv("MVPOSE_DET_DW");  // A/B: 1 = LDS-staged weights
-        return e && e[0] == '1';
-    }();
-    if (variant && G == 8)
-        hipLaunchKernelGGL(dw5b_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
-    else if (variant)
-        hipLaunchKernelGGL(dw5b_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
-    else if (G == 8)
+    if (G == 8)
         hipLaunchKernelGGL(dw5_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
     else
         hipLaunchKernelGGL(dw5_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);

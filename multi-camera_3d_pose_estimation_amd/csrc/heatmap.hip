@@ -750,10 +750,8 @@ extern "C" int mvp_heatmap_moments(const float* hm, int N, int K, int h, int w, 
                         (size_t)((h + 2) & ~1) * 8 + (size_t)(h + 1) * 48;
     MVP_REQUIRE(lds0 <= kMomMaxLds, "mvp_heatmap_moments: map %dx%d + image %dx%d exceed the LDS budget", h, w,
                 img_h, img_w);
-    // the mixed-column closed forms need a 48-B prefix row per image row (separable == 1 only;
-    // MVPOSE_MOM_NO_MIXCF=1 walks every mixed column, for tests)
-    const char* nm = getenv("MVPOSE_MOM_NO_MIXCF");
-    const bool mixcf = separable == 1 && !(nm && nm[0] == '1') && lds0 + (size_t)img_h * 48 <= kMomMaxLdsCf;
+    // the mixed-column closed forms need a 48-B prefix row per image row (separable == 1 only)
+    const bool mixcf = separable == 1 && lds0 + (size_t)img_h * 48 <= kMomMaxLdsCf;
     const size_t lds = mixcf ? lds0 + (size_t)img_h * 48 : lds0;
     static bool attr = false;
     if (!attr) {

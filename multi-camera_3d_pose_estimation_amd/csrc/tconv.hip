@@ -100,7 +100,6 @@ struct TParams {
     const uint16_t* zero;
     uint16_t* sink;
     int N, Cout, n_tiles, ncb;  // ncb = Cout / BM column blocks (1 when weights are resident)
-    int diag;                   // diagnostics (MVPOSE_TCONV_DIAG): 2 = no stores
 };
 
 template <int CIN, int H, int W, int TH, int NB, bool WRES, bool RES, int BM, bool PM>
@@ -112,7 +111,6 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
     const int mg = wave % G::MG, pg = wave / G::MG;
     if ((int)blockIdx.x >= p.n_tiles) return;
     constexpr int tiles_h = H / TH;
-    const bool do_st = !(p.diag & 2);
 
     // weight slot (within one chunk's [tap][q][cout] image) -> element offset in w[cout][3][3][Cin]
     auto wsrc_off = [&](int ws) {
@@ -289,7 +287,7 @@ __global__ __launch_bounds__(512, 1) void tconv_kernel(TParams p) {
             __builtin_amdgcn_sched_barrier(0);
         }
 
-        if (last && do_st) {
+        if (last) {
             if (RES) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::PPW) : "memory");
 #pragma unroll
             for (int t = 0; t < G::NT; t++) {
@@ -345,9 +343,7 @@ void launch_t(const ConvLaunch& c, hipStream_t s) {
     MVP_REQUIRE(c.Cout % BM == 0, "tconv: Cout %d not a multiple of %d", c.Cout, BM);
     const long tiles = (long)((c.N + NB - 1) / NB) * (H / TH) * (c.Cout / BM);
     MVP_REQUIRE(tiles < (1L << 30), "tconv: too many tiles");
-    const char* dg = getenv("MVPOSE_TCONV_DIAG");
-    TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM,
-              dg ? atoi(dg) : 0};
+    TParams p{c.x, c.w, c.bias, c.res, c.y, conv_zero_region(), g_t_sink, c.N, c.Cout, (int)tiles, c.Cout / BM};
     // pixel-major halo wherever its 25 % larger ring slot still fits the LDS (+2.4-2.9 %
     // frames/s on the 64- and 256-ch planes, round 2), plane-major otherwise
     constexpr bool PM = TCfg<CIN, H, W, TH, NB, WRES, BM, true>::LDS <= 160 * 1024;

@@ -106,7 +106,6 @@ struct T16Params {
     const uint16_t* zero;
     uint16_t* sink;
     int N, Cout, n_tiles, ncb;
-    int diag;  // MVPOSE_TCONV16_DIAG (timing only): 2 = no stores
 };
 
 template <int CIN, int H, int W, int TH, int NB, int BM, bool RES>
@@ -118,7 +117,6 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
     const int mg = wave % G::MG, pg = wave / G::MG;
     if ((int)blockIdx.x >= p.n_tiles) return;
     constexpr int tiles_h = H / TH;
-    const bool do_st = !(p.diag & 2);
 
     // ---- per-lane DMA geometry (fixed for the launch): kind << 29 | nb << 24 | hy << 19 | offset.
     // Waves 0-3 issue the pieces of "virtual waves" vw = wave and wave + 4 (their SIMD partner),
@@ -280,7 +278,7 @@ __global__ __launch_bounds__(512, 1) void tconv16_kernel(T16Params p) {
             __builtin_amdgcn_sched_barrier(0);
         }
 
-        if (last && do_st) {
+        if (last) {
             // the residual loads precede this item's DMA pieces (PPW, or PPW - 1 on the waves whose
             // last piece is past the item): wait for all but PPW - 1 of them
             if (RES) {
@@ -348,9 +346,7 @@ void launch_t16(const ConvLaunch& c, hipStream_t s) {
     int grid = (int)std::min<long>(tiles, g_t16_cus);
     if (grid < tiles) grid -= grid % (8 * ncb);  // fixed cout block per workgroup
     MVP_REQUIRE(grid > 0, "tconv16: %d CUs", g_t16_cus);
-    const char* dg = getenv("MVPOSE_TCONV16_DIAG");
-    T16Params p{c.x, c.w_img, c.bias, c.res, c.y, conv_zero_region(), g_t16_sink, c.N, c.Cout, (int)tiles, ncb,
-                dg ? atoi(dg) : 0};
+    T16Params p{c.x, c.w_img, c.bias, c.res, c.y, conv_zero_region(), g_t16_sink, c.N, c.Cout, (int)tiles, ncb};
     if (c.res)
         launch_k16<CIN, H, W, TH, NB, BM, true>(p, grid, s);
     else

@@ -41,6 +41,7 @@ SIGNATURES = {
     "mvp_triangulate": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_int, P(c_int), c_int, c_int,
                                 c_void_p, c_void_p, c_void_p]),
     "mvp_triangulate_points_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mvp_triangulate_fallback_total": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),
     "mvp_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, P(c_float), P(c_float),
                                c_int, c_int, c_void_p, c_void_p]),
     "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,

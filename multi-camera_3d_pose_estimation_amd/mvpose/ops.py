@@ -79,11 +79,14 @@ def triangulate(kpts: torch.Tensor, cams: torch.Tensor, cam_idx: Sequence[int] =
                 return_xyzw: bool = False, exact: bool = False, tolerance: bool = False):
     """kpts (..., 3, V) float32 on GPU (reference layout) -> (..., 3) float32.
 
-    cams: (n_cams, 40) float64 on GPU (pack_cameras).  Default: OpenCV's rounding sequence
-    (bit-identical to the restatement), QR + inverse iteration with the Jacobi restatement
-    where that has not converged; exact=True: the JacobiSVDImpl_ restatement for every point;
-    tolerance=True: the throughput solver (MVP_TRI_TOLERANCE, reference mode with two listed
-    cameras), within 1e-4 world units of the exact path."""
+    cams: (n_cams, 40) float64 on GPU (pack_cameras).  Every solver returns the exact path's
+    float32 bits (OpenCV 4.9's rounding sequence restated).  Default: QR + inverse iteration,
+    the Jacobi restatement where that has not converged or is not certified; exact=True: the
+    JacobiSVDImpl_ restatement for every point; tolerance=True: the throughput solver
+    (MVP_TRI_TOLERANCE, reference mode with two listed cameras), certified per point, the
+    exact path by a second launch where it is not.  return_xyzw: the float64 null vectors
+    (diagnostic; bit-identical to the exact path's only where that path solved the point —
+    every point in tolerance mode)."""
     if exact and tolerance:
         raise ValueError("exact and tolerance exclude each other")
     if exact:
@@ -110,6 +113,14 @@ def triangulate(kpts: torch.Tensor, cams: torch.Tensor, cam_idx: Sequence[int] =
     call("mvp_triangulate", _ptr(kpts), n, V, _ptr(cams), cams.shape[0], ci, len(cam_idx), int(mode),
          _ptr(out), _ptr(xyzw) if xyzw is not None else None, _stream(kpts.device))
     return (out, xyzw) if return_xyzw else out
+
+
+def triangulate_fallback_total(device=None) -> int:
+    """Points the MVP_TRI_TOLERANCE solver has re-solved on the exact path on the current stream
+    so far (mvp_triangulate_fallback_total; synchronises the stream)."""
+    out = ctypes.c_ulonglong(0)
+    call("mvp_triangulate_fallback_total", _stream(device), ctypes.byref(out))
+    return int(out.value)
 
 
 def triangulate_points_f64(kpts: torch.Tensor, cams: torch.Tensor, return_xyzw: bool = False):

@@ -101,6 +101,58 @@ void orc_undistort_points_f64(const double* src, int64_t n, const double* K, con
         undistort_one(src[2 * i], src[2 * i + 1], A, k, 5, &dst[2 * i], &dst[2 * i + 1]);
 }
 
+/* ---- glibc 2.35 __ieee754_hypot restated (sysdeps/ieee754/dbl-64/e_hypot.c, non-FMA kernel) ---
+ * The oracle's Jacobi calls libm's hypot, as OpenCV's does; this restatement is the text the
+ * device's exact path (csrc/triangulate.hip hypot_glibc) follows, checked against libm by
+ * tests/test_oracle_triangulate.py. */
+static double orc_hypot_kernel(double ax, double ay)
+{
+    double h = sqrt(ax * ax + ay * ay), t1, t2;
+    if (h <= 2.0 * ay) {
+        double delta = h - ay;
+        t1 = ax * (2.0 * delta - ax);
+        t2 = (delta - 2.0 * (ax - ay)) * delta;
+    } else {
+        double delta = h - ax;
+        t1 = 2.0 * delta * (ax - 2.0 * ay);
+        t2 = (4.0 * delta - ay) * ay + delta * delta;
+    }
+    h -= (t1 + t2) / (2.0 * h);
+    return h;
+}
+
+double orc_hypot_restated(double x, double y)
+{
+    if (!isfinite(x) || !isfinite(y)) {
+        if (isinf(x) || isinf(y)) return INFINITY;
+        return x + y;
+    }
+    x = fabs(x);
+    y = fabs(y);
+    double ax = x < y ? y : x, ay = x < y ? x : y;
+    if (ax > 0x1p+511) {
+        if (ay <= ax * 0x1p-54) return ax + ay;
+        return orc_hypot_kernel(ax * 0x1p-600, ay * 0x1p-600) / 0x1p-600;
+    }
+    if (ay < 0x1p-511) {
+        if (ax >= ay / 0x1p-54) return ax + ay;
+        return orc_hypot_kernel(ax / 0x1p-600, ay / 0x1p-600) * 0x1p-600;
+    }
+    if (ay <= ax * 0x1p-54) return ax + ay;
+    return orc_hypot_kernel(ax, ay);
+}
+
+/* n pairs -> number of pairs where the restatement differs from libm's hypot */
+int64_t orc_hypot_check(const double* x, const double* y, int64_t n)
+{
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; i++) {
+        double a = hypot(x[i], y[i]), b = orc_hypot_restated(x[i], y[i]);
+        if (memcmp(&a, &b, sizeof a) != 0) bad++;
+    }
+    return bad;
+}
+
 /* ---- lapack.cpp JacobiSVDImpl_<double>, Vt only ------------------------- */
 /* At: n rows of length m (row stride m), i.e. At = Aᵀ for A (m x n).  Vt: n x n. */
 void orc_jacobi_svd(double* At, int m, int n, double* Wout, double* Vt)

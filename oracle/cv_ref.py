@@ -44,6 +44,8 @@ def _load():
     lib.orc_undistort_points_f64.argtypes = [f64p, ctypes.c_int64, f64p, f64p, ctypes.c_int, f64p]
     lib.orc_triangulate_nview_f64.argtypes = [f64p, ctypes.c_int, f64p, ctypes.c_int64, f64p]
     lib.orc_from_homogeneous_f64.argtypes = [f64p, ctypes.c_int64, f64p]
+    lib.orc_hypot_check.argtypes = [f64p, f64p, ctypes.c_int64]
+    lib.orc_hypot_check.restype = ctypes.c_int64
     _lib = lib
     return lib
 
@@ -119,6 +121,14 @@ def convert_points_from_homogeneous(src):
     out = np.empty((src.shape[0], 3), np.float32)
     lib.orc_from_homogeneous_f32(_p(src, ctypes.c_float), src.shape[0], _p(out, ctypes.c_float))
     return out.reshape(-1, 1, 3)
+
+
+def hypot_restatement_mismatches(x, y):
+    """Pairs where glibc's hypot restated (the device exact path's text) differs from libm's."""
+    lib = _load()
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    return int(lib.orc_hypot_check(_p(x, ctypes.c_double), _p(y, ctypes.c_double), x.size))
 
 
 def jacobi_svd(A):

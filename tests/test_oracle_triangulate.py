@@ -64,3 +64,18 @@ def test_all_views_extension_consistent():
     cp = [(c["K"], c["R"], c["T"], c["dist"]) for c in cams]
     out = cv_ref.triangulate_all_views(cp, k, [0, 1, 2, 3])
     np.testing.assert_allclose(out, poses, atol=1e-3)
+
+
+def test_hypot_restatement_matches_libm():
+    """OpenCV's JacobiSVDImpl_ calls std::hypot = libm's (glibc 2.35 on this image and the GPU
+    box).  The device's exact path restates glibc's algorithm (csrc/triangulate.hip hypot_glibc);
+    the same text in C must equal libm on random pairs incl. near-equal magnitudes, wide exponent
+    ranges, zeros and the rotation angles' typical (2p, a - b) pairs."""
+    rng = np.random.default_rng(3)
+    n = 400_000
+    x = rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-30, 30, n)
+    y = rng.uniform(-1, 1, n) * 10.0 ** rng.uniform(-30, 30, n)
+    y[::3] = x[::3] * (1 + rng.uniform(-1e-3, 1e-3, n)[::3])
+    y[1::7] = 0.0
+    x[2::11] = rng.uniform(-1, 1, len(x[2::11])) * 1e300
+    assert cv_ref.hypot_restatement_mismatches(x, y) == 0

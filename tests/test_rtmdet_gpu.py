@@ -28,6 +28,9 @@ from oracle import rtmdet_ref as R
 pytestmark = pytest.mark.gpu
 PEAK_BAND = 3.0   # logits below the fp32 selection that count as the frame's peak region
 SAT = 16.6355     # f32 sigmoid(x) == 1.0 above this logit (1 - 2^-24 rounds up)
+# fixed decidability margin of the peaked end-to-end test: 2 x the median peak-region bf16 logit
+# error measured in round 4 (0.865, profiles/r04d_det_peaked.log), committed as a constant
+DECIDE_MARGIN = 1.74
 
 
 def _frames(n, h, w, seed):
@@ -234,20 +237,20 @@ def test_end_to_end_vs_fp32_oracle(sd, det640):
 
 def test_end_to_end_peaked_vs_fp32_oracle():
     """The selected prior on a trained-like detector: rtmdet.peaked_state_dict (classification
-    head fitted to one clear best prior per person, tools/train_peaked_rtmdet.py) on skeleton
+    head fitted to one clear best prior per person, tools/train_peaked_rtmdet.py) on 64 skeleton
     frames the fit never saw.  The fp32 side selects as the reference does: the highest f32
     score among the priors that survive post-processing (score > score_thr, a box of positive
-    size), the lowest index on ties.  A frame is decidable when no other prior can overturn
-    that under the bf16 path's own logit error on the frame's peak region (max |GPU - fp32|
-    over priors within PEAK_BAND of the selection; bf16 error grows with the logit): each is
-    below the selection by twice that error, or a robustly saturated (score 1.0) tie with a
-    later index.  There the GPU must select the same prior (>= 95 % of those frames), and
-    most frames must be decidable."""
+    size), the lowest index on ties.  A frame is decidable when every other valid prior is below
+    the selection by more than the FIXED margin DECIDE_MARGIN (2 x round 4's measured median
+    peak-region bf16 logit error, independent of the output under test), or a robustly
+    saturated (score 1.0) tie with a later index.  There the GPU must select the same prior
+    (>= 95 % of those frames), >= 40 frames must be decidable, and the bf16 path's peak-region
+    logit error itself is bounded (its median within the margin)."""
     from mvpose import synthetic as syn
     sd = D.peaked_state_dict()
     m = R.build_model(sd)
     det = D.RTMDetector(sd, max_batch=8)
-    n = 32
+    n = 64
     frames, _ = syn.make_skeleton_frames(n, seed=77)
     cands, bests = [], []
     for i0 in range(0, n, 8):
@@ -273,17 +276,19 @@ def test_end_to_end_peaked_vs_fp32_oracle():
         # so saturated peaks tie and the index decides, in mmdet and on the GPU alike
         scv = sc.masked_fill(~ok, -1.0)
         sel = int(torch.nonzero(scv == scv.max())[0])
-        # the bf16 path's logit error where it matters: over the frame's peak region (priors
-        # within PEAK_BAND of the selected logit), the largest |GPU - fp32| logit difference
+        # the bf16 path's logit error where it matters, reported and bounded below: over the
+        # frame's peak region (priors within PEAK_BAND of the selected logit), the largest
+        # |GPU - fp32| logit difference
         near = lg >= lg[sel] - PEAK_BAND
         e = float((cand[i, :, 5] - lg).abs()[near].max())
         errs.append(e)
-        # decidable: every other valid prior is either clearly below the selection (by 2 e), or a
-        # robust saturated tie the index decides (both above SAT + 2 e, the other later)
+        # decidable by the fp32 logits alone: every other valid prior is clearly below the
+        # selection (by the fixed margin), or a robust saturated tie the index decides (both
+        # above SAT + margin, the other later)
         idx = torch.arange(len(lg))
         other = ok & (idx != sel)
-        below = lg[sel] - lg > 2 * e
-        tie = (lg > SAT + 2 * e) & (lg[sel] > SAT + 2 * e) & (idx > sel)
+        below = lg[sel] - lg > DECIDE_MARGIN
+        tie = (lg > SAT + DECIDE_MARGIN) & (lg[sel] > SAT + DECIDE_MARGIN) & (idx > sel)
         lead = float((lg[sel] - lg[other & ~tie]).min()) if bool((other & ~tie).any()) else float("inf")
         leads.append(lead)
         decs.append(bool((below | tie | ~other).all()))
@@ -298,8 +303,9 @@ def test_end_to_end_peaked_vs_fp32_oracle():
           f"|d logit| median {np.median(errs):.3f} (max {errs.max():.3f}); fp32 top-1 lead median "
           f"{np.median(leads):.2f}; decidable {dec.sum()}/{n}, agreement there "
           f"{agree[dec].mean():.3f}; agreement overall {agree.mean():.3f}")
-    assert dec.mean() >= 0.6
+    assert dec.sum() >= 40
     assert agree[dec].mean() >= 0.95
+    assert np.median(errs) <= DECIDE_MARGIN
 
 
 def test_pose_estimator_with_detector(det640):

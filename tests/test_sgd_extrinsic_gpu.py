@@ -205,11 +205,12 @@ def test_triangulate_points_f64_dropin_vs_oracle():
         got = triangulate_points(pts, *a, *b)
         ref = cv_ref.triangulate_points(pts, *a, *b)
         assert got.dtype == np.float64 and ref.dtype == np.float64 and got.shape == ref.shape
-        # double outputs: no f32 rounding absorbs the last-bit differences of the device's fp64
-        # sqrt / hypot / division sequences (measured: ~40 % of coordinates bit-identical)
+        # double outputs, no f32 rounding to absorb anything: the device's fp64 sequence is the
+        # restatement's bit for bit (IEEE division and sqrt, glibc's hypot restated — round 4's
+        # 40 % identity was the compiler's hypot)
         print(f"f64 drop-in ({np.dtype(dt).name} cameras): max rel {np.max(np.abs(got - ref) / np.abs(ref)):.2e}, "
               f"bit-identical {np.mean(got == ref):.3f}")
-        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-9)
+        np.testing.assert_array_equal(got, ref)
     # float32 keypoints keep the float32 pipeline path
     got32 = triangulate_points(pts.astype(np.float32), *a, *b)
     assert got32.dtype == np.float32
