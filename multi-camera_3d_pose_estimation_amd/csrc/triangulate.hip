@@ -25,6 +25,7 @@
 
 #include "mvp_common.h"
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdlib>
 #include <map>
@@ -313,12 +314,11 @@ __device__ __forceinline__ void jacobi_null_vector(double (&At)[4][M], double (&
 // the same bits.  That midpoint has c's sign, exponent and upper 23 mantissa bits and mantissa bit
 // 28 set (one v_and_or_b32); c - m is exact (Sterbenz).  The factor 2 covers the finer f32 grid
 // just below a power of two.  NaN / Inf / 0 / f32-subnormal c never pass (|c - m| is NaN or
-// below any delta used here).  The comparison runs in f32 (|c - m| rounded to f32; delta2 carries
-// the solvers' safety factors).
-__device__ __forceinline__ bool f32_rounding_stable(double c, float delta2) {
+// below any delta used here).
+__device__ __forceinline__ bool f32_rounding_stable(double c, double delta2) {
     const unsigned long long b = (unsigned long long)__double_as_longlong(c);
     const unsigned long long mb = (b & 0xFFFFFFFFE0000000ull) | 0x10000000ull;
-    return fabsf((float)(c - __longlong_as_double((long long)mb))) > delta2;
+    return fabs(c - __longlong_as_double((long long)mb)) > delta2;
 }
 
 // Error bound of a certified null vector (unit vector, absolute per component):
@@ -330,13 +330,13 @@ __device__ __forceinline__ bool f32_rounding_stable(double c, float delta2) {
 //        <= 0.025 of it, the normal equations' floor <= 0.0033, D₂/λ₃ <= 1.4, on 1.4 M synthetic
 //        and random points: tools/tri_cert_emu.c)
 // + 2^-50 (normalisation).  Returned doubled for f32_rounding_stable.
-__device__ __forceinline__ float null_vector_delta2(double dd, double prev, double cond2) {
+__device__ __forceinline__ double null_vector_delta2(double dd, double prev, double cond2) {
     const float d = (float)dd, pv = (float)prev;
     const float it_err = d * __builtin_amdgcn_rsqf(fmaxf(fmaxf(d, pv), 1e-37f));
-    return 16.f * it_err + 0.4f * 2.220446e-16f * __builtin_sqrtf((float)cond2) + 0x1p-49f;
+    return (double)(16.f * it_err + 0.4f * 2.220446e-16f * __builtin_sqrtf((float)cond2) + 0x1p-49f);
 }
 
-__device__ __forceinline__ bool null_vector_certified(const double (&nv)[4], float delta2) {
+__device__ __forceinline__ bool null_vector_certified(const double (&nv)[4], double delta2) {
     return f32_rounding_stable(nv[0], delta2) && f32_rounding_stable(nv[1], delta2) &&
            f32_rounding_stable(nv[2], delta2) && f32_rounding_stable(nv[3], delta2);
 }
@@ -605,17 +605,23 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
     }
     // error of the f32 correction: kappa = 8 roundings of the terms it is built from (X0 and the
     // iterate x rounded to f32, poly, the tangential terms, the approximate reciprocal),
-    // propagated through each later iteration by L
-    const f2v A1 = {t0.a1, t1.a1}, A2 = {t0.a2, t1.a2}, A3 = {t0.a3, t1.a3}, B = {t0.b, t1.b};
-    const f2v ax = __builtin_elementwise_abs(x) + __builtin_elementwise_abs(y);
-    const f2v L = ic * __builtin_elementwise_fma(
-                           r2, __builtin_elementwise_fma(__builtin_elementwise_fma(A3, r2, A2), r2, A1), B * ax);
-    const f2v terms = __builtin_elementwise_fma(__builtin_elementwise_abs(X0) + __builtin_elementwise_abs(Y0),
-                                                __builtin_elementwise_abs(poly),
-                                                __builtin_elementwise_abs(dX) + __builtin_elementwise_abs(dY));
-    f2v err = (8.f * 0x1p-24f) * terms * ic;
+    // propagated through each later iteration by L.  Scalar f32 (|.| is a free source modifier
+    // there; packed instructions would need an and-mask per absolute value).  |x| + |y| <=
+    // 0.5 + r² bounds the tangential Jacobian's (|x| + |y|) factor without absolute values.
+    const CamTol* tt[2] = {&t0, &t1};
+    float errq[2];
 #pragma unroll
-    for (int j = 0; j < NF64; j++) err = err * L;
+    for (int q = 0; q < 2; q++) {
+        const float r2q = q ? r2.y : r2.x, icq = q ? ic.y : ic.x, pq = q ? poly.y : poly.x;
+        const float L = icq * __builtin_fmaf(r2q, __builtin_fmaf(__builtin_fmaf(tt[q]->a3, r2q, tt[q]->a2), r2q, tt[q]->a1),
+                                             tt[q]->b * (0.5f + r2q));
+        const float terms = __builtin_fmaf(fabsf(q ? X0.y : X0.x) + fabsf(q ? Y0.y : Y0.x), fabsf(pq),
+                                           fabsf(q ? dX.y : dX.x) + fabsf(q ? dY.y : dY.x));
+        float e = (8.f * 0x1p-24f) * terms * icq;
+#pragma unroll
+        for (int j = 0; j < NF64; j++) e *= L;
+        errq[q] = e;
+    }
     double xd[2] = {x0[0] + (double)cx.x, x0[1] + (double)cx.y};
     double yd[2] = {y0[0] + (double)cy.x, y0[1] + (double)cy.y};
     double dmin[2] = {(double)den_min.x, (double)den_min.y};
@@ -635,8 +641,6 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
             yd[q] = (y0[q] - ddY) * icd;
         }
     }
-    const CamTol* tt[2] = {&t0, &t1};
-    const float errq[2] = {err.x, err.y};
 #pragma unroll
     for (int q = 0; q < 2; q++) {
         const double* c = cc[q];
@@ -645,11 +649,10 @@ __device__ __forceinline__ void undistort_pair_tol(const float (&u)[2], const fl
         const double oyd = (c[3] * xd[q] + c[4] * yd[q] + c[5]) * ww;
         ox[q] = (float)oxd;
         oy[q] = (float)oyd;
-        // pixel error bound, doubled: kn · (f32 error + fp64 rounding of the iterates, 2^-46 |x|)
-        // + the K application's rounding (2^-45 of |ox|, |oy|, |cx|, |cy|)
-        const float axy = fabsf((float)xd[q]) + fabsf((float)yd[q]);
-        const float d2 = 2.f * tt[q]->kn * __builtin_fmaf(0x1p-46f, axy, errq[q]) +
-                         __builtin_fmaf(0x1p-44f, fabsf(ox[q]) + fabsf(oy[q]), tt[q]->floor2);
+        // pixel error bound, doubled: kn · (the f32 error carried through) + 2^-44 (|ox| + |oy|)
+        // + floor2 (2^-44 (|cx| + |cy|)): the fp64 iterations' and the K application's rounding
+        // (kn |x| <= |ox| + |cx|, so this covers 2^-46 kn |x| with a factor 4)
+        const double d2 = __builtin_fma(0x1p-44, fabs(oxd) + fabs(oyd), (double)(2.f * tt[q]->kn * errq[q] + tt[q]->floor2));
         // OpenCV's icdist < 0 branch (keep the initial guess) and a near-zero denominator are left
         // to the exact path: the f32 and fp64 denominators could disagree on the sign
         certified = certified && tt[q]->ok && dmin[q] > 0x1p-10 && f32_rounding_stable(oxd, d2) &&
@@ -672,9 +675,11 @@ __device__ __forceinline__ bool normal_eq_null_vector(const double (&m)[4][4], d
     const double r2 = rcp_nr(b22);
     const double l32 = b32 * r2;
     double D3 = b33 - l32 * b32;
-    // an exactly singular M (noise-free data): a pivot far below the factorisation's rounding
-    // keeps the solves finite and changes nothing else
-    if (!(fabs(D3) >= 1e-30 * D0)) D3 = 1e-30 * D0;
+    // an exactly singular M (noise-free data): the last pivot is rounding noise of either sign;
+    // a positive pivot far below the factorisation's rounding keeps the solves finite and M⁻¹
+    // positive definite (a negative one flipped the iterate's sign every step, so 27 % of the
+    // noise-free points never converged) and changes nothing else
+    if (!(D3 >= 1e-30 * D0)) D3 = 1e-30 * D0;
     const double r3 = rcp_nr(D3);
     auto solve = [&](double (&y)[4]) {  // y <- M⁻¹ y
         const double z1 = y[1] - l10 * y[0];
@@ -955,8 +960,13 @@ __device__ __forceinline__ void normal_matrix_2v(const double (&x)[2], const dou
     }
 }
 
+// Grid-stride: a grid of (CUs x resident blocks per CU) blocks loops over the points, so the
+// per-block set-up (camera records into LDS, their reciprocals and bound constants) is paid once
+// per resident block instead of once per 256 points.  The point's live state is ~100 VGPRs; 5
+// waves per SIMD (96 VGPRs, 4 spilled) measured 0.500 ms per 1 M frames against 0.525 for one
+// point per thread at 5 waves and 0.556 at 4 (same box, gpurun_out/r05b).
 template <int NF32>
-__global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void triangulate_tol2_kernel(
     const float* __restrict__ kpts, int64_t n, int V, const double* __restrict__ cams, int n_cams, CamIdx ci,
     float* __restrict__ out, double* __restrict__ out4, FbList fb) {
     __shared__ double scam[kMaxCams][MVP_CAM_DOUBLES];
@@ -965,52 +975,53 @@ __global__ __launch_bounds__(kBlock) void triangulate_tol2_kernel(
     load_cams(scam, sfast, cams, n_cams);
     if (threadIdx.x < 2) stol[threadIdx.x] = make_cam_tol(cams + threadIdx.x * MVP_CAM_DOUBLES);
     __syncthreads();
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (p >= n) return;
-    const Tol2Sel sel = tol2_select(kpts + p * 3 * V, V, ci);
-    const double* cp[2] = {scam[sel.pos0], scam[sel.pos1]};
-    bool ok;
-    if (isnan(sel.u[0]) || isnan(sel.u[1]) || isnan(sel.v[0]) || isnan(sel.v[1])) {
-        // a NaN coordinate makes every entry of its view's rows, hence the whole SVD, NaN on
-        // the exact path: all outputs NaN
-        const double qn = __builtin_nan("");
-        const double nv[4] = {qn, qn, qn, qn};
-        write_result(nv, p, out, out4);
-        ok = true;
-    } else {
-        float ux[2], uy[2];
-        bool cert = !fb.force;
-        undistort_pair_tol<NF32>(sel.u, sel.v, cp[0], cp[1], sfast[sel.pos0], sfast[sel.pos1], stol[sel.pos0],
-                                 stol[sel.pos1], ux, uy, cert);
-        double m[4][4];
-        // the camera at the world origin (block-uniform): its rows in closed form, whichever
-        // order the confidences put the two views in (the order only changes M's rounding)
-        const int origin = stol[0].origin ? 0 : (stol[1].origin ? 1 : -1);
-        if (origin >= 0) {
-            const int io = sel.pos0 == origin ? 0 : 1;  // the origin camera's view slot
-            const double xs[2] = {(double)(io == 0 ? ux[0] : ux[1]), (double)(io == 0 ? ux[1] : ux[0])};
-            const double ys[2] = {(double)(io == 0 ? uy[0] : uy[1]), (double)(io == 0 ? uy[1] : uy[0])};
-            normal_matrix_2v<true>(xs, ys, scam[origin], scam[1 - origin], m);
+    // the camera at the world origin (block-uniform): its rows in closed form, whichever order
+    // the confidences put the two views in (the order only changes M's rounding)
+    const int origin = stol[0].origin ? 0 : (stol[1].origin ? 1 : -1);
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += stride) {
+        const Tol2Sel sel = tol2_select(kpts + p * 3 * V, V, ci);
+        const double* cp[2] = {scam[sel.pos0], scam[sel.pos1]};
+        bool ok;
+        if (isnan(sel.u[0]) || isnan(sel.u[1]) || isnan(sel.v[0]) || isnan(sel.v[1])) {
+            // a NaN coordinate makes every entry of its view's rows, hence the whole SVD, NaN on
+            // the exact path: all outputs NaN
+            const double qn = __builtin_nan("");
+            const double nv[4] = {qn, qn, qn, qn};
+            write_result(nv, p, out, out4);
+            ok = true;
         } else {
-            const double xs[2] = {(double)ux[0], (double)ux[1]}, ys[2] = {(double)uy[0], (double)uy[1]};
-            normal_matrix_2v<false>(xs, ys, cp[0], cp[1], m);
+            float ux[2], uy[2];
+            bool cert = !fb.force;
+            undistort_pair_tol<NF32>(sel.u, sel.v, cp[0], cp[1], sfast[sel.pos0], sfast[sel.pos1], stol[sel.pos0],
+                                     stol[sel.pos1], ux, uy, cert);
+            double m[4][4];
+            if (origin >= 0) {
+                const int io = sel.pos0 == origin ? 0 : 1;  // the origin camera's view slot
+                const double xs[2] = {(double)(io == 0 ? ux[0] : ux[1]), (double)(io == 0 ? ux[1] : ux[0])};
+                const double ys[2] = {(double)(io == 0 ? uy[0] : uy[1]), (double)(io == 0 ? uy[1] : uy[0])};
+                normal_matrix_2v<true>(xs, ys, scam[origin], scam[1 - origin], m);
+            } else {
+                const double xs[2] = {(double)ux[0], (double)ux[1]}, ys[2] = {(double)uy[0], (double)uy[1]};
+                normal_matrix_2v<false>(xs, ys, cp[0], cp[1], m);
+            }
+            double nv[4];
+            ok = normal_eq_null_vector(m, nv) && cert;
+            if (ok) write_result(nv, p, out, out4);
+            else reinterpret_cast<unsigned*>(out)[3 * p] = kFbSentinel;
         }
-        double nv[4];
-        ok = normal_eq_null_vector(m, nv) && cert;
-        if (ok) write_result(nv, p, out, out4);
-        else reinterpret_cast<unsigned*>(out)[3 * p] = kFbSentinel;
-    }
-    // wave-aggregated append of the uncertified points
-    const unsigned long long msk = __ballot(!ok);
-    if (msk) {
-        const int lane = __lane_id();
-        const int leader = __ffsll((long long)msk) - 1;
-        unsigned base = 0;
-        if (lane == leader) base = atomicAdd(&fb.hdr->count, (unsigned)__popcll(msk));
-        base = __shfl(base, leader);
-        if (!ok) {
-            const unsigned slot = base + (unsigned)__popcll(msk & ((1ull << lane) - 1));
-            if (slot < (unsigned)kFbCap) fb.idx[slot] = (unsigned)p;
+        // wave-aggregated append of the uncertified points
+        const unsigned long long msk = __ballot(!ok);
+        if (msk) {
+            const int lane = __lane_id();
+            const int leader = __ffsll((long long)msk) - 1;
+            unsigned base = 0;
+            if (lane == leader) base = atomicAdd(&fb.hdr->count, (unsigned)__popcll(msk));
+            base = __shfl(base, leader);
+            if (!ok) {
+                const unsigned slot = base + (unsigned)__popcll(msk & ((1ull << lane) - 1));
+                if (slot < (unsigned)kFbCap) fb.idx[slot] = (unsigned)p;
+            }
         }
     }
 }
@@ -1181,7 +1192,15 @@ extern "C" int mvp_triangulate(const float* kpts, int64_t n_points, int V, const
             fb.force = (ff && ff[0] == '1') || out_xyzw != nullptr;
             // 3 f32 + 2 fp64 undistortion iterations: 4 + 1 sends ~0.6 % of the synthetic rigs'
             // points to the exact path (0.013 % with 3 + 2, tools/tri_cert_emu.c)
-            hipLaunchKernelGGL(triangulate_tol2_kernel<3>, grid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
+            static int cus = 0;
+            if (cus == 0) {
+                int dev = 0;
+                MVP_HIP(hipGetDevice(&dev));
+                MVP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+            }
+            // 5 blocks of 4 waves per CU = the kernel's 5 waves per SIMD (88 VGPRs)
+            const dim3 tgrid((unsigned)std::min<int64_t>(blocks, (int64_t)cus * 5));
+            hipLaunchKernelGGL(triangulate_tol2_kernel<3>, tgrid, block, 0, s, kpts, n_points, V, cams, n_cams, ci,
                                out_xyz, out_xyzw, fb);
             hipLaunchKernelGGL(triangulate_tol2_fallback_kernel, dim3(kFbBlocks), block, 0, s, kpts, n_points, V, cams,
                                n_cams, ci, out_xyz, out_xyzw, fb);

@@ -1,13 +1,15 @@
 """Summarise rocprofv3 --pmc passes of one kernel into a profiles/*_pmc.json record.
 
-    python tools/tri_pmc_json.py KERNEL_SUBSTR OUT.json pass1/run_counter_collection.csv [pass2 ...]
+    python tools/tri_pmc_json.py KERNEL_SUBSTR OUT.json [--points N] pass1/run_counter_collection.csv [pass2 ...]
 
 Per pass: the kernel's dispatches, their counters summed, and each dispatch's duration from the
 CSV's own Start/End timestamps.  Derived (MI355X_MICROARCH.md, "DVFS give-back"):
   clock_GHz      = GRBM_GUI_ACTIVE / 8 XCDs / duration (per dispatch, then the median);
   valu_busy      = SQ_ACTIVE_INST_VALU x 4 cycles / 1,024 SIMDs / (GRBM_GUI_ACTIVE / 8): the
                    fraction of each SIMD's cycles the kernel spent issuing VALU instructions;
-  per_wave       = every counter / SQ_WAVES.
+  per_wave       = every counter / SQ_WAVES;
+  per_64_points  = every counter per 64 points (--points N = points per dispatch; a grid-stride
+                   kernel's waves each handle many points, so per_wave is not per point).
 The bench's `valu_issue` and DESIGN.md quote these numbers from the same file."""
 import csv
 import json
@@ -16,6 +18,9 @@ import sys
 from collections import defaultdict
 
 sub, out_path, passes = sys.argv[1], sys.argv[2], sys.argv[3:]
+points = None
+if passes and passes[0] == "--points":
+    points, passes = int(passes[1]), passes[2:]
 counters = defaultdict(float)
 durations, clocks = [], []
 dispatches = set()
@@ -44,6 +49,10 @@ res = {"source": f"rocprofv3 --kernel-trace --pmc, {len(passes)} pass(es): " + "
        "kernel": sub, "dispatches_per_pass": n_first, "counters": dict(counters)}
 if waves:
     res["per_wave"] = {k: v / waves for k, v in counters.items() if k.startswith("SQ_") and k != "SQ_WAVES"}
+if points:
+    groups = n_first * points / 64.0
+    res["points_per_dispatch"] = points
+    res["per_64_points"] = {k: v / groups for k, v in counters.items() if k.startswith("SQ_") and k != "SQ_WAVES"}
 if clocks:
     res["clock_GHz_median"] = statistics.median(clocks)
     res["duration_ms_median"] = statistics.median(durations) * 1e3
