@@ -413,6 +413,27 @@ int mvp_linear_interpolation(const float* pts_dev, int T, int P, int D, int k, f
                              int use_rolling_average, int filter_distance_from_median, float* out_dev,
                              void* stream);
 
+/* ---------------------------------------------------------------------------
+ * MPEG-4 Part 2 ('mp4v') decoding, host side — replaces cv.VideoCapture on the reference's
+ * recordings (utils.py:849-909 read_video_as_frames; synchronize_videos.py:64,240 writes them with
+ * cv2.VideoWriter_fourcc(*'mp4v')).  Simple Profile: I / P-VOPs, video packets, H.263 or MPEG
+ * quantisation; frames out as BGR24 (cv2's channel order) or I420.  No device memory involved.
+ *
+ * mvp_mp4v_create : config = the VOS/VO/VOL headers (an MP4 'esds' DecoderSpecificInfo, or the
+ *                   head of an elementary stream); returns the frame size.
+ * mvp_mp4v_decode : one sample (any GOV / VOL headers and VOPs it holds); writes the frame after
+ *                   its last VOP (a not-coded VOP repeats the previous frame) to bgr_out
+ *                   [H][W][3] and / or yuv_out (I420, W x H luma then two (W+1)/2 x (H+1)/2
+ *                   chroma planes); *vops_out = VOPs in the sample.
+ * mvp_mp4v_selfcheck : verifies the decoder's VLC / scan tables (prefix-free, complete, the intra
+ *                   TCOEF codes a permutation of the inter ones, LMAX order).
+ * ------------------------------------------------------------------------- */
+int mvp_mp4v_create(const uint8_t* config, size_t config_bytes, void** handle, int* width, int* height);
+int mvp_mp4v_decode(void* handle, const uint8_t* data, size_t bytes, uint8_t* bgr_out, uint8_t* yuv_out,
+                    int* vops_out);
+int mvp_mp4v_destroy(void* handle);
+int mvp_mp4v_selfcheck(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,6 +42,10 @@ SIGNATURES = {
                                 c_void_p, c_void_p, c_void_p]),
     "mvp_triangulate_points_f64": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mvp_triangulate_fallback_total": (c_int, [c_void_p, P(ctypes.c_ulonglong)]),
+    "mvp_mp4v_create": (c_int, [c_void_p, c_size_t, P(c_void_p), P(c_int), P(c_int)]),
+    "mvp_mp4v_decode": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_void_p, P(c_int)]),
+    "mvp_mp4v_destroy": (c_int, [c_void_p]),
+    "mvp_mp4v_selfcheck": (c_int, []),
     "mvp_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, P(c_float), P(c_float),
                                c_int, c_int, c_void_p, c_void_p]),
     "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,

@@ -10,13 +10,19 @@ rocDecode), so the containers whose codecs ARE available are read here:
 * Directories of "frame<N>.jpg" files, ordered by N (the reference's
   process_image_files, utils.py:851-860).
 * .npy (T, H, W, 3) uint8 stacks, memory-mapped (the build's own recording format).
+* MPEG-4 Part 2 ('mp4v') video — what the reference's synchronize_videos.py:64,240 writes
+  with cv2.VideoWriter_fourcc(*'mp4v') — in MP4 / QuickTime containers (ISO BMFF: the
+  'mp4v' sample entry's esds decoder config, stsc / stco / stsz sample tables), in AVI
+  (XVID / DIVX / DX50 / FMP4 / MP4V FourCCs) and as raw elementary streams (.m4v / .cmp),
+  decoded by the native Simple Profile decoder in libmvpose.so (csrc/mp4v.cpp; host code).
 
 Every reader returns (T, H, W, 3) uint8 frames in the channel order cv2 returns them
 (BGR), so the rest of the pipeline applies the reference's cvtColor(RGB2BGR) swap exactly
-as for decoded video.  MPEG-4 / H.264 files raise NotImplementedError.  Decoded pixels
-are libjpeg's (islow IDCT, fancy upsampling), which is what cv2.imread uses; cv2's
-VideoCapture decodes MJPEG with FFmpeg's decoder instead, so MJPEG parity with the
-reference is unpinned (no cv2 here to compare with).
+as for decoded video.  H.264 / HEVC (QuickTime's usual .mov codecs, record_from_webcams_
+with_quicktime.py:39) raise NotImplementedError: this image has no decoder for them.  Decoded
+pixels are libjpeg's for MJPEG (islow IDCT, fancy upsampling), which is what cv2.imread uses;
+cv2's VideoCapture decodes MJPEG and MPEG-4 with FFmpeg, which is absent here, so parity of
+both with the reference is unpinned.
 """
 from __future__ import annotations
 
@@ -30,6 +36,7 @@ import numpy as np
 
 _BI_RGB = 0
 _MJPG = (b"MJPG", b"mjpg", b"AVRn", b"LJPG", b"JPGL", b"dmb1")
+_MP4V = (b"XVID", b"xvid", b"DIVX", b"divx", b"DX50", b"dx50", b"FMP4", b"fmp4", b"MP4V", b"mp4v", b"M4S2", b"m4s2")
 
 
 class AviInfo:
@@ -102,8 +109,11 @@ def parse_avi(buf) -> AviInfo:
     _, width, height, _, bit_count, comp = struct.unpack_from("<IiiHHI", buf, fd)
     comp_cc = struct.pack("<I", comp)
     codec = "rgb" if comp == _BI_RGB else ("mjpeg" if comp_cc in _MJPG or handler in _MJPG else
+                                          "mp4v" if comp_cc in _MP4V or handler in _MP4V else
                                           comp_cc.decode("latin-1"))
-    return AviInfo(width, height, codec, bit_count, rate / scale if scale else 0.0, st["chunks"])
+    info = AviInfo(width, height, codec, bit_count, rate / scale if scale else 0.0, st["chunks"])
+    info.strf_extra = bytes(buf[fd + 40:fd + n_strf]) if (n_strf := st["strf"][vid][1]) > 40 else b""
+    return info
 
 
 def _decode_jpeg(data: bytes) -> np.ndarray:
@@ -131,6 +141,8 @@ def read_avi(path, start=0, end=None, threads=None) -> np.ndarray:
                         raise ValueError(f"{path}: frame {i} truncated")
                     rows = np.frombuffer(buf[d:d + stride * H], np.uint8).reshape(H, stride)[:, :W * 3]
                     out[i] = (rows[::-1] if info.height > 0 else rows).reshape(H, W, 3)   # DIB rows are BGR
+            elif info.codec == "mp4v":
+                return decode_mp4v(info.strf_extra, (bytes(buf[d:d + n]) for d, n in info.chunks), start, end)
             elif info.codec == "mjpeg":
                 datas = [bytes(buf[d:d + n]) for d, n in chunks]
                 workers = max(1, min(int(threads or os.cpu_count() or 1), 16))
@@ -190,9 +202,248 @@ def read_recording(path, start=0, end=-1):
         head = f.read(12)
     if head[0:4] == b"RIFF" and head[8:12] == b"AVI ":
         return read_avi(p, start, end)
+    if head[4:8] in (b"ftyp", b"moov", b"mdat", b"free", b"wide", b"skip"):
+        return read_mp4(p, start, end)
+    if head[0:3] == b"\0\0\1" and (head[3] in (0xB0, 0xB3, 0xB5, 0xB6) or head[3] <= 0x2F):
+        return read_m4v(p, start, end)
     raise NotImplementedError(
-        f"{p}: no decoder for this container/codec in this image (MJPEG/uncompressed AVI, frame*.jpg "
-        "directories and .npy stacks are supported; convert other videos to one of these)")
+        f"{p}: no decoder for this container/codec in this image (MPEG-4 Part 2 in MP4/MOV/AVI/raw, MJPEG and "
+        "uncompressed AVI, frame*.jpg directories and .npy stacks are supported)")
+
+
+# ------------------------------------------------------------------ MPEG-4 Part 2 ('mp4v')
+class Mp4vDecoder:
+    """The native Simple Profile decoder (mvp_mp4v_*, csrc/mp4v.cpp): feed the decoder config (VOL
+    headers), then one sample at a time; each call returns the frame after the sample's last VOP."""
+
+    def __init__(self, config: bytes):
+        import ctypes
+        from . import _lib
+        self._lib = _lib
+        self._h = ctypes.c_void_p()
+        w, h = ctypes.c_int(), ctypes.c_int()
+        cfg = (ctypes.c_uint8 * max(1, len(config))).from_buffer_copy(config or b"\0")
+        _lib.call("mvp_mp4v_create", cfg, len(config), ctypes.byref(self._h), ctypes.byref(w), ctypes.byref(h))
+        self.width, self.height = w.value, h.value
+
+    def decode(self, sample: bytes, yuv: bool = False) -> np.ndarray:
+        import ctypes
+        data = np.frombuffer(sample, np.uint8)
+        n = ctypes.c_int()
+        if yuv:
+            cw, ch = (self.width + 1) // 2, (self.height + 1) // 2
+            out = np.empty(self.width * self.height + 2 * cw * ch, np.uint8)
+            self._lib.call("mvp_mp4v_decode", self._h, data.ctypes.data, data.size, None, out.ctypes.data,
+                           ctypes.byref(n))
+            return out
+        out = np.empty((self.height, self.width, 3), np.uint8)
+        self._lib.call("mvp_mp4v_decode", self._h, data.ctypes.data, data.size, out.ctypes.data, None,
+                       ctypes.byref(n))
+        return out
+
+    def close(self):
+        if self._h:
+            self._lib.call("mvp_mp4v_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
+def split_vops(stream: bytes):
+    """An elementary stream -> (config = everything before the first VOP, [samples]).  A sample
+    runs from the end of the previous VOP's payload (its next start code) to the end of its own
+    VOP's payload, so GOV headers or a repeated VOL travel with the VOP that follows them."""
+    idx = []
+    i = stream.find(b"\0\0\1")
+    while i >= 0:
+        idx.append(i)
+        i = stream.find(b"\0\0\1", i + 3)
+    vops = [i for i in idx if i + 3 < len(stream) and stream[i + 3] == 0xB6]
+    if not vops:
+        return stream, []
+    ends = []
+    for v in vops:
+        nxt = next((j for j in idx if j > v), len(stream))
+        ends.append(nxt)
+    samples = [stream[vops[0]:ends[0]]] + [stream[ends[k - 1]:ends[k]] for k in range(1, len(vops))]
+    return stream[:vops[0]], samples
+
+
+def decode_mp4v(config: bytes, samples, start=0, end=None) -> np.ndarray:
+    """Decode every sample (P-VOPs need their predecessors) and keep frames [start:end)."""
+    samples = list(samples)
+    if not config and samples:
+        config = samples[0]       # VOL headers in the first sample (AVI without strf extra data)
+    dec = Mp4vDecoder(config)
+    try:
+        frames = []
+        keep = range(len(samples))[slice(start, end)]
+        lo, hi = (keep.start, keep.stop) if len(keep) else (0, 0)
+        for i, smp in enumerate(samples):
+            if i >= hi:
+                break
+            fr = dec.decode(smp)
+            if i >= lo:
+                frames.append(fr)
+        if not frames:
+            return np.empty((0, dec.height, dec.width, 3), np.uint8)
+        return np.stack(frames)
+    finally:
+        dec.close()
+
+
+def read_m4v(path, start=0, end=None) -> np.ndarray:
+    """A raw MPEG-4 Part 2 elementary stream (.m4v / .cmp)."""
+    with open(path, "rb") as f:
+        config, samples = split_vops(f.read())
+    return decode_mp4v(config, samples, start, end)
+
+
+class Mp4Info:
+    def __init__(self, width, height, fps, config, samples):
+        self.width, self.height, self.fps, self.config, self.samples = width, height, fps, config, samples
+
+    def __len__(self):
+        return len(self.samples)
+
+
+def _boxes(buf, start, end):
+    p = start
+    while p + 8 <= end:
+        size, kind = struct.unpack_from(">I4s", buf, p)
+        hdr = 8
+        if size == 1:
+            size = struct.unpack_from(">Q", buf, p + 8)[0]
+            hdr = 16
+        elif size == 0:
+            size = end - p
+        if size < hdr or p + size > end:
+            break
+        yield kind, p + hdr, p + size
+        p += size
+
+
+def _descriptor(buf, p):
+    """MPEG-4 descriptor at p -> (tag, payload start, payload end)."""
+    tag = buf[p]
+    p += 1
+    size = 0
+    for _ in range(4):
+        b = buf[p]
+        p += 1
+        size = (size << 7) | (b & 0x7F)
+        if not b & 0x80:
+            break
+    return tag, p, p + size
+
+
+def _esds_config(buf, start, end):
+    p = start + 4                                     # full box version / flags
+    tag, p, e = _descriptor(buf, p)
+    if tag != 0x03:
+        return b""
+    flags = buf[p + 2]
+    p += 3
+    if flags & 0x80:
+        p += 2
+    if flags & 0x40:
+        p += 1 + buf[p]
+    if flags & 0x20:
+        p += 2
+    while p < e:
+        tag, q, qe = _descriptor(buf, p)
+        if tag == 0x04:                               # DecoderConfigDescriptor
+            oti = buf[q]
+            if oti != 0x20:
+                raise NotImplementedError(f"MP4 objectTypeIndication 0x{oti:02x} (only MPEG-4 Visual, 0x20)")
+            r = q + 13
+            while r < qe:
+                t2, s2, e2 = _descriptor(buf, r)
+                if t2 == 0x05:                        # DecoderSpecificInfo: the VOS / VOL headers
+                    return bytes(buf[s2:e2])
+                r = e2
+        p = qe
+    return b""
+
+
+def parse_mp4(buf) -> Mp4Info:
+    """The first video track of an ISO BMFF (MP4 / QuickTime) file: its 'mp4v' decoder config and
+    the (offset, size) of every sample, from stsd / stsc / stco|co64 / stsz / stts / mdhd."""
+    moov = next(((s, e) for k, s, e in _boxes(buf, 0, len(buf)) if k == b"moov"), None)
+    if moov is None:
+        raise ValueError("MP4: no moov box")
+    for k, ts, te in _boxes(buf, *moov):
+        if k != b"trak":
+            continue
+        mdia = next(((s, e) for kk, s, e in _boxes(buf, ts, te) if kk == b"mdia"), None)
+        if mdia is None:
+            continue
+        parts = {kk: (s, e) for kk, s, e in _boxes(buf, *mdia)}
+        if "hdlr".encode() not in parts or bytes(buf[parts[b"hdlr"][0] + 8:parts[b"hdlr"][0] + 12]) != b"vide":
+            continue
+        ms = parts[b"mdhd"][0]
+        timescale = struct.unpack_from(">I", buf, ms + (20 if buf[ms] == 1 else 12))[0]
+        minf = parts[b"minf"]
+        stbl = next((s, e) for kk, s, e in _boxes(buf, *minf) if kk == b"stbl")
+        t = {kk: (s, e) for kk, s, e in _boxes(buf, *stbl)}
+        ss, se = t[b"stsd"]
+        entry = next(_boxes(buf, ss + 8, se))
+        kind, es, ee = entry
+        if kind not in (b"mp4v", b"MP4V"):
+            raise NotImplementedError(f"MP4 video codec {kind.decode('latin-1')!r}: only MPEG-4 Part 2 ('mp4v') "
+                                      "can be decoded in this image (no H.264 / HEVC decoder)")
+        width, height = struct.unpack_from(">HH", buf, es + 24)
+        config = b""
+        for kk, s, e in _boxes(buf, es + 78, ee):
+            if kk == b"esds":
+                config = _esds_config(buf, s, e)
+        s, _ = t[b"stsz"]
+        fixed, count = struct.unpack_from(">II", buf, s + 4)
+        sizes = [fixed] * count if fixed else list(struct.unpack_from(f">{count}I", buf, s + 12))
+        if b"stco" in t:
+            s, _ = t[b"stco"]
+            n = struct.unpack_from(">I", buf, s + 4)[0]
+            chunks = list(struct.unpack_from(f">{n}I", buf, s + 8))
+        else:
+            s, _ = t[b"co64"]
+            n = struct.unpack_from(">I", buf, s + 4)[0]
+            chunks = list(struct.unpack_from(f">{n}Q", buf, s + 8))
+        s, _ = t[b"stsc"]
+        n = struct.unpack_from(">I", buf, s + 4)[0]
+        stsc = [struct.unpack_from(">III", buf, s + 8 + 12 * i) for i in range(n)]
+        samples, si = [], 0
+        for ci, off in enumerate(chunks, start=1):
+            per = next((spc for first, spc, _ in reversed(stsc) if first <= ci), 0)
+            for _ in range(per):
+                if si >= count:
+                    break
+                samples.append((off, sizes[si]))
+                off += sizes[si]
+                si += 1
+        fps = 0.0
+        if b"stts" in t and timescale:
+            s, _ = t[b"stts"]
+            n = struct.unpack_from(">I", buf, s + 4)[0]
+            if n:
+                delta = struct.unpack_from(">II", buf, s + 8)[1]
+                fps = timescale / delta if delta else 0.0
+        return Mp4Info(width, height, fps, config, samples)
+    raise ValueError("MP4: no video track")
+
+
+def read_mp4(path, start=0, end=None) -> np.ndarray:
+    """Frames [start:end) of an MP4 / QuickTime file with MPEG-4 Part 2 video -> (T, H, W, 3) BGR."""
+    with open(path, "rb") as f:
+        buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+        try:
+            info = parse_mp4(buf)
+            return decode_mp4v(info.config, (bytes(buf[o:o + n]) for o, n in info.samples), start, end)
+        finally:
+            buf.close()
 
 
 def write_avi(path, frames, fps=30.0, codec="mjpeg", quality=90):
