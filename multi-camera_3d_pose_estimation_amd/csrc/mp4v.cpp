@@ -216,17 +216,41 @@ inline void idct_col(const int16_t* c, int (&o)[8]) {
 
 inline uint8_t clip8(int v) { return (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v); }
 
-// block: 64 coefficients, raster (8 * row + column); add = add to dst instead of put
-void idct_write(int16_t* blk, uint8_t* dst, int stride, bool add) {
-    for (int r = 0; r < 8; r++) idct_row(blk + 8 * r);
+// block: 64 coefficients, raster (8 * row + column); ADD = add to dst instead of put.  When the
+// row pass leaves only row 0 non-zero (DC-only and first-row-only blocks, most of a real frame)
+// every column reduces to its c[0] term, which is what the full column pass computes for it.
+template <bool ADD>
+void idct_write_t(int16_t* blk, uint8_t* dst, int stride) {
+    int rows = 0;
+    for (int r = 0; r < 8; r++) {
+        int16_t* q = blk + 8 * r;
+        if (r && !(q[0] | q[1] | q[2] | q[3] | q[4] | q[5] | q[6] | q[7])) continue;
+        idct_row(q);
+        rows |= 1 << r;
+    }
+    if (rows <= 1) {
+        for (int c = 0; c < 8; c++) {
+            const int o = (W4 * (blk[c] + ((1 << (COL_SHIFT - 1)) / W4))) >> COL_SHIFT;
+            for (int r = 0; r < 8; r++) {
+                uint8_t& d = dst[r * stride + c];
+                d = clip8(ADD ? d + o : o);
+            }
+        }
+        return;
+    }
     for (int c = 0; c < 8; c++) {
         int o[8];
         idct_col(blk + c, o);
         for (int r = 0; r < 8; r++) {
             uint8_t& d = dst[r * stride + c];
-            d = clip8(add ? d + o[r] : o[r]);
+            d = clip8(ADD ? d + o[r] : o[r]);
         }
     }
+}
+
+void idct_write(int16_t* blk, uint8_t* dst, int stride, bool add) {
+    if (add) idct_write_t<true>(blk, dst, stride);
+    else idct_write_t<false>(blk, dst, stride);
 }
 
 // ------------------------------------------------------------------ decoder
@@ -909,29 +933,29 @@ struct Decoder {
     void write_bgr(uint8_t* out) const {
         // per-component tables (BT.601 limited range, 8-bit fixed point): y298[Y], then the
         // chroma terms shared by each 2 x 2 luma quad
-        static const struct Lut {
-            int y[256], bu[256], gu[256], gv[256], rv[256];
-            Lut() {
-                for (int i = 0; i < 256; i++) {
-                    y[i] = 298 * (i - 16) + 128;
-                    bu[i] = 516 * (i - 128);
-                    gu[i] = -100 * (i - 128);
-                    gv[i] = -208 * (i - 128);
-                    rv[i] = 409 * (i - 128);
-                }
-            }
-        } L;
+        // BT.601 limited range in 8-bit fixed point: per row, the chroma terms of each 2 x 2
+        // luma quad are spread to the row's columns first, so the per-pixel loop is plain
+        // vectorisable integer arithmetic
         const Frame& f = cur;
+        std::vector<int32_t> tb(width), tg(width), tr(width);
         for (int y = 0; y < height; y++) {
             const uint8_t* Y = f.p[0].row(y);
-            const uint8_t* U = f.p[1].row(y >> 1);
-            const uint8_t* V = f.p[2].row(y >> 1);
             uint8_t* o = out + (size_t)y * width * 3;
+            if (!(y & 1)) {
+                const uint8_t* U = f.p[1].row(y >> 1);
+                const uint8_t* V = f.p[2].row(y >> 1);
+                for (int x = 0; x < width; x++) {
+                    const int u = U[x >> 1] - 128, v = V[x >> 1] - 128;
+                    tb[x] = 516 * u + 128 - 298 * 16;
+                    tg[x] = -100 * u - 208 * v + 128 - 298 * 16;
+                    tr[x] = 409 * v + 128 - 298 * 16;
+                }
+            }
             for (int x = 0; x < width; x++) {
-                const int c = L.y[Y[x]], u = U[x >> 1], v = V[x >> 1];
-                o[3 * x + 0] = clip8((c + L.bu[u]) >> 8);
-                o[3 * x + 1] = clip8((c + L.gu[u] + L.gv[v]) >> 8);
-                o[3 * x + 2] = clip8((c + L.rv[v]) >> 8);
+                const int c = 298 * Y[x];
+                o[3 * x + 0] = (uint8_t)std::min(std::max((c + tb[x]) >> 8, 0), 255);
+                o[3 * x + 1] = (uint8_t)std::min(std::max((c + tg[x]) >> 8, 0), 255);
+                o[3 * x + 2] = (uint8_t)std::min(std::max((c + tr[x]) >> 8, 0), 255);
             }
         }
     }
