@@ -74,9 +74,13 @@ struct Proj {
 // here NaN; in torch x = P0 / P2 is ~1e30 or more, whose square overflows f32 in the
 // distortion polynomial, so the term is non-finite there too and nan_mean's mask drops it in
 // both — they differ only for a point within ~1e-38 cm of the camera centre itself) and
-// returns 0 for |b| > 2^126 (a depth of 1e38 cm: here 0, in torch a quotient below 1e-38).  A per-lane
+// returns 0 for |b| > 2^126, a camera-frame depth beyond 8.5e37 cm.  torch returns a / b there:
+// ~0 for a moderate |a|, but O(1) when |a| is as large (a point ~1e38 cm away along any ray), so
+// a trajectory that has diverged to the f32 overflow scale projects to the principal point here
+// and to its true direction in torch — the two costs differ for such a point.  Every trajectory
+// the reference's own runs produce stays many orders of magnitude inside that range; a per-lane
 // range guard with an IEEE fallback measured +4.5-8 % per SGD iteration
-// (profiles/r04_sgd_guard_ab.txt) for no observable difference, so there is none.
+// (profiles/r04_sgd_guard_ab.txt), so there is none.
 __device__ __forceinline__ void div2_fast(float a0, float a1, float b, float& q0, float& q1) {
     const float r = __builtin_amdgcn_rcpf(b);
     const float p0 = a0 * r, p1 = a1 * r;
@@ -84,8 +88,12 @@ __device__ __forceinline__ void div2_fast(float a0, float a1, float b, float& q0
     q1 = __builtin_fmaf(__builtin_fmaf(-p1, b, a1), r, p1);
 }
 
-// project_points_torch (pose_refinement.py:118-177) for one point, torch op order.
-__device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, float X1, float X2, bool ign) {
+// project_points_torch (pose_refinement.py:118-177) for one point, torch op order.  kstd: K's
+// last row is (0, 0, 1) (camera-uniform), so h2 = xd·0 + yd·0 + 1 is exactly 1 for finite xd, yd
+// and u = h0 / 1 = h0: the division is skipped with identical results (a non-finite xd or yd
+// gives a non-finite cost either way, which the likelihood's finite mask drops).
+__device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, float X1, float X2, bool ign,
+                                        bool kstd) {
     const float* K = c;
     const float* R = c + 9;
     const float* T = c + 18;
@@ -116,24 +124,37 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
     }
     const float h0 = o.xd * K[0] + o.yd * K[1] + K[2];
     const float h1 = o.xd * K[3] + o.yd * K[4] + K[5];
-    const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
-    o.h2 = h2;
-    div2_fast(h0, h1, h2, o.u, o.v);
+    if (kstd) {
+        o.h2 = 1.f;
+        o.u = h0;
+        o.v = h1;
+    } else {
+        const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
+        o.h2 = h2;
+        div2_fast(h0, h1, h2, o.u, o.v);
+    }
     return o;
 }
 
 // d(u,v)/dX transposed applied to (gu, gv): the adjoint of project().
-__device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const Proj& o, bool ign, float gu,
-                                                float gv, float& g0, float& g1, float& g2, float (&dP)[3]) {
+__device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const Proj& o, bool ign, bool kstd,
+                                                float gu, float gv, float& g0, float& g1, float& g2,
+                                                float (&dP)[3]) {
     const float* K = c;
     const float* R = c + 9;
     const float* d = c + 21;
     // (u, v) = (h0, h1) / h2, h = K·[xd, yd, 1].  The adjoint's reciprocals are v_rcp_f32
     // (1 ulp): only the forward value needs torch's correctly rounded divisions, the gradient
     // already differs from autograd's by f32 summation order (an IEEE 1/x is ~10 VALU ops)
-    const float ih2 = __builtin_amdgcn_rcpf(o.h2);
-    const float gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
-    const float gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
+    float gxd, gyd;
+    if (kstd) {  // K6 = K7 = 0, h2 = 1: the same values without the zero terms
+        gxd = K[0] * gu + K[3] * gv;
+        gyd = K[1] * gu + K[4] * gv;
+    } else {
+        const float ih2 = __builtin_amdgcn_rcpf(o.h2);
+        gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
+        gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
+    }
     float gx = gxd, gy = gyd;
     if (!ign) {
         const float x = o.x, y = o.y, r2 = o.r2, rad = o.rad;
@@ -221,7 +242,29 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[NC]) {
 
 __device__ __forceinline__ bool finite(float x) { return !(isnan(x) || isinf(x)); }
 
-template <int BS, bool LEARN>
+// (q / d, q % d) for 0 <= q < 2^24 and d >= 1 with rd = 1.f / d: the f32 product is within one
+// of the quotient, and one correction step each way makes it exact (the integer division
+// expands to ~25 VALU instructions, this to ~8)
+__device__ __forceinline__ void divmod_small(int q, int d, float rd, int& quo, int& rem) {
+    int i = (int)((float)q * rd);
+    int r = q - i * d;
+    if (r < 0) {
+        i--;
+        r += d;
+    }
+    if (r >= d) {
+        i++;
+        r -= d;
+    }
+    quo = i;
+    rem = r;
+}
+
+// XL: the trajectory lives in LDS (T·J·3 floats within the LDS budget).  A template parameter,
+// not a runtime pointer choice: through a pointer that may be either, every trajectory access
+// compiles to a FLAT instruction (the vector-memory path, waits on both counters) instead of
+// ds_read / ds_write.
+template <int BS, bool LEARN, bool XL>
 __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     extern __shared__ float lds_traj[];
     __shared__ float cam_s[kMaxSgdCams * MVP_SGD_CAM_FLOATS];
@@ -232,6 +275,7 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     __shared__ int jseg_over;
     __shared__ double red_s[BS / 64][kRedCols];
     __shared__ int learn_slot[kMaxSgdCams];            // camera -> learnable index, -1 = fixed
+    __shared__ int cam_kstd[kMaxSgdCams];              // K's last row is (0, 0, 1)
     __shared__ float cstate[kMaxLearn * 2 * kCamGrad];  // Adam m | v of the learnable R, T
     __shared__ float cgrad[kMaxLearn * kCamGrad];       // the window's reduced camera gradient
 
@@ -239,6 +283,7 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     const int m = blockIdx.x, tid = threadIdx.x;
     const int T = a.T, V = a.V, J = a.J, B = a.B, NS = a.n_seg;
     const int TJ = T * J, n3 = TJ * 3;
+    const float rJ = 1.f / (float)J, rB = 1.f / (float)B;
     const bool ign = a.p.ignore_distortions != 0;
     const bool own = a.p.own_camera_gaussians != 0;
     const bool use_s = a.p.lambda_smooth > 0, use_b = a.p.lambda_body_length > 0;
@@ -246,12 +291,12 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
 
     const int Vg = own ? V : 1;                     // cameras with their own Gaussian
     float* ws = a.ws + (size_t)m * ((size_t)4 * n3 + T + (size_t)T * V * J * 6);
-    float* X = a.traj_in_lds ? lds_traj : ws;
+    float* X = XL ? lds_traj : ws;
     float* mo = ws + n3;
     float* ve = ws + 2 * (size_t)n3;
     float* gb = ws + 3 * (size_t)n3;
-    float* sterm = ws + 4 * (size_t)n3;            // per-window smoothness terms ‖D‖²
-    float* tgt = sterm + T;                         // [T][Vg][J][6] Target records
+    float* sterm = XL ? lds_traj + n3 : ws + 4 * (size_t)n3;  // per-window smoothness terms ‖D‖²
+    float* tgt = ws + 4 * (size_t)n3 + T;           // [T][Vg][J][6] Target records
     const float* G = a.gauss + (size_t)m * T * V * J * 6;
     const float* X0 = a.traj0 + (size_t)m * n3;
     float* best = a.best_traj + (size_t)m * n3;
@@ -259,6 +304,8 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
     for (int i = tid; i < V * MVP_SGD_CAM_FLOATS; i += BS) cam_s[i] = a.cams[i];
     const int NL = LEARN ? a.n_learn : 0;  // LEARN = false: the trajectory-only kernel, unchanged
     for (int c = tid; c < V; c += BS) {
+        const float* K = a.cams + c * MVP_SGD_CAM_FLOATS;
+        cam_kstd[c] = K[6] == 0.f && K[7] == 0.f && K[8] == 1.f;
         int sl = -1;
         for (int l = 0; l < NL; l++)
             if (a.learn[l] == c) sl = l;
@@ -337,8 +384,9 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
 #pragma unroll
                 for (int u = 0; u < kU; u++) {
                     const int q = min(q0 + u * BS, nq - 1);
-                    tq[u] = t0 + q / J;
-                    jq[u] = q - (q / J) * J;
+                    int qi;
+                    divmod_small(q, J, rJ, qi, jq[u]);
+                    tq[u] = t0 + qi;
                     const float* x = X + 3 * (tq[u] * J + jq[u]);
                     xs[u][0] = x[0];
                     xs[u][1] = x[1];
@@ -353,7 +401,8 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                     int lcnt = 0;
                     for (int c = 0; c < V; c++) {
                         const float* cam = cam_s + c * MVP_SGD_CAM_FLOATS;
-                        const Proj o = project(cam, xs[u][0], xs[u][1], xs[u][2], ign);
+                        const bool kstd = cam_kstd[c] != 0;  // camera-uniform
+                        const Proj o = project(cam, xs[u][0], xs[u][1], xs[u][2], ign, kstd);
                         const Target g =
                             own ? load_target(tgt + (((size_t)tq[u] * Vg + c) * J + jq[u]) * 6) : tg[u];
                         const float d0 = o.u - g.m0, d1 = o.v - g.m1;
@@ -365,7 +414,7 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                         const float gu = 0.5f * (2.f * g.a00 * d0 + s01 * d1);
                         const float gv = 0.5f * (s01 * d0 + 2.f * g.a11 * d1);
                         float h0, h1, h2, dP[3];
-                        project_adjoint(cam, o, ign, gu, gv, h0, h1, h2, dP);
+                        project_adjoint(cam, o, ign, kstd, gu, gv, h0, h1, h2, dP);
                         if constexpr (LEARN) {
                             const int ls = learn_slot[c];
                             auto add_cam = [&](float (&cg)[kCamGrad]) {  // dP/dR_ij = X_j, dP/dT_i = 1
@@ -413,7 +462,9 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                 }
             if (use_b)
                 for (int r = tid; r < NS * B; r += BS) {
-                    const int s = r / B, t = t0 + (r - s * B);
+                    int s, tr;
+                    divmod_small(r, B, rB, s, tr);
+                    const int t = t0 + tr;
                     const float* xa = X + 3 * (t * J + seg_s[2 * s]);
                     const float* xb = X + 3 * (t * J + seg_s[2 * s + 1]);
                     const float e0 = xb[0] - xa[0], e1 = xb[1] - xa[1], e2 = xb[2] - xa[2];
@@ -447,7 +498,9 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
             // ---- pass B: gradient of the window's total cost, pulled per owned point
             double acc2[2] = {0, 0};   // ‖g‖², Σ r²
             for (int q = tid; q < nq; q += BS) {
-                const int i = q / J, j = q - i * J, t = t0 + i;
+                int i, j;
+                divmod_small(q, J, rJ, i, j);
+                const int t = t0 + i;
                 float g0 = gb[3 * q + 0] * lscale, g1 = gb[3 * q + 1] * lscale, g2 = gb[3 * q + 2] * lscale;
                 if (use_s) {
                     // terms centred at t (coef +1), t+1 (-2), t+2 (+1), each 2·λs/n·D
@@ -493,7 +546,9 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
             }
             if (use_b)
                 for (int r = tid; r < NS * B; r += BS) {
-                    const int s = r / B, t = t0 + (r - s * B);
+                    int s, tr;
+                    divmod_small(r, B, rB, s, tr);
+                    const int t = t0 + tr;
                     const float* xa = X + 3 * (t * J + seg_s[2 * s]);
                     const float* xb = X + 3 * (t * J + seg_s[2 * s + 1]);
                     const float e0 = xb[0] - xa[0], e1 = xb[1] - xa[1], e2 = xb[2] - xa[2];
@@ -626,7 +681,7 @@ __global__ void project_kernel(const float* __restrict__ pts, long n, const floa
     float c[MVP_SGD_CAM_FLOATS];
 #pragma unroll
     for (int k = 0; k < MVP_SGD_CAM_FLOATS; k++) c[k] = cam[k];
-    const Proj o = project(c, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], ign != 0);
+    const Proj o = project(c, pts[3 * i], pts[3 * i + 1], pts[3 * i + 2], ign != 0, false);
     uv[2 * i] = o.u;
     uv[2 * i + 1] = o.v;
 }
@@ -656,7 +711,7 @@ __global__ __launch_bounds__(kExtBlock) void extrinsic_grad_kernel(const float* 
     for (long i = (long)blockIdx.x * kExtBlock + threadIdx.x; i < n_points; i += (long)gridDim.x * kExtBlock) {
         const float X0 = samples[3 * i], X1 = samples[3 * i + 1], X2 = samples[3 * i + 2];
         const Target g = load_target(tgt + (i / n_samples) * 6);
-        const Proj o = project(c, X0, X1, X2, ign != 0);
+        const Proj o = project(c, X0, X1, X2, ign != 0, false);
         const float d0 = o.u - g.m0, d1 = o.v - g.m1;
         const float val = quad_cost(g, d0, d1);
         if (!finite(val)) continue;
@@ -797,6 +852,8 @@ void sgd_launch(const float* gauss, const float* traj0, const float* cams, int M
     MVP_REQUIRE(M > 0 && T > 0 && V > 0 && J > 0, "mvp_sgd_refine: M, T, V, J must be positive");
     MVP_REQUIRE(V <= kMaxSgdCams, "mvp_sgd_refine: V=%d > %d cameras", V, kMaxSgdCams);
     MVP_REQUIRE(J <= kMaxJ, "mvp_sgd_refine: J=%d > %d joints", J, kMaxJ);
+    MVP_REQUIRE((int64_t)T * J * 3 < (1 << 24), "mvp_sgd_refine: T*J*3 = %lld >= 2^24 coordinates",
+                (long long)T * J * 3);  // divmod_small's exact range (and far past any real recording)
     MVP_REQUIRE(n_seg >= 0 && n_seg <= kMaxSeg, "mvp_sgd_refine: n_seg=%d outside [0, %d]", n_seg, kMaxSeg);
     MVP_REQUIRE(n_seg == 0 || (seg && seg_len), "mvp_sgd_refine: segments missing");
     MVP_REQUIRE(p->lambda_body_length <= 0 || n_seg > 0,
@@ -839,23 +896,24 @@ void sgd_launch(const float* gauss, const float* traj0, const float* cams, int M
     }
     a.cams_final = cams_final;
     a.cams_best = cams_best;
-    const size_t traj_bytes = (size_t)T * J * 3 * sizeof(float);
+    const size_t traj_bytes = ((size_t)T * J * 3 + T) * sizeof(float);  // trajectory + smoothness terms
     constexpr size_t kLdsBudget = 120 * 1024;
     a.traj_in_lds = traj_bytes <= kLdsBudget;
     const size_t lds = a.traj_in_lds ? traj_bytes : 0;
     hipStream_t s = (hipStream_t)stream;
+    auto launch = [&](auto kern, int bs) {
+        MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBudget));
+        hipLaunchKernelGGL(kern, dim3(M), dim3(bs), lds, s, a);
+    };
     if (n_learn > 0) {  // joint branch: one kernel width (the camera gradient's registers)
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kLdsBudget));
-        hipLaunchKernelGGL((sgd_kernel<256, true>), dim3(M), dim3(256), lds, s, a);
+        if (a.traj_in_lds) launch(sgd_kernel<256, true, true>, 256);
+        else launch(sgd_kernel<256, true, false>, 256);
     } else if (T * J > 1024) {  // 16 waves: 4 per SIMD (M = 256 config 5: 0.211 -> 0.170 ms per iteration vs 512)
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<1024, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kLdsBudget));
-        hipLaunchKernelGGL((sgd_kernel<1024, false>), dim3(M), dim3(1024), lds, s, a);
+        if (a.traj_in_lds) launch(sgd_kernel<1024, false, true>, 1024);
+        else launch(sgd_kernel<1024, false, false>, 1024);
     } else {
-        MVP_HIP(hipFuncSetAttribute((const void*)sgd_kernel<256, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)kLdsBudget));
-        hipLaunchKernelGGL((sgd_kernel<256, false>), dim3(M), dim3(256), lds, s, a);
+        if (a.traj_in_lds) launch(sgd_kernel<256, false, true>, 256);
+        else launch(sgd_kernel<256, false, false>, 256);
     }
     MVP_HIP(hipGetLastError());
 }

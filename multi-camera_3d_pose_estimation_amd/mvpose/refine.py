@@ -35,6 +35,7 @@ from __future__ import annotations
 import ctypes
 import math
 import random
+import threading
 
 import numpy as np
 import torch
@@ -81,10 +82,43 @@ def _stream(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+_PINNED = {}
+_PINNED_LOCK = threading.Lock()
+
+
+def _h2d_words(words, dev):
+    """A small int32 host array on the device through a reused pinned staging buffer and an
+    asynchronous copy (a pageable copy synchronises the stream: tens of microseconds of idle
+    device per call).  The buffer is rewritten only after its previous copy has completed."""
+    n = int(words.size)
+    with _PINNED_LOCK:
+        buf, ev = _PINNED.get(dev, (None, None))
+        if buf is None or buf.numel() < n:
+            buf, ev = torch.empty(max(n, 4096), dtype=torch.int32).pin_memory(), None
+        if ev is not None:
+            ev.synchronize()
+        buf[:n].numpy()[:] = words
+        out = buf[:n].to(dev, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dev))
+        _PINNED[dev] = (buf, ev)
+    return out
+
+
+def _on_device_f32(a, dev):
+    """a as a contiguous float32 tensor on dev (device-resident float32 inputs pass through
+    without a .to() call, which costs tens of microseconds even when it is a no-op)."""
+    if isinstance(a, torch.Tensor) and a.dtype == torch.float32 and a.device == dev and a.is_contiguous():
+        return a
+    return torch.as_tensor(a).to(device=dev, dtype=torch.float32).contiguous()
+
+
 def _device(device):
     dev = torch.device(device if device is not None else "cuda")
     if dev.type != "cuda":
         raise ValueError("mvpose refinement runs on the GPU only (no CPU fallback)")
+    if dev.index is None and torch.cuda.is_available():
+        dev = torch.device("cuda", torch.cuda.current_device())
     return dev
 
 
@@ -113,6 +147,14 @@ def rotation_conversion(rotation_rep, to_vector=True):
 def camera_record(K, R, T, dist) -> np.ndarray:
     """One MVP_SGD_CAM_FLOATS f32 record [K | R (matrix) | T | dist] from the reference's
     decomposed parameters (R may be a 3x3 matrix or an axis-angle vector)."""
+    if not any(isinstance(a, torch.Tensor) for a in (K, R, T, dist)) and np.size(R) == 9:
+        # numpy in, R a matrix: the float32 casts alone (what the torch path below computes for
+        # it, without its per-camera tensor round trips)
+        d = np.asarray(dist, dtype=np.float32).reshape(-1)
+        if d.size != 5:
+            raise ValueError("dist_coeffs must have shape (1, 5)")
+        return np.concatenate([np.asarray(K, dtype=np.float32).reshape(9), np.asarray(R, dtype=np.float32).reshape(9),
+                               np.asarray(T, dtype=np.float32).reshape(3), d])
     f32 = (lambda a: torch.as_tensor(np.asarray(a) if not isinstance(a, torch.Tensor) else a).to(torch.float32))
     Rm = rotation_conversion(f32(R), to_vector=False)
     d = f32(dist).reshape(-1)
@@ -209,8 +251,8 @@ def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=N
     (mvp_sgd_refine_cams); adds cams_final / cams_best (M, n_learn, 12) = [R row-major | T]
     (best NaN if never improved)."""
     dev = _device(device)
-    G = torch.as_tensor(gaussians).to(device=dev, dtype=torch.float32).contiguous()
-    X0 = torch.as_tensor(initial_trajectories).to(device=dev, dtype=torch.float32).contiguous()
+    G = _on_device_f32(gaussians, dev)
+    X0 = _on_device_f32(initial_trajectories, dev)
     if G.dim() != 5 or G.shape[-1] != 6 or X0.dim() != 4 or X0.shape[-1] != 3:
         raise ValueError("gaussians must be (M,T,V,J,6) and initial_trajectories (M,T,J,3)")
     M, T, V, J = G.shape[:4]
@@ -223,15 +265,20 @@ def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=N
         raise ValueError(f"batch_size {B} must be in [2, T={T}]")
     if lambda_body_length > 0 and not body_lengths:
         raise ValueError("lambda_body_length > 0 needs body_lengths (reference create_body_length_vect)")
-    cams = torch.from_numpy(np.stack([camera_record(*c) for c in cameras])).to(dev)
+    # the constant tables (camera records, segment pairs and lengths: all 4-byte words) in one
+    # host-to-device copy
+    recs = np.stack([camera_record(*c) for c in cameras]).astype(np.float32).reshape(-1)
     if body_lengths:
         pairs, lens = segments_for(body_lengths)
-        seg = torch.from_numpy(pairs).to(dev)
-        seg_len = torch.from_numpy(lens).to(dev)
         n_seg = len(lens)
+        words = np.concatenate([recs.view(np.int32), pairs.astype(np.int32).reshape(-1), lens.view(np.int32)])
     else:
-        seg = seg_len = None
         n_seg = 0
+        words = recs.view(np.int32)
+    tab = _h2d_words(words, dev)
+    cams = tab[:recs.size].view(torch.float32).view(V, -1)
+    seg = tab[recs.size:recs.size + 2 * n_seg] if n_seg else None
+    seg_len = tab[recs.size + 2 * n_seg:].view(torch.float32) if n_seg else None
     p = SgdParams(lr=float(lr), beta1=float(betas[0]), beta2=float(betas[1]), adam_eps=float(adam_eps),
                   lambda_smooth=float(lambda_smooth), lambda_body_length=float(lambda_body_length),
                   tolerance=float(tolerance), max_grad_norm=float(max_grad_norm), patience=int(patience),
@@ -245,9 +292,12 @@ def refine_trajectories(gaussians, initial_trajectories, cameras, body_lengths=N
     best = torch.empty_like(X0)
     final = torch.empty_like(X0)
     n_it = int(max_iter) + 1
-    batch_costs = torch.zeros((M, n_it, n_win, N_COSTS), dtype=torch.float32, device=dev)
-    iter_means = torch.zeros((M, n_it, N_COSTS), dtype=torch.float32, device=dev)
-    iters = torch.zeros(M, dtype=torch.int32, device=dev)
+    # the three zero-initialised outputs: one fill
+    n_bc, n_im = M * n_it * n_win * N_COSTS, M * n_it * N_COSTS
+    zero = torch.zeros(n_bc + n_im + M, dtype=torch.int32, device=dev)
+    batch_costs = zero[:n_bc].view(torch.float32).view(M, n_it, n_win, N_COSTS)
+    iter_means = zero[n_bc:n_bc + n_im].view(torch.float32).view(M, n_it, N_COSTS)
+    iters = zero[n_bc + n_im:]
     out = {"best": best, "final": final, "batch_costs": batch_costs, "iter_means": iter_means, "iters": iters}
     if learn_cams:
         nl = len(learn_cams)

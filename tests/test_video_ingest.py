@@ -107,8 +107,12 @@ def test_load_frames_dispatch_and_errors(tmp_path):
     assert pose_estimation.load_frames("not-a-list") is None
     m = tmp_path / "c.mp4"
     m.write_bytes(b"\0\0\0\x18ftypmp42" + b"\0" * 32)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):          # an MP4 without its moov box
         pose_estimation.load_frames([str(m)])
+    k = tmp_path / "d.mkv"
+    k.write_bytes(b"\x1a\x45\xdf\xa3" + b"\0" * 32)   # Matroska: no demuxer here
+    with pytest.raises(NotImplementedError):
+        pose_estimation.load_frames([str(k)])
     with pytest.raises(FileNotFoundError):
         pose_estimation.load_frames([str(tmp_path / "missing.avi")])
     with pytest.raises(ValueError):
