@@ -226,17 +226,23 @@ class Mp4vDecoder:
         _lib.call("mvp_mp4v_create", cfg, len(config), ctypes.byref(self._h), ctypes.byref(w), ctypes.byref(h))
         self.width, self.height = w.value, h.value
 
-    def decode(self, sample: bytes, yuv: bool = False) -> np.ndarray:
+    def decode(self, sample: bytes, yuv: bool = False, out: np.ndarray | None = None) -> np.ndarray:
+        """One sample -> the frame after its last VOP: (H, W, 3) BGR, or the I420 planes with
+        yuv=True; out: a C-contiguous uint8 array of that shape to decode into."""
         import ctypes
         data = np.frombuffer(sample, np.uint8)
         n = ctypes.c_int()
         if yuv:
             cw, ch = (self.width + 1) // 2, (self.height + 1) // 2
-            out = np.empty(self.width * self.height + 2 * cw * ch, np.uint8)
+            if out is None:
+                out = np.empty(self.width * self.height + 2 * cw * ch, np.uint8)
             self._lib.call("mvp_mp4v_decode", self._h, data.ctypes.data, data.size, None, out.ctypes.data,
                            ctypes.byref(n))
             return out
-        out = np.empty((self.height, self.width, 3), np.uint8)
+        if out is None:
+            out = np.empty((self.height, self.width, 3), np.uint8)
+        if out.shape != (self.height, self.width, 3) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError(f"out must be a C-contiguous ({self.height}, {self.width}, 3) uint8 array")
         self._lib.call("mvp_mp4v_decode", self._h, data.ctypes.data, data.size, out.ctypes.data, None,
                        ctypes.byref(n))
         return out
@@ -273,27 +279,53 @@ def split_vops(stream: bytes):
     return stream[:vops[0]], samples
 
 
-def decode_mp4v(config: bytes, samples, start=0, end=None) -> np.ndarray:
-    """Decode every sample (P-VOPs need their predecessors) and keep frames [start:end)."""
+def vop_coding_type(sample) -> int:
+    """vop_coding_type of the sample's first VOP (0 I, 1 P, 2 B, 3 S), -1 if it holds none."""
+    data = bytes(sample)
+    i = data.find(b"\0\0\1\xb6")
+    return data[i + 4] >> 6 if 0 <= i and i + 4 < len(data) else -1
+
+
+def decode_mp4v(config: bytes, samples, start=0, end=None, threads=None) -> np.ndarray:
+    """Decode frames [start:end) of a sample sequence.  P-VOPs need their predecessors back to
+    the last I-VOP, so the sequence splits into independent GOPs (each starting at an I-VOP);
+    the GOPs that hold wanted frames decode on a thread pool, one decoder each (the native
+    decoder releases the GIL), straight into the output array."""
     samples = list(samples)
     if not config and samples:
         config = samples[0]       # VOL headers in the first sample (AVI without strf extra data)
-    dec = Mp4vDecoder(config)
-    try:
-        frames = []
-        keep = range(len(samples))[slice(start, end)]
-        lo, hi = (keep.start, keep.stop) if len(keep) else (0, 0)
-        for i, smp in enumerate(samples):
-            if i >= hi:
-                break
-            fr = dec.decode(smp)
-            if i >= lo:
-                frames.append(fr)
-        if not frames:
-            return np.empty((0, dec.height, dec.width, 3), np.uint8)
-        return np.stack(frames)
-    finally:
-        dec.close()
+    keep = range(len(samples))[slice(start, end)]
+    lo, hi = (keep.start, keep.stop) if len(keep) and keep.step == 1 else (0, 0)
+    probe = Mp4vDecoder(config)
+    H, W = probe.height, probe.width
+    probe.close()
+    out = np.empty((max(hi - lo, 0), H, W, 3), np.uint8)
+    if hi <= lo:
+        return out
+    # GOP starts: I-VOPs (the first sample always starts one: a P-VOP there fails in the decoder)
+    starts = [i for i in range(hi) if i == 0 or vop_coding_type(samples[i]) == 0]
+    gops = [(a, b) for a, b in zip(starts, starts[1:] + [hi]) if b > lo]
+
+    def run(g):
+        a, b = g
+        dec = Mp4vDecoder(config)
+        try:
+            for i in range(a, b):
+                if i >= lo:
+                    dec.decode(samples[i], out=out[i - lo])
+                else:
+                    dec.decode(samples[i])
+        finally:
+            dec.close()
+
+    workers = max(1, min(int(threads or os.cpu_count() or 1), 16, len(gops)))
+    if workers == 1:
+        for g in gops:
+            run(g)
+    else:
+        with ThreadPoolExecutor(workers) as pool:
+            list(pool.map(run, gops))
+    return out
 
 
 def read_m4v(path, start=0, end=None) -> np.ndarray:

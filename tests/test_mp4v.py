@@ -302,3 +302,28 @@ def test_bgr_conversion_is_bt601_limited_range():
     bgr = dec.decode(vw.i_vop(mbs, 2))
     dec.close()
     assert (bgr[:, :16] == 0).all() and (bgr[:, 16:] == 255).all()
+
+
+def test_parallel_gop_decode_equals_serial():
+    """decode_mp4v splits the stream at I-VOPs and decodes the GOPs holding wanted frames on a
+    thread pool: the same frames as one decoder walking every sample, for every slice."""
+    w, h = WH
+    rng = np.random.default_rng(11)
+    mw, mh = w // 16, h // 16
+    vw = W.VopWriter(w, h)
+    samples = []
+    for n_p in (2, 3, 1, 0, 2):
+        samples.append(vw.i_vop([[_rand_intra_mb(rng, 4) for _ in range(mw)] for _ in range(mh)], 4))
+        for f in range(n_p):
+            mbs = [[{"type": "inter", "mv": (int(rng.integers(-5, 6)), int(rng.integers(-5, 6))),
+                     "blocks": _rand_residual(rng)} for _ in range(mw)] for _ in range(mh)]
+            samples.append(vw.p_vop(mbs, 4, rounding=f % 2))
+    cfg = W.vol_header(w, h)
+    assert [video.vop_coding_type(s) for s in samples] == [0, 1, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1]
+    dec = video.Mp4vDecoder(cfg)
+    serial = np.stack([dec.decode(s) for s in samples])
+    dec.close()
+    for sl in [(0, None), (0, -1), (2, 9), (4, 5), (8, None), (12, 13), (5, 3)]:
+        for threads in (1, 4):
+            got = video.decode_mp4v(cfg, samples, *sl, threads=threads)
+            np.testing.assert_array_equal(got, serial[slice(*sl)], err_msg=f"{sl} threads={threads}")
