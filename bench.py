@@ -432,6 +432,51 @@ def ingest_line(est, V, n_frames=512, batch=128):
                     "moments on the compute stream (2D stage only, serial moments)"}
 
 
+def video_decode_line(gops=16, gop=12, threads=16):
+    """the native MPEG-4 Part 2 decoder on a synthetic 1280x720 mp4v
+    stream (GOPs of one I-VOP + 11 P-VOPs written by tests/mp4v_writer.py: ~5 % non-zero
+    intra coefficients, +-3 px motion, ~1 % non-zero residuals), decoded to BGR frames in host
+    RAM as cv2.VideoCapture would (utils.py:849-909): one thread, and the GOPs on a thread pool.
+    Host CPU work, outside every GPU figure."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import mp4v_writer as W
+    from mvpose import video
+    w, h = 1280, 720
+    rng = np.random.default_rng(7)
+    mw, mh = w // 16, h // 16
+
+    def intra_mb():
+        b = np.zeros((6, 64), np.int64)
+        for n in range(6):
+            b[n, 0] = rng.integers(40, 160) if n < 4 else rng.integers(80, 140)
+            m = rng.random(63) < 0.05
+            b[n, 1:][m] = rng.integers(-4, 5, m.sum())
+        return {"q": 6, "blocks": b, "ac_pred": False}
+
+    def inter_mb():
+        b = np.zeros((6, 64), np.int64)
+        m = rng.random((6, 64)) < 0.01
+        b[m] = rng.integers(-2, 3, m.sum())
+        return {"type": "inter", "mv": (int(rng.integers(-3, 4)), int(rng.integers(-3, 4))), "blocks": b}
+
+    vw = W.VopWriter(w, h)
+    i_vop = vw.i_vop([[intra_mb() for _ in range(mw)] for _ in range(mh)], 6)
+    p_vops = [vw.p_vop([[inter_mb() for _ in range(mw)] for _ in range(mh)], 6, rounding=k % 2) for k in range(3)]
+    samples = ([i_vop] + [p_vops[k % 3] for k in range(gop - 1)]) * gops
+    cfg = W.vol_header(w, h)
+    res = {}
+    for th in (1, threads):
+        video.decode_mp4v(cfg, samples[:gop], threads=th)
+        t0 = time.perf_counter()
+        out = video.decode_mp4v(cfg, samples, threads=th)
+        res[th] = len(samples) / (time.perf_counter() - t0)
+        assert out.shape == (len(samples), h, w, 3)
+    return {"frames_per_s": res[threads], "threads": threads, "frames_per_s_1thread": res[1],
+            "frames": len(samples), "stream": f"1280x720 mp4v, GOP {gop} (I + {gop - 1} P), "
+                                            f"{sum(map(len, samples)) * 8 / len(samples) * 30 / 1e6:.1f} Mbit/s at 30 fps",
+            "path": "mvpose.video.decode_mp4v: native Simple Profile decoder (csrc/mp4v.cpp), GOPs on a thread pool"}
+
+
 def detector_line(dev, est, cams_params, V, batch=None, reps=5):
     """the person detector the reference runs on every camera-frame
     (RTMDet-m, mmpose_pose_estimation.py:234-250), alone (letterbox -> graph -> per-frame
@@ -577,6 +622,7 @@ def main():
             extra["sgd"] = sgd_line(dev)
             extra["sgd_extrinsic"] = extrinsic_line(dev)
             extra["host_ingest"] = ingest_line(est, V)
+            extra["video_decode"] = video_decode_line()
             extra["detector"] = detector_line(dev, est, syn.reference_camera_params(cams), V)
 
     if rank == 0:

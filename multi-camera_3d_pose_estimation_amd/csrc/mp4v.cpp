@@ -253,6 +253,57 @@ void idct_write(int16_t* blk, uint8_t* dst, int stride, bool add) {
     else idct_write_t<false>(blk, dst, stride);
 }
 
+// BT.601 limited range in 8-bit fixed point (y = 298 (Y - 16) + 128, then >> 8 after the chroma
+// terms): per row, the chroma terms of each 2 x 2 luma quad are spread to the row's columns,
+// B, G and R are formed as three planar rows (plain integer loops the compiler vectorises) and
+// interleaved into BGR24.  One body, compiled twice: for the baseline ISA and for AVX2 (picked
+// at run time), whose 32-bit min / max the vectoriser needs.
+#define MP4V_BGR_ROWS_BODY                                                                        \
+    std::vector<int32_t> tb(width), tg(width), tr(width);                                         \
+    std::vector<uint8_t> pb(width), pg(width), pr(width);                                         \
+    for (int y = 0; y < height; y++) {                                                            \
+        const uint8_t* Y = Yp + (size_t)y * ys;                                                   \
+        uint8_t* o = out + (size_t)y * width * 3;                                                 \
+        if (!(y & 1)) {                                                                           \
+            const uint8_t* U = Up + (size_t)(y >> 1) * cs;                                        \
+            const uint8_t* V = Vp + (size_t)(y >> 1) * cs;                                        \
+            for (int x = 0; x < width; x++) {                                                     \
+                const int u = U[x >> 1] - 128, v = V[x >> 1] - 128;                               \
+                tb[x] = 516 * u + 128 - 298 * 16;                                                 \
+                tg[x] = -100 * u - 208 * v + 128 - 298 * 16;                                      \
+                tr[x] = 409 * v + 128 - 298 * 16;                                                 \
+            }                                                                                     \
+        }                                                                                         \
+        const int32_t* __restrict__ cb = tb.data();                                               \
+        const int32_t* __restrict__ cg = tg.data();                                               \
+        const int32_t* __restrict__ cr = tr.data();                                               \
+        uint8_t* __restrict__ ob = pb.data();                                                     \
+        uint8_t* __restrict__ og = pg.data();                                                     \
+        uint8_t* __restrict__ orr = pr.data();                                                    \
+        for (int x = 0; x < width; x++) {                                                         \
+            const int c = 298 * Y[x];                                                             \
+            ob[x] = (uint8_t)std::min(std::max((c + cb[x]) >> 8, 0), 255);                        \
+            og[x] = (uint8_t)std::min(std::max((c + cg[x]) >> 8, 0), 255);                        \
+            orr[x] = (uint8_t)std::min(std::max((c + cr[x]) >> 8, 0), 255);                       \
+        }                                                                                         \
+        for (int x = 0; x < width; x++) {                                                         \
+            o[3 * x + 0] = ob[x];                                                                 \
+            o[3 * x + 1] = og[x];                                                                 \
+            o[3 * x + 2] = orr[x];                                                                \
+        }                                                                                         \
+    }
+
+void bgr_rows_plain(const uint8_t* Yp, const uint8_t* Up, const uint8_t* Vp, int ys, int cs, int width, int height,
+                    uint8_t* out) {
+    MP4V_BGR_ROWS_BODY
+}
+
+__attribute__((target("avx2"))) void bgr_rows_x86avx2(const uint8_t* Yp, const uint8_t* Up, const uint8_t* Vp, int ys,
+                                                      int cs, int width, int height, uint8_t* out) {
+    MP4V_BGR_ROWS_BODY
+}
+#undef MP4V_BGR_ROWS_BODY
+
 // ------------------------------------------------------------------ decoder
 struct Plane {
     int w = 0, h = 0;  // MB-aligned
@@ -933,31 +984,12 @@ struct Decoder {
     void write_bgr(uint8_t* out) const {
         // per-component tables (BT.601 limited range, 8-bit fixed point): y298[Y], then the
         // chroma terms shared by each 2 x 2 luma quad
-        // BT.601 limited range in 8-bit fixed point: per row, the chroma terms of each 2 x 2
-        // luma quad are spread to the row's columns first, so the per-pixel loop is plain
-        // vectorisable integer arithmetic
         const Frame& f = cur;
-        std::vector<int32_t> tb(width), tg(width), tr(width);
-        for (int y = 0; y < height; y++) {
-            const uint8_t* Y = f.p[0].row(y);
-            uint8_t* o = out + (size_t)y * width * 3;
-            if (!(y & 1)) {
-                const uint8_t* U = f.p[1].row(y >> 1);
-                const uint8_t* V = f.p[2].row(y >> 1);
-                for (int x = 0; x < width; x++) {
-                    const int u = U[x >> 1] - 128, v = V[x >> 1] - 128;
-                    tb[x] = 516 * u + 128 - 298 * 16;
-                    tg[x] = -100 * u - 208 * v + 128 - 298 * 16;
-                    tr[x] = 409 * v + 128 - 298 * 16;
-                }
-            }
-            for (int x = 0; x < width; x++) {
-                const int c = 298 * Y[x];
-                o[3 * x + 0] = (uint8_t)std::min(std::max((c + tb[x]) >> 8, 0), 255);
-                o[3 * x + 1] = (uint8_t)std::min(std::max((c + tg[x]) >> 8, 0), 255);
-                o[3 * x + 2] = (uint8_t)std::min(std::max((c + tr[x]) >> 8, 0), 255);
-            }
-        }
+        const uint8_t *Y = f.p[0].row(0), *U = f.p[1].row(0), *V = f.p[2].row(0);
+        if (__builtin_cpu_supports("avx2"))
+            bgr_rows_x86avx2(Y, U, V, f.p[0].w, f.p[1].w, width, height, out);
+        else
+            bgr_rows_plain(Y, U, V, f.p[0].w, f.p[1].w, width, height, out);
     }
 };
 
