@@ -23,9 +23,13 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
 // before the residual, 1 = ReLU after it)
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s, const uint16_t* wimg = nullptr);
+                          hipStream_t s, const uint16_t* wimg = nullptr, const uint16_t* wband = nullptr);
 // The GEMM kernel's weight image (same element count as w: npad x K, K = ks * ks * cin)
 void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hipStream_t s);
+// The band-halo kernel (3x3/s1, >= 96 input channels, 80x80 / 40x40 planes, couts in blocks of 64):
+// whether a conv qualifies, and its weight image (same element count as w)
+bool det_band_eligible(int H, int W, int cin, int npad, int ks, int stride);
+void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, hipStream_t s);
 // channel attention in place; scratch: [n][17][C] f32 (per-split partial sums + scales)
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
                    hipStream_t s);

@@ -597,6 +597,176 @@ __global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GPa
     }
 }
 
+// 3x3/s1 convs with >= 3 input chunks on the 80x80 and 40x40 planes (the CSPNeXt stage-3
+// blocks, the neck's 40x40 blocks and out_convs, the head's stacked convs: ~18 of the 38.9
+// GMAC per frame).  The im2col GEMM above re-DMAs every input pixel once per tap, 20 KB per
+// 786 K MAC (39 MAC/B from L2), which bounds it near a quarter of the MFMA peak.  Here a work
+// item is a band of TR output rows x the whole width (320 pixels: 4 x 80 or 8 x 40) of one
+// frame and 64 couts; per 32-channel input chunk its (TR + 2) x (W + 2) input halo (64 B per
+// pixel, zero borders) and the chunk's weights for all 9 taps ([tap][cout][4 chunks], a
+// contiguous 36 KB slice of the packed image, det_pack_band_weights) arrive by one round of
+// LDS-DMA into one of two buffers while the previous chunk computes (~88 MAC per byte moved),
+// and the taps are address offsets into the halo.  4 waves, each 80 output pixels (5
+// fragments of 16) x the 64 couts (4 tiles): every A fragment read feeds 5 MFMAs, every B
+// fragment 4 (v_mfma_f32_16x16x32_bf16).  Persistent workgroups, one per CU (137 KB of LDS),
+// walk their items chunk by chunk with the next step's DMA in flight.  XCD-aware: the
+// workgroups of one XCD (blockIdx % 8) form groups of n_nb (couts / 64) that take the same
+// band together, one cout block each, so a band's input comes from HBM once into that XCD's
+// L2.  Same swizzled row images as the GEMM kernel (a row = cout or halo pixel, its four 16-B
+// channel chunks at 4r + (kg ^ swz(r))).  K order (chunk, tap, channel): equal to the GEMM
+// kernel's (tap, chunk, channel) sums to f32 rounding.
+constexpr int kBandBN = 64;
+
+template <int W, int TR>
+struct BandCfg {
+    static constexpr int HWD = W + 2, HP = (TR + 2) * HWD;  // halo row pitch, halo pixels
+    static constexpr int P = TR * W;                        // output pixels per item
+    static constexpr int A_SLOTS = 9 * 4 * kBandBN;         // [tap][cout][4]
+    static constexpr int A_R64 = A_SLOTS / 64;
+    static constexpr int B_R64 = (HP * 4 + 63) / 64;
+    static constexpr int BUF = (A_SLOTS + B_R64 * 64) * 16;
+    static constexpr int LDS = 2 * BUF;
+    static constexpr int FPW = P / 64;                      // 16-pixel fragments per wave (4 waves)
+    static_assert(P == 320 && FPW == 5, "band: 320-pixel items");
+    static_assert(LDS <= 160 * 1024, "band: LDS budget");
+};
+
+template <int W, int TR>
+__global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const uint16_t* __restrict__ wband) {
+    using C = BandCfg<W, TR>;
+    constexpr int FP = C::FPW;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    // item assignment (see above): WG b on XCD b % 8, group g of n_nb consecutive slots
+    const int n_nb = p.n_nb, nck = p.cin / 32;
+    const int G = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, sl = b >> 3, spx = G >> 3;
+    const int ng = spx / n_nb;
+    if (sl >= ng * n_nb) return;  // whole workgroup: uniform
+    const int nb = sl % n_nb, g = sl / n_nb;
+    const int tpi = p.H / TR;  // bands per frame
+    const int tiles = (int)(p.M / ((long)p.H * W)) * tpi;
+    const int n_items = tiles > (g * 8 + xcd) ? (tiles - (g * 8 + xcd) + ng * 8 - 1) / (ng * 8) : 0;
+    if (n_items == 0) return;
+    const int steps = n_items * nck;
+    auto item_tile = [&](int k) { return (k * ng + g) * 8 + xcd; };
+    // one step's DMA: chunk c of item k into buffer buf
+    auto issue = [&](int st, int buf) {
+        const int k = st / nck, c = st - k * nck;
+        const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
+        uint8_t* base = lds + buf * C::BUF;
+        const uint16_t* wsrc = wband + ((size_t)(nb * nck + c) * C::A_SLOTS) * 8;
+        for (int r = wave; r < C::A_R64; r += 4)
+            glds16_det(wsrc + (size_t)(r * 64 + lane) * 8, base + r * 64 * 16);
+        const uint16_t* xb = p.x + (size_t)n * p.H * W * p.xs + c * 32;
+        for (int r = wave; r < C::B_R64; r += 4) {
+            const int s2 = r * 64 + lane, hp = s2 >> 2, kq = (s2 & 3) ^ swz(hp);
+            const int hy = hp / C::HWD, hx = hp - hy * C::HWD;
+            const int gy = row0 + hy - 1, gx = hx - 1;
+            const bool in = hp < C::HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)W;
+            const void* src = in ? (const void*)(xb + ((size_t)gy * W + gx) * p.xs + kq * 8)
+                                 : (const void*)(p.zero + (s2 & 1023) * 8);
+            glds16_det(src, base + (C::A_SLOTS + s2) * 16);
+        }
+    };
+    const int kg = lane >> 4, r16 = lane & 15;
+    const int soffA = (r16 * 4 + (kg ^ swz(r16))) * 16;
+    int hb[FP];  // halo index of tap (0, 0) for this lane's pixel of each fragment
+#pragma unroll
+    for (int i = 0; i < FP; i++) {
+        const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
+        hb[i] = pr * C::HWD + pc;
+    }
+    f32x4 acc[FP][4];
+    issue(0, 0);
+    int buf = 0;
+    for (int st = 0; st < steps; st++) {
+        const int k = st / nck, c = st - k * nck;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step st (and stores)
+        __builtin_amdgcn_s_barrier();                         // every wave's; buffer buf ^ 1 is free
+        asm volatile("" ::: "memory");
+        if (st + 1 < steps) issue(st + 1, buf ^ 1);
+        if (c == 0) {
+#pragma unroll
+            for (int i = 0; i < FP; i++)
+#pragma unroll
+                for (int ct = 0; ct < 4; ct++) acc[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        const uint8_t* base = lds + buf * C::BUF;
+#pragma unroll
+        for (int tp = 0; tp < 9; tp++) {
+            const int toff = (tp / 3) * C::HWD + (tp % 3);
+            bf16x8 a[4], bb[FP];
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++)
+                a[ct] = *reinterpret_cast<const bf16x8*>(base + (tp * 4 * kBandBN + ct * 64) * 16 + soffA);
+#pragma unroll
+            for (int i = 0; i < FP; i++) {
+                const int hp = hb[i] + toff;
+                bb[i] = *reinterpret_cast<const bf16x8*>(base + (C::A_SLOTS + hp * 4 + (kg ^ swz(hp))) * 16);
+            }
+#pragma unroll
+            for (int i = 0; i < FP; i++)
+#pragma unroll
+                for (int ct = 0; ct < 4; ct++)
+                    acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bb[i], acc[i][ct], 0, 0, 0);
+        }
+        if (c == nck - 1) {  // epilogue of item k: lane holds couts 16 ct + 4 kg + j of its pixel
+            const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++) {
+                const int co = nb * kBandBN + ct * 16 + kg * 4;
+                if (co >= p.N) continue;
+                const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
+#pragma unroll
+                for (int i = 0; i < FP; i++) {
+                    const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
+                    const long m = ((long)n * p.H + row0 + pr) * W + pc;
+                    const f32x4 ac = acc[i][ct];
+                    float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
+                    if (p.act == 2)
+#pragma unroll
+                        for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+                    if (p.res) {
+                        const uint2 rr = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                        v[0] += bf(rr.x & 0xffff), v[1] += bf(rr.x >> 16), v[2] += bf(rr.y & 0xffff),
+                            v[3] += bf(rr.y >> 16);
+                    }
+                    if (p.act == 1)
+#pragma unroll
+                        for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+                    *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
+                        uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+                }
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        buf ^= 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// band weight image: [nb][chunk][tap][cout 64][4 swizzled 16-B chunks] from w [npad][3][3][cin]
+__global__ __launch_bounds__(256) void det_pack_band_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ img,
+                                                          int npad, int cin) {
+    const int nck = cin / 32;
+    const long n = (long)npad * 9 * cin / 8;  // 16-B slots
+    for (long d = blockIdx.x * 256L + threadIdx.x; d < n; d += (long)gridDim.x * 256) {
+        const int q = (int)(d & 3);
+        const long r = d >> 2;                  // (nb, chunk, tap, co)
+        const int co = (int)(r % kBandBN);
+        const long r2 = r / kBandBN;
+        const int tp = (int)(r2 % 9);
+        const long r3 = r2 / 9;
+        const int c = (int)(r3 % nck), nb = (int)(r3 / nck);
+        const int kg = q ^ ((-(co >> 2)) & 3);
+        *reinterpret_cast<uint4*>(img + d * 8) = *reinterpret_cast<const uint4*>(
+            w + ((size_t)(nb * kBandBN + co) * 9 + tp) * cin + c * 32 + kg * 8);
+    }
+}
+
 // ------------------------------------------------------------------ channel attention
 // Channel means: kCaSplit workgroups per image each sum a contiguous pixel range (f32
 // per-thread partial sums, then an LDS tree) into part[n][split][C]; then one workgroup per
@@ -1086,9 +1256,43 @@ void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hi
     MVP_HIP(hipGetLastError());
 }
 
+bool det_band_eligible(int H, int W, int cin, int npad, int ks, int stride) {
+    return ks == 3 && stride == 1 && H == W && (W == 80 || W == 40) && cin % 32 == 0 && cin / 32 >= 3 &&
+           npad % kBandBN == 0;
+}
+
+void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, hipStream_t s) {
+    MVP_REQUIRE(npad % kBandBN == 0 && cin % 32 == 0, "det_pack_band_weights: npad %d, cin %d", npad, cin);
+    hipLaunchKernelGGL(det_pack_band_kernel, dim3(512), dim3(256), 0, s, w, img, npad, cin);
+    MVP_HIP(hipGetLastError());
+}
+
+namespace {
+int g_det_cus = 0;
+
+template <int W, int TR>
+void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
+    using C = BandCfg<W, TR>;
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)det_conv_band_kernel<W, TR>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
+        attr = true;
+    }
+    if (g_det_cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_det_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    // one workgroup per CU, a multiple of 8 (the XCD round robin of blockIdx)
+    const int grid = std::max(8, g_det_cus / 8 * 8);
+    hipLaunchKernelGGL((det_conv_band_kernel<W, TR>), dim3(grid), dim3(256), C::LDS, s, p, wband);
+}
+}  // namespace
+
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s, const uint16_t* wimg) {
+                          hipStream_t s, const uint16_t* wimg, const uint16_t* wband) {
     MVP_REQUIRE(cin % 32 == 0 && N % 4 == 0 && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
                 "det conv: cin=%d cout=%d strides %d/%d", cin, N, xs, ys);
     MVP_REQUIRE((ks == 1 && stride == 1) || (ks == 3 && (stride == 1 || stride == 2)), "det conv: ks %d stride %d", ks,
@@ -1103,6 +1307,22 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, H, W, Ho, Wo, wimg};
+    // band-halo kernel for the 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40
+    // planes (det_conv_band_kernel)
+    if (wband && det_band_eligible(H, W, cin, npad, ks, stride)) {
+        const char* e = getenv("MVPOSE_DET_BAND");  // tests: 0 = the im2col GEMM kernel
+        if (!(e && e[0] == '0')) {
+            if (n == 0) return;
+            GParams pb = p;
+            pb.n_nb = npad / kBandBN;
+            MVP_REQUIRE(pb.n_nb <= 32, "det band conv: %d cout blocks", pb.n_nb);  // <= workgroups per XCD
+            MVP_REQUIRE((long)n * H / (W == 80 ? 4 : 8) < (1L << 24), "det band conv: too many bands");
+            if (W == 80) launch_band<80, 4>(pb, wband, s);
+            else launch_band<40, 8>(pb, wband, s);
+            MVP_HIP(hipGetLastError());
+            return;
+        }
+    }
     // halo-tile kernel for the 32- and 64-channel 3x3/s1 convs (<= 64 couts): 14.03 -> 13.77
     // and 13.90 -> 13.86 ms per 64 frames against the im2col GEMM (same-box tools/det_ab.sh)
     if (ks == 3 && stride == 1 && (cin == 32 || cin == 64) && npad <= 64) {

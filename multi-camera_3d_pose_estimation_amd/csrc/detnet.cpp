@@ -24,7 +24,8 @@ struct DetNet {
     int64_t arena_bytes = 0;
     char* arena = nullptr;
     float* ca_scratch = nullptr;
-    std::vector<uint16_t*> wimg;  // per conv op: the GEMM kernel's weight image (owned)
+    std::vector<uint16_t*> wimg;   // per conv op: the GEMM kernel's weight image (owned)
+    std::vector<uint16_t*> wband;  // per band-eligible conv op: the band kernel's weight image (owned)
 };
 
 void free_det(DetNet& g) {
@@ -32,9 +33,12 @@ void free_det(DetNet& g) {
     if (g.ca_scratch) (void)hipFree(g.ca_scratch);
     for (uint16_t* p : g.wimg)
         if (p) (void)hipFree(p);
+    for (uint16_t* p : g.wband)
+        if (p) (void)hipFree(p);
     g.arena = nullptr;
     g.ca_scratch = nullptr;
     g.wimg.clear();
+    g.wband.clear();
 }
 
 int64_t per_image_bytes(const mvp_tensor_desc& t) { return (int64_t)t.h * t.w * t.c * 2; }
@@ -219,12 +223,18 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
         MVP_HIP(hipMalloc(&g->ca_scratch, (size_t)max_batch * 17 * g->max_ca * sizeof(float)));  // launch_det_ca scratch
         // conv weight images for the GEMM kernel (the blobs are not rewritten after create)
         g->wimg.assign(g->ops.size(), nullptr);
+        g->wband.assign(g->ops.size(), nullptr);
         for (size_t k = 0; k < g->ops.size(); k++) {
             const mvp_det_op& op = g->ops[k];
             if (op.kind != MVP_DET_CONV) continue;
             const int npad = mvp::det_cout_pad(op.out.c), K = op.ks * op.ks * op.in.c;
             MVP_HIP(hipMalloc(&g->wimg[k], (size_t)npad * K * sizeof(uint16_t)));
             mvp::det_pack_gemm_weights(w_dev + op.w_off, g->wimg[k], npad, K, nullptr);
+            const mvp_tensor_desc& xt = g->tensors[op.in.t];
+            if (mvp::det_band_eligible(xt.h, xt.w, op.in.c, npad, op.ks, op.stride)) {
+                MVP_HIP(hipMalloc(&g->wband[k], (size_t)npad * K * sizeof(uint16_t)));
+                mvp::det_pack_band_weights(w_dev + op.w_off, g->wband[k], npad, op.in.c, nullptr);
+            }
         }
         MVP_HIP(hipDeviceSynchronize());
     } catch (...) {
@@ -262,7 +272,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
                                      op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
                                      vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                     op.act, s, g->wimg[k]);
+                                     op.act, s, g->wimg[k], g->wband[k]);
                 break;
             }
             case MVP_DET_DW: {

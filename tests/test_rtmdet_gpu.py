@@ -132,6 +132,40 @@ def test_halo_rows_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
+def test_band_conv_vs_gemm(sd, monkeypatch):
+    """The 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40 planes run on the
+    band-halo kernel (det_conv_band_kernel, the default): each one, on the forward's own input,
+    against the im2col GEMM kernel (MVPOSE_DET_BAND=0).  K order (chunk, tap, channel) vs (tap,
+    chunk, channel): equal to f32 rounding, so the bf16 outputs agree to within a bf16 ulp where
+    the f32 sums straddle a rounding boundary (3 frames: the bands' XCD groups are uneven)."""
+    n = 3
+    det = D.RTMDetector(sd, max_batch=n, size=640)
+    spec = det.spec
+    frames = torch.from_numpy(_frames(n, 720, 1280, seed=9)).cuda()
+    det.run_ops(frames, 0, len(spec.ops))
+    torch.cuda.synchronize()
+    eligible = [k for k, op in enumerate(spec.ops)
+                if op.kind == D.DET_CONV and op.ks == 3 and op.stride == 1 and op.in_.c >= 96 and op.in_.c % 32 == 0
+                and spec.tensors[op.in_.t][0] in (80, 40) and (op.out.c + 31) // 32 * 32 % 64 == 0]
+    assert len(eligible) >= 15, eligible
+    for k in eligible:
+        op = spec.ops[k]
+        lo, hi = op.out.coff, op.out.coff + op.out.c
+        outs = []
+        for band in ("1", "0"):
+            monkeypatch.setenv("MVPOSE_DET_BAND", band)
+            det.run_ops(frames, k, k + 1)
+            torch.cuda.synchronize()
+            outs.append(det.tensor(op.out.t, n).float().cpu()[..., lo:hi])
+        a, b = outs
+        assert torch.isfinite(a).all(), spec.names[k]
+        diff = (a - b).abs()
+        ulp = b.abs() * 2 ** -7 + 1e-30
+        assert float((diff > ulp).float().mean()) == 0.0, (spec.names[k], float(diff.max()))
+        assert float((diff > 0).float().mean()) < 0.05, (spec.names[k], float((diff > 0).float().mean()))
+    det.close()
+
+
 @pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
 def test_head_staged_bitwise(sd, size, n, monkeypatch):
     """The head predictions with the [cls | reg] features staged through LDS
