@@ -631,6 +631,9 @@ struct BandCfg {
     static_assert(LDS <= 160 * 1024, "band: LDS budget");
 };
 
+// (Measured and dropped: a plane-major halo — [4 channel chunks][halo pixel] 16-B slots, tap
+// offsets as immediates, no swizzle, 16-B DMA pieces — 23.80 vs 23.32 ms per 128-frame forward,
+// gpurun_out/detband4: four times the DMA pieces cost more than the address arithmetic saved.)
 template <int W, int TR>
 __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const uint16_t* __restrict__ wband) {
     using C = BandCfg<W, TR>;
@@ -652,22 +655,36 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
     if (n_items == 0) return;
     const int steps = n_items * nck;
     auto item_tile = [&](int k) { return (k * ng + g) * 8 + xcd; };
-    // one step's DMA: chunk c of item k into buffer buf
-    auto issue = [&](int st, int buf) {
-        const int k = st / nck, c = st - k * nck;
+    // DMA of step st (chunk c of item k) into buffer buf, in 9 parts: part j = this wave's
+    // weight round j (9 per wave) and halo round j (<= 8 per wave).  The parts are issued one
+    // per tap in the middle of the previous step's MFMAs, so their address arithmetic rides in
+    // the MFMA shadow; the halo rounds use per-item source offsets (hoff, recomputed when the
+    // next step starts a new item: -1 = outside the frame, the zero region).
+    constexpr int HR = (C::B_R64 + 3) / 4;  // halo rounds per wave (the last wave may have one fewer)
+    static_assert(HR <= 9 && C::A_R64 == 36, "band: 9 DMA parts per wave");
+    int hoff[HR];
+    const uint16_t* xframe = p.x;
+    auto set_item = [&](int k) {
         const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
-        uint8_t* base = lds + buf * C::BUF;
-        const uint16_t* wsrc = wband + ((size_t)(nb * nck + c) * C::A_SLOTS) * 8;
-        for (int r = wave; r < C::A_R64; r += 4)
-            glds16_det(wsrc + (size_t)(r * 64 + lane) * 8, base + r * 64 * 16);
-        const uint16_t* xb = p.x + (size_t)n * p.H * W * p.xs + c * 32;
-        for (int r = wave; r < C::B_R64; r += 4) {
-            const int s2 = r * 64 + lane, hp = s2 >> 2, kq = (s2 & 3) ^ swz(hp);
+        xframe = p.x + (size_t)n * p.H * W * p.xs;
+#pragma unroll
+        for (int j = 0; j < HR; j++) {
+            const int s2 = (wave + 4 * j) * 64 + lane, hp = s2 >> 2, kq = (s2 & 3) ^ swz(hp);
             const int hy = hp / C::HWD, hx = hp - hy * C::HWD;
             const int gy = row0 + hy - 1, gx = hx - 1;
             const bool in = hp < C::HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)W;
-            const void* src = in ? (const void*)(xb + ((size_t)gy * W + gx) * p.xs + kq * 8)
-                                 : (const void*)(p.zero + (s2 & 1023) * 8);
+            hoff[j] = in ? (gy * W + gx) * p.xs + kq * 8 : -1;
+        }
+    };
+    auto issue_part = [&](int st, int buf, int j) {
+        const int k = st / nck, c = st - k * nck;
+        uint8_t* base = lds + buf * C::BUF;
+        const int r = wave + 4 * j;
+        glds16_det(wband + ((size_t)(nb * nck + c) * C::A_SLOTS + r * 64 + lane) * 8, base + r * 64 * 16);
+        if (j < HR && r < C::B_R64) {
+            const int s2 = r * 64 + lane;
+            const void* src = hoff[j] >= 0 ? (const void*)(xframe + hoff[j] + c * 32)
+                                           : (const void*)(p.zero + (s2 & 1023) * 8);
             glds16_det(src, base + (C::A_SLOTS + s2) * 16);
         }
     };
@@ -680,70 +697,103 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
         hb[i] = pr * C::HWD + pc;
     }
     f32x4 acc[FP][4];
-    issue(0, 0);
-    int buf = 0;
-    for (int st = 0; st < steps; st++) {
-        const int k = st / nck, c = st - k * nck;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step st (and stores)
-        __builtin_amdgcn_s_barrier();                         // every wave's; buffer buf ^ 1 is free
-        asm volatile("" ::: "memory");
-        if (st + 1 < steps) issue(st + 1, buf ^ 1);
-        if (c == 0) {
-#pragma unroll
-            for (int i = 0; i < FP; i++)
-#pragma unroll
-                for (int ct = 0; ct < 4; ct++) acc[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        const uint8_t* base = lds + buf * C::BUF;
-#pragma unroll
-        for (int tp = 0; tp < 9; tp++) {
-            const int toff = (tp / 3) * C::HWD + (tp % 3);
-            bf16x8 a[4], bb[FP];
+    // one chunk's 9 taps from LDS buffer `base`, with the DMA parts of step `nst` in its first
+    // taps (nst < 0: none); tap t + 1's fragments are read in the middle of tap t's MFMAs (two
+    // register sets).
+    auto compute = [&](const uint8_t* base, int nst, int nbuf) {
+        bf16x8 fa[2][4], fbv[2][FP];
+        auto load_a = [&](int tp, int sl) {
 #pragma unroll
             for (int ct = 0; ct < 4; ct++)
-                a[ct] = *reinterpret_cast<const bf16x8*>(base + (tp * 4 * kBandBN + ct * 64) * 16 + soffA);
+                fa[sl][ct] = *reinterpret_cast<const bf16x8*>(base + (tp * 4 * kBandBN + ct * 64) * 16 + soffA);
+        };
+        auto load_b = [&](int tp, int sl) {
+            const int toff = (tp / 3) * C::HWD + (tp % 3);
 #pragma unroll
             for (int i = 0; i < FP; i++) {
                 const int hp = hb[i] + toff;
-                bb[i] = *reinterpret_cast<const bf16x8*>(base + (C::A_SLOTS + hp * 4 + (kg ^ swz(hp))) * 16);
+                fbv[sl][i] = *reinterpret_cast<const bf16x8*>(base + (C::A_SLOTS + hp * 4 + (kg ^ swz(hp))) * 16);
             }
+        };
+        load_b(0, 0);
+        load_a(0, 0);
+        // per tap: 8 MFMAs, then tap t + 1's 9 fragment reads and this tap's DMA part, then the
+        // other 12 MFMAs: the compiler's wait before the next tap (it can only wait for every
+        // outstanding LDS read while LDS-DMA is in flight) then covers reads 12 MFMAs old
 #pragma unroll
-            for (int i = 0; i < FP; i++)
+        for (int tp = 0; tp < 9; tp++) {
+            const int sl = tp & 1;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 2; i++)
 #pragma unroll
                 for (int ct = 0; ct < 4; ct++)
-                    acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ct], bb[i], acc[i][ct], 0, 0, 0);
+                    acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sl][ct], fbv[sl][i], acc[i][ct], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (tp + 1 < 9) {
+                load_b(tp + 1, sl ^ 1);
+                load_a(tp + 1, sl ^ 1);
+            }
+            // the next step's DMA in the first 5 taps (2 parts each): it lands well before the
+            // step's vmcnt wait
+            if (nst >= 0 && 2 * tp < 9) issue_part(nst, nbuf, 2 * tp);
+            if (nst >= 0 && 2 * tp + 1 < 9) issue_part(nst, nbuf, 2 * tp + 1);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 2; i < FP; i++)
+#pragma unroll
+                for (int ct = 0; ct < 4; ct++)
+                    acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sl][ct], fbv[sl][i], acc[i][ct], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
-        if (c == nck - 1) {  // epilogue of item k: lane holds couts 16 ct + 4 kg + j of its pixel
-            const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
+    };
+    set_item(0);
 #pragma unroll
-            for (int ct = 0; ct < 4; ct++) {
-                const int co = nb * kBandBN + ct * 16 + kg * 4;
-                if (co >= p.N) continue;
-                const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
+    for (int j = 0; j < 9; j++) issue_part(0, 0, j);
+    int buf = 0, st = 0;
+    for (int k = 0; k < n_items; k++) {
 #pragma unroll
-                for (int i = 0; i < FP; i++) {
-                    const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
-                    const long m = ((long)n * p.H + row0 + pr) * W + pc;
-                    const f32x4 ac = acc[i][ct];
-                    float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
-                    if (p.act == 2)
+        for (int i = 0; i < FP; i++)
 #pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
-                    if (p.res) {
-                        const uint2 rr = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
-                        v[0] += bf(rr.x & 0xffff), v[1] += bf(rr.x >> 16), v[2] += bf(rr.y & 0xffff),
-                            v[3] += bf(rr.y >> 16);
-                    }
-                    if (p.act == 1)
+            for (int ct = 0; ct < 4; ct++) acc[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < nck; c++, st++) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step st (and stores)
+            __builtin_amdgcn_s_barrier();                         // every wave's; buffer buf ^ 1 is free
+            asm volatile("" ::: "memory");
+            const bool more = st + 1 < steps;
+            if (more && c + 1 == nck) set_item(k + 1);  // the next step starts item k + 1
+            compute(lds + buf * C::BUF, more ? st + 1 : -1, buf ^ 1);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            buf ^= 1;
+        }
+        // epilogue of item k: lane holds couts 16 ct + 4 kg + j of its pixel
+        const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
 #pragma unroll
-                        for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
-                    *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
-                        uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+        for (int ct = 0; ct < 4; ct++) {
+            const int co = nb * kBandBN + ct * 16 + kg * 4;
+            if (co >= p.N) continue;
+            const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
+#pragma unroll
+            for (int i = 0; i < FP; i++) {
+                const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
+                const long m = ((long)n * p.H + row0 + pr) * W + pc;
+                const f32x4 ac = acc[i][ct];
+                float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
+                if (p.act == 2)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+                if (p.res) {
+                    const uint2 rr = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                    v[0] += bf(rr.x & 0xffff), v[1] += bf(rr.x >> 16), v[2] += bf(rr.y & 0xffff),
+                        v[3] += bf(rr.y >> 16);
                 }
+                if (p.act == 1)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+                *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
+                    uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        buf ^= 1;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }

@@ -151,18 +151,20 @@ def test_band_conv_vs_gemm(sd, monkeypatch):
     for k in eligible:
         op = spec.ops[k]
         lo, hi = op.out.coff, op.out.coff + op.out.c
-        outs = []
-        for band in ("1", "0"):
+        outs = {}
+        for band in ("0", "1"):  # the GEMM kernel, the band kernel
             monkeypatch.setenv("MVPOSE_DET_BAND", band)
             det.run_ops(frames, k, k + 1)
             torch.cuda.synchronize()
-            outs.append(det.tensor(op.out.t, n).float().cpu()[..., lo:hi])
-        a, b = outs
-        assert torch.isfinite(a).all(), spec.names[k]
+            outs[band] = det.tensor(op.out.t, n).float().cpu()[..., lo:hi]
+        a, b = outs["1"], outs["0"]
+        finite = bool(torch.isfinite(a).all())
         diff = (a - b).abs()
-        ulp = b.abs() * 2 ** -7 + 1e-30
-        assert float((diff > ulp).float().mean()) == 0.0, (spec.names[k], float(diff.max()))
-        assert float((diff > 0).float().mean()) < 0.05, (spec.names[k], float((diff > 0).float().mean()))
+        scale = float(b.abs().max().clamp(min=1.0))
+        # a bf16 ulp of the value, or of the f32 sum's cancellation (terms ~ scale) near zero
+        n_bad = int((diff > b.abs() * 2 ** -7 + 2 ** -9 * scale).sum())
+        frac_diff = float((diff > 0).float().mean())
+        assert finite and n_bad == 0 and frac_diff < 0.05, (spec.names[k], n_bad, float(diff.max()), frac_diff)
     det.close()
 
 
