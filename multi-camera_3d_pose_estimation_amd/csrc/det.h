@@ -29,6 +29,7 @@ void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hi
 // The band-halo kernel (3x3/s1, >= 96 input channels, 80x80 / 40x40 planes, couts in blocks of 64):
 // whether a conv qualifies, and its weight image (same element count as w)
 bool det_band_eligible(int H, int W, int cin, int npad, int ks, int stride);
+int det_band_rows(int npad);  // cout rows of the band image (npad rounded up to the 64-cout blocks)
 void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, hipStream_t s);
 // channel attention in place; scratch: [n][17][C] f32 (per-split partial sums + scales)
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,

@@ -634,13 +634,18 @@ struct BandCfg {
 // (Measured and dropped: a plane-major halo — [4 channel chunks][halo pixel] 16-B slots, tap
 // offsets as immediates, no swizzle, 16-B DMA pieces — 23.80 vs 23.32 ms per 128-frame forward,
 // gpurun_out/detband4: four times the DMA pieces cost more than the address arithmetic saved.)
-template <int W, int TR>
-__global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const uint16_t* __restrict__ wband) {
+// NWV waves: 4 (one per SIMD, each 80 pixels x the 64 couts) or 8 (two per SIMD, each 80 pixels
+// x 32 couts: more LDS reads, but a second wave to hide each one's waits).
+template <int W, int TR, int NWV>
+__global__ __launch_bounds__(64 * NWV, 1) void det_conv_band_kernel(GParams p, const uint16_t* __restrict__ wband) {
     using C = BandCfg<W, TR>;
     constexpr int FP = C::FPW;
+    constexpr int CT = 4 * 4 / NWV;  // 16-cout tiles per wave
+    static_assert(NWV == 4 || NWV == 8, "band: 4 or 8 waves");
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave & 3, wc = wave >> 2;  // pixel group, cout group
     auto swz = [](int r) { return (-(r >> 2)) & 3; };
     // item assignment (see above): WG b on XCD b % 8, group g of n_nb consecutive slots
     const int n_nb = p.n_nb, nck = p.cin / 32;
@@ -660,8 +665,10 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
     // per tap in the middle of the previous step's MFMAs, so their address arithmetic rides in
     // the MFMA shadow; the halo rounds use per-item source offsets (hoff, recomputed when the
     // next step starts a new item: -1 = outside the frame, the zero region).
-    constexpr int HR = (C::B_R64 + 3) / 4;  // halo rounds per wave (the last wave may have one fewer)
-    static_assert(HR <= 9 && C::A_R64 == 36, "band: 9 DMA parts per wave");
+    constexpr int HR = (C::B_R64 + NWV - 1) / NWV;  // halo rounds per wave (some waves one fewer)
+    constexpr int AR = (C::A_R64 + NWV - 1) / NWV;  // weight rounds per wave (some waves one fewer)
+    constexpr int NPART = AR > HR ? AR : HR;         // DMA parts per wave and step
+    static_assert(NPART <= 9, "band: DMA parts");
     int hoff[HR];
     const uint16_t* xframe = p.x;
     auto set_item = [&](int k) {
@@ -669,7 +676,7 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
         xframe = p.x + (size_t)n * p.H * W * p.xs;
 #pragma unroll
         for (int j = 0; j < HR; j++) {
-            const int s2 = (wave + 4 * j) * 64 + lane, hp = s2 >> 2, kq = (s2 & 3) ^ swz(hp);
+            const int s2 = (wave + NWV * j) * 64 + lane, hp = s2 >> 2, kq = (s2 & 3) ^ swz(hp);
             const int hy = hp / C::HWD, hx = hp - hy * C::HWD;
             const int gy = row0 + hy - 1, gx = hx - 1;
             const bool in = hp < C::HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx < (unsigned)W;
@@ -679,8 +686,9 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
     auto issue_part = [&](int st, int buf, int j) {
         const int k = st / nck, c = st - k * nck;
         uint8_t* base = lds + buf * C::BUF;
-        const int r = wave + 4 * j;
-        glds16_det(wband + ((size_t)(nb * nck + c) * C::A_SLOTS + r * 64 + lane) * 8, base + r * 64 * 16);
+        const int r = wave + NWV * j;
+        if (j < AR && r < C::A_R64)
+            glds16_det(wband + ((size_t)(nb * nck + c) * C::A_SLOTS + r * 64 + lane) * 8, base + r * 64 * 16);
         if (j < HR && r < C::B_R64) {
             const int s2 = r * 64 + lane;
             const void* src = hoff[j] >= 0 ? (const void*)(xframe + hoff[j] + c * 32)
@@ -693,19 +701,20 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
     int hb[FP];  // halo index of tap (0, 0) for this lane's pixel of each fragment
 #pragma unroll
     for (int i = 0; i < FP; i++) {
-        const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
+        const int px = wp * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
         hb[i] = pr * C::HWD + pc;
     }
-    f32x4 acc[FP][4];
+    f32x4 acc[FP][CT];
     // one chunk's 9 taps from LDS buffer `base`, with the DMA parts of step `nst` in its first
     // taps (nst < 0: none); tap t + 1's fragments are read in the middle of tap t's MFMAs (two
     // register sets).
     auto compute = [&](const uint8_t* base, int nst, int nbuf) {
-        bf16x8 fa[2][4], fbv[2][FP];
+        bf16x8 fa[2][CT], fbv[2][FP];
         auto load_a = [&](int tp, int sl) {
 #pragma unroll
-            for (int ct = 0; ct < 4; ct++)
-                fa[sl][ct] = *reinterpret_cast<const bf16x8*>(base + (tp * 4 * kBandBN + ct * 64) * 16 + soffA);
+            for (int ct = 0; ct < CT; ct++)
+                fa[sl][ct] =
+                    *reinterpret_cast<const bf16x8*>(base + (tp * 4 * kBandBN + (wc * CT + ct) * 64) * 16 + soffA);
         };
         auto load_b = [&](int tp, int sl) {
             const int toff = (tp / 3) * C::HWD + (tp % 3);
@@ -727,7 +736,7 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
 #pragma unroll
             for (int i = 0; i < 2; i++)
 #pragma unroll
-                for (int ct = 0; ct < 4; ct++)
+                for (int ct = 0; ct < CT; ct++)
                     acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sl][ct], fbv[sl][i], acc[i][ct], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
             if (tp + 1 < 9) {
@@ -736,26 +745,30 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
             }
             // the next step's DMA in the first 5 taps (2 parts each): it lands well before the
             // step's vmcnt wait
-            if (nst >= 0 && 2 * tp < 9) issue_part(nst, nbuf, 2 * tp);
-            if (nst >= 0 && 2 * tp + 1 < 9) issue_part(nst, nbuf, 2 * tp + 1);
+            if constexpr (NPART > 5) {  // 2 parts per tap
+                if (nst >= 0 && 2 * tp < NPART) issue_part(nst, nbuf, 2 * tp);
+                if (nst >= 0 && 2 * tp + 1 < NPART) issue_part(nst, nbuf, 2 * tp + 1);
+            } else {
+                if (nst >= 0 && tp < NPART) issue_part(nst, nbuf, tp);
+            }
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int i = 2; i < FP; i++)
 #pragma unroll
-                for (int ct = 0; ct < 4; ct++)
+                for (int ct = 0; ct < CT; ct++)
                     acc[i][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[sl][ct], fbv[sl][i], acc[i][ct], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
         }
     };
     set_item(0);
 #pragma unroll
-    for (int j = 0; j < 9; j++) issue_part(0, 0, j);
+    for (int j = 0; j < NPART; j++) issue_part(0, 0, j);
     int buf = 0, st = 0;
     for (int k = 0; k < n_items; k++) {
 #pragma unroll
         for (int i = 0; i < FP; i++)
 #pragma unroll
-            for (int ct = 0; ct < 4; ct++) acc[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int ct = 0; ct < CT; ct++) acc[i][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
         for (int c = 0; c < nck; c++, st++) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of step st (and stores)
             __builtin_amdgcn_s_barrier();                         // every wave's; buffer buf ^ 1 is free
@@ -769,13 +782,13 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
         // epilogue of item k: lane holds couts 16 ct + 4 kg + j of its pixel
         const int t = item_tile(k), n = t / tpi, row0 = (t - n * tpi) * TR;
 #pragma unroll
-        for (int ct = 0; ct < 4; ct++) {
-            const int co = nb * kBandBN + ct * 16 + kg * 4;
+        for (int ct = 0; ct < CT; ct++) {
+            const int co = nb * kBandBN + (wc * CT + ct) * 16 + kg * 4;
             if (co >= p.N) continue;
             const float4 bv = *reinterpret_cast<const float4*>(p.bias + co);
 #pragma unroll
             for (int i = 0; i < FP; i++) {
-                const int px = wave * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
+                const int px = wp * (FP * 16) + i * 16 + r16, pr = px / W, pc = px - pr * W;
                 const long m = ((long)n * p.H + row0 + pr) * W + pc;
                 const f32x4 ac = acc[i][ct];
                 float v[4] = {ac[0] + bv.x, ac[1] + bv.y, ac[2] + bv.z, ac[3] + bv.w};
@@ -798,11 +811,13 @@ __global__ __launch_bounds__(256, 1) void det_conv_band_kernel(GParams p, const 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// band weight image: [nb][chunk][tap][cout 64][4 swizzled 16-B chunks] from w [npad][3][3][cin]
+// band weight image: [nb][chunk][tap][cout 64][4 swizzled 16-B chunks] from w [npad][3][3][cin];
+// couts past npad (the last block of a 96-cout conv) are zero rows
 __global__ __launch_bounds__(256) void det_pack_band_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ img,
                                                           int npad, int cin) {
     const int nck = cin / 32;
-    const long n = (long)npad * 9 * cin / 8;  // 16-B slots
+    const int rows = (npad + kBandBN - 1) / kBandBN * kBandBN;
+    const long n = (long)rows * 9 * cin / 8;  // 16-B slots
     for (long d = blockIdx.x * 256L + threadIdx.x; d < n; d += (long)gridDim.x * 256) {
         const int q = (int)(d & 3);
         const long r = d >> 2;                  // (nb, chunk, tap, co)
@@ -812,8 +827,10 @@ __global__ __launch_bounds__(256) void det_pack_band_kernel(const uint16_t* __re
         const long r3 = r2 / 9;
         const int c = (int)(r3 % nck), nb = (int)(r3 / nck);
         const int kg = q ^ ((-(co >> 2)) & 3);
-        *reinterpret_cast<uint4*>(img + d * 8) = *reinterpret_cast<const uint4*>(
-            w + ((size_t)(nb * kBandBN + co) * 9 + tp) * cin + c * 32 + kg * 8);
+        const int row = nb * kBandBN + co;
+        *reinterpret_cast<uint4*>(img + d * 8) =
+            row < npad ? *reinterpret_cast<const uint4*>(w + ((size_t)row * 9 + tp) * cin + c * 32 + kg * 8)
+                       : uint4{0u, 0u, 0u, 0u};
     }
 }
 
@@ -1308,11 +1325,13 @@ void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hi
 
 bool det_band_eligible(int H, int W, int cin, int npad, int ks, int stride) {
     return ks == 3 && stride == 1 && H == W && (W == 80 || W == 40) && cin % 32 == 0 && cin / 32 >= 3 &&
-           npad % kBandBN == 0;
+           npad % 32 == 0 && npad <= 32 * kBandBN;
 }
 
+int det_band_rows(int npad) { return (npad + kBandBN - 1) / kBandBN * kBandBN; }
+
 void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, hipStream_t s) {
-    MVP_REQUIRE(npad % kBandBN == 0 && cin % 32 == 0, "det_pack_band_weights: npad %d, cin %d", npad, cin);
+    MVP_REQUIRE(npad % 32 == 0 && cin % 32 == 0, "det_pack_band_weights: npad %d, cin %d", npad, cin);
     hipLaunchKernelGGL(det_pack_band_kernel, dim3(512), dim3(256), 0, s, w, img, npad, cin);
     MVP_HIP(hipGetLastError());
 }
@@ -1320,12 +1339,12 @@ void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, 
 namespace {
 int g_det_cus = 0;
 
-template <int W, int TR>
+template <int W, int TR, int NWV>
 void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
     using C = BandCfg<W, TR>;
     static bool attr = false;
     if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)det_conv_band_kernel<W, TR>,
+        MVP_HIP(hipFuncSetAttribute((const void*)det_conv_band_kernel<W, TR, NWV>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
         attr = true;
     }
@@ -1336,7 +1355,7 @@ void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
     }
     // one workgroup per CU, a multiple of 8 (the XCD round robin of blockIdx)
     const int grid = std::max(8, g_det_cus / 8 * 8);
-    hipLaunchKernelGGL((det_conv_band_kernel<W, TR>), dim3(grid), dim3(256), C::LDS, s, p, wband);
+    hipLaunchKernelGGL((det_conv_band_kernel<W, TR, NWV>), dim3(grid), dim3(64 * NWV), C::LDS, s, p, wband);
 }
 }  // namespace
 
@@ -1364,11 +1383,14 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
         if (!(e && e[0] == '0')) {
             if (n == 0) return;
             GParams pb = p;
-            pb.n_nb = npad / kBandBN;
+            pb.n_nb = det_band_rows(npad) / kBandBN;
             MVP_REQUIRE(pb.n_nb <= 32, "det band conv: %d cout blocks", pb.n_nb);  // <= workgroups per XCD
             MVP_REQUIRE((long)n * H / (W == 80 ? 4 : 8) < (1L << 24), "det band conv: too many bands");
-            if (W == 80) launch_band<80, 4>(pb, wband, s);
-            else launch_band<40, 8>(pb, wband, s);
+            // 8 waves (two per SIMD) by default: 22.30 vs 23.33 ms per 128-frame forward with 4
+            // (gpurun_out/detband5); MVPOSE_DET_BAND=4 keeps the 4-wave form (tests: bit-identical)
+            const bool w4 = e && e[0] == '4';
+            if (W == 80) w4 ? launch_band<80, 4, 4>(pb, wband, s) : launch_band<80, 4, 8>(pb, wband, s);
+            else w4 ? launch_band<40, 8, 4>(pb, wband, s) : launch_band<40, 8, 8>(pb, wband, s);
             MVP_HIP(hipGetLastError());
             return;
         }

@@ -232,7 +232,7 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
             mvp::det_pack_gemm_weights(w_dev + op.w_off, g->wimg[k], npad, K, nullptr);
             const mvp_tensor_desc& xt = g->tensors[op.in.t];
             if (mvp::det_band_eligible(xt.h, xt.w, op.in.c, npad, op.ks, op.stride)) {
-                MVP_HIP(hipMalloc(&g->wband[k], (size_t)npad * K * sizeof(uint16_t)));
+                MVP_HIP(hipMalloc(&g->wband[k], (size_t)mvp::det_band_rows(npad) * K * sizeof(uint16_t)));
                 mvp::det_pack_band_weights(w_dev + op.w_off, g->wband[k], npad, op.in.c, nullptr);
             }
         }
