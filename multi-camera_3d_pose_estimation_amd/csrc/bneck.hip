@@ -1,0 +1,423 @@
+// Streaming fused HRNet Bottleneck on layer1's 256-channel 64x48 plane (gfx950):
+//   y = relu( conv1x1(relu(conv3x3(relu(conv1x1(x, w1) + b1), w2) + b2), w3) + b3 + x )
+// (x, y: 256 ch; the two intermediates: 64 ch).  Layer1's blocks 2-4 ran as a 3x3 tconv
+// launch plus a Bottleneck join (conv3 + the next block's conv1, conv1x1_pair_kernel): per
+// block 0.4 GB of 64-ch intermediates were written and read back beside the 1.6 GB 256-ch
+// tensor's read and write (4.8 GB per 1,024 crops).  Here the block reads x once and writes y
+// once (3.2 GB); the intermediates live in LDS.
+//
+// * One workgroup per CU (8 waves) walks WHOLE crops top to bottom, two output rows per
+//   step.  x rows arrive by LDS-DMA into a 5-row ring (24 KiB per row) one step ahead of
+//   use; a row stays resident from conv1 (which reads it) to conv3 (whose residual it is),
+//   and conv3's output overwrites its residual in place, so the ring row is also the
+//   output's staging buffer: the next step stores it with whole-1-KiB coalesced writes and
+//   refills the slot with the DMA of a later row.
+// * Warp-specialised, weights in VGPRs for the launch.  Waves 0-3 (C13): conv1 (wave j:
+//   couts 16j..16j+15, 16x16x32 MFMAs over the row's 3 pixel tiles) into a 4-row ring of
+//   the 64-ch intermediate, then conv3 (wave j: couts 64j..64j+63) + b3 + residual + ReLU.
+//   Waves 4-7 (C2): conv2 on 32x32x16 MFMAs (wave 4 + gr: 32-cout group gr, fragments 0 and
+//   2 of the step's 96 pixels; waves 6-7: fragment 1), and the step's row stores and DMAs.
+//   Phases (one barrier each): P1 conv1 | stores + DMA, P2 conv2, P3 conv3.
+// * x ring rows are pixel-major (512 B per pixel) with the 16-B chunk index XOR-swizzled by
+//   the pixel (bn_swz): a DMA / store instruction moves 2 whole pixels (1 KiB contiguous in
+//   HBM), and both conv1's B-fragment reads and conv3's residual reads are conflict-free.
+//
+// Numerics (bit-identical to the unfused graph): conv1 sums K in the pair kernel's order
+// (perm = 1: its second GEMM's permuted chunks, the graph's Bottleneck-join path) or the
+// 1x1 kernel's (perm = 0), from 0, + b1, ReLU, bf16; conv2 = tconv_kernel's sequence
+// (accumulators start at b2; chunk, tap, 16-channel half), ReLU, bf16; conv3 = the pair
+// kernel's first GEMM (2 chunks from 0) + b3 + residual, ReLU, bf16.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "conv.h"
+#include "mfma_tile.h"
+#include "mvp_common.h"
+
+namespace mvp {
+namespace {
+
+using namespace mfma_tile;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct BN {
+    static constexpr int H = 64, W = 48, C = 256, M = 64;
+    static constexpr int XROW = W * C * 2;          // one x row: 24 KiB
+    static constexpr int NX = 5;                    // x ring rows
+    static constexpr int PIECES = XROW / 1024;      // 1-KiB DMA / store pieces per row (2 pixels each)
+    static constexpr int RS = W + 1;                // intermediate row pitch (slots; slot 48 is zero)
+    static constexpr int TR = 4;                    // intermediate ring rows
+    static constexpr int TPL = (1 + TR * RS) * 16;  // one 8-channel plane of the ring (leading zero slot)
+    static constexpr int TOFF = NX * XROW;
+    static constexpr int T2PL = 2 * W * 16;         // one 8-channel plane of conv2's output (2 rows)
+    static constexpr int T2OFF = TOFF + 8 * TPL;
+    static constexpr int BOFF = T2OFF + 8 * T2PL;   // conv2's 64 biases (f32)
+    static constexpr int LDS = BOFF + 64 * 4;
+    static constexpr int STEPS = H / 2;             // 2 output rows per step
+    static constexpr int KS = 36;                   // conv2 k-steps: 2 chunks x 9 taps x 2 halves
+    static_assert(LDS <= 160 * 1024, "LDS budget");
+    static_assert(7 * TPL + 32 < 65536 && 2 * 8192 + 256 < 65536, "ds_read offset range");
+};
+
+constexpr int wait_vm(int n) { return ((n >> 4) << 14) | 0x0F70 | (n & 15); }
+constexpr int kWaitLgkm0 = 0xC07F;
+
+__device__ __forceinline__ void barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// x-ring swizzle: chunk c16 of pixel p sits at slot p * 32 + ((c16 & 16) | ((c16 & 15) ^ bn_swz(p))).
+// ds_read_b128 serves lanes {0-3, 12-15, 20-27} (and the complementary set) together: conv1's
+// fragment lanes (pixel px, 16-channel group g) and conv3's residual lanes then hit 16
+// distinct bank groups for every chunk (mfma_tile.h, lane_rank).
+__device__ __forceinline__ int bn_swz(int p) {
+    const int x = p & 15;
+    return x < 4 ? x : x < 12 ? x + 4 : x - 8;
+}
+__device__ __forceinline__ int xoff(int p, int c16) { return p * 512 + ((c16 & 16) | ((c16 & 15) ^ bn_swz(p))) * 16; }
+// x ring slot of row r of crop-local index cl (rows of a workgroup's crops in stream order)
+__device__ __forceinline__ int xslot(int cl, int r) { return (cl * BN::H + r) % BN::NX; }
+
+struct BNParams {
+    const uint16_t* x;
+    const uint16_t* w1;
+    const float* b1;
+    const uint16_t* w2;
+    const float* b2;
+    const uint16_t* w3;
+    const float* b3;
+    uint16_t* y;
+    int N, perm;
+};
+
+// ------------------------------------------------------------------ C2 waves
+// Piece n = jw + 4m of a row holds pixels 2n, 2n + 1; lane -> (pixel 2n + (lane >> 5), chunk
+// c16): the element offset within the row is 512 m + lane_off(m & 1) (pixel & 15 depends on m's
+// parity only).
+__device__ __forceinline__ int piece_lane_off(int jw, int lane, int odd) {
+    const int px = 2 * jw + (lane >> 5), cs = lane & 31;  // pixel of piece jw (m = 0)
+    return px * BN::C + ((cs & 16) | ((cs & 15) ^ bn_swz(px + 8 * odd))) * 8;
+}
+
+// Row traffic of step s (x rows conv1 reads in it): rows 0-2 of the crop at its first step,
+// rows 2k+1, 2k+2 (< 64) after.  Wave jw moves pieces jw, jw + 4, ... of each row.
+__device__ __forceinline__ void dma_step(const BNParams& p, uint8_t* lds, int crop0, int s, int jw, int lane) {
+    const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
+    const int r0 = k == 0 ? 0 : 2 * k + 1, r1 = k == 0 ? 3 : min(2 * k + 3, BN::H);
+    const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
+    for (int r = r0; r < r1; r++) {
+        const uint16_t* src = p.x + ((long)(crop0 + cl) * BN::H + r) * BN::W * BN::C;
+        uint8_t* dst = lds + xslot(cl, r) * BN::XROW + jw * 1024;
+#pragma unroll
+        for (int m = 0; m < BN::PIECES / 4; m++) glds16(src + 2048 * m + ((m & 1) ? lo1 : lo0), dst + m * 4096);
+    }
+}
+
+// Stores of step s's output rows 2k, 2k+1 (staged in their x ring slots by conv3).
+__device__ __forceinline__ void store_step(const BNParams& p, const uint8_t* lds, int crop0, int s, int jw,
+                                           int lane) {
+    const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
+#pragma unroll 1
+    for (int rr = 0; rr < 2; rr++) {
+        const uint8_t* src = lds + xslot(cl, 2 * k + rr) * BN::XROW + lane * 16;
+        uint4 v[BN::PIECES / 4];
+#pragma unroll
+        for (int m = 0; m < BN::PIECES / 4; m++) v[m] = *reinterpret_cast<const uint4*>(src + (jw + 4 * m) * 1024);
+        uint16_t* dst = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rr) * BN::W * BN::C;
+        const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
+#pragma unroll
+        for (int m = 0; m < BN::PIECES / 4; m++)
+#ifdef BNECK_DIAG_NO_STORE  // timing harness only (no output)
+            if (v[m].x == 0x12345678u && v[m].y == 0x9abcdef0u)
+#endif
+            *reinterpret_cast<uint4*>(dst + 2048 * m + ((m & 1) ? lo1 : lo0)) = v[m];
+    }
+    // the slots are refilled by this wave's DMA next: its reads must have returned
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    asm volatile("" ::: "memory");
+}
+
+#ifndef BNECK_PF2
+#define BNECK_PF2 2
+#endif
+
+__device__ __forceinline__ void c2_role(const BNParams& p, uint8_t* lds, int jw, int lane, int crop0, int n_steps) {
+    constexpr int kPF = BNECK_PF2;
+    const int h = lane >> 5, r32 = lane & 31, gr = jw & 1, fr = jw >> 1;
+    // A fragments, k-step s = chunk * 18 + tap * 2 + half: W2[cout][tap][32 chunk + 16 half + 8h .. +7]
+    bf16x8 wa[BN::KS];
+    {
+        const int cout = gr * 32 + row_cout(r32);
+#pragma unroll
+        for (int s = 0; s < BN::KS; s++) {
+            const int c = s / 18, tap = (s % 18) >> 1, ks = s & 1;
+            wa[s] = *reinterpret_cast<const bf16x8*>(p.w2 + (cout * 9 + tap) * BN::M + c * 32 + ks * 16 + 8 * h);
+        }
+    }
+    // fragments of the step's 96 pixels (2 rows, row-major): waves 4-5 take 0 and 2, waves 6-7
+    // take 1 (their second fragment duplicates it: computed, never stored)
+    int fpp[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) fpp[t] = frag_pixel<BN::W, 2, 1>(fr == 0 ? 2 * t : 1, r32);
+    const bool pad1 = fr != 0;
+
+    dma_step(p, lds, crop0, 0, jw, lane);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    barrier();  // prologue: step 0's rows, the zeroed intermediate ring
+    for (int s = 0; s < n_steps; s++) {
+        // ---- P1: stores of step s-1, DMA of step s+1's rows (the conv1 waves compute)
+        if (s > 0) store_step(p, lds, crop0, s - 1, jw, lane);
+#ifndef BNECK_DIAG_NO_DMA  // timing harness only (stale rows, wrong results)
+        if (s + 1 < n_steps) dma_step(p, lds, crop0, s + 1, jw, lane);
+#endif
+        barrier();
+        // ---- P2: conv2 of rows 2k, 2k+1 from intermediate rows 2k-1 .. 2k+2
+        {
+            const int k = s % BN::STEPS;
+            int bv[2][3];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const int rho = fpp[t] / BN::W, x = fpp[t] - rho * BN::W;
+#pragma unroll
+                for (int dy = 0; dy < 3; dy++)
+                    bv[t][dy] = BN::TOFF + h * BN::TPL + (((2 * k + rho + dy) & 3) * BN::RS + x) * 16;  // + dx: column x + dx - 1
+            }
+            // accumulators start at the lane's 16 biases (couts 32gr + 16h ..), from LDS
+            f32x16 acc[2];
+            {
+                const float4* bq = reinterpret_cast<const float4*>(lds + BN::BOFF + (gr * 32 + 16 * h) * 4);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float4 b4 = bq[q];
+                    acc[0][4 * q] = b4.x;
+                    acc[0][4 * q + 1] = b4.y;
+                    acc[0][4 * q + 2] = b4.z;
+                    acc[0][4 * q + 3] = b4.w;
+                }
+                acc[1] = acc[0];
+            }
+            bf16x8 fb[kPF + 1][2];
+            auto load = [&](auto Ss) {
+                constexpr int st = Ss, c = st / 18, tap = (st % 18) >> 1, ks = st & 1;
+                constexpr int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+                for (int t = 0; t < 2; t++)
+                    fb[st % (kPF + 1)][t] =
+                        *reinterpret_cast<const bf16x8*>(lds + bv[t][dy] + ((4 * c + 2 * ks) * BN::TPL + dx * 16));
+            };
+            static_for<0, kPF>(load);
+            static_for<0, BN::KS>([&](auto Ss) {
+                constexpr int st = Ss;
+                if constexpr (st + kPF < BN::KS) load(std::integral_constant<int, st + kPF>{});
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int t = 0; t < 2; t++)
+                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[st], fb[st % (kPF + 1)][t], acc[t], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            });
+            // ReLU, bf16 -> conv2's output planes (lane: couts 32gr + 16h .. +15 of its pixel)
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                if (t == 1 && pad1) break;
+                uint32_t o[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) o[e] = pack_bf16x2(relu1(acc[t][2 * e]), relu1(acc[t][2 * e + 1]));
+                uint8_t* d = lds + BN::T2OFF + (4 * gr + 2 * h) * BN::T2PL + fpp[t] * 16;
+                *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
+                *reinterpret_cast<uint4*>(d + BN::T2PL) = uint4{o[4], o[5], o[6], o[7]};
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        barrier();
+        // ---- P3: the conv1/conv3 waves run conv3; this wave's DMA must land before the next step
+        __builtin_amdgcn_s_waitcnt(wait_vm(0));
+        barrier();
+    }
+    store_step(p, lds, crop0, n_steps - 1, jw, lane);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+}
+
+// ------------------------------------------------------------------ C13 waves
+__device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j, int lane, int n_steps) {
+    const int px = lane & 15, g = lane >> 4;
+    // conv1 A (row px -> cout 16j + px) and the lane's x-ring chunk offsets, chunk jc
+    bf16x8 w1f[8];
+    int xo[8];
+#pragma unroll
+    for (int jc = 0; jc < 8; jc++) {
+        const int c16 = p.perm ? 16 * (jc >> 2) + 4 * g + (jc & 3) : 4 * jc + g;
+        w1f[jc] = *reinterpret_cast<const bf16x8*>(p.w1 + (16 * j + px) * BN::C + c16 * 8);
+        xo[jc] = xoff(px, c16);
+    }
+    // conv3 A: tile ct row r -> cout 64j + 16 (r >> 2) + 4ct + (r & 3), so that lane group g owns
+    // couts 64j + 16g .. + 15 of its pixel across the 4 tiles
+    bf16x8 w3f[4][2];
+#pragma unroll
+    for (int ct = 0; ct < 4; ct++)
+#pragma unroll
+        for (int ch = 0; ch < 2; ch++) {
+            const int cout = 64 * j + 16 * (px >> 2) + 4 * ct + (px & 3);
+            w3f[ct][ch] = *reinterpret_cast<const bf16x8*>(p.w3 + cout * BN::M + ch * 32 + 8 * g);
+        }
+    float b1v[4], b3v[16];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b1v[i] = p.b1[16 * j + 4 * g + i];
+#pragma unroll
+    for (int i = 0; i < 16; i++) b3v[i] = p.b3[64 * j + 16 * g + i];
+    int ro[2];
+#pragma unroll
+    for (int e = 0; e < 2; e++) ro[e] = xoff(px, 8 * j + 2 * g + e);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+
+    // intermediate row r (-1 .. 64) of the current crop: ring row (r + 1) & 3
+    auto zero_row = [&](int r) {
+        const int pos = (r + 1) & 3;
+        for (int i = lane; i < 2 * BN::W; i += 64) {
+            const int q = 2 * j + (i >= BN::W), x = i - (i >= BN::W) * BN::W;
+            *reinterpret_cast<uint4*>(lds + BN::TOFF + q * BN::TPL + (1 + pos * BN::RS + x) * 16) =
+                uint4{0u, 0u, 0u, 0u};
+        }
+    };
+    auto conv1_row = [&](int cl, int r) {
+        const uint8_t* xb = lds + xslot(cl, r) * BN::XROW;
+        f32x4 acc[3];
+#pragma unroll
+        for (int t = 0; t < 3; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 b[8][3];
+#pragma unroll
+        for (int jc = 0; jc < 8; jc++)
+#pragma unroll
+            for (int t = 0; t < 3; t++) b[jc][t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc] + t * 8192);
+#pragma unroll
+        for (int jc = 0; jc < 8; jc++)
+#pragma unroll
+            for (int t = 0; t < 3; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[jc], b[jc][t], acc[t], 0, 0, 0);
+        const int pos = (r + 1) & 3;
+        uint8_t* d = lds + BN::TOFF + (2 * j + (g >> 1)) * BN::TPL + (1 + pos * BN::RS + px) * 16 + (g & 1) * 8;
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+            float v[4];
+#pragma unroll
+            for (int i = 0; i < 4; i++) v[i] = fmaxf(acc[t][i] + b1v[i], 0.f);
+            *reinterpret_cast<uint2*>(d + t * 256) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+        }
+    };
+
+    barrier();  // prologue
+    for (int s = 0; s < n_steps; s++) {
+        const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
+        // ---- P1: conv1 of intermediate rows 2k+1, 2k+2 (first step: -1 (zero), 0, 1, 2)
+        if (k == 0) {
+            zero_row(-1);
+            conv1_row(cl, 0);
+            conv1_row(cl, 1);
+            conv1_row(cl, 2);
+        } else {
+            conv1_row(cl, 2 * k + 1);
+            if (2 * k + 2 < BN::H)
+                conv1_row(cl, 2 * k + 2);
+            else
+                zero_row(BN::H);
+        }
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        barrier();
+        // ---- P2: conv2 (the C2 waves)
+        barrier();
+        // ---- P3: conv3 of rows 2k, 2k+1 + b3 + residual (x ring) + ReLU, in place over the residual
+#pragma unroll 1
+        for (int tt = 0; tt < 6; tt++) {
+            const int rho = tt >= 3, tc = tt - 3 * rho, pp = rho * BN::W + tc * 16 + px;
+            uint8_t* xr = lds + xslot(cl, 2 * k + rho) * BN::XROW + tc * 8192;
+            const uint4 r0 = *reinterpret_cast<const uint4*>(xr + ro[0]);
+            const uint4 r1 = *reinterpret_cast<const uint4*>(xr + ro[1]);
+            bf16x8 bch[2];
+#pragma unroll
+            for (int ch = 0; ch < 2; ch++)
+                bch[ch] = *reinterpret_cast<const bf16x8*>(lds + BN::T2OFF + (4 * ch + g) * BN::T2PL + pp * 16);
+            f32x4 acc[4];
+#pragma unroll
+            for (int ct = 0; ct < 4; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ch = 0; ch < 2; ch++)
+#pragma unroll
+                for (int ct = 0; ct < 4; ct++)
+                    acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[ct][ch], bch[ch], acc[ct], 0, 0, 0);
+            const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+            uint32_t o[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const int ct = q >> 1, i = 2 * (q & 1);
+                float v0 = acc[ct][i] + b3v[2 * q], v1 = acc[ct][i + 1] + b3v[2 * q + 1];
+                v0 += lo_bf16(rw[q]);
+                v1 += hi_bf16(rw[q]);
+                o[q] = pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+            }
+            *reinterpret_cast<uint4*>(xr + ro[0]) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(xr + ro[1]) = uint4{o[4], o[5], o[6], o[7]};
+        }
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        barrier();
+    }
+}
+
+__global__ __launch_bounds__(512, 1) void bneck_kernel(BNParams p) {
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int crop0 = (int)(((long)p.N * b) / nb), crop1 = (int)(((long)p.N * (b + 1)) / nb);
+    const int n_steps = (crop1 - crop0) * BN::STEPS;
+    if (n_steps == 0) return;  // whole workgroup: uniform
+    // the intermediate ring (its leading and pad slots stay zero)
+    for (int i = tid; i < 8 * BN::TPL / 16; i += 512)
+        *reinterpret_cast<uint4*>(lds + BN::TOFF + i * 16) = uint4{0u, 0u, 0u, 0u};
+    if (tid < 64) reinterpret_cast<float*>(lds + BN::BOFF)[tid] = p.b2[tid];
+    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+    if (wave < 4)
+        c13_role(p, lds, wave, lane, n_steps);
+    else
+        c2_role(p, lds, wave - 4, lane, crop0, n_steps);
+}
+
+int g_bn_cus = 0;
+
+}  // namespace
+
+bool bneck_supported(int H, int W, int C, int M) {
+    const char* e = getenv("MVPOSE_NO_BNECK");  // tests / A/B: the tconv + Bottleneck-join path
+    if (e && e[0] == '1') return false;
+    return H == BN::H && W == BN::W && C == BN::C && M == BN::M;
+}
+
+void launch_bneck(const BneckLaunch& c, hipStream_t s) {
+    MVP_REQUIRE(c.H == BN::H && c.W == BN::W, "bneck: plane %dx%d", c.H, c.W);
+    MVP_REQUIRE(c.N >= 0 && c.N < (1 << 24), "bneck: %d crops", c.N);
+    if (c.N == 0) return;
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)bneck_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, BN::LDS));
+        attr = true;
+    }
+    if (g_bn_cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_bn_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    BNParams p{c.x, c.w1, c.b1, c.w2, c.b2, c.w3, c.b3, c.y, c.N, c.perm ? 1 : 0};
+    const int grid = std::min(c.N, g_bn_cus);
+    hipLaunchKernelGGL(bneck_kernel, dim3(grid), dim3(512), BN::LDS, s, p);
+    MVP_HIP(hipGetLastError());
+}
+
+}  // namespace mvp

@@ -75,6 +75,27 @@ bool conv1x1_pair_supported(int cin_total, int cmid, int cout2);
 void launch_conv1x1_pair(const PairLaunch& p, hipStream_t s);
 
 
+// Streaming fused Bottleneck on layer1's 256-ch 64x48 plane (bneck.hip): y = relu(W3 ·
+// relu(conv3x3(relu(W1 · x + b1), W2) + b2) + b3 + x), W1 [64][256], W2 [64][3][3][64], W3
+// [256][64] bf16; the two 64-ch intermediates never leave LDS.  perm selects conv1's K order:
+// the Bottleneck join's (conv1x1_pair second GEMM, 1) or the plain 1x1 kernel's (0), so the
+// result is bit-identical to the unfused graph either way.  bneck_supported is false for
+// other shapes (or MVPOSE_NO_BNECK=1).
+struct BneckLaunch {
+    const uint16_t* x = nullptr;
+    const uint16_t* w1 = nullptr;
+    const float* b1 = nullptr;
+    const uint16_t* w2 = nullptr;
+    const float* b2 = nullptr;
+    const uint16_t* w3 = nullptr;
+    const float* b3 = nullptr;
+    uint16_t* y = nullptr;
+    int N = 0, H = 0, W = 0;
+    int perm = 1;
+};
+bool bneck_supported(int H, int W, int C, int M);
+void launch_bneck(const BneckLaunch& c, hipStream_t s);
+
 // Lean 3x3/s1 conv on 32x32x16 MFMAs for 384-pixel x 64-cout tiles (tconv.hip):
 // 64 ch @ 32x24 and 64x48, 128 ch @ 16x12, 256 ch @ 8x6 (ReLU epilogue).  false
 // when the conv is not one of those (or MVPOSE_NO_TCONV=1).

@@ -38,6 +38,9 @@ struct Graph {
     std::vector<uint16_t*> t16_w;       // tconv16 weight image of a 128/256-ch branch-plane conv (owned)
     std::vector<uint16_t*> tr_w;        // trans1 weight image of a twin-fused transition (owned)
     std::vector<int> head_src;          // heatmap head that also runs the (absorbed) fuse op head_src[k] (-1: none)
+    std::vector<int> bneck;             // Bottleneck conv3 whose (absorbed) conv1 bneck[k] and conv2 run in its launch (-1: none)
+    std::vector<int> bneck_mid;         // and its (absorbed) conv2
+    std::vector<int> bneck_perm;        // its conv1 sums K in the Bottleneck join's order (bneck.hip)
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -219,6 +222,62 @@ void pair_fuse(Graph& g, bool enable) {
         if (!conv1x1_pair_supported(cin, A.cout, B.cout)) continue;
         g.pair_tail[a] = b;
         g.absorbed[b] = 1;
+    }
+}
+
+// Bottleneck-fusion pass (bneck.hip): layer1's Bottleneck on the 256-ch 64x48 plane — conv1
+// (1x1 256 -> 64, ReLU), conv2 (3x3 64 -> 64, ReLU), conv3 (1x1 64 -> 256, + the block's
+// input, ReLU), intermediates read by nothing else — runs as one streaming launch; the two
+// 64-ch intermediates are never allocated.  Runs before pair_fuse (which would otherwise join
+// conv1 to the previous block's conv3); conv1 keeps the K order the join would have given it
+// (bneck_perm) so the result stays bit-identical to the unfused graph.
+void bneck_fuse(Graph& g, bool enable, bool pair_enabled) {
+    const int no = (int)g.ops.size(), nt = (int)g.tensors.size();
+    g.bneck.assign(no, -1);
+    g.bneck_mid.assign(no, -1);
+    g.bneck_perm.assign(no, 0);
+    if (!enable) return;
+    std::vector<int> uses(nt, 0), producer(nt, -1);
+    for (int k = 0; k < no; k++) {
+        const mvp_op_desc& op = g.ops[k];
+        producer[op.out] = k;
+        for (int i = 0; i < op.n_in; i++)
+            if (op.in[i] >= 0 && !(g.block_head[k] && i == 0)) uses[op.in[i]]++;
+    }
+    auto conv = [&](int k, int ks, int cin, int cout) {
+        if (k < 0 || g.absorbed[k] || g.block_head[k] || g.cat_src[k] >= 0) return false;
+        const mvp_op_desc& op = g.ops[k];
+        return op.kind == MVP_OP_CONV && op.ks == ks && op.stride == 1 && op.relu && op.cin == cin &&
+               op.cout == cout && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
+    };
+    auto no_res = [&](int k) { return g.ops[k].n_in < 2 || g.ops[k].in[1] < 0; };
+    for (int c = 0; c < no; c++) {
+        if (!conv(c, 1, 64, 256) || no_res(c)) continue;
+        const mvp_op_desc& C = g.ops[c];
+        const int b = producer[C.in[0]];
+        if (!conv(b, 3, 64, 64) || !no_res(b) || uses[g.ops[b].out] != 1) continue;
+        const int a = producer[g.ops[b].in[0]];
+        if (!conv(a, 1, 256, 64) || !no_res(a) || uses[g.ops[a].out] != 1) continue;
+        const mvp_op_desc& A = g.ops[a];
+        if (A.in[0] != C.in[1] || A.segment != C.segment || g.ops[b].segment != C.segment) continue;
+        if (g.ops[b].out == g.output || A.out == g.output) continue;
+        const mvp_tensor_desc& x = g.tensors[A.in[0]];
+        if (!bneck_supported(x.h, x.w, x.c, A.cout)) continue;
+        // would pair_fuse have joined conv1 to its producer (a 1x1 256-cout ReLU conv)?
+        int perm = 0;
+        const int f = producer[A.in[0]];
+        if (pair_enabled && f >= 0 && !g.absorbed[f] && !g.block_head[f]) {
+            const mvp_op_desc& F = g.ops[f];
+            const int cin = F.cin + (g.cat_src[f] >= 0 ? g.ops[g.cat_src[f]].cin : 0);
+            perm = F.kind == MVP_OP_CONV && F.ks == 1 && F.stride == 1 && F.relu && F.cout == 256 &&
+                   F.segment == A.segment && g.tensors[F.out].dtype == MVP_DT_BF16_NHWC &&
+                   conv1x1_pair_supported(cin, 256, 64);
+        }
+        g.absorbed[a] = 1;
+        g.absorbed[b] = 1;
+        g.bneck[c] = a;
+        g.bneck_mid[c] = b;
+        g.bneck_perm[c] = perm;
     }
 }
 
@@ -409,7 +468,7 @@ void cat_fill(Graph& g) {
 // Weight images of the convs tconv16.hip serves (alloc at create, refilled with the blobs).
 long t16_elems(const Graph& g, int k) {
     const mvp_op_desc& op = g.ops[k];
-    if (op.kind != MVP_OP_CONV || g.absorbed[k] || g.cat_src[k] >= 0 || g.pair_tail[k] >= 0 ||
+    if (op.kind != MVP_OP_CONV || g.absorbed[k] || g.cat_src[k] >= 0 || g.pair_tail[k] >= 0 || g.bneck[k] >= 0 ||
         (op.stride == 1 && !op.relu) || g.tensors[op.out].dtype == MVP_DT_F32_NCHW || !g.sib[k].empty() ||
         g.twin[k] >= 0 || g.stem_head[k] >= 0)
         return 0;
@@ -483,6 +542,7 @@ void plan(Graph& g) {
             if (g.stem_head[k] >= 0 && i == 0) continue;                 // fused stem: LDS-only
             if (g.head_src[k] >= 0 && i == 0) continue;                  // fused head: never materialised
             if (g.cat_src[k] >= 0 && i == 1) continue;                  // cat-fused: never materialised
+            if (g.bneck[k] >= 0 && i == 0) continue;                     // fused Bottleneck: LDS-only
             last[op.in[i]] = std::max(last[op.in[i]], k);
             touch(op.in[i]);
         }
@@ -544,7 +604,7 @@ void plan(Graph& g) {
         widen(op.out);
         for (int i = 0; i < op.n_in; i++)
             if (!(g.block_head[k] && i == 0) && !(g.cat_src[k] >= 0 && i == 1) && !(g.stem_head[k] >= 0 && i == 0) &&
-                !(g.head_src[k] >= 0 && i == 0))
+                !(g.head_src[k] >= 0 && i == 0) && !(g.bneck[k] >= 0 && i == 0))
                 widen(op.in[i]);
         if (g.head_src[k] >= 0)
             for (int i = 0; i < g.ops[g.head_src[k]].n_in; i++) widen(g.ops[g.head_src[k]].in[i]);
@@ -625,7 +685,9 @@ extern "C" int mvp_graph_create(const mvp_tensor_desc* tensors, int n_tensors, c
         const char* nc = getenv("MVPOSE_NO_CATFUSE");  // diagnostics: keep the downsample conv separate
         mvp::cat_fuse(*g, !(nc && nc[0] == '1') && !(nf && nf[0] == '1'));
         const char* np = getenv("MVPOSE_NO_PAIRFUSE");  // diagnostics: keep conv3 / next conv1 apart
-        mvp::pair_fuse(*g, !(np && np[0] == '1') && !(nf && nf[0] == '1'));
+        const bool pair_on = !(np && np[0] == '1') && !(nf && nf[0] == '1');
+        mvp::bneck_fuse(*g, !(nf && nf[0] == '1'), pair_on && mvp::conv1x1_pair_supported(64, 256, 64));
+        mvp::pair_fuse(*g, pair_on);
         mvp::stem_fuse(*g, !(nf && nf[0] == '1'));
         mvp::twin_fuse(*g, !(nf && nf[0] == '1'));
         mvp::sib_fuse(*g, !(nf && nf[0] == '1'));
@@ -716,6 +778,26 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
             for (int i = 0; i < f.n_in; i++) ins[i] = (const uint16_t*)ptr(f.in[i]);
             mvp::launch_head_fuse(ins, f.up, f.n_in, f.relu, g->wb + op.w_off, g->fb + op.b_off, (float*)ptr(op.out),
                                   nb, fo.h, fo.w, s);
+            return;
+        }
+        if (g->bneck[k] >= 0) {  // the whole Bottleneck: conv1 + conv2 (absorbed) + this conv3
+            const mvp_op_desc& a = g->ops[g->bneck[k]];
+            const mvp_op_desc& c2 = g->ops[g->bneck_mid[k]];
+            const mvp_tensor_desc& x = g->tensors[op.in[1]];
+            mvp::BneckLaunch bl;
+            bl.x = (const uint16_t*)ptr(op.in[1]);
+            bl.w1 = g->wb + a.w_off;
+            bl.b1 = g->fb + a.b_off;
+            bl.w2 = g->wb + c2.w_off;
+            bl.b2 = g->fb + c2.b_off;
+            bl.w3 = g->wb + op.w_off;
+            bl.b3 = g->fb + op.b_off;
+            bl.y = (uint16_t*)ptr(op.out);
+            bl.N = nb;
+            bl.H = x.h;
+            bl.W = x.w;
+            bl.perm = g->bneck_perm[k];
+            mvp::launch_bneck(bl, s);
             return;
         }
         if (g->stem_head[k] >= 0) {  // stem conv1 + this conv2 in one launch

@@ -404,6 +404,39 @@ def join_spec(h: int, w: int, seed: int = 0, cat: bool = False):
     return g, x, out, sd
 
 
+def bottleneck_spec(seed: int = 0, n_blocks: int = 4, lead: bool = True):
+    """HRNet-W32 layer1 on the 64x48 plane: n_blocks Bottlenecks (1x1 -> 64 + ReLU, 3x3 64 -> 64
+    + ReLU, 1x1 -> 256 + identity + ReLU).  lead=True: the first block takes a 64-ch input with
+    its 1x1 downsample as the identity (HRNet's layer1.0, whose conv3 the graph cat-fuses), the
+    rest run on 256 ch; lead=False: every block on a 256-ch input.  For kernel tests.
+    Returns (spec, input id, output id, state dict)."""
+    gen = torch.Generator().manual_seed(seed)
+    sd = {}
+
+    def mk(name, co, ci, k):
+        sd[f"{name}.weight"] = torch.randn((co, ci, k, k), generator=gen) * (2.0 / (k * k * ci)) ** 0.5
+        sd[f"{name}bn.weight"] = 1.0 + 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{name}bn.bias"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{name}bn.running_mean"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{name}bn.running_var"] = 1.0 + 0.2 * torch.rand((co,), generator=gen)
+
+    g = GraphSpec()
+    x_in = x = g.tensor(64, 48, 64 if lead else 256)
+    for b in range(n_blocks):
+        first = lead and b == 0
+        cin = 64 if first else 256
+        mk(f"b{b}.conv1", 64, cin, 1)
+        mk(f"b{b}.conv2", 64, 64, 3)
+        mk(f"b{b}.conv3", 256, 64, 1)
+        if first:
+            mk(f"b{b}.ds", 256, 64, 1)
+        idn = g.conv(sd, f"b{b}.ds", f"b{b}.dsbn", x, 1, False) if first else x
+        y = g.conv(sd, f"b{b}.conv1", f"b{b}.conv1bn", x, 1, True)
+        y = g.conv(sd, f"b{b}.conv2", f"b{b}.conv2bn", y, 1, True)
+        x = g.conv(sd, f"b{b}.conv3", f"b{b}.conv3bn", y, 1, True, res=idn)
+    return g, x_in, x, sd
+
+
 def stem_spec(seed: int = 0):
     """HRNet's stem on a 256x192 crop: conv1 (3x3/s2 4 -> 64) and conv2 (3x3/s2 64 -> 64),
     BN + ReLU each (the pattern the graph's stem-fusion pass runs as one launch), for
