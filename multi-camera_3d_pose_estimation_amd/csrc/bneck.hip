@@ -52,8 +52,8 @@ struct BN {
     static constexpr int TOFF = NX * XROW;
     static constexpr int T2PL = 2 * W * 16;         // one 8-channel plane of conv2's output (2 rows)
     static constexpr int T2OFF = TOFF + 8 * TPL;
-    static constexpr int BOFF = T2OFF + 8 * T2PL;   // conv2's 64 biases (f32)
-    static constexpr int LDS = BOFF + 64 * 4;
+    static constexpr int BOFF = T2OFF + 8 * T2PL;   // biases (f32): conv2's 64 | conv1's 64 | conv3's 256
+    static constexpr int LDS = BOFF + (64 + 64 + 256) * 4;
     static constexpr int STEPS = H / 2;             // 2 output rows per step
     static constexpr int KS = 36;                   // conv2 k-steps: 2 chunks x 9 taps x 2 halves
     static_assert(LDS <= 160 * 1024, "LDS budget");
@@ -86,8 +86,36 @@ __device__ __forceinline__ int bn_swz(int p) {
     return x < 4 ? x : x < 12 ? x + 4 : x - 8;
 }
 __device__ __forceinline__ int xoff(int p, int c16) { return p * 512 + ((c16 & 16) | ((c16 & 15) ^ bn_swz(p))) * 16; }
+// The row DMA as raw instructions: through the builtin, the compiler treats the LDS-DMA as an
+// LDS store of unknown extent and waits for it (vmcnt(0)) before the next LDS read, which put
+// the whole DMA latency in front of conv2.  The ring protocol orders it instead: a slot is
+// refilled only after the barrier that retired its readers, and published by the explicit
+// vmcnt wait before the barrier that precedes its next reader.  lds_off: byte offset in the
+// dynamic LDS (the kernel has no static LDS), wave-uniform; lane i writes lds_off + 16 i.
+__device__ __forceinline__ void glds16_ring(const void* src, uint32_t lds_off) {
+    uint32_t saved;  // m0 is the compiler's: restored after the issue (the DMA reads it at issue)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "v"(src), "s"(lds_off)
+        : "memory");
+}
+
 // x ring slot of row r of crop-local index cl (rows of a workgroup's crops in stream order)
 __device__ __forceinline__ int xslot(int cl, int r) { return (cl * BN::H + r) % BN::NX; }
+
+#ifdef BNECK_STAMPS  // timing harness (tools/bneck_stamps.py): workgroup 0's phase times, in y
+#define BN_STAMP(s, b)                                                                                     \
+    do {                                                                                                   \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                       \
+        if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (s) < 128)                                       \
+            reinterpret_cast<unsigned long long*>(p.y)[((threadIdx.x >> 6) * 128 + (s)) * 8 + (b)] = t_; \
+    } while (0)
+#else
+#define BN_STAMP(s, b) \
+    do {               \
+    } while (0)
+#endif
 
 struct BNParams {
     const uint16_t* x;
@@ -110,42 +138,25 @@ __device__ __forceinline__ int piece_lane_off(int jw, int lane, int odd) {
     return px * BN::C + ((cs & 16) | ((cs & 15) ^ bn_swz(px + 8 * odd))) * 8;
 }
 
+// x rows conv1 reads in step s (all but the first of a crop: 2, the crop's last: 1)
+__device__ __forceinline__ int step_rows(int s) {
+    const int k = s % BN::STEPS;
+    return k == 0 ? 3 : k == BN::STEPS - 1 ? 1 : 2;
+}
+
 // Row traffic of step s (x rows conv1 reads in it): rows 0-2 of the crop at its first step,
 // rows 2k+1, 2k+2 (< 64) after.  Wave jw moves pieces jw, jw + 4, ... of each row.
-__device__ __forceinline__ void dma_step(const BNParams& p, uint8_t* lds, int crop0, int s, int jw, int lane) {
+__device__ __forceinline__ void dma_step(const BNParams& p, int crop0, int s, int jw, int lane) {
     const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
     const int r0 = k == 0 ? 0 : 2 * k + 1, r1 = k == 0 ? 3 : min(2 * k + 3, BN::H);
     const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
     for (int r = r0; r < r1; r++) {
         const uint16_t* src = p.x + ((long)(crop0 + cl) * BN::H + r) * BN::W * BN::C;
-        uint8_t* dst = lds + xslot(cl, r) * BN::XROW + jw * 1024;
-#pragma unroll
-        for (int m = 0; m < BN::PIECES / 4; m++) glds16(src + 2048 * m + ((m & 1) ? lo1 : lo0), dst + m * 4096);
-    }
-}
-
-// Stores of step s's output rows 2k, 2k+1 (staged in their x ring slots by conv3).
-__device__ __forceinline__ void store_step(const BNParams& p, const uint8_t* lds, int crop0, int s, int jw,
-                                           int lane) {
-    const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
-#pragma unroll 1
-    for (int rr = 0; rr < 2; rr++) {
-        const uint8_t* src = lds + xslot(cl, 2 * k + rr) * BN::XROW + lane * 16;
-        uint4 v[BN::PIECES / 4];
-#pragma unroll
-        for (int m = 0; m < BN::PIECES / 4; m++) v[m] = *reinterpret_cast<const uint4*>(src + (jw + 4 * m) * 1024);
-        uint16_t* dst = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rr) * BN::W * BN::C;
-        const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
+        const uint32_t dst = xslot(cl, r) * BN::XROW + jw * 1024;
 #pragma unroll
         for (int m = 0; m < BN::PIECES / 4; m++)
-#ifdef BNECK_DIAG_NO_STORE  // timing harness only (no output)
-            if (v[m].x == 0x12345678u && v[m].y == 0x9abcdef0u)
-#endif
-            *reinterpret_cast<uint4*>(dst + 2048 * m + ((m & 1) ? lo1 : lo0)) = v[m];
+            glds16_ring(src + 2048 * m + ((m & 1) ? lo1 : lo0), __builtin_amdgcn_readfirstlane(dst + m * 4096));
     }
-    // the slots are refilled by this wave's DMA next: its reads must have returned
-    __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-    asm volatile("" ::: "memory");
 }
 
 #ifndef BNECK_PF2
@@ -165,182 +176,199 @@ __device__ __forceinline__ void c2_role(const BNParams& p, uint8_t* lds, int jw,
             wa[s] = *reinterpret_cast<const bf16x8*>(p.w2 + (cout * 9 + tap) * BN::M + c * 32 + ks * 16 + 8 * h);
         }
     }
-    // fragments of the step's 96 pixels (2 rows, row-major): waves 4-5 take 0 and 2, waves 6-7
-    // take 1 (their second fragment duplicates it: computed, never stored)
+    // fragments of the step's 96 pixels (2 rows, row-major): waves 4-5 take 0 and 2, waves 6-7 take 1
     int fpp[2];
 #pragma unroll
     for (int t = 0; t < 2; t++) fpp[t] = frag_pixel<BN::W, 2, 1>(fr == 0 ? 2 * t : 1, r32);
-    const bool pad1 = fr != 0;
 
-    dma_step(p, lds, crop0, 0, jw, lane);
-    __builtin_amdgcn_s_waitcnt(wait_vm(0));
-    barrier();  // prologue: step 0's rows, the zeroed intermediate ring
-    for (int s = 0; s < n_steps; s++) {
-        // ---- P1: stores of step s-1, DMA of step s+1's rows (the conv1 waves compute)
-        if (s > 0) store_step(p, lds, crop0, s - 1, jw, lane);
-#ifndef BNECK_DIAG_NO_DMA  // timing harness only (stale rows, wrong results)
-        if (s + 1 < n_steps) dma_step(p, lds, crop0, s + 1, jw, lane);
-#endif
-        barrier();
-        // ---- P2: conv2 of rows 2k, 2k+1 from intermediate rows 2k-1 .. 2k+2
-        {
-            const int k = s % BN::STEPS;
-            int bv[2][3];
+    // conv2 of step k's rows: NF fragments (waves 4-5: 0 and 2; waves 6-7: 1)
+    auto conv2 = [&](auto nf_tag, int k) {
+        constexpr int NF = decltype(nf_tag)::value;
+        int bv[NF][3];
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-                const int rho = fpp[t] / BN::W, x = fpp[t] - rho * BN::W;
+        for (int t = 0; t < NF; t++) {
+            const int rho = fpp[t] / BN::W, x = fpp[t] - rho * BN::W;
 #pragma unroll
-                for (int dy = 0; dy < 3; dy++)
-                    bv[t][dy] = BN::TOFF + h * BN::TPL + (((2 * k + rho + dy) & 3) * BN::RS + x) * 16;  // + dx: column x + dx - 1
-            }
-            // accumulators start at the lane's 16 biases (couts 32gr + 16h ..), from LDS
-            f32x16 acc[2];
-            {
-                const float4* bq = reinterpret_cast<const float4*>(lds + BN::BOFF + (gr * 32 + 16 * h) * 4);
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    const float4 b4 = bq[q];
-                    acc[0][4 * q] = b4.x;
-                    acc[0][4 * q + 1] = b4.y;
-                    acc[0][4 * q + 2] = b4.z;
-                    acc[0][4 * q + 3] = b4.w;
-                }
-                acc[1] = acc[0];
-            }
-            bf16x8 fb[kPF + 1][2];
-            auto load = [&](auto Ss) {
-                constexpr int st = Ss, c = st / 18, tap = (st % 18) >> 1, ks = st & 1;
-                constexpr int dy = tap / 3, dx = tap % 3;
-#pragma unroll
-                for (int t = 0; t < 2; t++)
-                    fb[st % (kPF + 1)][t] =
-                        *reinterpret_cast<const bf16x8*>(lds + bv[t][dy] + ((4 * c + 2 * ks) * BN::TPL + dx * 16));
-            };
-            static_for<0, kPF>(load);
-            static_for<0, BN::KS>([&](auto Ss) {
-                constexpr int st = Ss;
-                if constexpr (st + kPF < BN::KS) load(std::integral_constant<int, st + kPF>{});
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < 2; t++)
-                    acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[st], fb[st % (kPF + 1)][t], acc[t], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-            });
-            // ReLU, bf16 -> conv2's output planes (lane: couts 32gr + 16h .. +15 of its pixel)
-#pragma unroll
-            for (int t = 0; t < 2; t++) {
-                if (t == 1 && pad1) break;
-                uint32_t o[8];
-#pragma unroll
-                for (int e = 0; e < 8; e++) o[e] = pack_bf16x2(relu1(acc[t][2 * e]), relu1(acc[t][2 * e + 1]));
-                uint8_t* d = lds + BN::T2OFF + (4 * gr + 2 * h) * BN::T2PL + fpp[t] * 16;
-                *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
-                *reinterpret_cast<uint4*>(d + BN::T2PL) = uint4{o[4], o[5], o[6], o[7]};
-            }
+            for (int dy = 0; dy < 3; dy++)  // + dx * 16: column x + dx - 1
+                bv[t][dy] = BN::TOFF + h * BN::TPL + (((2 * k + rho + dy) & 3) * BN::RS + x) * 16;
         }
-        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        // accumulators start at the lane's 16 biases (couts 32gr + 16h ..), from LDS
+        f32x16 acc[NF];
+        {
+            const float4* bq = reinterpret_cast<const float4*>(lds + BN::BOFF + (gr * 32 + 16 * h) * 4);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float4 b4 = bq[q];
+                acc[0][4 * q] = b4.x;
+                acc[0][4 * q + 1] = b4.y;
+                acc[0][4 * q + 2] = b4.z;
+                acc[0][4 * q + 3] = b4.w;
+            }
+#pragma unroll
+            for (int t = 1; t < NF; t++) acc[t] = acc[0];
+        }
+        bf16x8 fb[kPF + 1][NF];
+        auto load = [&](auto Ss) {
+            constexpr int st = Ss, c = st / 18, tap = (st % 18) >> 1, ks = st & 1;
+            constexpr int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+            for (int t = 0; t < NF; t++)
+                fb[st % (kPF + 1)][t] =
+                    *reinterpret_cast<const bf16x8*>(lds + bv[t][dy] + ((4 * c + 2 * ks) * BN::TPL + dx * 16));
+        };
+        static_for<0, kPF>(load);
+        static_for<0, BN::KS>([&](auto Ss) {
+            constexpr int st = Ss;
+            if constexpr (st + kPF < BN::KS) load(std::integral_constant<int, st + kPF>{});
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int t = 0; t < NF; t++)
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[st], fb[st % (kPF + 1)][t], acc[t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+        // ReLU, bf16 -> conv2's output planes (lane: couts 32gr + 16h .. +15 of its pixel)
+#pragma unroll
+        for (int t = 0; t < NF; t++) {
+            uint32_t o[8];
+#pragma unroll
+            for (int e = 0; e < 8; e++) o[e] = pack_bf16x2(relu1(acc[t][2 * e]), relu1(acc[t][2 * e + 1]));
+            uint8_t* d = lds + BN::T2OFF + (4 * gr + 2 * h) * BN::T2PL + fpp[t] * 16;
+            *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(d + BN::T2PL) = uint4{o[4], o[5], o[6], o[7]};
+        }
+    };
+
+    dma_step(p, crop0, 0, jw, lane);
+    if (n_steps > 1) dma_step(p, crop0, 1, jw, lane);
+    __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    barrier();  // prologue: steps 0 and 1's rows, the zeroed intermediate ring
+    for (int s = 0; s < n_steps; s++) {
+        BN_STAMP(s, 0);
+        // ---- P1: the conv1 waves read step s's rows
         barrier();
-        // ---- P3: the conv1/conv3 waves run conv3; this wave's DMA must land before the next step
-        __builtin_amdgcn_s_waitcnt(wait_vm(0));
+        BN_STAMP(s, 2);
+        // ---- P2: conv2 of rows 2k, 2k+1 from intermediate rows 2k-1 .. 2k+2 (the conv1/conv3
+        // waves issue the row DMAs meanwhile)
+        if (fr == 0)
+            conv2(std::integral_constant<int, 2>{}, s % BN::STEPS);
+        else
+            conv2(std::integral_constant<int, 1>{}, s % BN::STEPS);
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        BN_STAMP(s, 3);
+        barrier();
+        BN_STAMP(s, 4);
+        // ---- P3: the conv1/conv3 waves run conv3
+        BN_STAMP(s, 5);
         barrier();
     }
-    store_step(p, lds, crop0, n_steps - 1, jw, lane);
-    __builtin_amdgcn_s_waitcnt(wait_vm(0));
 }
 
 // ------------------------------------------------------------------ C13 waves
-__device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j, int lane, int n_steps) {
+// conv3's output lanes: wave j, lane group g owns two runs of 8 couts, chunks cap(g, 0..1) —
+// the x chunks conv1's lane (px, g) reads as its K chunks 2j and 2j+1 — so the residual of a
+// row is read once, beside conv1's fragments, while the row is in the ring, and kept in VGPRs
+// until conv3 of that row; the x ring then holds rows only until conv1 has read them.
+__device__ __forceinline__ int cap_chunk(int perm, int j, int g, int e) {
+    return perm ? 16 * (j >> 1) + 4 * g + 2 * (j & 1) + e : 4 * (2 * j + e) + g;
+}
+
+struct Resid {
+    uint4 v[3][2];  // [pixel tile][run]
+};
+
+__device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j, int lane, int crop0, int n_steps) {
     const int px = lane & 15, g = lane >> 4;
-    // conv1 A (row px -> cout 16j + px) and the lane's x-ring chunk offsets, chunk jc
-    bf16x8 w1f[8];
-    int xo[8];
+    // conv1: wave j computes couts 32 (j & 1) .. + 31 (two 16-cout tiles: A row px of tile c ->
+    // cout 32 (j & 1) + 16c + px) of one of the step's two rows (j >> 1), so each x fragment is
+    // read by two waves, not four; the lane's x-ring chunk offsets per K chunk jc
+    const int cb = 32 * (j & 1), half = j >> 1;
+    bf16x8 w1f[2][8];
+    int xo[4];  // chunk jc at xo[jc & 3] + 256 (jc >> 2) in either K order
 #pragma unroll
     for (int jc = 0; jc < 8; jc++) {
         const int c16 = p.perm ? 16 * (jc >> 2) + 4 * g + (jc & 3) : 4 * jc + g;
-        w1f[jc] = *reinterpret_cast<const bf16x8*>(p.w1 + (16 * j + px) * BN::C + c16 * 8);
-        xo[jc] = xoff(px, c16);
+#pragma unroll
+        for (int c = 0; c < 2; c++)
+            w1f[c][jc] = *reinterpret_cast<const bf16x8*>(p.w1 + (cb + 16 * c + px) * BN::C + c16 * 8);
+        if (jc < 4) xo[jc] = xoff(px, c16);
     }
-    // conv3 A: tile ct row r -> cout 64j + 16 (r >> 2) + 4ct + (r & 3), so that lane group g owns
-    // couts 64j + 16g .. + 15 of its pixel across the 4 tiles
+    // conv3 A: tile ct, row r (D lane group r >> 2) -> cout 8 cap(r >> 2, ct >> 1) + 4 (ct & 1) + (r & 3)
     bf16x8 w3f[4][2];
 #pragma unroll
     for (int ct = 0; ct < 4; ct++)
 #pragma unroll
         for (int ch = 0; ch < 2; ch++) {
-            const int cout = 64 * j + 16 * (px >> 2) + 4 * ct + (px & 3);
+            const int cout = 8 * cap_chunk(p.perm, j, px >> 2, ct >> 1) + 4 * (ct & 1) + (px & 3);
             w3f[ct][ch] = *reinterpret_cast<const bf16x8*>(p.w3 + cout * BN::M + ch * 32 + 8 * g);
         }
-    float b1v[4], b3v[16];
+    int cap[2], ro[2];
 #pragma unroll
-    for (int i = 0; i < 4; i++) b1v[i] = p.b1[16 * j + 4 * g + i];
-#pragma unroll
-    for (int i = 0; i < 16; i++) b3v[i] = p.b3[64 * j + 16 * g + i];
-    int ro[2];
-#pragma unroll
-    for (int e = 0; e < 2; e++) ro[e] = xoff(px, 8 * j + 2 * g + e);
+    for (int e = 0; e < 2; e++) {
+        cap[e] = cap_chunk(p.perm, j, g, e);
+        ro[e] = xoff(px, cap[e]);
+    }
+    const float* b1s = reinterpret_cast<const float*>(lds + BN::BOFF) + 64;
+    const float* b3s = b1s + 64;
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
 
     // intermediate row r (-1 .. 64) of the current crop: ring row (r + 1) & 3
+    // (this wave's 4 planes of it)
     auto zero_row = [&](int r) {
         const int pos = (r + 1) & 3;
-        for (int i = lane; i < 2 * BN::W; i += 64) {
-            const int q = 2 * j + (i >= BN::W), x = i - (i >= BN::W) * BN::W;
+        for (int i = lane; i < 4 * BN::W; i += 64) {
+            const int q = 4 * (j & 1) + i / BN::W, x = i % BN::W;
             *reinterpret_cast<uint4*>(lds + BN::TOFF + q * BN::TPL + (1 + pos * BN::RS + x) * 16) =
                 uint4{0u, 0u, 0u, 0u};
         }
     };
+    // the residual of x row r for conv3 (this wave's couts), while the row is in the ring
+    auto resid_row = [&](int cl, int r, Resid& res) {
+        const uint8_t* xb = lds + xslot(cl, r) * BN::XROW;
+#pragma unroll
+        for (int t = 0; t < 3; t++)
+#pragma unroll
+            for (int e = 0; e < 2; e++) res.v[t][e] = *reinterpret_cast<const uint4*>(xb + ro[e] + t * 8192);
+    };
     auto conv1_row = [&](int cl, int r) {
         const uint8_t* xb = lds + xslot(cl, r) * BN::XROW;
-        f32x4 acc[3];
+        f32x4 acc[2][3];
 #pragma unroll
-        for (int t = 0; t < 3; t++) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-        bf16x8 b[8][3];
+        for (int c = 0; c < 2; c++)
 #pragma unroll
-        for (int jc = 0; jc < 8; jc++)
+            for (int t = 0; t < 3; t++) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int t = 0; t < 3; t++) b[jc][t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc] + t * 8192);
+        for (int jc = 0; jc < 8; jc++) {
+            bf16x8 b[3];
 #pragma unroll
-        for (int jc = 0; jc < 8; jc++)
+            for (int t = 0; t < 3; t++) b[t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc & 3] + (jc >> 2) * 256 + t * 8192);
 #pragma unroll
-            for (int t = 0; t < 3; t++) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[jc], b[jc][t], acc[t], 0, 0, 0);
+            for (int c = 0; c < 2; c++)
+#pragma unroll
+                for (int t = 0; t < 3; t++)
+                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[c][jc], b[t], acc[c][t], 0, 0, 0);
+        }
         const int pos = (r + 1) & 3;
-        uint8_t* d = lds + BN::TOFF + (2 * j + (g >> 1)) * BN::TPL + (1 + pos * BN::RS + px) * 16 + (g & 1) * 8;
 #pragma unroll
-        for (int t = 0; t < 3; t++) {
-            float v[4];
+        for (int c = 0; c < 2; c++) {
+            const float4 bb = *reinterpret_cast<const float4*>(b1s + cb + 16 * c + 4 * g);
+            const float b1v[4] = {bb.x, bb.y, bb.z, bb.w};
+            uint8_t* d = lds + BN::TOFF + (4 * (j & 1) + 2 * c + (g >> 1)) * BN::TPL + (1 + pos * BN::RS + px) * 16 +
+                         (g & 1) * 8;
 #pragma unroll
-            for (int i = 0; i < 4; i++) v[i] = fmaxf(acc[t][i] + b1v[i], 0.f);
-            *reinterpret_cast<uint2*>(d + t * 256) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+            for (int t = 0; t < 3; t++) {
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) v[i] = fmaxf(acc[c][t][i] + b1v[i], 0.f);
+                *reinterpret_cast<uint2*>(d + t * 256) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+            }
         }
     };
-
-    barrier();  // prologue
-    for (int s = 0; s < n_steps; s++) {
-        const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
-        // ---- P1: conv1 of intermediate rows 2k+1, 2k+2 (first step: -1 (zero), 0, 1, 2)
-        if (k == 0) {
-            zero_row(-1);
-            conv1_row(cl, 0);
-            conv1_row(cl, 1);
-            conv1_row(cl, 2);
-        } else {
-            conv1_row(cl, 2 * k + 1);
-            if (2 * k + 2 < BN::H)
-                conv1_row(cl, 2 * k + 2);
-            else
-                zero_row(BN::H);
-        }
-        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
-        barrier();
-        // ---- P2: conv2 (the C2 waves)
-        barrier();
-        // ---- P3: conv3 of rows 2k, 2k+1 + b3 + residual (x ring) + ReLU, in place over the residual
-#pragma unroll 1
-        for (int tt = 0; tt < 6; tt++) {
-            const int rho = tt >= 3, tc = tt - 3 * rho, pp = rho * BN::W + tc * 16 + px;
-            uint8_t* xr = lds + xslot(cl, 2 * k + rho) * BN::XROW + tc * 8192;
-            const uint4 r0 = *reinterpret_cast<const uint4*>(xr + ro[0]);
-            const uint4 r1 = *reinterpret_cast<const uint4*>(xr + ro[1]);
+    // conv3 of output row r (rho = its row in the step) + b3 + residual + ReLU -> y
+    auto conv3_row = [&](int cl, int k, int rho, const Resid& res) {
+        uint16_t* yrow = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rho) * BN::W * BN::C;
+#pragma unroll
+        for (int tc = 0; tc < 3; tc++) {
+            const int pp = rho * BN::W + tc * 16 + px;
             bf16x8 bch[2];
 #pragma unroll
             for (int ch = 0; ch < 2; ch++)
@@ -353,6 +381,18 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
 #pragma unroll
                 for (int ct = 0; ct < 4; ct++)
                     acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[ct][ch], bch[ch], acc[ct], 0, 0, 0);
+            float b3v[16];
+#pragma unroll
+            for (int e = 0; e < 2; e++)
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const float4 bb = *reinterpret_cast<const float4*>(b3s + 8 * cap[e] + 4 * q);
+                    b3v[8 * e + 4 * q] = bb.x;
+                    b3v[8 * e + 4 * q + 1] = bb.y;
+                    b3v[8 * e + 4 * q + 2] = bb.z;
+                    b3v[8 * e + 4 * q + 3] = bb.w;
+                }
+            const uint4 r0 = res.v[tc][0], r1 = res.v[tc][1];
             const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
             uint32_t o[8];
 #pragma unroll
@@ -363,10 +403,74 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
                 v1 += hi_bf16(rw[q]);
                 o[q] = pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
             }
-            *reinterpret_cast<uint4*>(xr + ro[0]) = uint4{o[0], o[1], o[2], o[3]};
-            *reinterpret_cast<uint4*>(xr + ro[1]) = uint4{o[4], o[5], o[6], o[7]};
+            uint16_t* yp = yrow + (tc * 16 + px) * BN::C;
+#ifdef BNECK_STAMPS
+            if (blockIdx.x == 0) continue;
+#endif
+            *reinterpret_cast<uint4*>(yp + cap[0] * 8) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(yp + cap[1] * 8) = uint4{o[4], o[5], o[6], o[7]};
+        }
+    };
+
+    Resid r_lo, r_hi, r_next;  // residuals of rows 2k, 2k+1, 2k+2
+    barrier();  // prologue
+    for (int s = 0; s < n_steps; s++) {
+        const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
+        BN_STAMP(s, 0);
+        // ---- P1: conv1 of intermediate rows 2k+1, 2k+2 (first step: -1 (zero), 0, 1, 2)
+        if (k == 0) {
+            resid_row(cl, 0, r_lo);
+            resid_row(cl, 1, r_hi);
+            resid_row(cl, 2, r_next);
+            if (half == 0) {
+                conv1_row(cl, 0);
+                conv1_row(cl, 2);
+            } else {
+                zero_row(-1);
+                conv1_row(cl, 1);
+            }
+        } else {
+            r_lo = r_next;
+            resid_row(cl, 2 * k + 1, r_hi);
+            if (2 * k + 2 < BN::H) resid_row(cl, 2 * k + 2, r_next);
+            if (half == 0)
+                conv1_row(cl, 2 * k + 1);
+            else if (2 * k + 2 < BN::H)
+                conv1_row(cl, 2 * k + 2);
+            else
+                zero_row(BN::H);
         }
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        BN_STAMP(s, 1);
+        barrier();
+        BN_STAMP(s, 2);
+        // ---- P2: conv2 (the C2 waves).  This wave issues its share of the DMA of step s+2's
+        // rows into the slots step s's conv1 has just released (and the one step s-1 released):
+        // the issue (~100 cycles per 1-KiB instruction) stays off the conv2 waves' critical path
+#ifndef BNECK_DIAG_NO_DMA  // timing harness only (stale rows, wrong results)
+        if (s + 2 < n_steps) dma_step(p, crop0, s + 2, j, lane);
+#endif
+        barrier();
+        BN_STAMP(s, 4);
+        // ---- P3: step s+1's rows (issued a step ago) land before the barrier that ends this
+        // step; step s+2's stay in flight.  Waited before conv3's stores, so that only DMAs are
+        // younger than the counted ones.
+        {
+            const int younger = s + 2 < n_steps ? step_rows(s + 2) : 0;
+            if (younger == 3)
+                __builtin_amdgcn_s_waitcnt(wait_vm(3 * BN::PIECES / 4));
+            else if (younger == 2)
+                __builtin_amdgcn_s_waitcnt(wait_vm(2 * BN::PIECES / 4));
+            else if (younger == 1)
+                __builtin_amdgcn_s_waitcnt(wait_vm(BN::PIECES / 4));
+            else
+                __builtin_amdgcn_s_waitcnt(wait_vm(0));
+        }
+        // ---- P3: conv3 of rows 2k, 2k+1
+        conv3_row(cl, k, 0, r_lo);
+        conv3_row(cl, k, 1, r_hi);
+        __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
+        BN_STAMP(s, 5);
         barrier();
     }
 }
@@ -382,10 +486,11 @@ __global__ __launch_bounds__(512, 1) void bneck_kernel(BNParams p) {
     // the intermediate ring (its leading and pad slots stay zero)
     for (int i = tid; i < 8 * BN::TPL / 16; i += 512)
         *reinterpret_cast<uint4*>(lds + BN::TOFF + i * 16) = uint4{0u, 0u, 0u, 0u};
-    if (tid < 64) reinterpret_cast<float*>(lds + BN::BOFF)[tid] = p.b2[tid];
+    for (int i = tid; i < 64 + 64 + 256; i += 512)
+        reinterpret_cast<float*>(lds + BN::BOFF)[i] = i < 64 ? p.b2[i] : i < 128 ? p.b1[i - 64] : p.b3[i - 128];
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     if (wave < 4)
-        c13_role(p, lds, wave, lane, n_steps);
+        c13_role(p, lds, wave, lane, crop0, n_steps);
     else
         c2_role(p, lds, wave - 4, lane, crop0, n_steps);
 }
