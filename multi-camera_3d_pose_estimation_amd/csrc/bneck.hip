@@ -160,7 +160,7 @@ __device__ __forceinline__ void dma_step(const BNParams& p, int crop0, int s, in
 }
 
 #ifndef BNECK_PF2
-#define BNECK_PF2 2
+#define BNECK_PF2 3
 #endif
 
 __device__ __forceinline__ void c2_role(const BNParams& p, uint8_t* lds, int jw, int lane, int crop0, int n_steps) {
@@ -336,17 +336,26 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
         for (int c = 0; c < 2; c++)
 #pragma unroll
             for (int t = 0; t < 3; t++) acc[c][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // chunk jc+1's fragments are read while chunk jc's 6 MFMAs run
+        bf16x8 b[2][3];
+        auto load = [&](auto Jc) {
+            constexpr int jc = Jc;
 #pragma unroll
-        for (int jc = 0; jc < 8; jc++) {
-            bf16x8 b[3];
-#pragma unroll
-            for (int t = 0; t < 3; t++) b[t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc & 3] + (jc >> 2) * 256 + t * 8192);
+            for (int t = 0; t < 3; t++)
+                b[jc & 1][t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc & 3] + (jc >> 2) * 256 + t * 8192);
+        };
+        load(std::integral_constant<int, 0>{});
+        static_for<0, 8>([&](auto Jc) {
+            constexpr int jc = Jc;
+            if constexpr (jc + 1 < 8) load(std::integral_constant<int, jc + 1>{});
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int c = 0; c < 2; c++)
 #pragma unroll
                 for (int t = 0; t < 3; t++)
-                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[c][jc], b[t], acc[c][t], 0, 0, 0);
-        }
+                    acc[c][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1f[c][jc], b[jc & 1][t], acc[c][t], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+        });
         const int pos = (r + 1) & 3;
 #pragma unroll
         for (int c = 0; c < 2; c++) {
@@ -366,13 +375,29 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
     // conv3 of output row r (rho = its row in the step) + b3 + residual + ReLU -> y
     auto conv3_row = [&](int cl, int k, int rho, const Resid& res) {
         uint16_t* yrow = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rho) * BN::W * BN::C;
+        float b3v[16];
+#pragma unroll
+        for (int e = 0; e < 2; e++)
+#pragma unroll
+            for (int q = 0; q < 2; q++) {
+                const float4 bb = *reinterpret_cast<const float4*>(b3s + 8 * cap[e] + 4 * q);
+                b3v[8 * e + 4 * q] = bb.x;
+                b3v[8 * e + 4 * q + 1] = bb.y;
+                b3v[8 * e + 4 * q + 2] = bb.z;
+                b3v[8 * e + 4 * q + 3] = bb.w;
+            }
+        const uint8_t* tb = lds + BN::T2OFF + g * BN::T2PL + (rho * BN::W + px) * 16;
+        bf16x8 bq[2][2];  // [tile parity][chunk]: the next tile's fragments read during this one
+#pragma unroll
+        for (int ch = 0; ch < 2; ch++) bq[0][ch] = *reinterpret_cast<const bf16x8*>(tb + 4 * ch * BN::T2PL);
 #pragma unroll
         for (int tc = 0; tc < 3; tc++) {
-            const int pp = rho * BN::W + tc * 16 + px;
-            bf16x8 bch[2];
+            if (tc + 1 < 3) {
 #pragma unroll
-            for (int ch = 0; ch < 2; ch++)
-                bch[ch] = *reinterpret_cast<const bf16x8*>(lds + BN::T2OFF + (4 * ch + g) * BN::T2PL + pp * 16);
+                for (int ch = 0; ch < 2; ch++)
+                    bq[(tc + 1) & 1][ch] = *reinterpret_cast<const bf16x8*>(tb + 4 * ch * BN::T2PL + (tc + 1) * 256);
+            }
+            const bf16x8(&bch)[2] = bq[tc & 1];
             f32x4 acc[4];
 #pragma unroll
             for (int ct = 0; ct < 4; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -381,17 +406,6 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
 #pragma unroll
                 for (int ct = 0; ct < 4; ct++)
                     acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[ct][ch], bch[ch], acc[ct], 0, 0, 0);
-            float b3v[16];
-#pragma unroll
-            for (int e = 0; e < 2; e++)
-#pragma unroll
-                for (int q = 0; q < 2; q++) {
-                    const float4 bb = *reinterpret_cast<const float4*>(b3s + 8 * cap[e] + 4 * q);
-                    b3v[8 * e + 4 * q] = bb.x;
-                    b3v[8 * e + 4 * q + 1] = bb.y;
-                    b3v[8 * e + 4 * q + 2] = bb.z;
-                    b3v[8 * e + 4 * q + 3] = bb.w;
-                }
             const uint4 r0 = res.v[tc][0], r1 = res.v[tc][1];
             const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
             uint32_t o[8];
@@ -446,7 +460,9 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
         BN_STAMP(s, 2);
         // ---- P2: conv2 (the C2 waves).  This wave issues its share of the DMA of step s+2's
         // rows into the slots step s's conv1 has just released (and the one step s-1 released):
-        // the issue (~100 cycles per 1-KiB instruction) stays off the conv2 waves' critical path
+        // the issue (~100 cycles per 1-KiB instruction) stays off the conv2 waves' critical path.
+        // (Issued by the conv2 waves during conv3 instead, it leaves conv2's LDS reads alone but
+        // has a step less lead: 714 -> 836 us per block.)
 #ifndef BNECK_DIAG_NO_DMA  // timing harness only (stale rows, wrong results)
         if (s + 2 < n_steps) dma_step(p, crop0, s + 2, j, lane);
 #endif

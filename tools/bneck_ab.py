@@ -13,7 +13,7 @@ spec, xi, yo, _ = hrnet.bottleneck_spec(seed=1, n_blocks=4, lead=True)
 x = torch.relu(torch.randn((n, 64, 48, 64), device="cuda")).bfloat16()
 out = torch.empty((n, 64, 48, 256), dtype=torch.bfloat16, device="cuda")
 graphs = {}
-for mode in ("1", "0"):
+for mode in (("0",) if os.environ.get("BNECK_AB_ONLY") == "fused" else ("1", "0")):
     os.environ["MVPOSE_NO_BNECK"] = mode
     graphs[mode] = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
 for rnd in range(3):
