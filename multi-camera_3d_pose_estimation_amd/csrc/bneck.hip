@@ -41,11 +41,16 @@ namespace {
 using namespace mfma_tile;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-struct BN {
-    static constexpr int H = 64, W = 48, C = 256, M = 64;
-    static constexpr int XROW = W * C * 2;          // one x row: 24 KiB
-    static constexpr int NX = 5;                    // x ring rows
-    static constexpr int PIECES = XROW / 1024;      // 1-KiB DMA / store pieces per row (2 pixels each)
+// LEAD: layer1's first block — x is the stem's 64-ch output and conv3 is cat-fused with the
+// downsample (K = [conv2's 64 | x's 64], no residual; graph cat_fuse).  x rows are then 6 KiB
+// and stay in an 8-row ring until conv3 has read them.
+template <bool LEAD>
+struct BNT {
+    static constexpr int H = 64, W = 48, M = 64, CO = 256;
+    static constexpr int C = LEAD ? 64 : 256;       // x channels
+    static constexpr int XROW = W * C * 2;          // one x row: 24 KiB (6 KiB)
+    static constexpr int NX = LEAD ? 8 : 5;         // x ring rows
+    static constexpr int PIECES = XROW / 1024;      // 1-KiB DMA pieces per row (2 or 8 pixels each)
     static constexpr int RS = W + 1;                // intermediate row pitch (slots; slot 48 is zero)
     static constexpr int TR = 4;                    // intermediate ring rows
     static constexpr int TPL = (1 + TR * RS) * 16;  // one 8-channel plane of the ring (leading zero slot)
@@ -85,7 +90,15 @@ __device__ __forceinline__ int bn_swz(int p) {
     const int x = p & 15;
     return x < 4 ? x : x < 12 ? x + 4 : x - 8;
 }
-__device__ __forceinline__ int xoff(int p, int c16) { return p * 512 + ((c16 & 16) | ((c16 & 15) ^ bn_swz(p))) * 16; }
+// LEAD (8 chunks per pixel): chunk c16 at slot p * 8 + (c16 ^ ((p >> 1) & 7)), conflict-free for
+// the same fragment lanes (checked by brute force over the lane groups)
+template <bool LEAD>
+__device__ __forceinline__ int xoff(int p, int c16) {
+    if constexpr (LEAD)
+        return p * 128 + ((c16 ^ (p >> 1)) & 7) * 16;
+    else
+        return p * 512 + ((c16 & 16) | ((c16 & 15) ^ bn_swz(p))) * 16;
+}
 // The row DMA as raw instructions: through the builtin, the compiler treats the LDS-DMA as an
 // LDS store of unknown extent and waits for it (vmcnt(0)) before the next LDS read, which put
 // the whole DMA latency in front of conv2.  The ring protocol orders it instead: a slot is
@@ -102,7 +115,11 @@ __device__ __forceinline__ void glds16_ring(const void* src, uint32_t lds_off) {
 }
 
 // x ring slot of row r of crop-local index cl (rows of a workgroup's crops in stream order)
-__device__ __forceinline__ int xslot(int cl, int r) { return (cl * BN::H + r) % BN::NX; }
+template <bool LEAD>
+__device__ __forceinline__ int xslot(int cl, int r) {
+    using BN = BNT<LEAD>;
+    return (cl * BN::H + r) % BN::NX;
+}
 
 #ifdef BNECK_STAMPS  // timing harness (tools/bneck_stamps.py): workgroup 0's phase times, in y
 #define BN_STAMP(s, b)                                                                                     \
@@ -135,27 +152,57 @@ struct BNParams {
 // parity only).
 __device__ __forceinline__ int piece_lane_off(int jw, int lane, int odd) {
     const int px = 2 * jw + (lane >> 5), cs = lane & 31;  // pixel of piece jw (m = 0)
-    return px * BN::C + ((cs & 16) | ((cs & 15) ^ bn_swz(px + 8 * odd))) * 8;
+    return px * 256 + ((cs & 16) | ((cs & 15) ^ bn_swz(px + 8 * odd))) * 8;
 }
 
 // x rows conv1 reads in step s (all but the first of a crop: 2, the crop's last: 1)
 __device__ __forceinline__ int step_rows(int s) {
-    const int k = s % BN::STEPS;
-    return k == 0 ? 3 : k == BN::STEPS - 1 ? 1 : 2;
+    const int k = s % 32;
+    return k == 0 ? 3 : k == 31 ? 1 : 2;
+}
+// DMA instructions wave jw issues per row: 24 pieces on 4 waves, or (LEAD) 6 pieces: 2, 2, 1, 1
+template <bool LEAD>
+__device__ __forceinline__ int wave_pieces(int jw) {
+    return LEAD ? (jw < 2 ? 2 : 1) : BNT<false>::PIECES / 4;
+}
+// s_waitcnt vmcnt(n) for a runtime n <= 18
+__device__ __forceinline__ void wait_vm_dyn(int n) {
+    switch (n) {
+#define BN_W(k) \
+    case k: __builtin_amdgcn_s_waitcnt(wait_vm(k)); break;
+        BN_W(1) BN_W(2) BN_W(3) BN_W(4) BN_W(5) BN_W(6) BN_W(7) BN_W(8) BN_W(9) BN_W(10) BN_W(11) BN_W(12)
+        BN_W(13) BN_W(14) BN_W(15) BN_W(16) BN_W(17) BN_W(18)
+#undef BN_W
+        default: __builtin_amdgcn_s_waitcnt(wait_vm(0)); break;
+    }
 }
 
 // Row traffic of step s (x rows conv1 reads in it): rows 0-2 of the crop at its first step,
 // rows 2k+1, 2k+2 (< 64) after.  Wave jw moves pieces jw, jw + 4, ... of each row.
+template <bool LEAD>
 __device__ __forceinline__ void dma_step(const BNParams& p, int crop0, int s, int jw, int lane) {
+    using BN = BNT<LEAD>;
     const int cl = s / BN::STEPS, k = s - cl * BN::STEPS;
     const int r0 = k == 0 ? 0 : 2 * k + 1, r1 = k == 0 ? 3 : min(2 * k + 3, BN::H);
-    const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
-    for (int r = r0; r < r1; r++) {
-        const uint16_t* src = p.x + ((long)(crop0 + cl) * BN::H + r) * BN::W * BN::C;
-        const uint32_t dst = xslot(cl, r) * BN::XROW + jw * 1024;
+    if constexpr (LEAD) {
+        // piece n = jw, jw + 4 (< 6): pixels 8n .. 8n + 7, lane -> pixel 8n + (lane >> 3), chunk slot lane & 7
+        for (int r = r0; r < r1; r++) {
+            const uint16_t* src = p.x + ((long)(crop0 + cl) * BN::H + r) * BN::W * BN::C;
+            const uint32_t dst = xslot<LEAD>(cl, r) * BN::XROW;
+            for (int n = jw; n < BN::PIECES; n += 4) {
+                const int px = 8 * n + (lane >> 3), c16 = ((lane & 7) ^ (px >> 1)) & 7;
+                glds16_ring(src + px * BN::C + c16 * 8, __builtin_amdgcn_readfirstlane(dst + n * 1024));
+            }
+        }
+    } else {
+        const int lo0 = piece_lane_off(jw, lane, 0), lo1 = piece_lane_off(jw, lane, 1);
+        for (int r = r0; r < r1; r++) {
+            const uint16_t* src = p.x + ((long)(crop0 + cl) * BN::H + r) * BN::W * BN::C;
+            const uint32_t dst = xslot<LEAD>(cl, r) * BN::XROW + jw * 1024;
 #pragma unroll
-        for (int m = 0; m < BN::PIECES / 4; m++)
-            glds16_ring(src + 2048 * m + ((m & 1) ? lo1 : lo0), __builtin_amdgcn_readfirstlane(dst + m * 4096));
+            for (int m = 0; m < BN::PIECES / 4; m++)
+                glds16_ring(src + 2048 * m + ((m & 1) ? lo1 : lo0), __builtin_amdgcn_readfirstlane(dst + m * 4096));
+        }
     }
 }
 
@@ -163,7 +210,9 @@ __device__ __forceinline__ void dma_step(const BNParams& p, int crop0, int s, in
 #define BNECK_PF2 3
 #endif
 
+template <bool LEAD>
 __device__ __forceinline__ void c2_role(const BNParams& p, uint8_t* lds, int jw, int lane, int crop0, int n_steps) {
+    using BN = BNT<LEAD>;
     constexpr int kPF = BNECK_PF2;
     const int h = lane >> 5, r32 = lane & 31, gr = jw & 1, fr = jw >> 1;
     // A fragments, k-step s = chunk * 18 + tap * 2 + half: W2[cout][tap][32 chunk + 16 half + 8h .. +7]
@@ -238,8 +287,8 @@ __device__ __forceinline__ void c2_role(const BNParams& p, uint8_t* lds, int jw,
         }
     };
 
-    dma_step(p, crop0, 0, jw, lane);
-    if (n_steps > 1) dma_step(p, crop0, 1, jw, lane);
+    dma_step<LEAD>(p, crop0, 0, jw, lane);
+    if (n_steps > 1) dma_step<LEAD>(p, crop0, 1, jw, lane);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // prologue: steps 0 and 1's rows, the zeroed intermediate ring
     for (int s = 0; s < n_steps; s++) {
@@ -276,36 +325,43 @@ struct Resid {
     uint4 v[3][2];  // [pixel tile][run]
 };
 
+template <bool LEAD>
 __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j, int lane, int crop0, int n_steps) {
+    using BN = BNT<LEAD>;
+    constexpr int KC1 = BN::C / 32;  // conv1 K chunks: 8 (2 for LEAD: the 1x1 kernel's natural order)
     const int px = lane & 15, g = lane >> 4;
     // conv1: wave j computes couts 32 (j & 1) .. + 31 (two 16-cout tiles: A row px of tile c ->
     // cout 32 (j & 1) + 16c + px) of one of the step's two rows (j >> 1), so each x fragment is
     // read by two waves, not four; the lane's x-ring chunk offsets per K chunk jc
     const int cb = 32 * (j & 1), half = j >> 1;
-    bf16x8 w1f[2][8];
-    int xo[4];  // chunk jc at xo[jc & 3] + 256 (jc >> 2) in either K order
+    bf16x8 w1f[2][KC1];
+    int xo[LEAD ? 2 : 4];  // chunk jc at xo[jc & 3] + 256 (jc >> 2) in either K order (LEAD: xo[jc])
 #pragma unroll
-    for (int jc = 0; jc < 8; jc++) {
-        const int c16 = p.perm ? 16 * (jc >> 2) + 4 * g + (jc & 3) : 4 * jc + g;
+    for (int jc = 0; jc < KC1; jc++) {
+        const int c16 = (p.perm && !LEAD) ? 16 * (jc >> 2) + 4 * g + (jc & 3) : 4 * jc + g;
 #pragma unroll
         for (int c = 0; c < 2; c++)
             w1f[c][jc] = *reinterpret_cast<const bf16x8*>(p.w1 + (cb + 16 * c + px) * BN::C + c16 * 8);
-        if (jc < 4) xo[jc] = xoff(px, c16);
+        if (jc < (LEAD ? 2 : 4)) xo[jc] = xoff<LEAD>(px, c16);
     }
-    // conv3 A: tile ct, row r (D lane group r >> 2) -> cout 8 cap(r >> 2, ct >> 1) + 4 (ct & 1) + (r & 3)
-    bf16x8 w3f[4][2];
+    // conv3 A, tile ct, row r (D lane group r >> 2): LEAD -> cout 64j + 16 (r >> 2) + 4ct + (r & 3)
+    // over K = 128 (4 chunks: conv2's output, then x); else -> cout 8 cap(r >> 2, ct >> 1) +
+    // 4 (ct & 1) + (r & 3) over K = 64
+    constexpr int KC3 = LEAD ? 4 : 2;
+    bf16x8 w3f[4][KC3];
 #pragma unroll
     for (int ct = 0; ct < 4; ct++)
 #pragma unroll
-        for (int ch = 0; ch < 2; ch++) {
-            const int cout = 8 * cap_chunk(p.perm, j, px >> 2, ct >> 1) + 4 * (ct & 1) + (px & 3);
-            w3f[ct][ch] = *reinterpret_cast<const bf16x8*>(p.w3 + cout * BN::M + ch * 32 + 8 * g);
+        for (int ch = 0; ch < KC3; ch++) {
+            const int cout = LEAD ? 64 * j + 16 * (px >> 2) + 4 * ct + (px & 3)
+                                  : 8 * cap_chunk(p.perm, j, px >> 2, ct >> 1) + 4 * (ct & 1) + (px & 3);
+            w3f[ct][ch] = *reinterpret_cast<const bf16x8*>(p.w3 + cout * (32 * KC3) + ch * 32 + 8 * g);
         }
-    int cap[2], ro[2];
+    int cap[2], ro[2];  // the lane's two 8-cout output runs (chunks) and their x-ring offsets
 #pragma unroll
     for (int e = 0; e < 2; e++) {
-        cap[e] = cap_chunk(p.perm, j, g, e);
-        ro[e] = xoff(px, cap[e]);
+        cap[e] = LEAD ? 8 * j + 2 * g + e : cap_chunk(p.perm, j, g, e);
+        ro[e] = LEAD ? 0 : xoff<LEAD>(px, cap[e]);
     }
     const float* b1s = reinterpret_cast<const float*>(lds + BN::BOFF) + 64;
     const float* b3s = b1s + 64;
@@ -323,14 +379,18 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
     };
     // the residual of x row r for conv3 (this wave's couts), while the row is in the ring
     auto resid_row = [&](int cl, int r, Resid& res) {
-        const uint8_t* xb = lds + xslot(cl, r) * BN::XROW;
+        if constexpr (!LEAD) {
+            const uint8_t* xb = lds + xslot<LEAD>(cl, r) * BN::XROW;
 #pragma unroll
-        for (int t = 0; t < 3; t++)
+            for (int t = 0; t < 3; t++)
 #pragma unroll
-            for (int e = 0; e < 2; e++) res.v[t][e] = *reinterpret_cast<const uint4*>(xb + ro[e] + t * 8192);
+                for (int e = 0; e < 2; e++) res.v[t][e] = *reinterpret_cast<const uint4*>(xb + ro[e] + t * 8192);
+        }
     };
+    // pixel tile t of an x row in the ring: + t * XTILE
+    constexpr int XTILE = 16 * BN::C * 2;
     auto conv1_row = [&](int cl, int r) {
-        const uint8_t* xb = lds + xslot(cl, r) * BN::XROW;
+        const uint8_t* xb = lds + xslot<LEAD>(cl, r) * BN::XROW;
         f32x4 acc[2][3];
 #pragma unroll
         for (int c = 0; c < 2; c++)
@@ -340,14 +400,14 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
         bf16x8 b[2][3];
         auto load = [&](auto Jc) {
             constexpr int jc = Jc;
+            const int off = LEAD ? xo[jc & 1] : xo[jc & 3] + (jc >> 2) * 256;
 #pragma unroll
-            for (int t = 0; t < 3; t++)
-                b[jc & 1][t] = *reinterpret_cast<const bf16x8*>(xb + xo[jc & 3] + (jc >> 2) * 256 + t * 8192);
+            for (int t = 0; t < 3; t++) b[jc & 1][t] = *reinterpret_cast<const bf16x8*>(xb + off + t * XTILE);
         };
         load(std::integral_constant<int, 0>{});
-        static_for<0, 8>([&](auto Jc) {
+        static_for<0, KC1>([&](auto Jc) {
             constexpr int jc = Jc;
-            if constexpr (jc + 1 < 8) load(std::integral_constant<int, jc + 1>{});
+            if constexpr (jc + 1 < KC1) load(std::integral_constant<int, jc + 1>{});
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int c = 0; c < 2; c++)
@@ -374,7 +434,7 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
     };
     // conv3 of output row r (rho = its row in the step) + b3 + residual + ReLU -> y
     auto conv3_row = [&](int cl, int k, int rho, const Resid& res) {
-        uint16_t* yrow = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rho) * BN::W * BN::C;
+        uint16_t* yrow = p.y + ((long)(crop0 + cl) * BN::H + 2 * k + rho) * BN::W * BN::CO;
         float b3v[16];
 #pragma unroll
         for (int e = 0; e < 2; e++)
@@ -387,37 +447,51 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
                 b3v[8 * e + 4 * q + 3] = bb.w;
             }
         const uint8_t* tb = lds + BN::T2OFF + g * BN::T2PL + (rho * BN::W + px) * 16;
-        bf16x8 bq[2][2];  // [tile parity][chunk]: the next tile's fragments read during this one
+        // LEAD: K chunks 2-3 are the block input's (x row 2k + rho, still in the ring)
+        const uint8_t* xb = lds + xslot<LEAD>(cl, 2 * k + rho) * BN::XROW;
+        bf16x8 bq[2][KC3];  // [tile parity][chunk]: the next tile's fragments read during this one
+        auto load = [&](int tc, bf16x8(&dst)[KC3]) {
 #pragma unroll
-        for (int ch = 0; ch < 2; ch++) bq[0][ch] = *reinterpret_cast<const bf16x8*>(tb + 4 * ch * BN::T2PL);
+            for (int ch = 0; ch < 2; ch++) dst[ch] = *reinterpret_cast<const bf16x8*>(tb + 4 * ch * BN::T2PL + tc * 256);
+            if constexpr (LEAD) {
+#pragma unroll
+                for (int ch = 2; ch < KC3; ch++)
+                    dst[ch] = *reinterpret_cast<const bf16x8*>(xb + xo[ch - 2] + tc * XTILE);
+            }
+        };
+        load(0, bq[0]);
 #pragma unroll
         for (int tc = 0; tc < 3; tc++) {
-            if (tc + 1 < 3) {
-#pragma unroll
-                for (int ch = 0; ch < 2; ch++)
-                    bq[(tc + 1) & 1][ch] = *reinterpret_cast<const bf16x8*>(tb + 4 * ch * BN::T2PL + (tc + 1) * 256);
-            }
-            const bf16x8(&bch)[2] = bq[tc & 1];
+            if (tc + 1 < 3) load(tc + 1, bq[(tc + 1) & 1]);
+            const bf16x8(&bch)[KC3] = bq[tc & 1];
             f32x4 acc[4];
 #pragma unroll
             for (int ct = 0; ct < 4; ct++) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int ch = 0; ch < 2; ch++)
+            for (int ch = 0; ch < KC3; ch++)
 #pragma unroll
                 for (int ct = 0; ct < 4; ct++)
                     acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w3f[ct][ch], bch[ch], acc[ct], 0, 0, 0);
-            const uint4 r0 = res.v[tc][0], r1 = res.v[tc][1];
-            const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
             uint32_t o[8];
+            if constexpr (LEAD) {  // cat-fused downsample: no residual
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int ct = q >> 1, i = 2 * (q & 1);
-                float v0 = acc[ct][i] + b3v[2 * q], v1 = acc[ct][i + 1] + b3v[2 * q + 1];
-                v0 += lo_bf16(rw[q]);
-                v1 += hi_bf16(rw[q]);
-                o[q] = pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+                for (int q = 0; q < 8; q++) {
+                    const int ct = q >> 1, i = 2 * (q & 1);
+                    o[q] = pack_bf16x2(fmaxf(acc[ct][i] + b3v[2 * q], 0.f), fmaxf(acc[ct][i + 1] + b3v[2 * q + 1], 0.f));
+                }
+            } else {
+                const uint4 r0 = res.v[tc][0], r1 = res.v[tc][1];
+                const uint32_t rw[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int ct = q >> 1, i = 2 * (q & 1);
+                    float v0 = acc[ct][i] + b3v[2 * q], v1 = acc[ct][i + 1] + b3v[2 * q + 1];
+                    v0 += lo_bf16(rw[q]);
+                    v1 += hi_bf16(rw[q]);
+                    o[q] = pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
+                }
             }
-            uint16_t* yp = yrow + (tc * 16 + px) * BN::C;
+            uint16_t* yp = yrow + (tc * 16 + px) * BN::CO;
 #ifdef BNECK_STAMPS
             if (blockIdx.x == 0) continue;
 #endif
@@ -444,7 +518,7 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
                 conv1_row(cl, 1);
             }
         } else {
-            r_lo = r_next;
+            if constexpr (!LEAD) r_lo = r_next;
             resid_row(cl, 2 * k + 1, r_hi);
             if (2 * k + 2 < BN::H) resid_row(cl, 2 * k + 2, r_next);
             if (half == 0)
@@ -459,29 +533,20 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
         barrier();
         BN_STAMP(s, 2);
         // ---- P2: conv2 (the C2 waves).  This wave issues its share of the DMA of step s+2's
-        // rows into the slots step s's conv1 has just released (and the one step s-1 released):
+        // rows into the slots step s's conv1 has just released (and the one step s-1 released;
+        // LEAD: slots conv3 has released):
         // the issue (~100 cycles per 1-KiB instruction) stays off the conv2 waves' critical path.
         // (Issued by the conv2 waves during conv3 instead, it leaves conv2's LDS reads alone but
         // has a step less lead: 714 -> 836 us per block.)
 #ifndef BNECK_DIAG_NO_DMA  // timing harness only (stale rows, wrong results)
-        if (s + 2 < n_steps) dma_step(p, crop0, s + 2, j, lane);
+        if (s + 2 < n_steps) dma_step<LEAD>(p, crop0, s + 2, j, lane);
 #endif
         barrier();
         BN_STAMP(s, 4);
         // ---- P3: step s+1's rows (issued a step ago) land before the barrier that ends this
         // step; step s+2's stay in flight.  Waited before conv3's stores, so that only DMAs are
         // younger than the counted ones.
-        {
-            const int younger = s + 2 < n_steps ? step_rows(s + 2) : 0;
-            if (younger == 3)
-                __builtin_amdgcn_s_waitcnt(wait_vm(3 * BN::PIECES / 4));
-            else if (younger == 2)
-                __builtin_amdgcn_s_waitcnt(wait_vm(2 * BN::PIECES / 4));
-            else if (younger == 1)
-                __builtin_amdgcn_s_waitcnt(wait_vm(BN::PIECES / 4));
-            else
-                __builtin_amdgcn_s_waitcnt(wait_vm(0));
-        }
+        wait_vm_dyn(s + 2 < n_steps ? step_rows(s + 2) * wave_pieces<LEAD>(j) : 0);
         // ---- P3: conv3 of rows 2k, 2k+1
         conv3_row(cl, k, 0, r_lo);
         conv3_row(cl, k, 1, r_hi);
@@ -491,7 +556,9 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
     }
 }
 
+template <bool LEAD>
 __global__ __launch_bounds__(512, 1) void bneck_kernel(BNParams p) {
+    using BN = BNT<LEAD>;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -506,9 +573,9 @@ __global__ __launch_bounds__(512, 1) void bneck_kernel(BNParams p) {
         reinterpret_cast<float*>(lds + BN::BOFF)[i] = i < 64 ? p.b2[i] : i < 128 ? p.b1[i - 64] : p.b3[i - 128];
     __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
     if (wave < 4)
-        c13_role(p, lds, wave, lane, crop0, n_steps);
+        c13_role<LEAD>(p, lds, wave, lane, crop0, n_steps);
     else
-        c2_role(p, lds, wave - 4, lane, crop0, n_steps);
+        c2_role<LEAD>(p, lds, wave - 4, lane, crop0, n_steps);
 }
 
 int g_bn_cus = 0;
@@ -518,27 +585,37 @@ int g_bn_cus = 0;
 bool bneck_supported(int H, int W, int C, int M) {
     const char* e = getenv("MVPOSE_NO_BNECK");  // tests / A/B: the tconv + Bottleneck-join path
     if (e && e[0] == '1') return false;
-    return H == BN::H && W == BN::W && C == BN::C && M == BN::M;
+    using BN = BNT<false>;
+    return H == BN::H && W == BN::W && (C == BNT<false>::C || C == BNT<true>::C) && M == BN::M;
+}
+
+template <bool LEAD>
+void launch_bneck_t(const BNParams& p, hipStream_t s) {
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)bneck_kernel<LEAD>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    BNT<LEAD>::LDS));
+        attr = true;
+    }
+    const int grid = std::min(p.N, g_bn_cus);
+    hipLaunchKernelGGL(bneck_kernel<LEAD>, dim3(grid), dim3(512), BNT<LEAD>::LDS, s, p);
+    MVP_HIP(hipGetLastError());
 }
 
 void launch_bneck(const BneckLaunch& c, hipStream_t s) {
-    MVP_REQUIRE(c.H == BN::H && c.W == BN::W, "bneck: plane %dx%d", c.H, c.W);
+    MVP_REQUIRE(c.H == BNT<false>::H && c.W == BNT<false>::W, "bneck: plane %dx%d", c.H, c.W);
     MVP_REQUIRE(c.N >= 0 && c.N < (1 << 24), "bneck: %d crops", c.N);
     if (c.N == 0) return;
-    static bool attr = false;
-    if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)bneck_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, BN::LDS));
-        attr = true;
-    }
     if (g_bn_cus == 0) {
         int dev = 0;
         MVP_HIP(hipGetDevice(&dev));
         MVP_HIP(hipDeviceGetAttribute(&g_bn_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     BNParams p{c.x, c.w1, c.b1, c.w2, c.b2, c.w3, c.b3, c.y, c.N, c.perm ? 1 : 0};
-    const int grid = std::min(c.N, g_bn_cus);
-    hipLaunchKernelGGL(bneck_kernel, dim3(grid), dim3(512), BN::LDS, s, p);
-    MVP_HIP(hipGetLastError());
+    if (c.lead)
+        launch_bneck_t<true>(p, s);
+    else
+        launch_bneck_t<false>(p, s);
 }
 
 }  // namespace mvp

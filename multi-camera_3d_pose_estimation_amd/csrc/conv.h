@@ -92,6 +92,9 @@ struct BneckLaunch {
     uint16_t* y = nullptr;
     int N = 0, H = 0, W = 0;
     int perm = 1;
+    // layer1's first block: x has 64 channels, w3 / b3 are the cat-fused [conv3 | downsample]
+    // weights [256][128] and summed biases (no residual)
+    int lead = 0;
 };
 bool bneck_supported(int H, int W, int C, int M);
 void launch_bneck(const BneckLaunch& c, hipStream_t s);

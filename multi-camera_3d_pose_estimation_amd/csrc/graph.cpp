@@ -41,6 +41,7 @@ struct Graph {
     std::vector<int> bneck;             // Bottleneck conv3 whose (absorbed) conv1 bneck[k] and conv2 run in its launch (-1: none)
     std::vector<int> bneck_mid;         // and its (absorbed) conv2
     std::vector<int> bneck_perm;        // its conv1 sums K in the Bottleneck join's order (bneck.hip)
+    std::vector<int> bneck_lead;        // layer1's first block: 64-ch input, conv3 cat-fused with the downsample
     std::vector<int64_t> offset;  // per-crop-batch arena offsets (bytes), -1 = external
     int64_t arena_bytes = 0;
     char* arena = nullptr;
@@ -208,7 +209,8 @@ void pair_fuse(Graph& g, bool enable) {
     for (int k = 0; k < no; k++) producer[g.ops[k].out] = k;
     auto plain_1x1 = [&](int k) {
         const mvp_op_desc& op = g.ops[k];
-        return !g.absorbed[k] && !g.block_head[k] && op.kind == MVP_OP_CONV && op.ks == 1 && op.stride == 1 &&
+        return !g.absorbed[k] && !g.block_head[k] && g.bneck[k] < 0 && op.kind == MVP_OP_CONV && op.ks == 1 &&
+               op.stride == 1 &&
                op.relu && g.tensors[op.out].dtype == MVP_DT_BF16_NHWC;
     };
     for (int b = 0; b < no; b++) {
@@ -236,6 +238,7 @@ void bneck_fuse(Graph& g, bool enable, bool pair_enabled) {
     g.bneck.assign(no, -1);
     g.bneck_mid.assign(no, -1);
     g.bneck_perm.assign(no, 0);
+    g.bneck_lead.assign(no, 0);
     if (!enable) return;
     std::vector<int> uses(nt, 0), producer(nt, -1);
     for (int k = 0; k < no; k++) {
@@ -278,6 +281,36 @@ void bneck_fuse(Graph& g, bool enable, bool pair_enabled) {
         g.bneck[c] = a;
         g.bneck_mid[c] = b;
         g.bneck_perm[c] = perm;
+    }
+    // layer1's first block: conv1 (1x1 64 -> 64) and the downsample (1x1 64 -> 256, cat-fused
+    // into conv3) read the same 64-ch tensor; conv3's K is [conv2's output | that tensor]
+    for (int c = 0; c < no; c++) {
+        const int d = g.cat_src[c];
+        if (d < 0 || g.absorbed[c] || g.block_head[c] || g.bneck[c] >= 0) continue;
+        const mvp_op_desc& C = g.ops[c];
+        if (C.kind != MVP_OP_CONV || C.ks != 1 || C.stride != 1 || !C.relu || C.cin != 64 || C.cout != 256 ||
+            g.tensors[C.out].dtype != MVP_DT_BF16_NHWC || g.ops[d].cin != 64)
+            continue;
+        const int b = producer[C.in[0]];
+        if (b < 0 || g.absorbed[b] || g.block_head[b] || g.cat_src[b] >= 0) continue;
+        const mvp_op_desc& B = g.ops[b];
+        if (B.kind != MVP_OP_CONV || B.ks != 3 || B.stride != 1 || !B.relu || B.cin != 64 || B.cout != 64 ||
+            !no_res(b) || uses[B.out] != 1 || B.out == g.output)
+            continue;
+        const int a = producer[B.in[0]];
+        if (a < 0 || g.absorbed[a] || g.block_head[a] || g.cat_src[a] >= 0) continue;
+        const mvp_op_desc& A = g.ops[a];
+        if (A.kind != MVP_OP_CONV || A.ks != 1 || A.stride != 1 || !A.relu || A.cin != 64 || A.cout != 64 ||
+            !no_res(a) || uses[A.out] != 1 || A.out == g.output || A.in[0] != g.ops[d].in[0])
+            continue;
+        if (A.segment != C.segment || B.segment != C.segment) continue;
+        const mvp_tensor_desc& x = g.tensors[A.in[0]];
+        if (!bneck_supported(x.h, x.w, x.c, A.cout)) continue;
+        g.absorbed[a] = 1;
+        g.absorbed[b] = 1;
+        g.bneck[c] = a;
+        g.bneck_mid[c] = b;
+        g.bneck_lead[c] = 1;
     }
 }
 
@@ -783,20 +816,22 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
         if (g->bneck[k] >= 0) {  // the whole Bottleneck: conv1 + conv2 (absorbed) + this conv3
             const mvp_op_desc& a = g->ops[g->bneck[k]];
             const mvp_op_desc& c2 = g->ops[g->bneck_mid[k]];
-            const mvp_tensor_desc& x = g->tensors[op.in[1]];
+            const bool lead = g->bneck_lead[k];
+            const mvp_tensor_desc& x = g->tensors[a.in[0]];
             mvp::BneckLaunch bl;
-            bl.x = (const uint16_t*)ptr(op.in[1]);
+            bl.x = (const uint16_t*)ptr(a.in[0]);
             bl.w1 = g->wb + a.w_off;
             bl.b1 = g->fb + a.b_off;
             bl.w2 = g->wb + c2.w_off;
             bl.b2 = g->fb + c2.b_off;
-            bl.w3 = g->wb + op.w_off;
-            bl.b3 = g->fb + op.b_off;
+            bl.w3 = lead ? g->cat_w[k] : g->wb + op.w_off;
+            bl.b3 = lead ? g->cat_b[k] : g->fb + op.b_off;
             bl.y = (uint16_t*)ptr(op.out);
             bl.N = nb;
             bl.H = x.h;
             bl.W = x.w;
             bl.perm = g->bneck_perm[k];
+            bl.lead = lead;
             mvp::launch_bneck(bl, s);
             return;
         }

@@ -13,7 +13,7 @@ import sys
 from collections import defaultdict
 
 GROUPS = {"backbone": ("conv_mfma_kernel", "stem_kernel", "stem_mfma_kernel", "fuse_sum_kernel", "fuse_sum_n_kernel", "conv1x1_kernel",
-                       "conv1x1_pair_kernel", "basic_block", "tconv_kernel", "tconv16_kernel", "tblock32_kernel",
+                       "conv1x1_pair_kernel", "bneck_kernel", "basic_block", "tconv_kernel", "tconv16_kernel", "tblock32_kernel",
                        "tblock32s_kernel", "tblock64_kernel", "s2conv_kernel", "stem2_kernel", "trans1_kernel",
                        "head1x1_kernel", "head_fuse_kernel"),
           "moments": ("moments_kernel",),
