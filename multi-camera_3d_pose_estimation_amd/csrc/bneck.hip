@@ -143,7 +143,7 @@ struct BNParams {
     const uint16_t* w3;
     const float* b3;
     uint16_t* y;
-    int N, perm;
+    int N, perm, planar;
 };
 
 // ------------------------------------------------------------------ C2 waves
@@ -491,12 +491,23 @@ __device__ __forceinline__ void c13_role(const BNParams& p, uint8_t* lds, int j,
                     o[q] = pack_bf16x2(fmaxf(v0, 0.f), fmaxf(v1, 0.f));
                 }
             }
-            uint16_t* yp = yrow + (tc * 16 + px) * BN::CO;
 #ifdef BNECK_STAMPS
             if (blockIdx.x == 0) continue;
 #endif
-            *reinterpret_cast<uint4*>(yp + cap[0] * 8) = uint4{o[0], o[1], o[2], o[3]};
-            *reinterpret_cast<uint4*>(yp + cap[1] * 8) = uint4{o[4], o[5], o[6], o[7]};
+            uint16_t* yq[2];
+            if (!LEAD && p.planar) {  // [crop][16-ch chunk][row][col][16]
+                const int row = 2 * k + rho, col = tc * 16 + px;
+#pragma unroll
+                for (int e = 0; e < 2; e++)
+                    yq[e] = p.y + ((((long)(crop0 + cl) * 16 + (cap[e] >> 1)) * BN::H + row) * BN::W + col) * 16 +
+                            (cap[e] & 1) * 8;
+            } else {
+                uint16_t* yp = yrow + (tc * 16 + px) * BN::CO;
+#pragma unroll
+                for (int e = 0; e < 2; e++) yq[e] = yp + cap[e] * 8;
+            }
+            *reinterpret_cast<uint4*>(yq[0]) = uint4{o[0], o[1], o[2], o[3]};
+            *reinterpret_cast<uint4*>(yq[1]) = uint4{o[4], o[5], o[6], o[7]};
         }
     };
 
@@ -611,7 +622,8 @@ void launch_bneck(const BneckLaunch& c, hipStream_t s) {
         MVP_HIP(hipGetDevice(&dev));
         MVP_HIP(hipDeviceGetAttribute(&g_bn_cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    BNParams p{c.x, c.w1, c.b1, c.w2, c.b2, c.w3, c.b3, c.y, c.N, c.perm ? 1 : 0};
+    MVP_REQUIRE(!(c.lead && c.planar), "bneck: planar output is for the 256-ch blocks");
+    BNParams p{c.x, c.w1, c.b1, c.w2, c.b2, c.w3, c.b3, c.y, c.N, c.perm ? 1 : 0, c.planar ? 1 : 0};
     if (c.lead)
         launch_bneck_t<true>(p, s);
     else

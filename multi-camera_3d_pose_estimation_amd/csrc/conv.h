@@ -95,6 +95,9 @@ struct BneckLaunch {
     // layer1's first block: x has 64 channels, w3 / b3 are the cat-fused [conv3 | downsample]
     // weights [256][128] and summed biases (no residual)
     int lead = 0;
+    // y in chunk-planar layout [N][16][64][48][16] (16-channel chunks; the graph sets it when y
+    // feeds only trans1, which then reads it planar)
+    int planar = 0;
 };
 bool bneck_supported(int H, int W, int C, int M);
 void launch_bneck(const BneckLaunch& c, hipStream_t s);
@@ -162,7 +165,7 @@ void launch_stem2(const uint16_t* x, const float* w1, const float* b1, const uin
 bool trans1_supported(int H, int W, int C, int cout0, int cout1);
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
                    const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s,
-                   const uint16_t* wimg = nullptr);
+                   const uint16_t* wimg = nullptr, bool planar = false);
 // trans1's weight image (9 x 2 x 96 16-B slots per 16-channel chunk, 221,184 elements)
 constexpr long kTrans1ImageElems = 16L * 9 * 2 * 96 * 8;
 void trans1_pack_weights(const uint16_t* wb, int64_t w0_off, int64_t w1_off, uint16_t* img, hipStream_t s);

@@ -77,6 +77,10 @@ struct TrParams {
     // the weight slots of every 16-channel chunk in LDS order (trans1_pack_weights): 1 KB
     // contiguous per weight DMA instruction instead of 64 scattered rows; nullptr: gather from wb
     const uint16_t* wimg;
+    // x in chunk-planar layout [N][16][64][48][16] (the fused Bottleneck's planar output): a
+    // 16-channel item's halo is then one contiguous run per row, and no item shares a cache line
+    // with another (NHWC: 4 items per 128-B line, re-fetched from HBM when L2 evicts it between them)
+    int planar;
 };
 
 template <bool PM>
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
                 if (xx < G::W) {
                     kind = 1;
                     hy = yy;
-                    off = (yy * G::W + xx) * G::C + q * 8;
+                    off = (yy * G::W + xx) * (p.planar ? 16 : G::C) + q * 8;
                 }
             }
         } else if (s < G::ITEM && p.wimg) {
@@ -132,7 +136,8 @@ __global__ __launch_bounds__(512, 1) void trans1_kernel(TrParams p) {
     auto issue = [&](int item, int buf) {
         const int tile = blockIdx.x + (item / G::NCH) * gridDim.x, chunk = item % G::NCH;
         const int n = tile / tiles_h, r0 = (tile - n * tiles_h) * G::TH;
-        const uint16_t* xb = p.x + ((long)n * G::H + r0 - 1) * G::W * G::C + chunk * 16;
+        const uint16_t* xb = p.planar ? p.x + (((long)n * G::NCH + chunk) * G::H + r0 - 1) * G::W * 16
+                                      : p.x + ((long)n * G::H + r0 - 1) * G::W * G::C + chunk * 16;
         uint8_t* dst = lds + buf * G::BUF;
         const uint16_t* wbase = p.wimg ? p.wimg + chunk * (G::ITEM - G::WA) * 8 : p.wb + chunk * 16;
         if (!dma_wave) return;
@@ -294,7 +299,8 @@ void trans1_pack_weights(const uint16_t* wb, int64_t w0_off, int64_t w1_off, uin
 }
 
 void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const float* b0, int64_t w1_off,
-                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s, const uint16_t* wimg) {
+                   const float* b1, uint16_t* y0, uint16_t* y1, int N, hipStream_t s, const uint16_t* wimg,
+                   bool planar) {
     MVP_REQUIRE(w0_off >= 0 && w1_off >= 0 && w0_off + 32 * 9 * 256 < (1LL << 31) && w1_off + 64 * 9 * 256 < (1LL << 31),
                 "trans1: weight offsets exceed 32 bits");
     if (N == 0) return;
@@ -311,7 +317,7 @@ void launch_trans1(const uint16_t* x, const uint16_t* wb, int64_t w0_off, const 
     }
     const long tiles = (long)N * (T1C<true>::H / T1C<true>::TH);
     MVP_REQUIRE(tiles * T1C<true>::NCH < (1L << 30), "trans1: too many tiles");
-    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles, wimg};
+    TrParams p{x, wb, (int)w0_off, (int)w1_off, b0, b1, y0, y1, conv_zero_region(), N, (int)tiles, wimg, planar ? 1 : 0};
     const int grid = (int)std::min<long>(tiles, g_tr_cus);
     // pixel-major halo (+0.4 % frames/s over plane-major, round 2)
     hipLaunchKernelGGL(trans1_kernel<true>, dim3(grid), dim3(T1C<true>::NTH), T1C<true>::LDS, s, p);

@@ -437,6 +437,24 @@ def bottleneck_spec(seed: int = 0, n_blocks: int = 4, lead: bool = True):
     return g, x_in, x, sd
 
 
+def layer1_transition_spec(seed: int = 0, output: int = 0):
+    """HRNet-W32 layer1 (bottleneck_spec, lead=True) followed by transition1 on its output: t0 =
+    3x3/s1 -> 32 ch, t1 = 3x3/s2 -> 64 ch (BN + ReLU).  The graph output is t0 (output=0) or t1;
+    the layer1 output then feeds only the transition, the case where the fused Bottleneck hands
+    it to trans1 in chunk-planar layout.  Returns (spec, input id, output id, state dict)."""
+    g, x, y, sd = bottleneck_spec(seed=seed, n_blocks=4, lead=True)
+    gen = torch.Generator().manual_seed(seed + 1)
+    for j, co in (("t0", 32), ("t1", 64)):
+        sd[f"{j}.weight"] = torch.randn((co, 256, 3, 3), generator=gen) * (2.0 / (9 * 256)) ** 0.5
+        sd[f"{j}bn.weight"] = 1.0 + 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.bias"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_mean"] = 0.1 * torch.randn((co,), generator=gen)
+        sd[f"{j}bn.running_var"] = 1.0 + 0.2 * torch.rand((co,), generator=gen)
+    t0 = g.conv(sd, "t0", "t0bn", y, 1, True)
+    t1 = g.conv(sd, "t1", "t1bn", y, 2, True)
+    return g, x, (t0, t1)[output], sd
+
+
 def stem_spec(seed: int = 0):
     """HRNet's stem on a 256x192 crop: conv1 (3x3/s2 4 -> 64) and conv2 (3x3/s2 64 -> 64),
     BN + ReLU each (the pattern the graph's stem-fusion pass runs as one launch), for

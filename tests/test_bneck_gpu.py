@@ -90,3 +90,29 @@ def test_bneck_vs_reference(monkeypatch):
     mx = (dev - ref).abs().max().item()
     print(f"bneck vs torch: rel L2 {rel:.2e}, max abs {mx:.3e} (max|ref| {ref.abs().max().item():.2f})")
     assert rel <= 4e-3 and mx <= 3 * ref.abs().max().item() * 2.0 ** -8
+
+
+@pytest.mark.parametrize("output", [0, 1])
+@pytest.mark.parametrize("n", [3, 300])
+def test_layer1_transition_planar_bitwise_equals_unfused(output, n, monkeypatch):
+    """Layer1 + transition1: with the fusion on, the last Bottleneck writes its output in
+    chunk-planar layout and trans1 reads it so (graph planar pass); t0 / t1 must equal the
+    unfused graph's (NHWC hand-off) bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mvpose import hrnet
+    spec, xi, yo, _ = hrnet.layer1_transition_spec(seed=81, output=output)
+    ho, wo, co = spec.tensors[yo][:3]
+    gen = torch.Generator().manual_seed(82)
+    x = torch.relu(torch.randn((n, 64, 48, 64), generator=gen)).bfloat16().cuda()
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setenv("MVPOSE_NO_BNECK", "0" if fused else "1")
+        g = hrnet.ConvGraph(spec, xi, yo, max_batch=n)
+        out = torch.full((n, ho, wo, co), float("nan"), dtype=torch.bfloat16, device="cuda")
+        g.run(x, out)
+        torch.cuda.synchronize()
+        g.close()
+        outs.append(out)
+    assert torch.isfinite(outs[1].float()).all()
+    assert torch.equal(outs[0].view(torch.int16), outs[1].view(torch.int16))

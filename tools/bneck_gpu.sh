@@ -7,7 +7,7 @@ O=gpurun_out/$N
 mkdir -p $O
 export PYTHONPATH=$PWD/multi-camera_3d_pose_estimation_amd
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_bneck_gpu.py \
-  tests/test_conv_planes_gpu.py -k "bneck or layer1 or join or transition" > $O/pytest.log 2>&1
+  tests/test_conv_planes_gpu.py -k "bneck or layer1 or join or transition or backbone" > $O/pytest.log 2>&1
 rc=$?; tail -5 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 240 python -u tools/bneck_ab.py > $O/ab.txt 2>&1 && cat $O/ab.txt || exit 1
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof -o run -- python3 $GRAFT_REPO_ROOT/tools/bneck_ab.py > $GRAFT_REPO_ROOT/$O/prof.log 2>&1
