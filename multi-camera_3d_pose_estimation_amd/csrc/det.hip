@@ -1469,8 +1469,10 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
 
 void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s) {
     MVP_REQUIRE(C % 8 == 0 && xs >= 4 * C && xs % 8 == 0, "spp: C=%d stride=%d", C, xs);
+    // three 16-B planes of the SPP input in LDS: H * W <= 1365 (the stride-32 plane of a detector
+    // input up to 1,184 x 1,184; 20 x 20 = 400 at the model's 640)
     const size_t lds = (size_t)3 * H * W * sizeof(uint4);
-    MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large", H, W);
+    MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large (H * W <= 1365)", H, W);
     if (n == 0) return;
     hipLaunchKernelGGL(spp_kernel, dim3((unsigned)(C / 8), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
     MVP_HIP(hipGetLastError());
