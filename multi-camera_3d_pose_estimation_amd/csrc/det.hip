@@ -213,9 +213,12 @@ __global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
     const int col = lane & 15, rp = lane >> 4;
     const int chunk = grp * G + wave;
     const float* wc = p.w + (size_t)chunk * 200;
-    float a0[8], a1[8];
+    // channel pairs on packed FMAs (v_pk_fma_f32: two fmaf per instruction, the same roundings):
+    // the kernel is VALU-issue-bound (~1,100 VALU instructions per wave with scalar fmaf)
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    f32x2v a0[4], a1[4];
 #pragma unroll
-    for (int c = 0; c < 8; c++) a0[c] = a1[c] = 0.f;
+    for (int c = 0; c < 4; c++) a0[c] = a1[c] = f32x2v{0.f, 0.f};
     // input rows one at a time (not unrolled): 8 unpacked values live, not 240, so the
     // kernel fits 8 waves per SIMD and the next block's halo load hides under this one
 #pragma unroll 1
@@ -225,26 +228,33 @@ __global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
             float v[8];
             unpack8(sh[wave][(2 * rp + ir) * kDwHW + col + kw], v);
             if (ir < 5) {
+                const float* wk = wc + (ir * 5 + kw) * 8;
 #pragma unroll
-                for (int c = 0; c < 8; c++) a0[c] = fmaf(v[c], wc[(ir * 5 + kw) * 8 + c], a0[c]);
+                for (int c = 0; c < 4; c++)
+                    a0[c] = __builtin_elementwise_fma(f32x2v{v[2 * c], v[2 * c + 1]},
+                                                      f32x2v{wk[2 * c], wk[2 * c + 1]}, a0[c]);
             }
             if (ir >= 1) {
+                const float* wk = wc + ((ir - 1) * 5 + kw) * 8;
 #pragma unroll
-                for (int c = 0; c < 8; c++) a1[c] = fmaf(v[c], wc[((ir - 1) * 5 + kw) * 8 + c], a1[c]);
+                for (int c = 0; c < 4; c++)
+                    a1[c] = __builtin_elementwise_fma(f32x2v{v[2 * c], v[2 * c + 1]},
+                                                      f32x2v{wk[2 * c], wk[2 * c + 1]}, a1[c]);
             }
         }
     }
     const int ho = th * kDwTH + 2 * rp, wo = tw * kDwTW + col;
     if (wo >= p.W) return;
     const float* bc = p.b + chunk * 8;
+    float o0[8], o1[8];
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-        a0[c] = act_f(a0[c] + bc[c], p.act);
-        a1[c] = act_f(a1[c] + bc[c], p.act);
+        o0[c] = act_f(a0[c >> 1][c & 1] + bc[c], p.act);
+        o1[c] = act_f(a1[c >> 1][c & 1] + bc[c], p.act);
     }
     uint16_t* yb = p.y + ((size_t)n * p.H * p.W + (size_t)ho * p.W + wo) * p.ys + chunk * 8;
-    if (ho < p.H) *reinterpret_cast<uint4*>(yb) = pack8(a0);
-    if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(a1);
+    if (ho < p.H) *reinterpret_cast<uint4*>(yb) = pack8(o0);
+    if (ho + 1 < p.H) *reinterpret_cast<uint4*>(yb + (size_t)p.W * p.ys) = pack8(o1);
 }
 
 // ------------------------------------------------------------------ conv = GEMM
