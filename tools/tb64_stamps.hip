@@ -82,30 +82,43 @@ int main(int argc, char** argv) {
     printf("N=%d grid=%d tiles=%d: %.1f us per launch (stamped build)\n", N, grid, tiles, ms * 1000 / reps);
     // per role, per segment: median over blocks, phases 2..13
     auto at = [&](int blk, int wave, int k, int i) { return (long long)h[((blk * 4 + wave) * 16 + k) * 4 + i]; };
-    std::vector<long long> c1_mfma, c1_epi, c1_bar, c2_mfma, c2_epi, c2_dma, c2_bar, phase;
-    for (int blk = 0; blk < grid; blk++)
-        for (int k = 2; k < 13; k++) {
-            for (int wv = 0; wv < 2; wv++) {
-                c1_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
-                c1_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
-                c1_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 2));
-            }
-            phase.push_back(at(blk, 0, k + 1, 0) - at(blk, 0, k, 0));
-            for (int wv = 2; wv < 4; wv++) {
-                c2_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
-                c2_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
-                c2_dma.push_back(at(blk, wv, k, 3) - at(blk, wv, k, 2));
-                c2_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 3));
-            }
-        }
+    // per tile kind: s = k % 4 == 0 (conv1 computes all 10 rows: 8 fragments) and s > 0 (rows 2-9: 6)
     auto med = [](std::vector<long long> v) {
         std::sort(v.begin(), v.end());
         return v.empty() ? 0LL : v[v.size() / 2];
     };
-    printf("phase %lld cycles (s_memtime ticks)\n", med(phase));
-    printf("conv1: mfma loop %lld, epilogue %lld, barrier wait %lld\n", med(c1_mfma), med(c1_epi), med(c1_bar));
-    printf("conv2: setup+mfma %lld, residual wait+epilogue %lld, dma wait %lld, barrier wait %lld\n", med(c2_mfma),
-           med(c2_epi), med(c2_dma), med(c2_bar));
-    printf("ideal conv1 mfma: %d cycles (288 x 32)\n", 288 * 32);
+    for (int kind = 0; kind < 2; kind++) {
+        std::vector<long long> c1_mfma, c1_epi, c1_bar, c2_mfma, c2_epi, c2_dma, c2_bar, phase;
+        for (int blk = 0; blk < grid; blk++)
+            for (int k = 2; k < 14; k++) {
+                if ((k % G::TILES_H == 0) != (kind == 0)) continue;
+                for (int wv = 0; wv < 2; wv++) {
+                    c1_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
+                    c1_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
+                    c1_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 2));
+                }
+                phase.push_back(at(blk, 0, k + 1, 0) - at(blk, 0, k, 0));
+                for (int wv = 2; wv < 4; wv++) {
+                    c2_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
+                    c2_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
+                    c2_dma.push_back(at(blk, wv, k, 3) - at(blk, wv, k, 2));
+                    c2_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 3));
+                }
+            }
+        printf("%s: phase %lld cycles (s_memtime ticks)\n", kind == 0 ? "first tile of a crop (8 conv1 fragments)"
+                                                                        : "tiles 1-3 (6 conv1 fragments)",
+               med(phase));
+        printf("  conv1: mfma loop %lld, epilogue %lld, barrier wait %lld\n", med(c1_mfma), med(c1_epi), med(c1_bar));
+        printf("  conv2: setup+mfma %lld, residual wait+epilogue %lld, dma wait %lld, barrier wait %lld\n",
+               med(c2_mfma), med(c2_epi), med(c2_dma), med(c2_bar));
+    }
+    // the tick rate: the whole launch over the per-block sum of phases
+    {
+        std::vector<long long> span;
+        for (int blk = 0; blk < grid; blk++) span.push_back(at(blk, 0, 15, 0) - at(blk, 0, 1, 0));
+        std::sort(span.begin(), span.end());
+        printf("phases 1-15 of block median: %lld ticks\n", span[span.size() / 2]);
+    }
+    printf("ideal per phase: 216 MFMAs x 32 = %d cycles (tiles 1-3), conv1 288 x 32 = %d (first tile)\n", 216 * 32, 288 * 32);
     return 0;
 }
