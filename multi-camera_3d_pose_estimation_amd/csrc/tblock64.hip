@@ -9,16 +9,19 @@
 // their first two intermediate rows from the previous tile instead of recomputing them, 8 -> 6
 // conv1 fragments; 120 -> 114.5 us per block, profiles/r04_tblock64_rowreuse_ab.txt).  The
 // waves specialise:
-//   waves 0, 1  conv1 for output rows -1 .. 8 (10 rows: conv2's halo), cout group 0 / 1
-//               -> the intermediate (bias, ReLU, bf16; rows outside the image = 0 = conv2's
-//               zero padding) in LDS;
-//   waves 2, 3  conv2 of the PREVIOUS tile from the other intermediate buffer, + b2 +
-//               residual (read from the input ring) + ReLU -> output, and the input
-//               halo DMA of the NEXT tile into the idle ring slot.
+//   waves 0, 1  conv1 for output rows -1 .. 8 (10 rows: conv2's halo), half of the
+//               fragments each -> the intermediate (bias, ReLU, bf16; rows outside the
+//               image = 0 = conv2's zero padding) in LDS;
+//   waves 2, 3  conv2 of the PREVIOUS tile from the other intermediate buffer, half of the
+//               fragments each, + b2 + residual (read from the input ring) + ReLU ->
+//               output, and the input halo DMA of the NEXT tile into the idle ring slot.
 // So each phase (one barrier) runs conv1 of tile k beside conv2 of tile k-1 on the other
 // two SIMDs, and the halo of tile k+1 streams in under both.  Each wave keeps its conv's
-// 32 couts x 576 K of weights in registers (144 VGPRs, loaded once per launch: no weight
-// traffic in the loop and only B fragments are read from LDS, one ds_read_b128 per MFMA).
+// 64 couts x 576 K of weights in registers (288 of the 512 a lone wave per SIMD has, AGPRs
+// included; loaded once per launch) and computes BOTH 32-cout groups of its fragments, so
+// every B fragment read from LDS feeds two MFMAs (round 5; with one cout group per wave
+// each MFMA had its own ds_read_b128 and LDS reads bound the kernel: 129 -> 123 us per
+// block, profiles/r05_tb64_2cg_ab.txt).
 //
 // LDS images (input halo ring 2 x 40 KiB, intermediate 2 x 32.5 KiB) are plane-major
 // (8 planes of 8 channels, 16-B slots) with a row pitch of 26 slots (zero pad | 24 pixels |
