@@ -215,62 +215,62 @@ __device__ __forceinline__ void tile_of64(int crop0, int k, int& n, int& s) {
 // waves.  A workgroup walks its crops' 4 tiles top to bottom, so tile k's intermediate rows
 // 0-1 (output rows ho0 - 1, ho0) are tile k-1's rows 8-9: for s > 0 they are copied from the
 // other buffer and only rows 2-9 are computed (6 fragments of 8x4 blocks); the first tile of a
-// crop computes all 10 rows (8 fragments, rows 0-7 as blocks, 8-9 as 2x16).  Wave w computes
-// BOTH cout groups of half the fragments (4w .. 4w+3 of the full set, 3w .. 3w+2 of the
-// shifted one): each B fragment read from LDS feeds two MFMAs (round 5: with one cout group
-// per wave, one ds_read_b128 per MFMA made LDS the bound -- a timing probe reading half the
-// fragments ran 134 -> 96 us per block, profiles/r05_tb64_2cg_ab.txt).  Same MFMA sequence per
-// accumulator either way: bit-identical.  Half A's epilogues at steps 40 + 7j.
+// crop computes all 10 rows (8 fragments, rows 0-7 as blocks, 8-9 as 2x16).  With crop ranges
+// (NCG = 2) wave w computes BOTH cout groups of half the fragments (4w .. 4w+3 of the full
+// set, 3w .. 3w+2 of the shifted one): each B fragment read from LDS feeds two MFMAs (round 5:
+// with one cout group per wave, one ds_read_b128 per MFMA made LDS the bound -- a timing probe
+// reading half the fragments ran 134 -> 96 us per block, profiles/r05_tb64_2cg_ab.txt).  The
+// strided mode (one or two tiles per workgroup) keeps one cout group per wave (NCG = 1: cout
+// group w, every fragment): there the twice-as-large weight load of the 2-group form is not
+// amortised (40 crops: 20.8 -> 24.1 us per block).  Same MFMA sequence per accumulator in
+// every form: bit-identical.  Half A's epilogues at steps 40 + 7j.
 template <bool ST>
 __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, int w, int lane, int n_items,
                                            int crop0) {
     using G = B64;
     constexpr int H = G::H, TH = G::TH, RS = G::RS, CGB = 4 * G::HSM * 16;  // cout group 1: planes 4-7
-    constexpr int PF = ST ? 1 : kPF;  // the strided variant's extra tile arithmetic: no VGPRs left for 2
+    constexpr int NCG = ST ? 1 : 2, FF = G::F1 / NCG, FS = 6 / NCG, PF = kPF;
     const int h = lane >> 5, r32 = lane & 31;
-    bf16x8 wa[2][G::KS];
-    load_weights(p.w1, 0, r32, h, wa[0]);
-    load_weights(p.w1, 1, r32, h, wa[1]);
+    auto cg_of = [&](int ci) { return NCG == 2 ? ci : w; };
+    bf16x8 wa[NCG][G::KS];
+#pragma unroll
+    for (int ci = 0; ci < NCG; ci++) load_weights(p.w1, cg_of(ci), r32, h, wa[ci]);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     // fragment t, lane r32: intermediate pixel (r, x); its input tap (0, 0) is halo pixel
     // (r, x - 1) = slot r * RS + x, and it lands in intermediate slot r * RS + x + 1 (cout
     // group 0's planes; group 1's are CGB bytes on).  Full set (first tile of a crop):
     // frag_pixel64; shifted set (s > 0): 8x4 blocks at rows 2-9.
-    int bvf[4], mwf[4], rf[4], bvs[3], mws[3], rs3[3];
+    int bvf[FF], mwf[FF], rf[FF], bvs[FS], mws[FS], rs3[FS];
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
+    for (int t = 0; t < FF; t++) {
         int r, x;
         bool pad;
-        frag_pixel64(4 * w + t, r32, r, x, pad);
+        frag_pixel64((NCG == 2 ? 4 * w : 0) + t, r32, r, x, pad);
         bvf[t] = (h * G::HSP + r * RS + x) * 16;
         mwf[t] = pad ? -1 : G::MOFF + (2 * h * G::HSM + r * RS + x + 1) * 16;
         rf[t] = r;
     }
     {  // fragment t of the shifted set is fragment 0's block moved 4 columns per step
-        const int r = 2 + blk_row(r32), x = 12 * w + blk_col(r32);
+        const int r = 2 + blk_row(r32), x = (NCG == 2 ? 12 * w : 0) + blk_col(r32);
         const int bv0 = (h * G::HSP + r * RS + x) * 16, mw0 = G::MOFF + (2 * h * G::HSM + r * RS + x + 1) * 16;
 #pragma unroll
-        for (int t = 0; t < 3; t++) {
+        for (int t = 0; t < FS; t++) {
             bvs[t] = bv0 + 64 * t;
             mws[t] = mw0 + 64 * t;
             rs3[t] = r;
         }
     }
-    // one tile: NA fragments in half A, NB in half B, both cout groups each
+    // one tile: NA fragments in half A, NB in half B, NCG cout groups each
     auto tile_body = [&](auto na_tag, auto nb_tag, const int* bv1, const int* mw, const int* rr, int k, int ho0) {
         constexpr int NA = decltype(na_tag)::value, NB = decltype(nb_tag)::value, NM = NA > NB ? NA : NB;
-        f32x16 accA[NA][2], accB[NB][2];
-        accA[0][0] = bias_acc(lds, 0, 0, h);
-        accA[0][1] = bias_acc(lds, 0, 1, h);
+        f32x16 accA[NA][NCG], accB[NB][NCG];
 #pragma unroll
-        for (int t = 0; t < NB; t++) {
-            accB[t][0] = accA[0][0];
-            accB[t][1] = accA[0][1];
-        }
+        for (int ci = 0; ci < NCG; ci++) {
+            accA[0][ci] = bias_acc(lds, 0, cg_of(ci), h);
 #pragma unroll
-        for (int t = 1; t < NA; t++) {
-            accA[t][0] = accA[0][0];
-            accA[t][1] = accA[0][1];
+            for (int t = 0; t < NB; t++) accB[t][ci] = accA[0][ci];
+#pragma unroll
+            for (int t = 1; t < NA; t++) accA[t][ci] = accA[0][ci];
         }
         const int xo = (k & 1) * G::XBYTES, mo = (k & 1) * G::MBYTES;
         bf16x8 fb[PF + 1][NM];
@@ -282,14 +282,14 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
                 fb[g % (PF + 1)][t] = *reinterpret_cast<const bf16x8*>(
                     lds + xo + bv1[t0 + t] + ((4 * c + 2 * ks) * G::HSP + dy * RS + dx) * 16);
         };
-        auto epilogue = [&](int t, int cg, const f32x16& a) {
+        auto epilogue = [&](int t, int ci, const f32x16& a) {
             if (mw[t] < 0) return;
             // rows outside the image are conv2's zero padding
             const bool live = (unsigned)(ho0 - 1 + rr[t]) < (unsigned)H;
             uint32_t o[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) o[e] = live ? pack_bf16x2(relu1(a[2 * e]), relu1(a[2 * e + 1])) : 0u;
-            uint8_t* d = lds + mw[t] + mo + cg * CGB;
+            uint8_t* d = lds + mw[t] + mo + cg_of(ci) * CGB;
             *reinterpret_cast<uint4*>(d) = uint4{o[0], o[1], o[2], o[3]};
             *reinterpret_cast<uint4*>(d + G::HSM * 16) = uint4{o[4], o[5], o[6], o[7]};
         };
@@ -302,28 +302,29 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
 #pragma unroll
                 for (int t = 0; t < NA; t++)
 #pragma unroll
-                    for (int cg = 0; cg < 2; cg++)
-                        accA[t][cg] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cg][s], fb[g % (PF + 1)][t], accA[t][cg], 0, 0, 0);
+                    for (int ci = 0; ci < NCG; ci++)
+                        accA[t][ci] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ci][s], fb[g % (PF + 1)][t], accA[t][ci], 0, 0, 0);
             } else {
 #pragma unroll
                 for (int t = 0; t < NB; t++)
 #pragma unroll
-                    for (int cg = 0; cg < 2; cg++)
-                        accB[t][cg] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cg][s], fb[g % (PF + 1)][t], accB[t][cg], 0, 0, 0);
+                    for (int ci = 0; ci < NCG; ci++)
+                        accB[t][ci] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ci][s], fb[g % (PF + 1)][t], accB[t][ci], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (g >= 40 && (g - 40) % 7 == 0 && (g - 40) / 7 < 2 * NA)
-                epilogue((g - 40) / 14, ((g - 40) / 7) & 1, accA[(g - 40) / 14][((g - 40) / 7) & 1]);
+            if constexpr (g >= 40 && (g - 40) % 7 == 0 && (g - 40) / 7 < NCG * NA) {
+                constexpr int j = (g - 40) / 7;
+                epilogue(j / NCG, j % NCG, accA[j / NCG][j % NCG]);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
         TB64_STAMP(k, 1);
 #pragma unroll
-        for (int t = 0; t < NB; t++) {
-            epilogue(NA + t, 0, accB[t][0]);
-            epilogue(NA + t, 1, accB[t][1]);
-        }
+        for (int t = 0; t < NB; t++)
+#pragma unroll
+            for (int ci = 0; ci < NCG; ci++) epilogue(NA + t, ci, accB[t][ci]);
     };
     barrier();  // prologue: tile 0's halo and the zeroed intermediate
     for (int k = 0; k < n_items; k++) {
@@ -332,7 +333,7 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
         tile_of64<ST>(crop0, k, n_, s);
         const int ho0 = s * TH;
         if (s == 0 || ST) {  // strided tiles: no previous tile of the crop in the other buffer
-            tile_body(std::integral_constant<int, 2>{}, std::integral_constant<int, 2>{}, bvf, mwf, rf, k, ho0);
+            tile_body(std::integral_constant<int, FF / 2>{}, std::integral_constant<int, FF / 2>{}, bvf, mwf, rf, k, ho0);
         } else {
             // rows 0-1 = the previous tile's rows 8-9 (planes 4w .. 4w+3, pads included)
             const int mo = (k & 1) * G::MBYTES, mp = ((k - 1) & 1) * G::MBYTES;
@@ -342,7 +343,8 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
                 *reinterpret_cast<uint4*>(lds + so + mo) =
                     *reinterpret_cast<const uint4*>(lds + so + mp + 8 * RS * 16);
             }
-            tile_body(std::integral_constant<int, 2>{}, std::integral_constant<int, 1>{}, bvs, mws, rs3, k, ho0);
+            tile_body(std::integral_constant<int, NCG == 2 ? 2 : 3>{}, std::integral_constant<int, NCG == 2 ? 1 : 3>{}, bvs,
+                      mws, rs3, k, ho0);
         }
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
         TB64_STAMP(k, 2);
@@ -409,30 +411,32 @@ __device__ __forceinline__ void issue_halo(const HaloSrc& hs, uint8_t* lds, int 
 
 // conv2 schedule over the 72 steps: DMA piece j at step 1 + 2j (all before the first
 // output store, so the phase-end vmcnt wait counts only stores); half A's epilogues (2
-// fragments x 2 cout groups) at steps 40, 47, 54, 61.
+// fragments x 2 cout groups; strided mode: 3 x 1) at steps 40 + 7j.
 constexpr int kDmaStep0 = 1, kDmaStride = 2;
 static_assert(kDmaStep0 + kDmaStride * (B64::XPPW - 1) < 40, "DMA pieces precede the stores");
 
 // conv2 waves (w = 0, 1): in phase k, the halo DMA of tile k+1 (planes w, w + 2, ...) and
 // conv2 of tile k-1 from intermediate buffer (k-1) & 1 + bias + residual (from the input ring)
-// + ReLU -> y, both cout groups of fragments 3w .. 3w+2 (half A: 2 fragments, half B: 1).
+// + ReLU -> y: both cout groups of fragments 3w .. 3w+2 (half A: 2 fragments, half B: 1), or in
+// the strided mode (NCG = 1) cout group w of all 6 fragments (3 + 3).
 template <bool ST>
 __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, int w, int lane, int n_items,
                                            const uint16_t* zl, int crop0) {
     using G = B64;
-    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS, NA = 2, NF = 3;
-    constexpr int PF = ST ? 1 : kPF;
-    const int h = lane >> 5, r32 = lane & 31, dw = w;
-    bf16x8 wa[2][G::KS];
-    load_weights(p.w2, 0, r32, h, wa[0]);
-    load_weights(p.w2, 1, r32, h, wa[1]);
+    constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS, PF = kPF;
+    constexpr int NCG = ST ? 1 : 2, NF = G::F2 / NCG, NA = NCG == 2 ? 2 : 3, NB = NF - NA, NM = NA > NB ? NA : NB;
+    const int h = lane >> 5, r32 = lane & 31, dw = w, f0 = NCG == 2 ? 3 * w : 0;
+    auto cg_of = [&](int ci) { return NCG == 2 ? ci : w; };
+    bf16x8 wa[NCG][G::KS];
+#pragma unroll
+    for (int ci = 0; ci < NCG; ci++) load_weights(p.w2, cg_of(ci), r32, h, wa[ci]);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
-    // fragment t, lane r32: output pixel (r, x) = (blk_row, 4 (3w + t) + blk_col); its tap
+    // fragment t, lane r32: output pixel (r, x) = (blk_row, 4 (f0 + t) + blk_col); its tap
     // (0, 0) is intermediate pixel (r, x - 1) = slot r * RS + x
     int bv2[NF];
     const int er = blk_row(r32), ex = blk_col(r32);
 #pragma unroll
-    for (int t = 0; t < NF; t++) bv2[t] = G::MOFF + (h * G::HSM + er * RS + 12 * w + ex) * 16 + 64 * t;
+    for (int t = 0; t < NF; t++) bv2[t] = G::MOFF + (h * G::HSM + er * RS + 4 * f0 + ex) * 16 + 64 * t;
     issue_halo(halo_src<ST>(p, crop0, 0, 0, true), lds, dw, lane, zl);
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
     barrier();  // prologue
@@ -446,50 +450,53 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
         tile_of64<ST>(crop0, kp, n, sp);
         const int ho0 = sp * TH;
         const long pix0 = ((long)n * H + ho0) * W;
-        f32x16 accA[NA][2], accB[2];
-        accA[0][0] = bias_acc(lds, 1, 0, h);
-        accA[0][1] = bias_acc(lds, 1, 1, h);
+        f32x16 accA[NA][NCG], accB[NB][NCG];
+#pragma unroll
+        for (int ci = 0; ci < NCG; ci++) accA[0][ci] = bias_acc(lds, 1, cg_of(ci), h);
         // the residual = tile k-1's input, still in ring slot (k-1) & 1 (halo rows 2-9): read
         // before this phase's DMA pieces start overwriting that slot with tile k+1
-        uint4 rv[NF][2][2];
+        uint4 rv[NF][NCG][2];
         {
             const uint8_t* rb = lds + (kp & 1) * G::XBYTES + (2 * h * G::HSP + (er + 2) * RS + ex + 1) * 16;
 #pragma unroll
             for (int t = 0; t < NF; t++)
 #pragma unroll
-                for (int cg = 0; cg < 2; cg++) {
-                    const uint8_t* q = rb + (4 * cg * G::HSP + 4 * (3 * w + t)) * 16;
-                    rv[t][cg][0] = *reinterpret_cast<const uint4*>(q);
-                    rv[t][cg][1] = *reinterpret_cast<const uint4*>(q + G::HSP * 16);
+                for (int ci = 0; ci < NCG; ci++) {
+                    const uint8_t* q = rb + (4 * cg_of(ci) * G::HSP + 4 * (f0 + t)) * 16;
+                    rv[t][ci][0] = *reinterpret_cast<const uint4*>(q);
+                    rv[t][ci][1] = *reinterpret_cast<const uint4*>(q + G::HSP * 16);
                 }
         }
-        accB[0] = accA[0][0];
-        accB[1] = accA[0][1];
-        accA[1][0] = accA[0][0];
-        accA[1][1] = accA[0][1];
+#pragma unroll
+        for (int ci = 0; ci < NCG; ci++) {
+#pragma unroll
+            for (int t = 0; t < NB; t++) accB[t][ci] = accA[0][ci];
+#pragma unroll
+            for (int t = 1; t < NA; t++) accA[t][ci] = accA[0][ci];
+        }
         __builtin_amdgcn_s_waitcnt(kWaitLgkm0);
         __builtin_amdgcn_sched_barrier(0);
         const HaloSrc hn = halo_src<ST>(p, crop0, k + 1, (k + 1) & 1, k + 1 < n_items);
         const uint16_t* blk = nullptr;
         const int mo = (kp & 1) * G::MBYTES;
-        bf16x8 fb[PF + 1][NA];
+        bf16x8 fb[PF + 1][NM];
         auto load = [&](auto Gs) {
-            constexpr int g = Gs, s = g % 36, t0 = g < 36 ? 0 : NA, nt = g < 36 ? NA : 1;
+            constexpr int g = Gs, s = g % 36, t0 = g < 36 ? 0 : NA, nt = g < 36 ? NA : NB;
             constexpr int c = s / 18, tap = (s % 18) >> 1, ks = s & 1, dy = tap / 3, dx = tap % 3;
 #pragma unroll
             for (int t = 0; t < nt; t++)
                 fb[g % (PF + 1)][t] = *reinterpret_cast<const bf16x8*>(
                     lds + mo + bv2[t0 + t] + ((4 * c + 2 * ks) * G::HSM + dy * RS + dx) * 16);
         };
-        auto epilogue = [&](int t, int cg, const f32x16& a) {
+        auto epilogue = [&](int t, int ci, const f32x16& a) {
             uint32_t o[8];
 #pragma unroll
             for (int e = 0; e < 8; e++) {
-                const uint4 rr = rv[t][cg][e >> 2];
+                const uint4 rr = rv[t][ci][e >> 2];
                 const uint32_t u = (e & 3) == 0 ? rr.x : (e & 3) == 1 ? rr.y : (e & 3) == 2 ? rr.z : rr.w;
                 o[e] = pack_bf16x2(relu1(a[2 * e] + lo_bf16(u)), relu1(a[2 * e + 1] + hi_bf16(u)));
             }
-            uint16_t* yp = p.y + (pix0 + er * W + 4 * (3 * w + t) + ex) * 64 + 32 * cg + 16 * h;
+            uint16_t* yp = p.y + (pix0 + er * W + 4 * (f0 + t) + ex) * 64 + 32 * cg_of(ci) + 16 * h;
             *reinterpret_cast<uint4*>(yp) = uint4{o[0], o[1], o[2], o[3]};
             *reinterpret_cast<uint4*>(yp + 8) = uint4{o[4], o[5], o[6], o[7]};
         };
@@ -502,13 +509,16 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
 #pragma unroll
                 for (int t = 0; t < NA; t++)
 #pragma unroll
-                    for (int cg = 0; cg < 2; cg++)
-                        accA[t][cg] =
-                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cg][s], fb[g % (PF + 1)][t], accA[t][cg], 0, 0, 0);
+                    for (int ci = 0; ci < NCG; ci++)
+                        accA[t][ci] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ci][s], fb[g % (PF + 1)][t], accA[t][ci], 0, 0, 0);
             } else {
 #pragma unroll
-                for (int cg = 0; cg < 2; cg++)
-                    accB[cg] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[cg][s], fb[g % (PF + 1)][0], accB[cg], 0, 0, 0);
+                for (int t = 0; t < NB; t++)
+#pragma unroll
+                    for (int ci = 0; ci < NCG; ci++)
+                        accB[t][ci] =
+                            __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa[ci][s], fb[g % (PF + 1)][t], accB[t][ci], 0, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (g >= kDmaStep0 && (g - kDmaStep0) % kDmaStride == 0 &&
@@ -517,17 +527,21 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
                 if constexpr (j % 4 == 0) blk = halo_block(hn, lane, zl, j / 4);
                 halo_piece(hn, blk, lds, dw, j);
             }
-            if constexpr (g >= 40 && (g - 40) % 7 == 0 && (g - 40) / 7 < 2 * NA)
-                epilogue((g - 40) / 14, ((g - 40) / 7) & 1, accA[(g - 40) / 14][((g - 40) / 7) & 1]);
+            if constexpr (g >= 40 && (g - 40) % 7 == 0 && (g - 40) / 7 < NCG * NA) {
+                constexpr int j = (g - 40) / 7;
+                epilogue(j / NCG, j % NCG, accA[j / NCG][j % NCG]);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
         TB64_STAMP(k, 1);
-        epilogue(NA, 0, accB[0]);
-        epilogue(NA, 1, accB[1]);
+#pragma unroll
+        for (int t = 0; t < NB; t++)
+#pragma unroll
+            for (int ci = 0; ci < NCG; ci++) epilogue(NA + t, ci, accB[t][ci]);
         TB64_STAMP(k, 2);
-        // the next tile's halo has landed (only this phase's 4 NF output stores, all issued
+        // the next tile's halo has landed (only this phase's 2 x 6 output stores, all issued
         // after the last DMA piece, may still be in flight)
-        __builtin_amdgcn_s_waitcnt(wait_vm(4 * NF));
+        __builtin_amdgcn_s_waitcnt(wait_vm(2 * G::F2));
         TB64_STAMP(k, 3);
         barrier();
     }
