@@ -71,7 +71,7 @@ def spawn_ranks(n):
 
 # The committed PMC traffic pass the roofline lines cite (tools/pmc_traffic.py): named explicitly —
 # a newest-file rule picked r04zz_ over r04zz2_ by lexicographic order in round 4.
-TRAFFIC_FILE = "profiles/r05i_traffic.json"
+TRAFFIC_FILE = "profiles/r05k_traffic.json"
 
 
 def committed_traffic():
