@@ -110,7 +110,7 @@ struct TB64Params {
     const uint16_t* zero;
     int N, n_tiles;
 #ifdef TB64_STAMPS
-    unsigned long long* stamps;  // [block][wave][phase < 16][4] s_memtime (tools/tb64_stamps.hip)
+    unsigned long long* stamps;  // [block][wave][4] s_memtime segment sums (tools/tb64_stamps.hip)
 #endif
 };
 
@@ -156,15 +156,38 @@ __device__ __forceinline__ f32x16 bias_acc(const uint8_t* lds, int conv, int cg,
 }
 
 #ifdef TB64_STAMPS
-#define TB64_STAMP(k, i)                                                                                     \
-    do {                                                                                                     \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                         \
-        if ((k) < 16 && (threadIdx.x & 63) == 0)                                                             \
-            p.stamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 + (k)) * 4 + (i)] = t_;                    \
+// Per-wave segment sums of s_memtime (tools/tb64_stamps.hip): stamp i closes segment i - 1 of
+// the phase (stamp 0 the role's last one); wave-uniform scalars, written once at the role's end
+// (per-phase stamps stored to memory needed VGPRs the two-group kernel does not have).
+#define TB64_STAMP_DECL(ns)                                     \
+    constexpr int tb_ns_ = (ns);                                \
+    unsigned long long tb_sum_[4] = {0, 0, 0, 0}, tb_last_ = 0; \
+    bool tb_on_ = false
+#define TB64_STAMP(k, i)                                                  \
+    do {                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();      \
+        if ((i) > 0)                                                      \
+            tb_sum_[(i) > 0 ? (i) - 1 : 0] += t_ - tb_last_;              \
+        else if (tb_on_)                                                  \
+            tb_sum_[tb_ns_ - 1] += t_ - tb_last_;                         \
+        tb_on_ = true;                                                    \
+        tb_last_ = t_;                                                    \
+    } while (0)
+#define TB64_STAMP_FLUSH()                                                                        \
+    do {                                                                                          \
+        if ((threadIdx.x & 63) == 0)                                                              \
+            for (int i_ = 0; i_ < 4; i_++)                                                        \
+                p.stamps[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + i_] = tb_sum_[i_];  \
     } while (0)
 #else
+#define TB64_STAMP_DECL(ns) \
+    do {                    \
+    } while (0)
 #define TB64_STAMP(k, i) \
     do {                 \
+    } while (0)
+#define TB64_STAMP_FLUSH() \
+    do {                   \
     } while (0)
 #endif
 
@@ -231,6 +254,7 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
     constexpr int H = G::H, TH = G::TH, RS = G::RS, CGB = 4 * G::HSM * 16;  // cout group 1: planes 4-7
     constexpr int NCG = ST ? 1 : 2, FF = G::F1 / NCG, FS = 6 / NCG, PF = kPF;
     const int h = lane >> 5, r32 = lane & 31;
+    TB64_STAMP_DECL(3);
     auto cg_of = [&](int ci) { return NCG == 2 ? ci : w; };
     bf16x8 wa[NCG][G::KS];
 #pragma unroll
@@ -351,6 +375,7 @@ __device__ __forceinline__ void conv1_role(const TB64Params& p, uint8_t* lds, in
         barrier();
     }
     barrier();  // the conv2 waves' last phase
+    TB64_STAMP_FLUSH();
 }
 
 // Input halo of tile k into ring slot buf, by the two conv2 waves (dw = 0, 1).  Piece
@@ -426,6 +451,7 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
     constexpr int W = G::W, H = G::H, TH = G::TH, RS = G::RS, PF = kPF;
     constexpr int NCG = ST ? 1 : 2, NF = G::F2 / NCG, NA = NCG == 2 ? 2 : 3, NB = NF - NA, NM = NA > NB ? NA : NB;
     const int h = lane >> 5, r32 = lane & 31, dw = w, f0 = NCG == 2 ? 3 * w : 0;
+    TB64_STAMP_DECL(4);
     auto cg_of = [&](int ci) { return NCG == 2 ? ci : w; };
     bf16x8 wa[NCG][G::KS];
 #pragma unroll
@@ -546,6 +572,7 @@ __device__ __forceinline__ void conv2_role(const TB64Params& p, uint8_t* lds, in
         barrier();
     }
     __builtin_amdgcn_s_waitcnt(wait_vm(0));
+    TB64_STAMP_FLUSH();
 }
 
 template <bool ST>

@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     int cus = 0;
     MVP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int tiles = N * G::TILES_H, grid = std::min(tiles, cus);
-    const size_t nst = (size_t)grid * 4 * 16 * 4;
+    const size_t nst = (size_t)grid * 4 * 4;
     MVP_HIP(hipMalloc(&x, nx * 2));
     MVP_HIP(hipMalloc(&y, nx * 2));
     MVP_HIP(hipMalloc(&w, 2 * nw * 2));
@@ -80,45 +80,28 @@ int main(int argc, char** argv) {
     std::vector<unsigned long long> h(nst);
     MVP_HIP(hipMemcpy(h.data(), st, nst * 8, hipMemcpyDeviceToHost));
     printf("N=%d grid=%d tiles=%d: %.1f us per launch (stamped build)\n", N, grid, tiles, ms * 1000 / reps);
-    // per role, per segment: median over blocks, phases 2..13
-    auto at = [&](int blk, int wave, int k, int i) { return (long long)h[((blk * 4 + wave) * 16 + k) * 4 + i]; };
-    // per tile kind: s = k % 4 == 0 (conv1 computes all 10 rows: 8 fragments) and s > 0 (rows 2-9: 6)
-    auto med = [](std::vector<long long> v) {
+    // per wave: s_memtime segment sums over the launch's phases (the last launch), per phase
+    const int phases = tiles / grid;  // tiles per workgroup (crop ranges: 4 per crop)
+    auto med = [](std::vector<double> v) {
         std::sort(v.begin(), v.end());
-        return v.empty() ? 0LL : v[v.size() / 2];
+        return v.empty() ? 0.0 : v[v.size() / 2];
     };
-    for (int kind = 0; kind < 2; kind++) {
-        std::vector<long long> c1_mfma, c1_epi, c1_bar, c2_mfma, c2_epi, c2_dma, c2_bar, phase;
-        for (int blk = 0; blk < grid; blk++)
-            for (int k = 2; k < 14; k++) {
-                if ((k % G::TILES_H == 0) != (kind == 0)) continue;
-                for (int wv = 0; wv < 2; wv++) {
-                    c1_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
-                    c1_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
-                    c1_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 2));
-                }
-                phase.push_back(at(blk, 0, k + 1, 0) - at(blk, 0, k, 0));
-                for (int wv = 2; wv < 4; wv++) {
-                    c2_mfma.push_back(at(blk, wv, k, 1) - at(blk, wv, k, 0));
-                    c2_epi.push_back(at(blk, wv, k, 2) - at(blk, wv, k, 1));
-                    c2_dma.push_back(at(blk, wv, k, 3) - at(blk, wv, k, 2));
-                    c2_bar.push_back(at(blk, wv, k + 1, 0) - at(blk, wv, k, 3));
-                }
-            }
-        printf("%s: phase %lld cycles (s_memtime ticks)\n", kind == 0 ? "first tile of a crop (8 conv1 fragments)"
-                                                                        : "tiles 1-3 (6 conv1 fragments)",
-               med(phase));
-        printf("  conv1: mfma loop %lld, epilogue %lld, barrier wait %lld\n", med(c1_mfma), med(c1_epi), med(c1_bar));
-        printf("  conv2: setup+mfma %lld, residual wait+epilogue %lld, dma wait %lld, barrier wait %lld\n",
-               med(c2_mfma), med(c2_epi), med(c2_dma), med(c2_bar));
+    const char* c1[3] = {"k-loop (+ half A epilogues)", "half B epilogue", "barrier wait (+ next row copy)"};
+    const char* c2[4] = {"setup + k-loop (+ DMA, half A epilogues)", "half B epilogue", "halo vmcnt wait",
+                         "barrier wait"};
+    for (int role = 0; role < 2; role++) {
+        printf("%s waves, cycles per phase (median over workgroups):\n", role ? "conv2" : "conv1");
+        double tot = 0;
+        for (int i = 0; i < (role ? 4 : 3); i++) {
+            std::vector<double> v;
+            for (int blk = 0; blk < grid; blk++)
+                for (int w = 2 * role; w < 2 * role + 2; w++) v.push_back((double)h[(blk * 4 + w) * 4 + i] / phases);
+            const double m = med(v);
+            tot += m;
+            printf("  %-44s %8.0f\n", role ? c2[i] : c1[i], m);
+        }
+        printf("  %-44s %8.0f\n", "sum", tot);
     }
-    // the tick rate: the whole launch over the per-block sum of phases
-    {
-        std::vector<long long> span;
-        for (int blk = 0; blk < grid; blk++) span.push_back(at(blk, 0, 15, 0) - at(blk, 0, 1, 0));
-        std::sort(span.begin(), span.end());
-        printf("phases 1-15 of block median: %lld ticks\n", span[span.size() / 2]);
-    }
-    printf("ideal per phase: 216 MFMAs x 32 = %d cycles (tiles 1-3), conv1 288 x 32 = %d (first tile)\n", 216 * 32, 288 * 32);
+    printf("ideal MFMA cycles per wave per phase: 216 x 32 = 6912 (tiles 1-3), conv1 288 x 32 = 9216 (first tile)\n");
     return 0;
 }
