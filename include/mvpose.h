@@ -78,7 +78,13 @@ int mvp_camera_pack(const double* K_host, const double* dist5_host, const double
 #define MVP_TRI_EXACT_JACOBI 0x10
 /* OR-ed into mode: throughput solver whose float32 outputs are certified bit-identical to the
  * exact path's (mixed f32/fp64 undistortion, normal-equation inverse iteration; a point whose
- * f32 roundings cannot be proven equal is re-solved on the exact path by a second launch).
+ * f32 roundings fall inside the error bound is re-solved on the exact path by a second launch).
+ * The certification is EMPIRICAL, not a proof: the null vector's rounding-floor term uses
+ * constants fitted on 1.4 M synthetic and random points (the exact Jacobi's own error measured
+ * <= 0.025 eps*sqrt(trM/D2) where 0.2 is used, and D2/lambda3 <= 1.4; triangulate.hip
+ * null_vector_delta2).  tests/test_triangulate_gpu.py also asserts bit-identity on adversarial rigs (tiny
+ * baselines, points near the epipoles, near-parallel rays).  Pass MVP_TRI_EXACT_JACOBI where a
+ * proof is required.
  * Reference mode with 2 listed cameras; other cases run the default solver.  With
  * out_xyzw_dev != NULL every point takes the exact path (the float64 vectors are diagnostics). */
 #define MVP_TRI_TOLERANCE 0x20
@@ -233,6 +239,14 @@ int mvp_graph_arena_bytes(void* handle, int64_t* bytes_out);
  * Blocking (device-synchronising). */
 int mvp_graph_refresh_weights(void* handle);
 int mvp_graph_destroy(void* handle);
+/* Diagnostics (no reference counterpart): the kernel launches one mvp_graph_forward of `batch`
+ * crops issues, in order, as records of 4 int64 {launching op, route, crops, MACs of every op
+ * the launch covers}; route 1 fused BasicBlock, 2 transition twin, 3 s2 siblings, 4 head +
+ * fuse, 5 Bottleneck, 6 stem pair, 7 stem, 8 conv, 9 1x1 pair, 10 fuse sum.  Fails unless every
+ * op is covered by exactly one launch.  *covered_macs_out (optional) = the sum.
+ * tools/fwd_breakdown.py pairs the records with a kernel trace. */
+int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, int* n_records,
+                   int64_t* covered_macs_out);
 
 /* ---------------------------------------------------------------------------
  * Person detector: RTMDet-m (the reference's `detectors.coco_base`,

@@ -1349,6 +1349,16 @@ void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, 
 namespace {
 int g_det_cus = 0;
 
+// one workgroup per CU, a multiple of 8 (the XCD round robin of blockIdx)
+int det_band_grid() {
+    if (g_det_cus == 0) {
+        int dev = 0;
+        MVP_HIP(hipGetDevice(&dev));
+        MVP_HIP(hipDeviceGetAttribute(&g_det_cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    return std::max(8, g_det_cus / 8 * 8);
+}
+
 template <int W, int TR, int NWV>
 void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
     using C = BandCfg<W, TR>;
@@ -1358,13 +1368,7 @@ void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
                                     hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
         attr = true;
     }
-    if (g_det_cus == 0) {
-        int dev = 0;
-        MVP_HIP(hipGetDevice(&dev));
-        MVP_HIP(hipDeviceGetAttribute(&g_det_cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    // one workgroup per CU, a multiple of 8 (the XCD round robin of blockIdx)
-    const int grid = std::max(8, g_det_cus / 8 * 8);
+    const int grid = det_band_grid();
     hipLaunchKernelGGL((det_conv_band_kernel<W, TR, NWV>), dim3(grid), dim3(64 * NWV), C::LDS, s, p, wband);
 }
 }  // namespace
@@ -1388,13 +1392,15 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
               (npad + bn - 1) / bn, H, W, Ho, Wo, wimg};
     // band-halo kernel for the 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40
     // planes (det_conv_band_kernel)
-    if (wband && det_band_eligible(H, W, cin, npad, ks, stride)) {
+    // The kernel splits each XCD's grid/8 workgroups into groups of n_nb (one per cout block):
+    // a part with fewer than 8 * n_nb CUs would get no group at all, so it takes the GEMM path.
+    if (wband && det_band_eligible(H, W, cin, npad, ks, stride) &&
+        det_band_rows(npad) / kBandBN <= det_band_grid() / 8) {
         const char* e = getenv("MVPOSE_DET_BAND");  // tests: 0 = the im2col GEMM kernel
         if (!(e && e[0] == '0')) {
             if (n == 0) return;
             GParams pb = p;
             pb.n_nb = det_band_rows(npad) / kBandBN;
-            MVP_REQUIRE(pb.n_nb <= 32, "det band conv: %d cout blocks", pb.n_nb);  // <= workgroups per XCD
             MVP_REQUIRE((long)n * H / (W == 80 ? 4 : 8) < (1L << 24), "det band conv: too many bands");
             // 8 waves (two per SIMD) by default: 22.30 vs 23.33 ms per 128-frame forward with 4
             // (gpurun_out/detband5); MVPOSE_DET_BAND=4 keeps the 4-wave form (tests: bit-identical)

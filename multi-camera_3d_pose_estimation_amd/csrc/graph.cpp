@@ -943,6 +943,82 @@ extern "C" int mvp_graph_forward(void* handle, const void* input_dev, int batch,
     MVP_ABI_END
 }
 
+// Launch plan of one forward (diagnostics for tools/fwd_breakdown.py: pairs the kernel trace with
+// the graph's MACs so each kernel family gets its FLOP and MFMA fraction).  One record per kernel
+// launch, in launch order: {launching op, route, crops in the launch, MACs of every op it covers}.
+// route: 1 fused BasicBlock, 2 transition twin, 3 s2 siblings, 4 head + fuse, 5 Bottleneck,
+// 6 stem pair, 7 stem, 8 conv, 9 1x1 pair, 10 fuse sum.
+namespace {
+int64_t op_macs(const Graph& g, int k) {
+    const mvp_op_desc& op = g.ops[k];
+    if (op.kind != MVP_OP_CONV && op.kind != MVP_OP_STEM) return 0;
+    const mvp_tensor_desc& o = g.tensors[op.out];
+    const int cin = op.kind == MVP_OP_STEM ? 3 : op.cin;
+    return (int64_t)o.h * o.w * op.cout * cin * op.ks * op.ks;
+}
+}  // namespace
+
+extern "C" int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, int* n_records,
+                              int64_t* covered_macs_out) {
+    MVP_ABI_BEGIN
+    Graph* g = static_cast<Graph*>(handle);
+    MVP_REQUIRE(g && rec_out && n_records, "mvp_graph_plan: NULL pointer");
+    MVP_REQUIRE(batch > 0 && batch <= g->max_batch, "mvp_graph_plan: batch %d", batch);
+    const int no = (int)g->ops.size();
+    std::vector<int> seen(no, 0);
+    int n = 0;
+    int64_t total = 0;
+    for (const mvp::Segment& sg : g->segs) {
+        if (sg.last_op < sg.first_op) continue;
+        const int mb = (sg.micro_batch > 0 && sg.micro_batch < batch) ? sg.micro_batch : batch;
+        for (int64_t b0 = 0; b0 < batch; b0 += mb) {
+            const int nb = (int)std::min<int64_t>(mb, batch - b0);
+            for (int k = sg.first_op; k <= sg.last_op; k++) {
+                if (g->absorbed[k]) continue;
+                const mvp_op_desc& op = g->ops[k];
+                std::vector<int> cov{k};
+                int route;
+                if (g->block_head[k]) { route = 1; cov.push_back(k - 1); }
+                else if (g->twin[k] >= 0) { route = 2; cov.push_back(g->twin[k]); }
+                else if (!g->sib[k].empty()) { route = 3; cov.insert(cov.end(), g->sib[k].begin(), g->sib[k].end()); }
+                else if (g->head_src[k] >= 0) { route = 4; cov.push_back(g->head_src[k]); }
+                else if (g->bneck[k] >= 0) {
+                    route = 5;
+                    cov.push_back(g->bneck[k]);
+                    cov.push_back(g->bneck_mid[k]);
+                    if (g->cat_src[k] >= 0) cov.push_back(g->cat_src[k]);
+                }
+                else if (g->stem_head[k] >= 0) { route = 6; cov.push_back(g->stem_head[k]); }
+                else if (op.kind == MVP_OP_STEM) route = 7;
+                else if (op.kind == MVP_OP_CONV) {
+                    route = g->pair_tail[k] >= 0 ? 9 : 8;
+                    if (g->cat_src[k] >= 0) cov.push_back(g->cat_src[k]);
+                    if (g->pair_tail[k] >= 0) cov.push_back(g->pair_tail[k]);
+                } else route = 10;
+                int64_t macs = 0;
+                for (int c : cov) {
+                    macs += op_macs(*g, c);
+                    if (b0 == 0) seen[c]++;
+                }
+                macs *= nb;
+                total += macs;
+                if (n < max_records) {
+                    rec_out[4 * n + 0] = k;
+                    rec_out[4 * n + 1] = route;
+                    rec_out[4 * n + 2] = nb;
+                    rec_out[4 * n + 3] = macs;
+                }
+                n++;
+            }
+        }
+    }
+    for (int k = 0; k < no; k++)
+        MVP_REQUIRE(seen[k] == 1, "mvp_graph_plan: op %d covered by %d launches", k, seen[k]);
+    *n_records = n;
+    if (covered_macs_out) *covered_macs_out = total;
+    MVP_ABI_END
+}
+
 // The blobs were rewritten in place (e.g. a weight broadcast from rank 0 after the graph was
 // built): re-derive every weight the graph copied out of them at create time.  Blocking.
 extern "C" int mvp_graph_refresh_weights(void* handle) {

@@ -393,11 +393,16 @@ struct Decoder {
         b.get1();
         if (b.get1()) b.get(time_inc_bits);  // fixed_vop_rate
         b.get1();
-        width = (int)b.get(13);
+        const int vol_w = (int)b.get(13);
         b.get1();
-        height = (int)b.get(13);
+        const int vol_h = (int)b.get(13);
         b.get1();
-        MVP_REQUIRE(width > 0 && height > 0 && width <= 8192 && height <= 8192, "mp4v: frame %dx%d", width, height);
+        MVP_REQUIRE(vol_w > 0 && vol_h > 0 && vol_w <= 8192 && vol_h <= 8192, "mp4v: frame %dx%d", vol_w, vol_h);
+        // the caller sizes its output buffers from the first VOL: a later VOL (repeated before
+        // I-VOPs by encoders without a global header) must describe the same frame size
+        MVP_REQUIRE(!have_vol || (vol_w == width && vol_h == height),
+                    "mp4v: VOL changes the frame size from %dx%d to %dx%d inside one stream", width, height,
+                    vol_w, vol_h);
         MVP_REQUIRE(b.get1() == 0, "mp4v: interlaced video is not supported");
         b.get1();  // obmc_disable
         const int sprite = (int)b.get(verid == 1 ? 1 : 2);
@@ -429,8 +434,15 @@ struct Decoder {
             MVP_REQUIRE(b.get1() == 0, "mp4v: reduced-resolution VOPs are not supported");
         }
         MVP_REQUIRE(b.get1() == 0, "mp4v: scalability is not supported");
+        // a repeated VOL only refreshes per-VOL state (time_inc_bits, quant matrices, resync):
+        // the reference frames survive it, so a following P-VOP or not-coded VOP still
+        // predicts from / repeats the previous picture
+        if (!have_vol) {
+            width = vol_w;
+            height = vol_h;
+            alloc();
+        }
         have_vol = 1;
-        alloc();
     }
 
     // Scan `data` for start codes; VOL headers configure, VOPs decode.  Returns VOPs decoded.

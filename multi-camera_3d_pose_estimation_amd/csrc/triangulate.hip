@@ -328,7 +328,8 @@ __device__ __forceinline__ bool f32_rounding_stable(double c, double delta2) {
 // + 0.2 · eps · sqrt(tr M / D₂) (rounding floor of both solvers; eps·σ₁/σ₃ with D₂ the third
 //        LDLᵀ pivot of M = AᵀA standing in for λ₃: the exact Jacobi's own error measured
 //        <= 0.025 of it, the normal equations' floor <= 0.0033, D₂/λ₃ <= 1.4, on 1.4 M synthetic
-//        and random points: tools/tri_cert_emu.c)
+//        and random points: tools/tri_cert_emu.c — an EMPIRICAL bound, not a proof; the GPU
+//        tests add adversarial rigs: tiny baselines, points near the epipoles)
 // + 2^-50 (normalisation).  Returned doubled for f32_rounding_stable.
 __device__ __forceinline__ double null_vector_delta2(double dd, double prev, double cond2) {
     const float d = (float)dd, pv = (float)prev;

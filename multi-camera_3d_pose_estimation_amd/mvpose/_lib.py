@@ -64,6 +64,7 @@ SIGNATURES = {
     "mvp_graph_arena_bytes": (c_int, None),
     "mvp_graph_refresh_weights": (c_int, [c_void_p]),
     "mvp_graph_destroy": (c_int, [c_void_p]),
+    "mvp_graph_plan": (c_int, [c_void_p, c_int, c_void_p, c_int, P(c_int), P(c_int64)]),
     "mvp_det_letterbox": (c_int, [c_void_p, c_int, c_int, c_int, c_int, P(c_float), P(c_float), c_void_p,
                                   c_void_p]),
     # detector graph argtypes with struct pointers are (re)declared in mvpose/rtmdet.py

@@ -584,6 +584,20 @@ class ConvGraph:
         call("mvp_graph_arena_bytes", self._h, ctypes.byref(b))
         return b.value
 
+    def launch_plan(self, batch: int) -> np.ndarray:
+        """(n_launches, 4) int64 {launching op, route, crops, MACs} of one forward of `batch`
+        crops in launch order (mvp_graph_plan; tools/fwd_breakdown.py pairs it with a trace)."""
+        cap = 4096
+        rec = np.zeros((cap, 4), np.int64)
+        n, tot = ctypes.c_int(), ctypes.c_int64()
+        call("mvp_graph_plan", self._h, int(batch), ctypes.c_void_p(rec.ctypes.data), cap, ctypes.byref(n),
+             ctypes.byref(tot))
+        if n.value > cap:
+            raise RuntimeError(f"{n.value} launches > {cap}")
+        rec = rec[:n.value].copy()
+        assert int(rec[:, 3].sum()) == tot.value == self.macs_per_crop() * batch
+        return rec
+
     def macs_per_crop(self) -> int:
         macs = 0
         for op in self.spec.ops:

@@ -234,8 +234,11 @@ class Mp4vDecoder:
         n = ctypes.c_int()
         if yuv:
             cw, ch = (self.width + 1) // 2, (self.height + 1) // 2
+            size = self.width * self.height + 2 * cw * ch
             if out is None:
-                out = np.empty(self.width * self.height + 2 * cw * ch, np.uint8)
+                out = np.empty(size, np.uint8)
+            if out.dtype != np.uint8 or out.size != size or not out.flags.c_contiguous:
+                raise ValueError(f"out must be a C-contiguous uint8 array of {size} bytes (I420 planes)")
             self._lib.call("mvp_mp4v_decode", self._h, data.ctypes.data, data.size, None, out.ctypes.data,
                            ctypes.byref(n))
             return out

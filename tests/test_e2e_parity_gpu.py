@@ -24,8 +24,8 @@ Asserted per workload (tolerances in LIMITS; measured rates printed and recorded
   (|h[x+1] - h[x-1]| <= MARGIN x max|h|: bf16 cannot decide it), and is bit-exact on
   >= exact_min of those maps;
 * where both views' x, y are bit-exact and the camera order (ascending score, the
-  reference's top-2 rule) agrees, kpts_3d is within 1e-4 world units — on >= k3_min of
-  all joints.
+  reference's top-2 rule) agrees, kpts_3d is bit-identical (the north_star's 1e-4 mm is
+  below one float32 ulp in cm) — on >= k3_min of all joints.
 """
 import numpy as np
 import pytest
@@ -172,12 +172,19 @@ def test_keypoints_where_argmax_agrees(runs):
 
 
 def test_kpts_3d_where_inputs_agree(runs):
+    """north_star: kpts_3d within 1e-4 mm of the reference triangulation on identical 2D inputs.
+    World units are cm, so the bound is 1e-5 cm, below one float32 ulp (~3e-5 cm at
+    these ~350 cm coordinates): it means BIT-IDENTICAL.  The pipeline's triangulation is
+    certified bit-identical to the OpenCV-4.9 restatement (tests/test_triangulate_gpu.py), so
+    wherever both views' x, y are bit-exact and the camera order agrees (np.argsort ascending:
+    camera 1 first only when score0 > score1, a tie keeps [0, 1]; pose_estimation.py:32-41),
+    kpts_3d is asserted array_equal — anything else is a bug, not rounding."""
     g2, o2 = runs["gpu"]["kpts_2d"], runs["k2"]
     xy_exact = (g2[:, :, :2, :] == o2[:, :, :2, :]).all(axis=(2, 3)) & _agree(runs).all(axis=2)  # (T, 17)
-    order_same = (g2[:, :, 2, 0] < g2[:, :, 2, 1]) == (o2[:, :, 2, 0] < o2[:, :, 2, 1])
+    order_same = (g2[:, :, 2, 0] > g2[:, :, 2, 1]) == (o2[:, :, 2, 0] > o2[:, :, 2, 1])
     sel = xy_exact & order_same
     d = np.abs(runs["gpu"]["kpts_3d"] - runs["k3"])[sel]
     print(f"[{runs['name']}] kpts_3d compared on {sel.sum()}/{sel.size} joints, "
-          f"max |d| {np.nanmax(d) if d.size else 0:.3g}")
+          f"max |d| {np.nanmax(d) if d.size else 0:.3g} cm")
     assert sel.sum() > 0 and sel.sum() >= runs["lim"]["k3_min"] * sel.size
-    np.testing.assert_allclose(runs["gpu"]["kpts_3d"][sel], runs["k3"][sel], rtol=0, atol=1e-4)
+    np.testing.assert_array_equal(runs["gpu"]["kpts_3d"][sel], runs["k3"][sel])

@@ -327,3 +327,32 @@ def test_parallel_gop_decode_equals_serial():
         for threads in (1, 4):
             got = video.decode_mp4v(cfg, samples, *sl, threads=threads)
             np.testing.assert_array_equal(got, serial[slice(*sl)], err_msg=f"{sl} threads={threads}")
+
+
+def test_repeated_vol_keeps_the_reference_frame():
+    """A VOL repeated in front of a P-VOP or a not-coded VOP (encoders without a global header
+    repeat it) refreshes per-VOL state only: the P-VOP still predicts from the previous picture
+    and a not-coded VOP still repeats it (alloc() used to reset both to grey)."""
+    cfg, samples = _stream(n_p=3)
+    dec = video.Mp4vDecoder(cfg)
+    plain = [dec.decode(s).copy() for s in samples]
+    dec.close()
+    dec = video.Mp4vDecoder(cfg)
+    again = [dec.decode(s if k == 0 else cfg + s).copy() for k, s in enumerate(samples)]
+    dec.close()
+    for k, (a, b) in enumerate(zip(plain, again)):
+        np.testing.assert_array_equal(a, b, err_msg=f"frame {k}")
+
+
+def test_vol_size_change_is_rejected():
+    """A later VOL that changes the frame size inside one stream raises instead of writing the
+    new size into buffers sized from the first VOL (heap overflow in host code)."""
+    cfg, samples = _stream(n_p=1)
+    w, h = WH
+    dec = video.Mp4vDecoder(cfg)
+    dec.decode(samples[0])
+    with pytest.raises(_lib.MvposeError, match="changes the frame size"):
+        dec.decode(W.vol_header(w + 16, h) + samples[1])
+    with pytest.raises(ValueError, match="I420"):
+        dec.decode(samples[1], yuv=True, out=np.empty(10, np.uint8))
+    dec.close()

@@ -348,3 +348,39 @@ def test_tolerance_mode_two_host_threads_one_stream(ops, monkeypatch):
     for i in range(2):
         for o in outs[i]:
             np.testing.assert_array_equal(o.cpu().numpy(), exact[i])
+
+
+def _adversarial_rig(baseline, seed):
+    """Camera 0 at the origin, camera 1 displaced by `baseline` cm sideways and slightly forward,
+    both looking at the subject: a tiny baseline makes the rays nearly parallel (sigma_4 close to
+    sigma_3 in A, the regime the empirical certification constants were not fitted on)."""
+    rng = np.random.default_rng(seed)
+    cams = syn.make_rig(2, seed=seed)
+    pos = np.array([baseline, rng.uniform(-0.1, 0.1) * baseline, 0.05 * baseline])
+    R, T = syn._look_at(pos, syn.SUBJECT_CENTER + np.array([0.0, 0.0, 0.0]))
+    cams[1]["R"], cams[1]["T"] = R, T
+    return cams
+
+
+@pytest.mark.parametrize("baseline", [0.05, 0.5, 5.0, 40.0])
+def test_tolerance_mode_adversarial_geometry(ops, baseline):
+    """the certification bound is empirical, so probe where it is weakest — tiny
+    baselines (near-parallel rays, ill-conditioned A), points on and near the baseline (the
+    epipoles: the two views see the point at the same spot), points far behind the subject and
+    sub-pixel noise.  Tolerance and default solvers stay bit-identical to the exact path, which
+    equals the oracle."""
+    cams = _adversarial_rig(baseline, seed=81)
+    cp = syn.reference_camera_params(cams)
+    rng = np.random.default_rng(82)
+    poses = syn.make_poses(400, seed=83)
+    c1 = -cams[1]["R"].T @ cams[1]["T"].reshape(3)                 # camera 1's centre
+    # frames 100-199: joints on the line through both centres (the epipoles) and beyond
+    s = rng.uniform(-3.0, 4.0, (100, 17, 1))
+    poses[100:200] = s * c1 + rng.normal(0.0, 1e-3 * max(baseline, 1.0), (100, 17, 3)) + np.array([0, 0, 0.5])
+    poses[200:300] *= rng.uniform(1.0, 30.0, (100, 17, 1))         # far points (up to ~100 m)
+    k = syn.make_kpts_2d(poses, cams, seed=84, noise_px=0.25)
+    (tol, ex), nfb = _fallbacks(ops, lambda: _tol_vs_exact(ops, cp, k))
+    print(f"baseline {baseline} cm: {nfb} of {k.shape[0] * 17} points re-solved on the exact path")
+    _check(ex, cv_ref.get_pose_3D(cp, k, camera_indices=[0, 1]))
+    _check(tol, ex)
+    _check(_run(ops, cp, k, [0, 1]), ex)
