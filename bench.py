@@ -72,6 +72,9 @@ def spawn_ranks(n):
 # The committed PMC traffic pass the roofline lines cite (tools/pmc_traffic.py): named explicitly —
 # a newest-file rule picked r04zz_ over r04zz2_ by lexicographic order in round 4.
 TRAFFIC_FILE = "profiles/r05k_traffic.json"
+# per-kernel-family breakdown of one 1,024-crop forward (tools/fwd_breakdown.sh: a kernel trace of
+# backbone forwards only, paired with the graph's launch plan for each launch's MACs)
+BREAKDOWN_FILE = "profiles/r06a_forward_breakdown.json"
 
 
 def committed_traffic():
@@ -650,7 +653,8 @@ def main():
                          "achieved": bb_tflops, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": bb_tflops / BF16_PEAK_TFLOPS,
                          "traffic": traffic.get("backbone", {}).get("hbm_bytes_per_launch"),
-                         "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": bb_ms},
+                         "traffic_source": traffic_src, "flops_per_launch": flops, "avg_launch_ms": bb_ms,
+                         "breakdown_source": BREAKDOWN_FILE},
         }
         res.update(extra)
         if world == 1 and not args.no_cpu_baseline:

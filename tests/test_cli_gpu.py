@@ -164,3 +164,65 @@ def test_cli_runs_the_detector_like_the_reference(project, monkeypatch, tmp_path
         for v in range(2):
             same = np.array_equal(whole[t, :, :, v], k2[t, :, :, v])
             assert same != bool(has_box[t, v]), (t, v, bool(has_box[t, v]))
+
+
+def _mp4v_recording(path, n_frames, w, h, seed):
+    """A per-camera mp4v MP4 (the reference's *_synced.mp4, synchronize_videos.py:64,240) written
+    from seeded coefficients and motion vectors by tests/mp4v_writer.py: I-VOP + P-VOPs."""
+    import mp4v_writer as W
+    rng = np.random.default_rng(seed)
+    mw, mh = w // 16, h // 16
+
+    def intra():
+        b = np.zeros((6, 64), np.int64)
+        for n in range(6):
+            b[n, 0] = rng.integers(40, 160) if n < 4 else rng.integers(80, 140)
+            m = rng.random(63) < 0.1
+            b[n, 1:][m] = rng.integers(-6, 7, m.sum())
+        return {"q": 4, "blocks": b, "ac_pred": False}
+
+    def inter():
+        b = np.zeros((6, 64), np.int64)
+        m = rng.random((6, 64)) < 0.03
+        b[m] = rng.integers(-3, 4, m.sum())
+        return {"type": "inter", "mv": (int(rng.integers(-9, 10)), int(rng.integers(-9, 10))), "blocks": b}
+
+    vw = W.VopWriter(w, h)
+    samples = [vw.i_vop([[intra() for _ in range(mw)] for _ in range(mh)], 4)]
+    samples += [vw.p_vop([[inter() for _ in range(mw)] for _ in range(mh)], 4, rounding=k % 2)
+                for k in range(n_frames - 1)]
+    with open(path, "wb") as f:
+        f.write(W.mp4_file(W.vol_header(w, h), samples, w, h))
+
+
+def test_mp4v_recordings_match_npy(project, monkeypatch, tmp_path):
+    """f2 on the GPU path: record_and_estimate_pose on per-camera mp4v MP4 recordings (what the
+    reference's synchronize_videos.py writes and utils.frame_generator reads back with
+    cv.VideoCapture, utils.py:849-909) writes kpts_2d / heatmaps_2d / kpts_3d equal, bit for bit,
+    to the run fed the same decoded frames as .npy stacks."""
+    from mvpose import cli, video
+    root, names, _, _ = project
+    monkeypatch.setenv("MVPOSE_RANDOM_WEIGHTS", "1")
+    monkeypatch.setenv("MVPOSE_NO_DETECTOR", "1")
+    monkeypatch.chdir(root)
+    runs = {}
+    for kind in ("mp4", "npy"):
+        rec = root / "configurations" / "1" / "recordings" / f"mp4v_{kind}"
+        rec.mkdir(parents=True, exist_ok=True)
+        paths = []
+        for v in range(2):
+            mp4 = tmp_path / f"camera{v}_synced.mp4"
+            if kind == "mp4":
+                _mp4v_recording(mp4, 5, 640, 352, seed=40 + v)
+                p = rec / f"camera{v}_synced.mp4"
+                p.write_bytes(mp4.read_bytes())
+            else:
+                p = rec / f"camera{v}.npy"
+                np.save(p, video.read_recording(mp4, 0, None))
+            paths.append(str(p))
+        log = cli.record_and_estimate_pose_main(["--camera_names", *names, "--configuration_number", "1",
+                                                 "--recording_paths", *paths])
+        runs[kind] = {k: np.load(log[k]) for k in ("kpts_2d", "heatmaps_2d", "kpts_3d")}
+    assert runs["mp4"]["kpts_2d"].shape == (4, 17, 3, 2)              # 5 frames, the last dropped ([0, -1])
+    for k in ("kpts_2d", "heatmaps_2d", "kpts_3d"):
+        np.testing.assert_array_equal(runs["mp4"][k], runs["npy"][k], err_msg=k)

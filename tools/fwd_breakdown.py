@@ -25,8 +25,8 @@ L = len(plan)
 
 
 def fam(r):
-    n = re.sub(r"\(mvp::.*|\(unsigned.*|\(.*", "", r["Kernel_Name"]).replace("void ", "")
-    return n.replace("mvp::(anonymous namespace)::", "").replace("mvp::", "")[:64]
+    n = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    return re.sub(r"\(.*", "", n).replace("mvp::", "")[:64]
 
 
 # the traced forwards: walk back from the end in blocks of L while the name sequence repeats
