@@ -448,6 +448,31 @@ int mvp_mp4v_decode(void* handle, const uint8_t* data, size_t bytes, uint8_t* bg
 int mvp_mp4v_destroy(void* handle);
 int mvp_mp4v_selfcheck(void);
 
+/* Split decode: the host entropy-decodes, the device reconstructs (bit-identical to
+ * mvp_mp4v_decode's frames; the decoded frames land in device memory).
+ *
+ * mvp_mp4v_parse : one sample with at most one VOP, on a handle that never decodes.  Writes one
+ *                  32-byte record per macroblock, raster order, to rec_out (host memory, rec_cap
+ *                  records >= macroblocks):
+ *                    uint8 kind (0 intra, 1 inter, 2 not coded = copy, 3 not reached), uint8 nnz[6],
+ *                    uint8 pad, int16 mv[4][2] (luma 8x8 vectors, half-pel), int16 cmv[2] (chroma),
+ *                    uint32 first coefficient entry;
+ *                  and the inverse-quantised coefficients as uint32 entries (raster position << 16 |
+ *                  uint16 value), block by block, to coef_out (*n_coef entries, at most coef_cap;
+ *                  384 per macroblock always suffices).  vop_out[0] = 1 coded VOP, 0 not coded,
+ *                  -1 no VOP in the sample; vop_out[1] = vop_rounding_type.
+ * mvp_mp4v_reconstruct : stream-ordered; jobs_dev = n_jobs device records of 48 bytes
+ *                  {const rec*, const coef*, uint8 cur*, const uint8 ref*, uint8 bgr* or NULL,
+ *                   int32 coded, int32 rounding}, all device pointers: the VOP's records and
+ *                  entries, the picture it writes and the previous one (each an I420 picture with
+ *                  macroblock-aligned planes: Y 16*mb_w x 16*mb_h, then U and V 8*mb_w x 8*mb_h;
+ *                  a slot's first pictures hold 128), and the [height][width][3] BGR frame out.
+ *                  Jobs must write distinct pictures; a coded VOP's cur is the slot's older
+ *                  picture (the host decoder's swap), a not-coded VOP outputs cur unchanged. */
+int mvp_mp4v_parse(void* handle, const uint8_t* data, size_t bytes, void* rec_out, int64_t rec_cap,
+                   uint32_t* coef_out, int64_t coef_cap, int64_t* n_coef, int* vop_out);
+int mvp_mp4v_reconstruct(const void* jobs_dev, int n_jobs, int width, int height, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

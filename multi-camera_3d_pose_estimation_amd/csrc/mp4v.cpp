@@ -29,6 +29,7 @@
 #include <cstring>
 #include <vector>
 
+#include "mp4v.h"
 #include "mp4v_tables.h"
 #include "mvp_common.h"
 
@@ -336,6 +337,32 @@ struct Decoder {
     // slice (video packet) state
     int resync_x = 0, resync_y = 0, first_line = 1;
     int mb_x = 0, mb_y = 0;
+    // split decode (mvp_mp4v_parse): one MbRec per macroblock and the inverse-quantised
+    // coefficients instead of pixels; the device reconstructs (mp4v_recon.hip).  A handle
+    // either decodes or parses (mode 1 / 2), never both: parsing leaves the host pictures stale.
+    int mode = 0;
+    MbRec* rec = nullptr;
+    uint32_t* coef = nullptr;
+    size_t coef_n = 0, coef_cap = 0;
+    int vop_coded = -1;
+
+    MbRec& cur_rec() { return rec[(size_t)mb_y * mb_w + mb_x]; }
+    void rec_begin(uint8_t kind) {
+        MbRec& r = cur_rec();
+        std::memset(&r, 0, sizeof(r));
+        r.kind = kind;
+        r.coef = (uint32_t)coef_n;
+    }
+    void emit_block(int n, const int16_t* blk) {
+        int k = 0;
+        for (int i = 0; i < 64; i++) {
+            if (!blk[i]) continue;
+            MVP_REQUIRE(coef_n < coef_cap, "mvp_mp4v_parse: coefficient buffer full (%zu entries)", coef_cap);
+            coef[coef_n++] = coef_entry(i, blk[i]);
+            k++;
+        }
+        cur_rec().nnz[n] = (uint8_t)k;
+    }
 
     int lidx(int bx, int by) const { return (by + 1) * b8s + bx + 1; }
     int cidx(int x, int y) const { return (y + 1) * cs + x + 1; }
@@ -484,7 +511,9 @@ struct Decoder {
         b.get1();
         b.get(time_inc_bits);
         b.get1();
+        vop_coded = 0;
         if (!b.get1()) return 0;  // vop_coded == 0: the previous frame again
+        vop_coded = 1;
         MVP_REQUIRE(vop_type == 0 || have_ref, "mp4v: P-VOP without a reference frame");
         if (vop_type == 1) rounding = b.get1();
         dc_thr = kDcThreshold[b.get(3)];
@@ -495,6 +524,11 @@ struct Decoder {
             MVP_REQUIRE(fcode > 0, "mp4v: vop_fcode_forward 0");
         }
         std::swap(cur, ref);  // cur becomes the new frame, ref the previous one
+        if (rec)
+            for (int i = 0; i < mb_w * mb_h; i++) {
+                std::memset(&rec[i], 0, sizeof(MbRec));
+                rec[i].kind = MB_LOST;
+            }
         resync_x = resync_y = 0;
         first_line = 1;
         for (mb_y = 0; mb_y < mb_h; mb_y++) {
@@ -706,6 +740,7 @@ struct Decoder {
 
     void intra_blocks(Bits& b, int cbp, bool ac_pred, bool use_dc_vlc) {
         const Tables& T = tables();
+        if (rec) rec_begin(MB_INTRA);
         for (int n = 0; n < 6; n++) {
             alignas(16) int16_t blk[64] = {};
             int dir = 0;
@@ -726,6 +761,10 @@ struct Decoder {
             store_dc(n, qdc);
             pred_ac(n, dir, ac_pred, blk);
             dequant(blk, true, n);
+            if (rec) {
+                emit_block(n, blk);
+                continue;
+            }
             int stride;
             uint8_t* d = block_dst(cur, n, &stride);
             idct_write(blk, d, stride, false);
@@ -887,7 +926,8 @@ struct Decoder {
             set_mv_all(0, 0);
             clear_intra_state();
             mbq[qidx(mb_x, mb_y)] = (int8_t)qscale;
-            copy_mb();
+            if (rec) rec_begin(MB_COPY);
+            else copy_mb();
             return;
         }
         int mcbpc;
@@ -935,6 +975,32 @@ struct Decoder {
             }
             set_mv_all(mvx[0], mvy[0]);
         }
+        int cmx, cmy;
+        if (mcbpc & 16) {
+            cmx = round_chroma4(mvx[0] + mvx[1] + mvx[2] + mvx[3]);
+            cmy = round_chroma4(mvy[0] + mvy[1] + mvy[2] + mvy[3]);
+        } else {
+            cmx = (mvx[0] >> 1) | (mvx[0] & 1);
+            cmy = (mvy[0] >> 1) | (mvy[0] & 1);
+        }
+        if (rec) {
+            rec_begin(MB_INTER);
+            MbRec& r = cur_rec();
+            for (int k = 0; k < 4; k++) {
+                r.mv[k][0] = (int16_t)mvx[k];
+                r.mv[k][1] = (int16_t)mvy[k];
+            }
+            r.cmv[0] = (int16_t)cmx;
+            r.cmv[1] = (int16_t)cmy;
+            for (int n = 0; n < 6; n++) {
+                if (!(cbp & (32 >> n))) continue;
+                alignas(16) int16_t blk[64] = {};
+                decode_ac(b, blk, false, 0, tables().scan_zz);
+                dequant(blk, false, n);
+                emit_block(n, blk);
+            }
+            return;
+        }
         // prediction
         int ls;
         uint8_t* ld = block_dst(cur, 0, &ls);
@@ -944,14 +1010,6 @@ struct Decoder {
                    ld + 8 * (k >> 1) * ls + 8 * (k & 1), ls);
         } else {
             mc(0, 16 * mb_x, 16 * mb_y, 16, 16, mvx[0], mvy[0], ld, ls);
-        }
-        int cmx, cmy;
-        if (mcbpc & 16) {
-            cmx = round_chroma4(mvx[0] + mvx[1] + mvx[2] + mvx[3]);
-            cmy = round_chroma4(mvy[0] + mvy[1] + mvy[2] + mvy[3]);
-        } else {
-            cmx = (mvx[0] >> 1) | (mvx[0] & 1);
-            cmy = (mvy[0] >> 1) | (mvy[0] & 1);
         }
         for (int c = 1; c < 3; c++) {
             int s;
@@ -1086,12 +1144,46 @@ extern "C" int mvp_mp4v_decode(void* handle, const uint8_t* data, size_t bytes, 
     MVP_ABI_BEGIN
     MVP_REQUIRE(handle && data, "mvp_mp4v_decode: NULL pointer");
     auto* d = static_cast<mp4v::Decoder*>(handle);
+    MVP_REQUIRE(d->mode != 2, "mvp_mp4v_decode: this handle parses (mvp_mp4v_parse); its pictures are not kept");
+    d->mode = 1;
     int coded = 0;
     const int vops = d->feed(data, bytes, &coded);
     MVP_REQUIRE(d->have_ref, "mvp_mp4v_decode: no frame decoded yet");
     if (bgr_out) d->write_bgr(bgr_out);
     if (yuv_out) d->write_yuv(yuv_out);
     if (vops_out) *vops_out = vops;
+    MVP_ABI_END
+}
+
+extern "C" int mvp_mp4v_parse(void* handle, const uint8_t* data, size_t bytes, void* rec_out, int64_t rec_cap,
+                              uint32_t* coef_out, int64_t coef_cap, int64_t* n_coef, int* vop_out) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(handle && data && rec_out && coef_out && n_coef && vop_out, "mvp_mp4v_parse: NULL pointer");
+    auto* d = static_cast<mp4v::Decoder*>(handle);
+    MVP_REQUIRE(d->mode != 1, "mvp_mp4v_parse: this handle decodes (mvp_mp4v_decode)");
+    d->mode = 2;
+    MVP_REQUIRE(rec_cap >= (int64_t)d->mb_w * d->mb_h, "mvp_mp4v_parse: %lld records for %d macroblocks",
+                (long long)rec_cap, d->mb_w * d->mb_h);
+    d->rec = static_cast<mp4v::MbRec*>(rec_out);
+    d->coef = coef_out;
+    d->coef_n = 0;
+    d->coef_cap = (size_t)std::max<int64_t>(coef_cap, 0);
+    d->vop_coded = -1;
+    int coded = 0;
+    int vops = 0;
+    try {
+        vops = d->feed(data, bytes, &coded);
+    } catch (...) {
+        d->rec = nullptr;
+        d->coef = nullptr;
+        throw;
+    }
+    d->rec = nullptr;
+    d->coef = nullptr;
+    MVP_REQUIRE(vops <= 1, "mvp_mp4v_parse: %d VOPs in one sample (the split decode takes one per sample)", vops);
+    *n_coef = (int64_t)d->coef_n;
+    vop_out[0] = vops ? d->vop_coded : -1;
+    vop_out[1] = d->rounding;
     MVP_ABI_END
 }
 

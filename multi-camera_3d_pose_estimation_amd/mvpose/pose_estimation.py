@@ -87,11 +87,22 @@ def get_pose_2D(frames, model, confidence=0.5, pose_keypoints=range(17)):
     return stacked, heat
 
 
-def load_frames(recording_paths, start_end_frames=(0, -1)):
+def video_device():
+    """Where load_frames reconstructs MPEG-4 Part 2 recordings: the GPU (split decode, frames land
+    in HBM) unless MVPOSE_VIDEO_DECODE=host or no GPU is visible."""
+    if os.environ.get("MVPOSE_VIDEO_DECODE", "device") == "host" or not torch.cuda.is_available():
+        return None
+    return torch.device("cuda", torch.cuda.current_device())
+
+
+def load_frames(recording_paths, start_end_frames=(0, -1), device=None):
     """{camera: (T', H, W, 3) uint8 BGR} sliced [start:end] (utils.py:903-909 ->
-    frame_generator :849-900).  A recording is a .npy stack (memory-mapped), an MJPEG or
-    uncompressed AVI, a directory of frame<N>.jpg files (mvpose.video), or an in-memory
-    array; other codecs raise NotImplementedError (no decoder in this image)."""
+    frame_generator :849-900).  A recording is a .npy stack (memory-mapped), an MPEG-4 Part 2
+    ('mp4v') MP4 / AVI / raw stream, an MJPEG or uncompressed AVI, a directory of frame<N>.jpg
+    files (mvpose.video), or an in-memory array / tensor; other codecs raise
+    NotImplementedError (no decoder in this image).  device: mp4v recordings are then
+    split-decoded onto it (host entropy decoding, GPU reconstruction) and come back as device
+    tensors, bit-identical to the host decoder's frames."""
     from . import video
     if isinstance(recording_paths, (list, tuple)):
         recording_paths = dict(enumerate(recording_paths))
@@ -100,10 +111,10 @@ def load_frames(recording_paths, start_end_frames=(0, -1)):
     a, b = (0, -1) if start_end_frames is None else start_end_frames
     out = {}
     for k, path in recording_paths.items():
-        if isinstance(path, np.ndarray):                 # already-decoded frames in memory
+        if isinstance(path, (np.ndarray, torch.Tensor)):  # already-decoded frames in memory
             out[k] = path[a:b]
             continue
-        out[k] = video.read_recording(path, a, b)
+        out[k] = video.read_recording(path, a, b, device=device)
     return out
 
 
@@ -207,6 +218,19 @@ class FrameStreamer:
         hm = torch.empty((T, self.V, N_JOINTS, 6), dtype=torch.float64, device=dev)
         chunks = [(t, min(T, t + self.step)) for t in range(0, T, self.step)]
         main = torch.cuda.current_stream(dev)
+        if any(isinstance(s, torch.Tensor) and s.is_cuda for s in stacks):
+            # frames already in device memory (split-decoded recordings): no host staging or H2D,
+            # each chunk's views interleaved (t, v)-major on the device
+            dstacks = [s.to(dev) if isinstance(s, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(s)).to(dev)
+                       for s in stacks]
+            for t0, t1 in chunks:
+                n = t1 - t0
+                fr = self.dev[0][:n]
+                for v, s in enumerate(dstacks):
+                    fr[:, v].copy_(s[t0:t1])
+                r = self.est.run(fr.reshape(n * self.V, self.H, self.W, 3), n_views=self.V, kpts_tkv=kp[t0:t1])
+                hm[t0:t1] = r["gaussians"].reshape(n, self.V, N_JOINTS, 6)
+            return kp, hm
         with ThreadPoolExecutor(max_workers=1) as pool:
             fut = pool.submit(self._gather, stacks, *chunks[0], 0) if chunks else None
             for i, (t0, t1) in enumerate(chunks):
@@ -245,13 +269,15 @@ def run_pose_est(model, confidence=0.5, camera_indices=None, recording_paths=Non
     any other per-frame callable with the reference's contract -> get_pose_2D frame by frame,
     as the reference loops (:184-190).  confidence does not change the output (it only
     selects what the reference draws, :117-131)."""
-    frames = load_frames(recording_paths, start_end_frames)
+    gpu_model = isinstance(model, str) or resolve_estimator(model) is not None
+    frames = load_frames(recording_paths, start_end_frames, device=video_device() if gpu_model else None)
     cams = list(frames.keys()) if camera_indices is None else list(camera_indices)
     stacks = [frames[c] for c in cams]
     V = len(stacks)
     H, W = stacks[0].shape[1:3]
     est = build_estimator(model, frame_hw=(H, W)) if isinstance(model, str) else resolve_estimator(model)
     if est is None:                                   # a generic per-frame callable
+        stacks = [s.cpu().numpy() if isinstance(s, torch.Tensor) else s for s in stacks]
         T = min(len(s) for s in stacks)
         res = [get_pose_2D([s[t] for s in stacks], model, confidence) for t in range(T)]
         return (np.array([r[0] for r in res], dtype=np.float32).reshape(T, N_JOINTS, 3, V),
@@ -279,9 +305,12 @@ def estimate_pose_from_video(camera_names, recording_paths, model, detector_mode
         kpts_2d = np.load(existing)
     else:
         paths = {i: recording_paths[i] for i in camera_indices}   # as :281 indexes them
-        frames = load_frames(paths, start_end_frames)          # decoded once
+        gpu_model = isinstance(model, str) or resolve_estimator(model) is not None
+        frames = load_frames(paths, start_end_frames,           # decoded once (mp4v: onto the GPU)
+                             device=video_device() if gpu_model else None)
         if isinstance(model, str):                             # :290-297: detector + pose model from the yaml
-            model = build_estimator(model, detector_model, model_yaml, frame_hw=frames[camera_indices[0]].shape[1:3])
+            model = build_estimator(model, detector_model, model_yaml,
+                                    frame_hw=tuple(frames[camera_indices[0]].shape[1:3]))
         kpts_2d, heatmaps = run_pose_est(model, confidence=confidence, camera_indices=camera_indices,
                                          recording_paths=frames, start_end_frames=(0, None))
     kpts_3d = get_pose_3D(camera_params, kpts_2d, camera_indices=[0, 1])

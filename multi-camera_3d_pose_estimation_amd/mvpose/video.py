@@ -123,8 +123,16 @@ def _decode_jpeg(data: bytes) -> np.ndarray:
     return rgb[:, :, ::-1]             # BGR, as cv2 returns frames
 
 
-def read_avi(path, start=0, end=None, threads=None) -> np.ndarray:
-    """Frames [start:end) of an MJPEG / uncompressed AVI -> (T, H, W, 3) uint8 BGR."""
+def _mp4v(config, samples, start, end, device):
+    """decode_mp4v on the host, or with device set the split decode (decode_mp4v_device)."""
+    if device is None:
+        return decode_mp4v(config, samples, start, end)
+    return decode_mp4v_device(config, samples, start, end, device=device)
+
+
+def read_avi(path, start=0, end=None, threads=None, device=None):
+    """Frames [start:end) of an MJPEG / uncompressed AVI -> (T, H, W, 3) uint8 BGR (mp4v streams
+    with device set: a tensor on that device, reconstructed there)."""
     with open(path, "rb") as f:
         buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
         try:
@@ -142,7 +150,7 @@ def read_avi(path, start=0, end=None, threads=None) -> np.ndarray:
                     rows = np.frombuffer(buf[d:d + stride * H], np.uint8).reshape(H, stride)[:, :W * 3]
                     out[i] = (rows[::-1] if info.height > 0 else rows).reshape(H, W, 3)   # DIB rows are BGR
             elif info.codec == "mp4v":
-                return decode_mp4v(info.strf_extra, (bytes(buf[d:d + n]) for d, n in info.chunks), start, end)
+                return _mp4v(info.strf_extra, (bytes(buf[d:d + n]) for d, n in info.chunks), start, end, device)
             elif info.codec == "mjpeg":
                 datas = [bytes(buf[d:d + n]) for d, n in chunks]
                 workers = max(1, min(int(threads or os.cpu_count() or 1), 16))
@@ -184,9 +192,12 @@ def read_image_dir(path, start=0, end=None, threads=None) -> np.ndarray:
     return np.stack(frames)
 
 
-def read_recording(path, start=0, end=-1):
+def read_recording(path, start=0, end=-1, device=None):
     """One camera's recording, sliced [start:end] with Python semantics (the reference's
-    default [0, -1] drops the last frame) -> (T, H, W, 3) uint8 BGR (memory-mapped for .npy)."""
+    default [0, -1] drops the last frame) -> (T, H, W, 3) uint8 BGR (memory-mapped for .npy).
+    device: MPEG-4 Part 2 recordings are then split-decoded — entropy decoding on the host,
+    reconstruction on the GPU (decode_mp4v_device) — and come back as a tensor on that device
+    (bit-identical frames); other formats still return host arrays."""
     p = str(path)
     if os.path.isdir(p):
         return read_image_dir(p, start, end)
@@ -201,11 +212,11 @@ def read_recording(path, start=0, end=-1):
     with open(p, "rb") as f:
         head = f.read(12)
     if head[0:4] == b"RIFF" and head[8:12] == b"AVI ":
-        return read_avi(p, start, end)
+        return read_avi(p, start, end, device=device)
     if head[4:8] in (b"ftyp", b"moov", b"mdat", b"free", b"wide", b"skip"):
-        return read_mp4(p, start, end)
+        return read_mp4(p, start, end, device=device)
     if head[0:3] == b"\0\0\1" and (head[3] in (0xB0, 0xB3, 0xB5, 0xB6) or head[3] <= 0x2F):
-        return read_m4v(p, start, end)
+        return read_m4v(p, start, end, device=device)
     raise NotImplementedError(
         f"{p}: no decoder for this container/codec in this image (MPEG-4 Part 2 in MP4/MOV/AVI/raw, MJPEG and "
         "uncompressed AVI, frame*.jpg directories and .npy stacks are supported)")
@@ -331,11 +342,150 @@ def decode_mp4v(config: bytes, samples, start=0, end=None, threads=None) -> np.n
     return out
 
 
-def read_m4v(path, start=0, end=None) -> np.ndarray:
+MB_REC_BYTES = 32     # csrc/mp4v.h MbRec
+JOB_DTYPE = np.dtype([("rec", "<u8"), ("coef", "<u8"), ("cur", "<u8"), ("ref", "<u8"), ("bgr", "<u8"),
+                      ("coded", "<i4"), ("rounding", "<i4")])  # csrc/mp4v.h Job, 48 B
+
+
+class Mp4vParser:
+    """Host half of the split decode (mvp_mp4v_parse): entropy decoding, DC / AC and motion-vector
+    prediction and inverse quantisation of one sample -> (records, coefficients, coded, rounding);
+    the pixels are reconstructed on the device (mvp_mp4v_reconstruct)."""
+
+    def __init__(self, config: bytes):
+        import ctypes
+        from . import _lib
+        self._lib = _lib
+        self._h = ctypes.c_void_p()
+        w, h = ctypes.c_int(), ctypes.c_int()
+        cfg = (ctypes.c_uint8 * max(1, len(config))).from_buffer_copy(config or b"\0")
+        _lib.call("mvp_mp4v_create", cfg, len(config), ctypes.byref(self._h), ctypes.byref(w), ctypes.byref(h))
+        self.width, self.height = w.value, h.value
+        self.n_mb = ((self.width + 15) // 16) * ((self.height + 15) // 16)
+        self._rec = np.empty(self.n_mb * MB_REC_BYTES, np.uint8)
+        self._coef = np.empty(self.n_mb * 384, np.uint32)
+
+    def parse(self, sample: bytes):
+        import ctypes
+        data = np.frombuffer(sample, np.uint8)
+        n = ctypes.c_int64()
+        vop = (ctypes.c_int * 2)()
+        self._lib.call("mvp_mp4v_parse", self._h, data.ctypes.data, data.size, self._rec.ctypes.data, self.n_mb,
+                       self._coef.ctypes.data, self._coef.size, ctypes.byref(n), vop)
+        coded = int(vop[0])
+        return (self._rec.copy() if coded == 1 else None, self._coef[:n.value].copy(), coded, int(vop[1]))
+
+    def close(self):
+        if self._h:
+            self._lib.call("mvp_mp4v_destroy", self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # pragma: no cover - interpreter shutdown
+            pass
+
+
+def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, device="cuda", stream=None):
+    """decode_mp4v with the pixels reconstructed on the GPU: frames [start:end) as a (n, H, W, 3)
+    uint8 BGR tensor on `device`, bit-identical to decode_mp4v's host frames.
+
+    The GOPs holding wanted frames are entropy-decoded on a host thread pool (mvp_mp4v_parse:
+    one 32-B record per macroblock + the non-zero inverse-quantised coefficients, ~5-10 % of a
+    BGR frame's bytes), copied to the device in one transfer, and reconstructed there by one
+    mvp_mp4v_reconstruct launch per GOP position: every GOP is an independent slot with its own
+    two pictures, so a launch runs one VOP of every GOP."""
+    import torch
+    from . import _lib
+    samples = list(samples)
+    if not config and samples:
+        config = samples[0]
+    keep = range(len(samples))[slice(start, end)]
+    lo, hi = (keep.start, keep.stop) if len(keep) and keep.step == 1 else (0, 0)
+    probe = Mp4vParser(config)
+    H, W, n_mb = probe.height, probe.width, probe.n_mb
+    probe.close()
+    dev = torch.device(device)
+    out = torch.empty((max(hi - lo, 0), H, W, 3), dtype=torch.uint8, device=dev)
+    if hi <= lo:
+        return out
+    starts = [i for i in range(hi) if i == 0 or vop_coding_type(samples[i]) == 0]
+    gops = [(a, b) for a, b in zip(starts, starts[1:] + [hi]) if b > lo]
+
+    def parse(g):
+        a, b = g
+        ps = Mp4vParser(config)
+        try:
+            return [ps.parse(samples[i]) for i in range(a, b)]
+        finally:
+            ps.close()
+
+    workers = max(1, min(int(threads or os.cpu_count() or 1), 16, len(gops)))
+    if workers == 1:
+        parsed = [parse(g) for g in gops]
+    else:
+        with ThreadPoolExecutor(workers) as pool:
+            parsed = list(pool.map(parse, gops))
+    # one host buffer of records + coefficients, one H2D copy
+    rec_list, coef_list, rec_off, coef_off = [], [], [], []
+    nr = nc = 0
+    for vops in parsed:
+        ro, co = [], []
+        for rec, coef, coded, _ in vops:
+            ro.append(nr)
+            co.append(nc)
+            if rec is not None:
+                rec_list.append(rec)
+                nr += 1
+            coef_list.append(coef)
+            nc += coef.size
+        rec_off.append(ro)
+        coef_off.append(co)
+    rec_h = torch.from_numpy(np.concatenate(rec_list) if rec_list else np.zeros(MB_REC_BYTES, np.uint8)).pin_memory()
+    coef_h = torch.from_numpy(np.concatenate(coef_list).view(np.int32) if nc else np.zeros(1, np.int32)).pin_memory()
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    pic_w, pic_h = 16 * ((W + 15) // 16), 16 * ((H + 15) // 16)
+    pic_bytes = pic_w * pic_h * 3 // 2
+    with torch.cuda.stream(s):
+        rec_d = rec_h.to(dev, non_blocking=True)
+        coef_d = coef_h.to(dev, non_blocking=True)
+        pics = torch.full((len(gops), 2, pic_bytes), 128, dtype=torch.uint8, device=dev)
+        steps = max(b - a for a, b in gops)
+        jobs = np.zeros((steps, len(gops)), JOB_DTYPE)
+        n_jobs = np.zeros(steps, np.int64)
+        cur_i = [0] * len(gops)
+        have = [False] * len(gops)
+        for g, ((a, b), vops) in enumerate(zip(gops, parsed)):
+            for k, (rec, coef, coded, rounding) in enumerate(vops):
+                i = a + k
+                if coded == 1:
+                    cur_i[g] ^= 1                      # the host decoder's swap: cur <-> ref
+                    have[g] = True
+                elif not have[g]:
+                    raise _lib.MvposeError(f"mp4v: sample {i} repeats a frame before any was decoded")
+                slot = pics.data_ptr() + g * 2 * pic_bytes
+                j = jobs[k, n_jobs[k]]
+                j["rec"] = rec_d.data_ptr() + rec_off[g][k] * n_mb * MB_REC_BYTES
+                j["coef"] = coef_d.data_ptr() + coef_off[g][k] * 4
+                j["cur"] = slot + cur_i[g] * pic_bytes
+                j["ref"] = slot + (cur_i[g] ^ 1) * pic_bytes
+                j["bgr"] = out.data_ptr() + (i - lo) * H * W * 3 if i >= lo else 0
+                j["coded"] = 1 if coded == 1 else 0
+                j["rounding"] = rounding
+                n_jobs[k] += 1
+        jobs_d = torch.from_numpy(jobs.view(np.uint8).reshape(-1)).pin_memory().to(dev, non_blocking=True)
+        row = len(gops) * JOB_DTYPE.itemsize
+        for k in range(steps):
+            _lib.call("mvp_mp4v_reconstruct", jobs_d.data_ptr() + k * row, int(n_jobs[k]), W, H, s.cuda_stream)
+    return out
+
+
+def read_m4v(path, start=0, end=None, device=None):
     """A raw MPEG-4 Part 2 elementary stream (.m4v / .cmp)."""
     with open(path, "rb") as f:
         config, samples = split_vops(f.read())
-    return decode_mp4v(config, samples, start, end)
+    return _mp4v(config, samples, start, end, device)
 
 
 class Mp4Info:
@@ -470,13 +620,13 @@ def parse_mp4(buf) -> Mp4Info:
     raise ValueError("MP4: no video track")
 
 
-def read_mp4(path, start=0, end=None) -> np.ndarray:
+def read_mp4(path, start=0, end=None, device=None):
     """Frames [start:end) of an MP4 / QuickTime file with MPEG-4 Part 2 video -> (T, H, W, 3) BGR."""
     with open(path, "rb") as f:
         buf = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
         try:
             info = parse_mp4(buf)
-            return decode_mp4v(info.config, (bytes(buf[o:o + n]) for o, n in info.samples), start, end)
+            return _mp4v(info.config, (bytes(buf[o:o + n]) for o, n in info.samples), start, end, device)
         finally:
             buf.close()
 

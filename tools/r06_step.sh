@@ -1,6 +1,8 @@
+#!/bin/bash
+# round-6 GPU step: the tests named in $1 (pytest node ids / files), then an optional python snippet file $2
 set -o pipefail
 export TMPDIR=/tmp
-mkdir -p gpurun_out/r06a
-timeout -k 10 600 python3 -u -m pytest tests/test_triangulate_gpu.py tests/test_e2e_parity_gpu.py -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r06a/pytest.log 2>&1 || { tail -40 gpurun_out/r06a/pytest.log; exit 1; }
-tail -3 gpurun_out/r06a/pytest.log
-bash tools/fwd_breakdown.sh r06a_bd 1024
+O=gpurun_out/${R06:-r06x}; mkdir -p $O
+timeout -k 10 600 python3 -u -m pytest $1 -x -v -s --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -60 $O/pytest.log; exit 1; }
+grep -E "passed|failed" $O/pytest.log | tail -3
+if [ -n "$2" ]; then timeout -k 10 600 python3 -u $2 > $O/extra.log 2>&1 || { tail -30 $O/extra.log; exit 1; }; tail -30 $O/extra.log; fi
