@@ -472,6 +472,12 @@ int mvp_mp4v_selfcheck(void);
 int mvp_mp4v_parse(void* handle, const uint8_t* data, size_t bytes, void* rec_out, int64_t rec_cap,
                    uint32_t* coef_out, int64_t coef_cap, int64_t* n_coef, int* vop_out);
 int mvp_mp4v_reconstruct(const void* jobs_dev, int n_jobs, int width, int height, void* stream);
+/* mvp_mp4v_parse over samples data[0..n) in one call (one GIL release per GOP from Python):
+ * sample k's records at rec_out + k * 32 * macroblocks, its coefficients packed after sample
+ * k-1's in coef_out (n_coef[k] entries), vop_out[2k..2k+1].  Stops before a sample that might not
+ * fit (fewer than 384 entries per macroblock left); *n_done = samples parsed. */
+int mvp_mp4v_parse_many(void* handle, int n, const uint8_t* const* data, const size_t* bytes, void* rec_out,
+                        uint32_t* coef_out, int64_t coef_cap, int64_t* n_coef, int* vop_out, int* n_done);
 
 #ifdef __cplusplus
 }

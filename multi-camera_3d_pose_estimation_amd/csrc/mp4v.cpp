@@ -1187,6 +1187,26 @@ extern "C" int mvp_mp4v_parse(void* handle, const uint8_t* data, size_t bytes, v
     MVP_ABI_END
 }
 
+extern "C" int mvp_mp4v_parse_many(void* handle, int n, const uint8_t* const* data, const size_t* bytes, void* rec_out,
+                                   uint32_t* coef_out, int64_t coef_cap, int64_t* n_coef, int* vop_out, int* n_done) {
+    MVP_ABI_BEGIN
+    MVP_REQUIRE(handle && n >= 0 && (n == 0 || (data && bytes && rec_out && coef_out && n_coef && vop_out)) && n_done,
+                "mvp_mp4v_parse_many: NULL pointer");
+    auto* d = static_cast<mp4v::Decoder*>(handle);
+    const int64_t n_mb = (int64_t)d->mb_w * d->mb_h, worst = n_mb * 384;
+    int64_t used = 0;
+    int k = 0;
+    *n_done = 0;
+    for (; k < n && coef_cap - used >= worst; k++) {
+        const int rc = mvp_mp4v_parse(handle, data[k], bytes[k], static_cast<uint8_t*>(rec_out) + k * n_mb * 32, n_mb,
+                                      coef_out + used, coef_cap - used, &n_coef[k], &vop_out[2 * k]);
+        if (rc != MVP_OK) return rc;  // mvp_last_error() holds the sample's message
+        used += n_coef[k];
+        *n_done = k + 1;
+    }
+    MVP_ABI_END
+}
+
 extern "C" int mvp_mp4v_destroy(void* handle) {
     MVP_ABI_BEGIN
     delete static_cast<mp4v::Decoder*>(handle);

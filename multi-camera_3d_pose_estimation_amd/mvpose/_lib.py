@@ -49,6 +49,8 @@ SIGNATURES = {
     "mvp_mp4v_parse": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p, c_int64, c_void_p, c_int64, P(c_int64),
                                P(c_int)]),
     "mvp_mp4v_reconstruct": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p]),
+    "mvp_mp4v_parse_many": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                    c_void_p, P(c_int)]),
     "mvp_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, P(c_float), P(c_float),
                                c_int, c_int, c_void_p, c_void_p]),
     "mvp_heatmap_decode": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, P(c_int), c_int, c_void_p,

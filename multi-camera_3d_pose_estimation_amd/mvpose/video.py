@@ -365,15 +365,21 @@ class Mp4vParser:
         self._rec = np.empty(self.n_mb * MB_REC_BYTES, np.uint8)
         self._coef = np.empty(self.n_mb * 384, np.uint32)
 
-    def parse(self, sample: bytes):
+    def parse(self, sample: bytes, rec_out: np.ndarray | None = None):
+        """-> (records (n_mb * 32 uint8; rec_out when given) or None for a sample without a coded
+        VOP, inverse-quantised coefficient entries (uint32, a view of this parser's scratch:
+        copy before the next parse), coded (1 / 0 not coded / -1 no VOP), vop_rounding_type)."""
         import ctypes
         data = np.frombuffer(sample, np.uint8)
+        rec = self._rec if rec_out is None else rec_out
+        if rec.dtype != np.uint8 or rec.size < self.n_mb * MB_REC_BYTES or not rec.flags.c_contiguous:
+            raise ValueError(f"rec_out must be a C-contiguous uint8 array of >= {self.n_mb * MB_REC_BYTES} bytes")
         n = ctypes.c_int64()
         vop = (ctypes.c_int * 2)()
-        self._lib.call("mvp_mp4v_parse", self._h, data.ctypes.data, data.size, self._rec.ctypes.data, self.n_mb,
+        self._lib.call("mvp_mp4v_parse", self._h, data.ctypes.data, data.size, rec.ctypes.data, self.n_mb,
                        self._coef.ctypes.data, self._coef.size, ctypes.byref(n), vop)
         coded = int(vop[0])
-        return (self._rec.copy() if coded == 1 else None, self._coef[:n.value].copy(), coded, int(vop[1]))
+        return (rec if coded == 1 else None, self._coef[:n.value], coded, int(vop[1]))
 
     def close(self):
         if self._h:
@@ -387,7 +393,8 @@ class Mp4vParser:
             pass
 
 
-def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, device="cuda", stream=None):
+def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, device="cuda", stream=None,
+                       timings: dict | None = None):
     """decode_mp4v with the pixels reconstructed on the GPU: frames [start:end) as a (n, H, W, 3)
     uint8 BGR tensor on `device`, bit-identical to decode_mp4v's host frames.
 
@@ -395,7 +402,9 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
     one 32-B record per macroblock + the non-zero inverse-quantised coefficients, ~5-10 % of a
     BGR frame's bytes), copied to the device in one transfer, and reconstructed there by one
     mvp_mp4v_reconstruct launch per GOP position: every GOP is an independent slot with its own
-    two pictures, so a launch runs one VOP of every GOP."""
+    two pictures, so a launch runs one VOP of every GOP.  timings: filled with the host phases'
+    seconds (parse, pack, launch; the launches are asynchronous)."""
+    import time
     import torch
     from . import _lib
     samples = list(samples)
@@ -413,71 +422,100 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
     starts = [i for i in range(hi) if i == 0 or vop_coding_type(samples[i]) == 0]
     gops = [(a, b) for a, b in zip(starts, starts[1:] + [hi]) if b > lo]
 
-    def parse(g):
-        a, b = g
+    n_s = sum(b - a for a, b in gops)
+    gop_base = np.concatenate([[0], np.cumsum([b - a for a, b in gops])]).astype(np.int64)
+    rb = n_mb * MB_REC_BYTES
+    # records straight into one pinned buffer (torch caches pinned blocks across calls)
+    rec_h = torch.empty(max(1, n_s * rb), dtype=torch.uint8, pin_memory=True)
+    rec_np = rec_h.numpy()
+
+    def parse(gi):
+        """One GOP in native calls (mvp_mp4v_parse_many: the GIL is released for the whole GOP)
+        -> (its coefficient entries, per-sample entry counts, per-sample [coded, rounding])."""
+        import ctypes
+        a, b = gops[gi]
+        base, n = int(gop_base[gi]), b - a
+        datas = [x if isinstance(x, bytes) else bytes(x) for x in samples[a:b]]
+        ptrs = (ctypes.c_char_p * n)(*datas)
+        sizes = np.array([len(x) for x in datas], np.uint64)
+        ncoef = np.zeros(n, np.int64)
+        vops = np.zeros((n, 2), np.int32)
+        chunks, k = [], 0
         ps = Mp4vParser(config)
         try:
-            return [ps.parse(samples[i]) for i in range(a, b)]
+            while k < n:
+                cap = max(2 * n_mb * 384, (n - k) * n_mb * 24)
+                buf = np.empty(cap, np.uint32)
+                done = ctypes.c_int()
+                _lib.call("mvp_mp4v_parse_many", ps._h, n - k, ctypes.addressof(ptrs) + 8 * k,
+                          sizes.ctypes.data + 8 * k, rec_np[(base + k) * rb:].ctypes.data, buf.ctypes.data, cap,
+                          ncoef.ctypes.data + 8 * k, vops.ctypes.data + 8 * k, ctypes.byref(done))
+                chunks.append(buf[:int(ncoef[k:k + done.value].sum())])
+                k += done.value
         finally:
             ps.close()
+        return np.concatenate(chunks) if len(chunks) > 1 else chunks[0], ncoef, vops
 
+    t_parse = time.perf_counter()
     workers = max(1, min(int(threads or os.cpu_count() or 1), 16, len(gops)))
     if workers == 1:
-        parsed = [parse(g) for g in gops]
+        parsed = [parse(g) for g in range(len(gops))]
     else:
         with ThreadPoolExecutor(workers) as pool:
-            parsed = list(pool.map(parse, gops))
-    # one host buffer of records + coefficients, one H2D copy
-    rec_list, coef_list, rec_off, coef_off = [], [], [], []
-    nr = nc = 0
-    for vops in parsed:
-        ro, co = [], []
-        for rec, coef, coded, _ in vops:
-            ro.append(nr)
-            co.append(nc)
-            if rec is not None:
-                rec_list.append(rec)
-                nr += 1
-            coef_list.append(coef)
-            nc += coef.size
-        rec_off.append(ro)
-        coef_off.append(co)
-    rec_h = torch.from_numpy(np.concatenate(rec_list) if rec_list else np.zeros(MB_REC_BYTES, np.uint8)).pin_memory()
-    coef_h = torch.from_numpy(np.concatenate(coef_list).view(np.int32) if nc else np.zeros(1, np.int32)).pin_memory()
+            parsed = list(pool.map(parse, range(len(gops))))
+    t_pack = time.perf_counter()
+    # per sample, in GOP order: coded flag, rounding, coefficient count
+    coded = np.concatenate([v[:, 0] for _, _, v in parsed]).astype(np.int64)
+    rnd = np.concatenate([v[:, 1] for _, _, v in parsed]).astype(np.int64)
+    ncoef = np.concatenate([c for _, c, _ in parsed])
+    coef_off = np.concatenate([[0], np.cumsum(ncoef)])[:-1]
+    nc = int(ncoef.sum())
+    coef_h = torch.empty(max(1, nc), dtype=torch.int32, pin_memory=True)
+    if nc:
+        np.concatenate([c for c, _, _ in parsed], out=coef_h.numpy()[:nc].view(np.uint32))
+    gop_of = np.repeat(np.arange(len(gops)), [b - a for a, b in gops])
+    step = np.arange(n_s) - gop_base[gop_of]
+    frame = np.array([a for a, _ in gops], np.int64)[gop_of] + step
+    # the host decoder's picture swap: a coded VOP writes the slot's other picture
+    is_coded = (coded == 1).astype(np.int64)
+    seen = np.zeros(n_s, np.int64)
+    for g in range(len(gops)):
+        sl = slice(int(gop_base[g]), int(gop_base[g + 1]))
+        seen[sl] = np.cumsum(is_coded[sl])
+    if (seen == 0).any():
+        raise _lib.MvposeError(f"mp4v: sample {int(frame[np.argmax(seen == 0)])} repeats a frame before any was "
+                               "decoded")
+    cur_i = seen & 1
     s = stream if stream is not None else torch.cuda.current_stream(dev)
     pic_w, pic_h = 16 * ((W + 15) // 16), 16 * ((H + 15) // 16)
     pic_bytes = pic_w * pic_h * 3 // 2
+    t_launch = time.perf_counter()
     with torch.cuda.stream(s):
         rec_d = rec_h.to(dev, non_blocking=True)
         coef_d = coef_h.to(dev, non_blocking=True)
         pics = torch.full((len(gops), 2, pic_bytes), 128, dtype=torch.uint8, device=dev)
-        steps = max(b - a for a, b in gops)
-        jobs = np.zeros((steps, len(gops)), JOB_DTYPE)
-        n_jobs = np.zeros(steps, np.int64)
-        cur_i = [0] * len(gops)
-        have = [False] * len(gops)
-        for g, ((a, b), vops) in enumerate(zip(gops, parsed)):
-            for k, (rec, coef, coded, rounding) in enumerate(vops):
-                i = a + k
-                if coded == 1:
-                    cur_i[g] ^= 1                      # the host decoder's swap: cur <-> ref
-                    have[g] = True
-                elif not have[g]:
-                    raise _lib.MvposeError(f"mp4v: sample {i} repeats a frame before any was decoded")
-                slot = pics.data_ptr() + g * 2 * pic_bytes
-                j = jobs[k, n_jobs[k]]
-                j["rec"] = rec_d.data_ptr() + rec_off[g][k] * n_mb * MB_REC_BYTES
-                j["coef"] = coef_d.data_ptr() + coef_off[g][k] * 4
-                j["cur"] = slot + cur_i[g] * pic_bytes
-                j["ref"] = slot + (cur_i[g] ^ 1) * pic_bytes
-                j["bgr"] = out.data_ptr() + (i - lo) * H * W * 3 if i >= lo else 0
-                j["coded"] = 1 if coded == 1 else 0
-                j["rounding"] = rounding
-                n_jobs[k] += 1
-        jobs_d = torch.from_numpy(jobs.view(np.uint8).reshape(-1)).pin_memory().to(dev, non_blocking=True)
-        row = len(gops) * JOB_DTYPE.itemsize
+        steps = int(step.max()) + 1
+        # one job per sample; launch k runs the k-th VOP of every GOP that has one
+        slot = pics.data_ptr() + gop_of * 2 * pic_bytes
+        jl = np.zeros(n_s, JOB_DTYPE)
+        jl["rec"] = rec_d.data_ptr() + np.arange(n_s, dtype=np.int64) * rb
+        jl["coef"] = coef_d.data_ptr() + coef_off * 4
+        jl["cur"] = slot + cur_i * pic_bytes
+        jl["ref"] = slot + (cur_i ^ 1) * pic_bytes
+        jl["bgr"] = np.where(frame >= lo, out.data_ptr() + (frame - lo) * (H * W * 3), 0)
+        jl["coded"] = is_coded
+        jl["rounding"] = rnd
+        order = np.lexsort((gop_of, step))                 # by step, then GOP
+        n_jobs = np.bincount(step, minlength=steps)
+        jobs_d = torch.from_numpy(jl[order].view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        first = np.concatenate([[0], np.cumsum(n_jobs)])
         for k in range(steps):
-            _lib.call("mvp_mp4v_reconstruct", jobs_d.data_ptr() + k * row, int(n_jobs[k]), W, H, s.cuda_stream)
+            _lib.call("mvp_mp4v_reconstruct", jobs_d.data_ptr() + int(first[k]) * JOB_DTYPE.itemsize, int(n_jobs[k]),
+                      W, H, s.cuda_stream)
+    if timings is not None:
+        t_end = time.perf_counter()
+        timings.update(parse=t_pack - t_parse, pack=t_launch - t_pack, launch=t_end - t_launch,
+                       coef_entries=nc, gops=len(gops), samples=n_s)
     return out
 
 

@@ -145,8 +145,12 @@ def _host_yuv(cfg, samples):
 
 def _parse(cfg, samples):
     ps = video.Mp4vParser(cfg)
+    out = []
     try:
-        return [ps.parse(s) for s in samples]
+        for s in samples:
+            rec, coef, coded, rnd = ps.parse(s)     # views of the parser's scratch: copy
+            out.append((None if rec is None else rec.copy(), coef.copy(), coded, rnd))
+        return out
     finally:
         ps.close()
 
@@ -175,4 +179,35 @@ def test_parse_and_decode_do_not_mix_on_one_handle():
         data = np.frombuffer(samples[1], np.uint8)
         n = ctypes.c_int()
         _lib.call("mvp_mp4v_decode", ps._h, data.ctypes.data, data.size, out.ctypes.data, None, ctypes.byref(n))
+    ps.close()
+
+
+def test_parse_many_equals_parse_and_stops_before_overflow():
+    """mvp_mp4v_parse_many (one native call per GOP) writes what per-sample mvp_mp4v_parse does,
+    packed, and stops before a sample that might not fit the coefficient buffer."""
+    import ctypes
+    cfg, samples, w, h = mixed_stream(4, 3, 3, 21)
+    ref = _parse(cfg, samples)
+    ps = video.Mp4vParser(cfg)
+    n, nmb = len(samples), ps.n_mb
+    ptrs = (ctypes.c_char_p * n)(*samples)
+    sizes = np.array([len(x) for x in samples], np.uint64)
+    rec = np.zeros(n * nmb * 32, np.uint8)
+    ncoef = np.zeros(n, np.int64)
+    vops = np.zeros((n, 2), np.int32)
+    cap = nmb * 384 + 8                  # one worst-case sample: the call stops after the I-VOP
+    buf = np.zeros(cap, np.uint32)
+    done = ctypes.c_int()
+    _lib.call("mvp_mp4v_parse_many", ps._h, n, ptrs, sizes.ctypes.data, rec.ctypes.data, buf.ctypes.data, cap,
+              ncoef.ctypes.data, vops.ctypes.data, ctypes.byref(done))
+    k = done.value
+    assert 1 <= k < n
+    off = 0
+    for i in range(k):
+        r, c, coded, rnd = ref[i]
+        assert (vops[i, 0], vops[i, 1]) == (coded, rnd)
+        np.testing.assert_array_equal(buf[off:off + ncoef[i]], c)
+        if r is not None:
+            np.testing.assert_array_equal(rec[i * nmb * 32:(i + 1) * nmb * 32], r)
+        off += int(ncoef[i])
     ps.close()
