@@ -353,6 +353,38 @@ struct Decoder {
         r.kind = kind;
         r.coef = (uint32_t)coef_n;
     }
+    // dequant(blk, false, n) + emit_block for quant_type 0 over the decoded positions only
+    void emit_inter_h263(int n, const int16_t* blk, const uint8_t* pos, int np) {
+        const int qmul = qscale << 1, qadd = (qscale - 1) | 1;
+        MVP_REQUIRE(coef_n + np <= coef_cap, "mvp_mp4v_parse: coefficient buffer full (%zu entries)", coef_cap);
+        int k = 0;
+        for (int i = 0; i < np; i++) {
+            const int l = blk[pos[i]];
+            if (!l) continue;
+            const int v = std::max(-2048, std::min(2047, l < 0 ? l * qmul - qadd : l * qmul + qadd));
+            coef[coef_n++] = coef_entry(pos[i], v);
+            k++;
+        }
+        cur_rec().nnz[n] = (uint8_t)k;
+    }
+    // dequant(blk, true, n) + emit_block for quant_type 0 over the positions in mask m (raster order)
+    void emit_intra_h263(int n, const int16_t* blk, uint64_t m) {
+        const int qmul = qscale << 1, qadd = (qscale - 1) | 1;
+        MVP_REQUIRE(coef_n + 64 <= coef_cap, "mvp_mp4v_parse: coefficient buffer full (%zu entries)", coef_cap);
+        int k = 0;
+        while (m) {
+            const int i = __builtin_ctzll(m);
+            m &= m - 1;
+            const int l = blk[i];
+            if (!l) continue;
+            const int v = i == 0 ? (int16_t)(l * dc_scale(qscale, n < 4))
+                                 : std::max(-2048, std::min(2047, l < 0 ? l * qmul - qadd : l * qmul + qadd));
+            if (!v) continue;
+            coef[coef_n++] = coef_entry(i, v);
+            k++;
+        }
+        cur_rec().nnz[n] = (uint8_t)k;
+    }
     void emit_block(int n, const int16_t* blk) {
         int k = 0;
         for (int i = 0; i < 64; i++) {
@@ -649,8 +681,10 @@ struct Decoder {
     }
     static int rdiv(int a, int b) { return (a >= 0 ? a + (b >> 1) : a - (b >> 1)) / b; }
 
-    // TCOEF events into blk (raster) through `scan`, starting at scan position `i`
-    void decode_ac(Bits& b, int16_t* blk, bool intra, int i, const uint8_t* scan) {
+    // TCOEF events into blk (raster) through `scan`, starting at scan position `i`; pos (optional):
+    // the raster positions written, *npos of them (a position is written at most once)
+    void decode_ac(Bits& b, int16_t* blk, bool intra, int i, const uint8_t* scan, uint8_t* pos = nullptr,
+                   int* npos = nullptr) {
         const Tables& T = tables();
         const Vlc& vlc = intra ? T.tc_intra : T.tc_inter;
         const int8_t* runs = intra ? kRunIntra : kRunInter;
@@ -693,6 +727,7 @@ struct Decoder {
             i += run;
             MVP_REQUIRE(i < 64, "mp4v: run past the block end at macroblock (%d, %d)", mb_x, mb_y);
             blk[scan[i]] = (int16_t)level;
+            if (pos) pos[(*npos)++] = scan[i];
             i++;
             if (last) break;
         }
@@ -755,11 +790,23 @@ struct Decoder {
                 blk[0] = (int16_t)diff;
                 start = 1;
             }
-            if (cbp & (32 >> n)) decode_ac(b, blk, true, start, scan);
+            const bool fast = rec && quant_type == 0;
+            uint8_t pos[64];
+            int np = 0;
+            if (cbp & (32 >> n)) decode_ac(b, blk, true, start, scan, fast ? pos : nullptr, &np);
             const int qdc = blk[0] + pred;
             blk[0] = (int16_t)qdc;
             store_dc(n, qdc);
             pred_ac(n, dir, ac_pred, blk);
+            if (fast) {
+                // the positions that can be non-zero: the DC, the decoded ones, and the first
+                // column (prediction from the left) or row (from above) AC prediction wrote
+                uint64_t m = 1;
+                for (int i = 0; i < np; i++) m |= 1ull << pos[i];
+                if (ac_pred) m |= dir == 0 ? 0x0101010101010100ull : 0xFEull;
+                emit_intra_h263(n, blk, m);
+                continue;
+            }
             dequant(blk, true, n);
             if (rec) {
                 emit_block(n, blk);
@@ -995,6 +1042,15 @@ struct Decoder {
             for (int n = 0; n < 6; n++) {
                 if (!(cbp & (32 >> n))) continue;
                 alignas(16) int16_t blk[64] = {};
+                if (quant_type == 0) {
+                    // H.263 inverse quantisation touches only the decoded positions: dequantise
+                    // and emit those (in decode order) instead of sweeping all 64 twice
+                    uint8_t pos[64];
+                    int np = 0;
+                    decode_ac(b, blk, false, 0, tables().scan_zz, pos, &np);
+                    emit_inter_h263(n, blk, pos, np);
+                    continue;
+                }
                 decode_ac(b, blk, false, 0, tables().scan_zz);
                 dequant(blk, false, n);
                 emit_block(n, blk);

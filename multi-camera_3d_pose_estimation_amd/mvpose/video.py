@@ -425,13 +425,21 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
     n_s = sum(b - a for a, b in gops)
     gop_base = np.concatenate([[0], np.cumsum([b - a for a, b in gops])]).astype(np.int64)
     rb = n_mb * MB_REC_BYTES
-    # records straight into one pinned buffer (torch caches pinned blocks across calls)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    # records straight into one pinned buffer (torch caches pinned blocks across calls); each
+    # GOP's records and coefficients go to the device on a copy stream as soon as it is parsed,
+    # under the other GOPs' parsing
     rec_h = torch.empty(max(1, n_s * rb), dtype=torch.uint8, pin_memory=True)
     rec_np = rec_h.numpy()
+    with torch.cuda.stream(s):
+        rec_d = torch.empty(max(1, n_s * rb), dtype=torch.uint8, device=dev)
+    copy_stream = torch.cuda.Stream(dev)
+    copy_stream.wait_stream(s)                           # rec_d's allocation precedes the copies
 
     def parse(gi):
-        """One GOP in native calls (mvp_mp4v_parse_many: the GIL is released for the whole GOP)
-        -> (its coefficient entries, per-sample entry counts, per-sample [coded, rounding])."""
+        """One GOP in native calls (mvp_mp4v_parse_many: the GIL is released for the whole GOP),
+        then its H2D copies -> (its coefficients on the device, per-sample entry counts,
+        per-sample [coded, rounding])."""
         import ctypes
         a, b = gops[gi]
         base, n = int(gop_base[gi]), b - a
@@ -444,7 +452,7 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
         ps = Mp4vParser(config)
         try:
             while k < n:
-                cap = max(2 * n_mb * 384, (n - k) * n_mb * 24)
+                cap = n_mb * 384 + (n - k) * n_mb * 24
                 buf = np.empty(cap, np.uint32)
                 done = ctypes.c_int()
                 _lib.call("mvp_mp4v_parse_many", ps._h, n - k, ctypes.addressof(ptrs) + 8 * k,
@@ -454,7 +462,15 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
                 k += done.value
         finally:
             ps.close()
-        return np.concatenate(chunks) if len(chunks) > 1 else chunks[0], ncoef, vops
+        cnt = int(ncoef.sum())
+        coef_h = torch.empty(max(1, cnt), dtype=torch.int32, pin_memory=True)
+        if cnt:
+            np.concatenate(chunks, out=coef_h.numpy()[:cnt].view(np.uint32))
+        with torch.cuda.stream(copy_stream):
+            rec_d[base * rb:(base + n) * rb].copy_(rec_h[base * rb:(base + n) * rb], non_blocking=True)
+            coef_d = coef_h.to(dev, non_blocking=True)
+        coef_d.record_stream(s)                           # read by the reconstruction launches
+        return coef_d, ncoef, vops
 
     t_parse = time.perf_counter()
     workers = max(1, min(int(threads or os.cpu_count() or 1), 16, len(gops)))
@@ -467,12 +483,9 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
     # per sample, in GOP order: coded flag, rounding, coefficient count
     coded = np.concatenate([v[:, 0] for _, _, v in parsed]).astype(np.int64)
     rnd = np.concatenate([v[:, 1] for _, _, v in parsed]).astype(np.int64)
-    ncoef = np.concatenate([c for _, c, _ in parsed])
-    coef_off = np.concatenate([[0], np.cumsum(ncoef)])[:-1]
-    nc = int(ncoef.sum())
-    coef_h = torch.empty(max(1, nc), dtype=torch.int32, pin_memory=True)
-    if nc:
-        np.concatenate([c for c, _, _ in parsed], out=coef_h.numpy()[:nc].view(np.uint32))
+    ncoef = [c for _, c, _ in parsed]
+    coef_ptr = np.concatenate([d.data_ptr() + 4 * (np.cumsum(c) - c) for d, c, _ in parsed])
+    nc = int(sum(int(c.sum()) for c in ncoef))
     gop_of = np.repeat(np.arange(len(gops)), [b - a for a, b in gops])
     step = np.arange(n_s) - gop_base[gop_of]
     frame = np.array([a for a, _ in gops], np.int64)[gop_of] + step
@@ -486,20 +499,17 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
         raise _lib.MvposeError(f"mp4v: sample {int(frame[np.argmax(seen == 0)])} repeats a frame before any was "
                                "decoded")
     cur_i = seen & 1
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
     pic_w, pic_h = 16 * ((W + 15) // 16), 16 * ((H + 15) // 16)
     pic_bytes = pic_w * pic_h * 3 // 2
     t_launch = time.perf_counter()
     with torch.cuda.stream(s):
-        rec_d = rec_h.to(dev, non_blocking=True)
-        coef_d = coef_h.to(dev, non_blocking=True)
         pics = torch.full((len(gops), 2, pic_bytes), 128, dtype=torch.uint8, device=dev)
         steps = int(step.max()) + 1
         # one job per sample; launch k runs the k-th VOP of every GOP that has one
         slot = pics.data_ptr() + gop_of * 2 * pic_bytes
         jl = np.zeros(n_s, JOB_DTYPE)
         jl["rec"] = rec_d.data_ptr() + np.arange(n_s, dtype=np.int64) * rb
-        jl["coef"] = coef_d.data_ptr() + coef_off * 4
+        jl["coef"] = coef_ptr
         jl["cur"] = slot + cur_i * pic_bytes
         jl["ref"] = slot + (cur_i ^ 1) * pic_bytes
         jl["bgr"] = np.where(frame >= lo, out.data_ptr() + (frame - lo) * (H * W * 3), 0)
@@ -508,6 +518,7 @@ def decode_mp4v_device(config: bytes, samples, start=0, end=None, threads=None, 
         order = np.lexsort((gop_of, step))                 # by step, then GOP
         n_jobs = np.bincount(step, minlength=steps)
         jobs_d = torch.from_numpy(jl[order].view(np.uint8).copy()).pin_memory().to(dev, non_blocking=True)
+        s.wait_stream(copy_stream)
         first = np.concatenate([[0], np.cumsum(n_jobs)])
         for k in range(steps):
             _lib.call("mvp_mp4v_reconstruct", jobs_d.data_ptr() + int(first[k]) * JOB_DTYPE.itemsize, int(n_jobs[k]),
