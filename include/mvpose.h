@@ -280,6 +280,12 @@ int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, i
  *                  writes cand rows [prior][6] = {sigmoid score, x1, y1, x2, y2, logit}
  *                  at prior offset `aux`, box = prior (x, y) * stride -+ exp(reg) * stride,
  *                  clipped to [0, size] (mmdet distance2bbox on img_shape).
+ *   MVP_DET_DWPW : a CSPNeXtBlock's conv2 (DepthwiseSeparableConvModule) in one launch:
+ *                  t = act(dw5x5(in) + b_dw) rounded to bf16 (never stored), then
+ *                  out = act(t . W_pw + b_pw) [+ res]; in.c = C in {64, 96, 192, 384},
+ *                  cout_pad(out.c) == C.  w_off: dw f32 weights [C/8][25][8]; b_off: f32
+ *                  [b_dw (C) | b_pw (C)]; aux: pw bf16 weights [C][1][1][C].  Bit-identical to
+ *                  MVP_DET_DW followed by a 1x1 MVP_DET_CONV.
  * act: 0 none, 1 ReLU (after a residual add), 2 SiLU (before it: CSPNeXtBlock's
  * conv2(conv1(x)) + x).
  * ------------------------------------------------------------------------- */
@@ -290,6 +296,7 @@ int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, i
 #define MVP_DET_SPP 4
 #define MVP_DET_UP2 5
 #define MVP_DET_HEAD 6
+#define MVP_DET_DWPW 7
 
 typedef struct mvp_det_view {
     int t;    /* tensor id, -1 = none */

@@ -24,6 +24,13 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
                           hipStream_t s, const uint16_t* wimg = nullptr, const uint16_t* wband = nullptr);
+// A CSPNeXtBlock's depthwise 5x5 (dw_w [C/8][25][8] f32, dw_b [C]) and pointwise 1x1 (wimg: the
+// GEMM weight image of the [det_cout_pad(N) == C][C] weights, pw_b [C]) in one launch, the
+// intermediate kept in LDS; bit-identical to launch_det_dw5 + launch_det_conv_gemm (ks 1).
+bool det_dwpw_supported(int C);
+void launch_det_dwpw(const uint16_t* x, int xs, const float* dw_w, const float* dw_b, const uint16_t* wimg,
+                     const float* pw_b, const uint16_t* res, int rs, uint16_t* y, int ys, int n, int H, int W, int C,
+                     int N, int act_dw, int act_pw, hipStream_t s);
 // The GEMM kernel's weight image (same element count as w: npad x K, K = ks * ks * cin)
 void det_pack_gemm_weights(const uint16_t* w, uint16_t* img, int npad, int K, hipStream_t s);
 // The band-halo kernel (3x3/s1, >= 96 input channels, 80x80 / 40x40 planes, couts in blocks of 64):

@@ -190,7 +190,7 @@ struct DwParams {
 };
 
 template <int G>
-__global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
+__global__ __launch_bounds__(G * 64, G > 8 ? 1 : 8 / G * 2) void dw5_kernel(DwParams p) {
     __shared__ uint4 sh[G][kDwHH * kDwHW];
     const int n_groups = p.C / (8 * G);
     const int grp = blockIdx.x % n_groups;
@@ -286,6 +286,7 @@ struct GParams {
     const uint16_t* zero;  // >= 16 KiB of zeros
     long M;                // n * Ho * Wo
     int cin, N, npad, xs, ys, rs, act, n_nb;
+    int xcd_order;         // GEMM kernel: XCD-contiguous logical block order
     int H, W, Ho, Wo;
     // GEMM kernel: w re-laid by det_pack_gemm_weights (per 32-channel K step, every cout's
     // four swizzled 16-B chunks in LDS slot order: a weight DMA instruction reads 1 KB
@@ -335,8 +336,18 @@ det_conv_gemm_kernel(GParams p) {
     // DMA instructions this wave issues per K step: its weight rounds + the pixel rounds
     const int ops = CPS * ((A_R64 - wave + NWV - 1) / NWV + B_SLOTS / NT);
     const int wp = wave % PW, wc = wave / PW;  // pixel quarter / half, cout half
-    const long tile = blockIdx.x / p.n_nb;
-    const int co0 = (int)(blockIdx.x - tile * p.n_nb) * BN;
+    // XCD-aware order: the dispatcher deals blockIdx round-robin over the 8 XCDs, so logical
+    // blocks (tile, cout block; couts fastest) are renumbered to give every XCD a contiguous
+    // range — the cout blocks of a tile then run on one XCD and share its input through that
+    // L2 (blockIdx order spread them over n_nb XCDs, each fetching the tile).  A bijection for
+    // any grid size: XCD x < r holds q + 1 logical blocks, the others q.
+    long lb = blockIdx.x;
+    if (p.xcd_order) {
+        const long nbk = gridDim.x, q = nbk >> 3, r = nbk & 7, x = blockIdx.x & 7, loc = blockIdx.x >> 3;
+        lb = x < r ? x * (q + 1) + loc : r * (q + 1) + (x - r) * q + loc;
+    }
+    const long tile = lb / p.n_nb;
+    const int co0 = (int)(lb - tile * p.n_nb) * BN;
     const long m0 = tile * BMP;
     const int kc = p.cin / 32;            // chunks per tap
     const int nq = KS * KS * kc;          // 32-channel K chunks
@@ -1256,6 +1267,228 @@ __global__ __launch_bounds__(1024) void det_nms_kernel(const float* cand, int n_
     if (tid == 0) counts[n] = kept;
 }
 
+// ------------------------------------------------------------------ depthwise 5x5 + pointwise 1x1
+// One CSPNeXtBlock's conv2 (DepthwiseSeparableConvModule: 5x5 depthwise + BN + SiLU, then 1x1
+// pointwise + BN + SiLU, + the block's identity) in one launch: the depthwise output never leaves
+// LDS.  Unfused, dw5_kernel wrote it (C channels per pixel) and the 1x1 GEMM read it back: 2 x C x
+// 2 B per pixel of HBM traffic and a launch per block, ~37 % of the pair's bytes.
+// A workgroup owns a TH x TW pixel tile of one frame and all C channels:
+//   dw phase   8-channel chunks, 8 per round (one per wave): the round's (TH+4) x (TW+4) halo
+//              is loaded coalesced into LDS (8 consecutive 16-B chunks of a pixel per lane
+//              group, dw5_kernel's layout), each wave computes its chunk for the tile (1 or 2
+//              outputs per lane: dw5_kernel's fma chains, taps in (kh, kw) order, packed
+//              channel pairs) and writes the bf16 result straight into the GEMM's B operand;
+//   pw phase   the tile x C couts GEMM on v_mfma_f32_16x16x32_bf16 with the B operand resident
+//              for all C/32 K steps and the weight image (det_pack_gemm_weights) streamed per K
+//              step through a 2-slot LDS ring (register-staged: step q+2 loads under step q);
+//              waves split pixel fragments x cout tiles;
+//   epilogue   det_conv_gemm_kernel's: bias, SiLU, + residual, bf16.
+// Bit-identical to dw5_kernel + det_conv_gemm_kernel<*, 1, 1>: the same per-output fma chains,
+// bf16 rounding of the intermediate, LDS operand layouts (row-major 16-B slots with chunk
+// kg at kg ^ swz(row)), MFMA operand roles and K order (tests/test_rtmdet_gpu.py).
+struct DwPwParams {
+    const uint16_t* x;      // depthwise input view (pixel stride xs)
+    const float* dw_w;      // [C/8][25][8]
+    const float* dw_b;      // [C]
+    const uint16_t* wimg;   // pointwise weight image: [C/32 K steps][C couts][4 swizzled 16-B chunks]
+    const float* pw_b;      // [C]
+    const uint16_t* res;    // residual view (stride rs) or nullptr
+    uint16_t* y;            // output view (stride ys)
+    int H, W, N, xs, ys, rs, act_dw, act_pw, tiles_w;
+};
+
+template <int C, int TW>
+struct DwPwCfg {
+    static constexpr int TH = 8, P = TH * TW, OUTS = P / 64;  // dw outputs per lane
+    static constexpr int HH = TH + 4, HWD = TW + 4;           // halo rows / columns
+    static constexpr int Q = C / 32, NCH = C / 8;             // K steps, 8-channel chunks
+    static constexpr int FP = P / 16, NT = C / 16;            // pixel fragments, cout tiles
+    static constexpr int PWV = FP < 8 ? FP : 8, CWV = 8 / PWV;
+    static constexpr int FPW = FP / PWV, TPW = NT / CWV;      // per wave
+    static constexpr int B_BYTES = Q * P * 64, A_BYTES = C * 64, H_BYTES = HH * HWD * 8 * 16;
+    static constexpr int LDS = B_BYTES + 2 * A_BYTES + H_BYTES;
+    static constexpr int AR = (C * 4 + 511) / 512;            // weight chunks per thread and K step
+    static_assert(FP % PWV == 0 && NT % CWV == 0 && (OUTS == 1 || OUTS == 2), "dwpw tiling");
+};
+
+template <int C, int TW>
+__global__ __launch_bounds__(512, C <= 96 ? 2 : 1) void dwpw_kernel(DwPwParams p) {
+    using G = DwPwCfg<C, TW>;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint8_t* Bt = lds;                        // [Q][P rows][4 slots]
+    uint8_t* At = lds + G::B_BYTES;           // 2 x [C rows][4 slots]
+    uint4* halo = reinterpret_cast<uint4*>(lds + G::B_BYTES + 2 * G::A_BYTES);  // [8 chunks][HH * HWD]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int th = blockIdx.x / p.tiles_w, tw = blockIdx.x - th * p.tiles_w;
+    const int n = blockIdx.y;
+    const int h0 = th * G::TH, w0 = tw * TW;
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    // weight ring: step q's C x 64 B slab is contiguous in the image
+    uint4 wr[G::AR];
+    auto load_w = [&](int q) {
+#pragma unroll
+        for (int j = 0; j < G::AR; j++) {
+            const int i = tid + j * 512;
+            if (i < C * 4) wr[j] = *reinterpret_cast<const uint4*>(p.wimg + ((size_t)q * C * 4 + i) * 8);
+        }
+    };
+    auto store_w = [&](int slot) {
+#pragma unroll
+        for (int j = 0; j < G::AR; j++) {
+            const int i = tid + j * 512;
+            if (i < C * 4) *reinterpret_cast<uint4*>(At + slot * G::A_BYTES + i * 16) = wr[j];
+        }
+    };
+    load_w(0);
+    // ---- depthwise phase
+    const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+#pragma unroll 1
+    for (int c0 = 0; c0 < G::NCH; c0 += 8) {
+        const int g = min(8, G::NCH - c0);   // chunks this round
+        for (int i = tid; i < G::HH * G::HWD * g; i += 512) {
+            const int pix = i / g, q = i - pix * g;
+            const int r = pix / G::HWD, c = pix - r * G::HWD;
+            const int hi = h0 - 2 + r, wi = w0 - 2 + c;
+            halo[q * G::HH * G::HWD + pix] =
+                (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                    ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + (c0 + q) * 8)
+                    : uint4{0u, 0u, 0u, 0u};
+        }
+        __syncthreads();
+        if (wave < g) {
+            const int chunk = c0 + wave;
+            const float* wc = p.dw_w + (size_t)chunk * 200;
+            const float* bc = p.dw_b + chunk * 8;
+            const uint4* hq = halo + wave * G::HH * G::HWD;
+            const int q = chunk >> 2, kg = chunk & 3;
+            if constexpr (G::OUTS == 2) {   // dw5_kernel's lane layout: 2 vertical outputs per lane
+                const int col = lane & 15, rp = lane >> 4;
+                f32x2v a0[4], a1[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++) a0[c] = a1[c] = f32x2v{0.f, 0.f};
+#pragma unroll 1
+                for (int ir = 0; ir < 6; ir++) {
+#pragma unroll
+                    for (int kw = 0; kw < 5; kw++) {
+                        float v[8];
+                        unpack8(hq[(2 * rp + ir) * G::HWD + col + kw], v);
+                        if (ir < 5) {
+                            const float* wk = wc + (ir * 5 + kw) * 8;
+#pragma unroll
+                            for (int c = 0; c < 4; c++)
+                                a0[c] = __builtin_elementwise_fma(f32x2v{v[2 * c], v[2 * c + 1]},
+                                                                  f32x2v{wk[2 * c], wk[2 * c + 1]}, a0[c]);
+                        }
+                        if (ir >= 1) {
+                            const float* wk = wc + ((ir - 1) * 5 + kw) * 8;
+#pragma unroll
+                            for (int c = 0; c < 4; c++)
+                                a1[c] = __builtin_elementwise_fma(f32x2v{v[2 * c], v[2 * c + 1]},
+                                                                  f32x2v{wk[2 * c], wk[2 * c + 1]}, a1[c]);
+                        }
+                    }
+                }
+                float o0[8], o1[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    o0[c] = act_f(a0[c >> 1][c & 1] + bc[c], p.act_dw);
+                    o1[c] = act_f(a1[c >> 1][c & 1] + bc[c], p.act_dw);
+                }
+                const int pa = (2 * rp) * TW + col, pb = pa + TW;
+                *reinterpret_cast<uint4*>(Bt + q * G::P * 64 + pa * 64 + ((kg ^ swz(pa)) * 16)) = pack8(o0);
+                *reinterpret_cast<uint4*>(Bt + q * G::P * 64 + pb * 64 + ((kg ^ swz(pb)) * 16)) = pack8(o1);
+            } else {                          // one output per lane, the same chain (taps in (kh, kw) order)
+                const int col = lane % TW, row = lane / TW;
+                f32x2v a0[4];
+#pragma unroll
+                for (int c = 0; c < 4; c++) a0[c] = f32x2v{0.f, 0.f};
+#pragma unroll 1
+                for (int kh = 0; kh < 5; kh++) {
+#pragma unroll
+                    for (int kw = 0; kw < 5; kw++) {
+                        float v[8];
+                        unpack8(hq[(row + kh) * G::HWD + col + kw], v);
+                        const float* wk = wc + (kh * 5 + kw) * 8;
+#pragma unroll
+                        for (int c = 0; c < 4; c++)
+                            a0[c] = __builtin_elementwise_fma(f32x2v{v[2 * c], v[2 * c + 1]},
+                                                              f32x2v{wk[2 * c], wk[2 * c + 1]}, a0[c]);
+                    }
+                }
+                float o0[8];
+#pragma unroll
+                for (int c = 0; c < 8; c++) o0[c] = act_f(a0[c >> 1][c & 1] + bc[c], p.act_dw);
+                const int pa = row * TW + col;
+                *reinterpret_cast<uint4*>(Bt + q * G::P * 64 + pa * 64 + ((kg ^ swz(pa)) * 16)) = pack8(o0);
+            }
+        }
+        __syncthreads();   // the halo is reloaded by the next round
+    }
+    store_w(0);
+    if (G::Q > 1) load_w(1);
+    __syncthreads();
+    // ---- pointwise phase
+    const int wp = wave % G::PWV, wc = wave / G::PWV;
+    const int kg = lane >> 4, r16 = lane & 15;
+    const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
+    f32x4 acc[G::FPW][G::TPW];
+#pragma unroll
+    for (int i = 0; i < G::FPW; i++)
+#pragma unroll
+        for (int j = 0; j < G::TPW; j++) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int q = 0; q < G::Q; q++) {
+        const uint8_t* ab = At + (q & 1) * G::A_BYTES;
+        const uint8_t* bb = Bt + q * G::P * 64;
+        bf16x8 a[G::TPW], b[G::FPW];
+#pragma unroll
+        for (int j = 0; j < G::TPW; j++)
+            a[j] = *reinterpret_cast<const bf16x8*>(ab + ((wc * G::TPW + j) * 16) * 64 + soff);
+#pragma unroll
+        for (int i = 0; i < G::FPW; i++)
+            b[i] = *reinterpret_cast<const bf16x8*>(bb + ((wp * G::FPW + i) * 16) * 64 + soff);
+#pragma unroll
+        for (int i = 0; i < G::FPW; i++)
+#pragma unroll
+            for (int j = 0; j < G::TPW; j++)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[j], b[i], acc[i][j], 0, 0, 0);
+        if (q + 1 < G::Q) {
+            store_w((q + 1) & 1);   // that slot was last read in step q - 1: every wave is past it
+            if (q + 2 < G::Q) load_w(q + 2);
+        }
+        __syncthreads();
+    }
+    // ---- epilogue (det_conv_gemm_kernel's)
+#pragma unroll
+    for (int j = 0; j < G::TPW; j++) {
+        const int co = (wc * G::TPW + j) * 16 + kg * 4;
+        if (co >= p.N) continue;
+        const float4 bb = *reinterpret_cast<const float4*>(p.pw_b + co);
+#pragma unroll
+        for (int i = 0; i < G::FPW; i++) {
+            const int px = (wp * G::FPW + i) * 16 + r16;
+            const int h = h0 + px / TW, w = w0 + px % TW;
+            if (h >= p.H || w >= p.W) continue;
+            const size_t m = ((size_t)n * p.H + h) * p.W + w;
+            float v[4] = {acc[i][j][0] + bb.x, acc[i][j][1] + bb.y, acc[i][j][2] + bb.z, acc[i][j][3] + bb.w};
+            if (p.act_pw == 2)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+            if (p.res) {
+                const uint2 r = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                v[0] += bf(r.x & 0xffff), v[1] += bf(r.x >> 16), v[2] += bf(r.y & 0xffff), v[3] += bf(r.y >> 16);
+            }
+            if (p.act_pw == 1)
+#pragma unroll
+                for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+            *reinterpret_cast<uint2*>(p.y + m * p.ys + co) =
+                uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+        }
+    }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- launchers
@@ -1304,12 +1537,18 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
                     int C, int act, hipStream_t s) {
     MVP_REQUIRE(C % 32 == 0 && xs % 8 == 0 && ys % 8 == 0, "dw5: channels must be a multiple of 32");
     DwParams p{x, y, w, b, H, W, C, xs, ys, act, (W + kDwTW - 1) / kDwTW};
-    const int G = C % 64 == 0 ? 8 : 4;
+    // G chunks of 8 channels per workgroup: 8 (128 B of every pixel, one cache line); the
+    // 96-channel planes take all 12 chunks (the whole 192-B pixel) — with G = 4 each workgroup
+    // read a 64-B third of every pixel and the PMC showed 2.07x the algorithmic bytes
+    // (gpurun_out/detbd: 509 us per 80x80x96 layer of 512 frames)
+    const int G = C % 64 == 0 ? 8 : C == 96 ? 12 : 4;
     const long blocks = (long)p.tiles_w * ((H + kDwTH - 1) / kDwTH) * (C / (8 * G));
     if (n == 0 || blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
     if (G == 8)
         hipLaunchKernelGGL(dw5_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
+    else if (G == 12)
+        hipLaunchKernelGGL(dw5_kernel<12>, dim3((unsigned)blocks, (unsigned)n), dim3(768), 0, s, p);
     else
         hipLaunchKernelGGL(dw5_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
     MVP_HIP(hipGetLastError());
@@ -1389,7 +1628,11 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     // a 4-slot ring level; removed with their environment switches in round 3.
     const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
-              (npad + bn - 1) / bn, H, W, Ho, Wo, wimg};
+              (npad + bn - 1) / bn, 0, H, W, Ho, Wo, wimg};
+    {
+        const char* e = getenv("MVPOSE_DET_XCD");  // A/B: 0 = blockIdx order
+        p.xcd_order = !(e && e[0] == '0');
+    }
     // band-halo kernel for the 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40
     // planes (det_conv_band_kernel)
     // The kernel splits each XCD's grid/8 workgroups into groups of n_nb (one per cout block):
@@ -1461,6 +1704,36 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
 #undef MVP_DET_CONV_BN
     MVP_HIP(hipGetLastError());
 }
+
+template <int C, int TW>
+void launch_dwpw_t(const DwPwParams& p, int n, hipStream_t s) {
+    using G = DwPwCfg<C, TW>;
+    static bool attr = false;
+    if (!attr) {
+        MVP_HIP(hipFuncSetAttribute((const void*)dwpw_kernel<C, TW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        attr = true;
+    }
+    const int tiles = ((p.H + G::TH - 1) / G::TH) * p.tiles_w;
+    hipLaunchKernelGGL((dwpw_kernel<C, TW>), dim3((unsigned)tiles, (unsigned)n), dim3(512), G::LDS, s, p);
+}
+
+void launch_det_dwpw(const uint16_t* x, int xs, const float* dw_w, const float* dw_b, const uint16_t* wimg,
+                     const float* pw_b, const uint16_t* res, int rs, uint16_t* y, int ys, int n, int H, int W, int C,
+                     int N, int act_dw, int act_pw, hipStream_t s) {
+    MVP_REQUIRE(det_dwpw_supported(C) && det_cout_pad(N) == C && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
+                "dwpw: C=%d cout=%d strides %d/%d", C, N, xs, ys);
+    if (n == 0) return;
+    MVP_REQUIRE(n < 65536 && (long)H * W < (1L << 26), "dwpw: grid too large");
+    const int TW = C <= 96 ? 16 : 8;
+    DwPwParams p{x, dw_w, dw_b, wimg, pw_b, res, y, H, W, N, xs, ys, rs, act_dw, act_pw, (W + TW - 1) / TW};
+    if (C == 64) launch_dwpw_t<64, 16>(p, n, s);
+    else if (C == 96) launch_dwpw_t<96, 16>(p, n, s);
+    else if (C == 192) launch_dwpw_t<192, 8>(p, n, s);
+    else launch_dwpw_t<384, 8>(p, n, s);
+    MVP_HIP(hipGetLastError());
+}
+
+bool det_dwpw_supported(int C) { return C == 64 || C == 96 || C == 192 || C == 384; }
 
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
                    hipStream_t s) {

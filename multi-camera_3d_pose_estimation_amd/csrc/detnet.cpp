@@ -102,6 +102,23 @@ void validate(DetNet& g, int64_t w_elems, int64_t f_elems) {
                 f_ok(op.b_off, op.in.c, k);
                 break;
             }
+            case MVP_DET_DWPW: {
+                const mvp_tensor_desc& x = view_ok(op.in, "in", k);
+                const mvp_tensor_desc& y = view_ok(op.out, "out", k);
+                const int C = op.in.c;
+                MVP_REQUIRE(det_dwpw_supported(C) && det_cout_pad(op.out.c) == C && op.ks == 5 && x.h == y.h &&
+                                x.w == y.w && op.in.t != op.out.t,
+                            "det dwpw %zu: C=%d cout=%d ks %d", k, C, op.out.c, op.ks);
+                if (op.res.t >= 0) {
+                    const mvp_tensor_desc& r = view_ok(op.res, "res", k);
+                    MVP_REQUIRE(r.h == y.h && r.w == y.w && op.res.c == op.out.c, "det dwpw %zu: residual shape", k);
+                }
+                f_ok(op.w_off, (int64_t)C * 25, k);
+                f_ok(op.b_off, 2 * (int64_t)C, k);
+                MVP_REQUIRE(op.aux >= 0 && op.aux % 8 == 0 && op.aux + (int64_t)C * C <= w_elems,
+                            "det dwpw %zu: pointwise weights out of the bf16 blob", k);
+                break;
+            }
             case MVP_DET_CA: {
                 view_ok(op.in, "in", k);
                 MVP_REQUIRE(op.in.c / 8 <= 256, "det ca %zu: %d channels", k, op.in.c);
@@ -154,9 +171,10 @@ void plan(DetNet& g) {
     for (int k = 0; k < no; k++) {
         const mvp_det_op& op = g.ops[k];
         touch(op.in.t, k);
-        if (op.kind == MVP_DET_STEM || op.kind == MVP_DET_CONV || op.kind == MVP_DET_DW || op.kind == MVP_DET_UP2)
+        if (op.kind == MVP_DET_STEM || op.kind == MVP_DET_CONV || op.kind == MVP_DET_DW || op.kind == MVP_DET_UP2 ||
+            op.kind == MVP_DET_DWPW)
             touch(op.out.t, k);
-        if (op.kind == MVP_DET_CONV) touch(op.res.t, k);
+        if (op.kind == MVP_DET_CONV || op.kind == MVP_DET_DWPW) touch(op.res.t, k);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
@@ -226,6 +244,12 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
         g->wband.assign(g->ops.size(), nullptr);
         for (size_t k = 0; k < g->ops.size(); k++) {
             const mvp_det_op& op = g->ops[k];
+            if (op.kind == MVP_DET_DWPW) {  // the pointwise weights' GEMM image
+                const int C = op.in.c;
+                MVP_HIP(hipMalloc(&g->wimg[k], (size_t)C * C * sizeof(uint16_t)));
+                mvp::det_pack_gemm_weights(w_dev + op.aux, g->wimg[k], C, C, nullptr);
+                continue;
+            }
             if (op.kind != MVP_DET_CONV) continue;
             const int npad = mvp::det_cout_pad(op.out.c), K = op.ks * op.ks * op.in.c;
             MVP_HIP(hipMalloc(&g->wimg[k], (size_t)npad * K * sizeof(uint16_t)));
@@ -279,6 +303,14 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 const mvp_tensor_desc& x = T(op.in.t);
                 launch_det_dw5(vp(op.in), x.c, vp(op.out), T(op.out.t).c, g->fb + op.w_off, g->fb + op.b_off, n, x.h,
                                x.w, op.in.c, op.act, s);
+                break;
+            }
+            case MVP_DET_DWPW: {
+                const mvp_tensor_desc& x = T(op.in.t);
+                launch_det_dwpw(vp(op.in), x.c, g->fb + op.w_off, g->fb + op.b_off, g->wimg[k],
+                                g->fb + op.b_off + op.in.c, op.res.t >= 0 ? vp(op.res) : nullptr,
+                                op.res.t >= 0 ? T(op.res.t).c : 0, vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c,
+                                op.out.c, op.act, op.act, s);
                 break;
             }
             case MVP_DET_CA: {

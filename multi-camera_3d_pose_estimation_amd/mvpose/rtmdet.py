@@ -47,7 +47,8 @@ DEEPEN, WIDEN = 0.67, 0.75
 NECK_OUT = 192
 FEAT = 192
 TEST_CFG = dict(nms_pre=1000, min_bbox_size=0, score_thr=0.05, iou_threshold=0.6, max_per_img=100)
-DET_STEM, DET_CONV, DET_DW, DET_CA, DET_SPP, DET_UP2, DET_HEAD = range(7)
+DET_STEM, DET_CONV, DET_DW, DET_CA, DET_SPP, DET_UP2, DET_HEAD, DET_DWPW = range(8)
+DWPW_CHANNELS = (64, 96, 192, 384)   # stored channel counts the fused dw5 + pw kernel is built for
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 
 
@@ -237,8 +238,11 @@ NONE_VIEW = DetView(-1, 0, 0)
 
 
 class DetSpec:
-    def __init__(self, size=SIZE, keep_f32=False):
+    def __init__(self, size=SIZE, keep_f32=False, fuse_dwpw=None):
         self.size = size
+        # CSPNeXtBlock conv2 as one fused op (default); MVPOSE_DET_DWPW=0 keeps the depthwise
+        # output as a tensor of its own (layer-by-layer parity tests, the fused-vs-unfused test)
+        self.fuse_dwpw = os.environ.get("MVPOSE_DET_DWPW", "1") != "0" if fuse_dwpw is None else bool(fuse_dwpw)
         self.f32_weights = {} if keep_f32 else None  # w_off -> unrounded conv weights (tests)
         self.tensors: list[tuple[int, int, int, int]] = []
         self.ops: list[DetOp] = []
@@ -334,6 +338,36 @@ class DetSpec:
         self.macs += h * ww * w.shape[0] * 25
         return out
 
+    def dwpw(self, sd, dw_name, pw_name, x: View, out: View, res: View | None = None):
+        """DepthwiseSeparableConvModule (5x5 depthwise + BN + SiLU, then 1x1 + BN + SiLU) as ONE
+        op (DET_DWPW, det.hip dwpw_kernel): the depthwise output stays in LDS.  w_off: the
+        depthwise f32 weights [C/8][25][8]; b_off: [depthwise bias (C) | pointwise bias (C)] f32;
+        aux: the pointwise bf16 weights [C][1][1][C]."""
+        wd, bd = fold(sd, dw_name)          # (c, 1, 5, 5)
+        wp, bp = fold(sd, pw_name)          # (cout, c, 1, 1)
+        h, ww = self.hw(x)
+        C = x.c
+        cout, cin = wp.shape[:2]
+        assert cin == len(x.cmap) and len(out.cmap) == cout and self.hw(out) == (h, ww), (dw_name, pw_name)
+        cp = cout_pad(out.c)
+        assert cp == C, (dw_name, cp, C)
+        wsd = np.zeros((C, 25))
+        wsd[x.cmap] = wd.reshape(wd.shape[0], 25)
+        wsd = wsd.reshape(C // 8, 8, 25).transpose(0, 2, 1)
+        bsd = np.zeros(C)
+        bsd[x.cmap] = bd
+        wsp = np.zeros((cp, 1, 1, C))
+        wsp[np.ix_(out.cmap, [0], [0], x.cmap)] = wp.transpose(0, 2, 3, 1)
+        bsp = np.zeros(cp)
+        bsp[out.cmap] = bp
+        aux = self._push_w(to_bf16_bits(wsp))
+        if self.f32_weights is not None:
+            self.f32_weights[aux] = wsp.astype(np.float32)
+        self._op(dw_name + "+" + pw_name, DET_DWPW, x, out, res, ks=5, w_off=self._push_f(wsd),
+                 b_off=self._push_f(np.concatenate([bsd, bsp])), aux=aux)
+        self.macs += h * ww * wd.shape[0] * 25 + h * ww * cout * cin
+        return out
+
     def attention(self, sd, name, x: View):
         wr = sd[name + ".fc.weight"].double().numpy()[:, :, 0, 0]  # (c_out, c_in)
         br = sd[name + ".fc.bias"].double().numpy()
@@ -353,6 +387,10 @@ class DetSpec:
         for b in range(n_blocks):
             q = f"{p}.blocks.{b}"
             t1 = self.conv(sd, f"{q}.conv1", main, 3)
+            if self.fuse_dwpw and t1.c in DWPW_CHANNELS:
+                self.dwpw(sd, f"{q}.conv2.depthwise_conv", f"{q}.conv2.pointwise_conv", t1, main,
+                          res=main if add_identity else None)
+                continue
             t2 = self.dw(sd, f"{q}.conv2.depthwise_conv", t1)
             self.conv(sd, f"{q}.conv2.pointwise_conv", t2, 1, out=main, res=main if add_identity else None)
         if attention:

@@ -60,6 +60,23 @@ def apply_op(spec: D.DetSpec, T: list, op, cand: torch.Tensor, device_weights: b
         w = fb[op.w_off:op.w_off + c * 25].view(c // 8, 25, 8).permute(0, 2, 1).reshape(c, 1, 5, 5)
         b = fb[op.b_off:op.b_off + c]
         put(op.out, _act(F.conv2d(get(op.in_), w, b, padding=2, groups=c), op.act))
+    elif op.kind == D.DET_DWPW:   # depthwise 5x5 + SiLU, then pointwise 1x1 + SiLU (+ identity)
+        c = op.in_.c
+        w = fb[op.w_off:op.w_off + c * 25].view(c // 8, 25, 8).permute(0, 2, 1).reshape(c, 1, 5, 5)
+        b = fb[op.b_off:op.b_off + c]
+        t = _act(F.conv2d(get(op.in_), w, b, padding=2, groups=c), op.act)
+        if device_weights:        # the kernel rounds the intermediate to bf16, as the unfused pair stores it
+            t = t.to(torch.bfloat16).float()
+        cout = op.out.c
+        cp = D.cout_pad(cout)
+        if spec.f32_weights is not None and not device_weights:
+            wp = torch.from_numpy(spec.f32_weights[op.aux])[:cout].permute(0, 3, 1, 2)
+        else:
+            wp = wf[op.aux:op.aux + cp * c].view(cp, 1, 1, c)[:cout].permute(0, 3, 1, 2)
+        y = _act(F.conv2d(t, wp, fb[op.b_off + c:op.b_off + c + cout]), op.act)
+        if op.res.t >= 0:
+            y = y + get(op.res)
+        put(op.out, y)
     elif op.kind == D.DET_CA:
         c = op.in_.c
         x = get(op.in_)

@@ -132,6 +132,28 @@ def test_halo_rows_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_dwpw_fused_bitwise(sd, size, n, monkeypatch):
+    """Every CSPNeXtBlock's conv2 as ONE launch (DET_DWPW: 5x5 depthwise + 1x1 pointwise, the
+    depthwise output kept in LDS; det.hip dwpw_kernel) against the unfused pair (dw5_kernel +
+    the 1x1 GEMM, MVPOSE_DET_DWPW=0): the same fma chains, bf16 rounding of the intermediate, MFMA
+    operands and K order, so the candidates of every prior and the selected boxes are
+    bit-identical (at 128 the 4x4 .. 32x32 planes exercise the partial tiles)."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=9)).cuda()
+    out = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("MVPOSE_DET_DWPW", fuse)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        kinds = [op.kind for op in det.spec.ops]
+        assert (D.DET_DWPW in kinds) == (fuse == "1") and (D.DET_DW in kinds) == (fuse == "0")
+        r = det.detect(frames)
+        torch.cuda.synchronize()
+        out[fuse] = (r["cand"].cpu(), r["best"].cpu())
+        det.close()
+    assert torch.equal(out["0"][0].view(torch.int32), out["1"][0].view(torch.int32))
+    assert torch.equal(out["0"][1].view(torch.int32), out["1"][1].view(torch.int32))
+
+
 def test_band_conv_vs_gemm(sd, monkeypatch):
     """The 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40 planes run on the
     band-halo kernel (det_conv_band_kernel, the default): each one, on the forward's own input,

@@ -1,0 +1,103 @@
+"""Per-op breakdown of one RTMDet-m forward from a kernel trace (+ optional PMC traffic):
+    python tools/det_breakdown.py run BATCH PLAN.npz          # on the GPU (under rocprofv3): 3 detects, saves the op plan
+    python tools/det_breakdown.py report TRACE.csv PLAN.npz [PMC_FETCH.csv PMC_WRITE.csv]
+Each graph op launches one kernel (channel attention three: pool, fc, scale), the letterbox one in
+front and the per-frame selection one after; the last forward's kernels pair with the op list
+in order.  Per op: us, algorithmic HBM bytes (input read once + output + residual, the stored
+channel counts) and MACs, so the roofline each op is held to is visible."""
+import csv
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd")]
+KIND = {0: "stem", 1: "conv", 2: "dw5", 3: "ca", 4: "spp", 5: "up2", 6: "head"}
+
+
+def plan(batch):
+    from mvpose import rtmdet as D
+    det = D.RTMDetector(seed=0, max_batch=batch)
+    sp = det.spec
+    rows = [("letterbox", "letterbox", 0.0, batch * (720 * 1280 * 3 + 640 * 640 * 4 * 2))]
+    T = sp.tensors
+    for name, op in zip(sp.names, sp.ops):
+        k = KIND[op.kind]
+        hi, wi, ci, _ = T[op.in_.t]
+        if op.out.t >= 0:
+            ho, wo, _, _ = T[op.out.t]
+        macs, byts = 0.0, 0.0
+        if k == "conv":
+            macs = ho * wo * op.out.c * op.in_.c * op.ks * op.ks
+            byts = hi * wi * op.in_.c * 2 + ho * wo * op.out.c * 2 * (2 if op.res.t >= 0 else 1)
+        elif k == "stem":
+            macs, byts = ho * wo * 32 * 27, hi * wi * 8 + ho * wo * 64
+        elif k == "dw5":
+            macs, byts = hi * wi * op.in_.c * 25, hi * wi * op.in_.c * 4
+        elif k in ("spp", "up2"):
+            byts = hi * wi * op.in_.c * (8 if k == "spp" else 10)
+        elif k == "head":
+            macs, byts = hi * wi * 5 * op.in_.c // 2, hi * wi * op.in_.c * 2
+        if k == "ca":
+            c = op.in_.c
+            rows += [(name + ".pool", "ca", 0.0, batch * hi * wi * c * 2.0), (name + ".fc", "ca", 0.0, batch * c * c * 4.0),
+                     (name + ".scale", "ca", 0.0, batch * hi * wi * c * 4.0)]
+        else:
+            rows.append((name, k, batch * float(macs), batch * float(byts)))
+    rows.append(("select", "select", 0.0, 0.0))
+    return det, rows
+
+
+if sys.argv[1] == "run":
+    import torch
+    batch = int(sys.argv[2])
+    det, rows = plan(batch)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    frames = torch.randint(0, 256, (batch, 720, 1280, 3), dtype=torch.uint8, device="cuda", generator=g)
+    for _ in range(3):
+        det.detect(frames)
+    torch.cuda.synchronize()
+    np.savez(sys.argv[3], names=np.array([r[0] for r in rows]), kinds=np.array([r[1] for r in rows]),
+             macs=np.array([r[2] for r in rows]), bytes=np.array([r[3] for r in rows]), batch=batch)
+    print("ok", len(rows), "launches per forward")
+    sys.exit(0)
+
+rows = sorted(csv.DictReader(open(sys.argv[2])), key=lambda r: int(r["Start_Timestamp"]))
+z = np.load(sys.argv[3])
+L = len(z["names"])
+last = rows[-L:]
+assert "letterbox" in last[0]["Kernel_Name"], last[0]["Kernel_Name"]
+traffic = None
+if len(sys.argv) > 5:
+    def pmc(path, counter):
+        vals = {}
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] == counter:
+                d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+                vals[d] = vals.get(d, 0.0) + float(r["Counter_Value"])
+        ids = sorted(vals)
+        return [vals[i] for i in ids[-L:]]
+    f, w = pmc(sys.argv[4], "FETCH_SIZE"), pmc(sys.argv[5], "WRITE_SIZE")
+    traffic = [(2 * a + b) * 1024 for a, b in zip(f, w)]   # gfx950: FETCH_SIZE counts half of a wide stream
+tot = 0.0
+print(f"RTMDet-m forward, {int(z['batch'])} camera-frames: {L} launches")
+print(f"{'us':>9} {'TB/s':>6} {'TF/s':>7} {'MFMA%':>6} {'PMC/alg':>7}  kernel / op")
+fam = {}
+for i, r in enumerate(last):
+    us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot += us
+    kn = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("mvp::", "").split("(")[0][:48]
+    tb = z["bytes"][i] / (us * 1e-6) / 1e12 if us else 0
+    tf = 2 * z["macs"][i] / (us * 1e-6) / 1e12 if us else 0
+    amp = f"{traffic[i] / z['bytes'][i]:7.2f}" if traffic and z["bytes"][i] else "      -"
+    print(f"{us:9.1f} {tb:6.2f} {tf:7.1f} {100 * tf / 2500:5.1f}% {amp}  {kn} / {z['names'][i]}")
+    a = fam.setdefault(kn, [0, 0.0, 0.0, 0.0])
+    a[0] += 1
+    a[1] += us
+    a[2] += z["macs"][i]
+    a[3] += z["bytes"][i]
+print(f"sum {tot / 1e3:.3f} ms")
+print("\nper kernel family:")
+for kn, (n, us, macs, byts) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+    print(f"{us:9.1f} us {n:3d} x  {byts / (us * 1e-6) / 1e12:5.2f} TB/s  {2 * macs / (us * 1e-6) / 1e12:7.1f} TFLOP/s  {kn}")
