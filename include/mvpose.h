@@ -282,7 +282,7 @@ int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, i
  *                  clipped to [0, size] (mmdet distance2bbox on img_shape).
  *   MVP_DET_DWPW : a CSPNeXtBlock's conv2 (DepthwiseSeparableConvModule) in one launch:
  *                  t = act(dw5x5(in) + b_dw) rounded to bf16 (never stored), then
- *                  out = act(t . W_pw + b_pw) [+ res]; in.c = C in {64, 96, 192, 384},
+ *                  out = act(t . W_pw + b_pw) [+ res]; in.c = C in {64, 96},
  *                  cout_pad(out.c) == C.  w_off: dw f32 weights [C/8][25][8]; b_off: f32
  *                  [b_dw (C) | b_pw (C)]; aux: pw bf16 weights [C][1][1][C].  Bit-identical to
  *                  MVP_DET_DW followed by a 1x1 MVP_DET_CONV.

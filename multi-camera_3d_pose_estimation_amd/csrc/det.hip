@@ -190,7 +190,7 @@ struct DwParams {
 };
 
 template <int G>
-__global__ __launch_bounds__(G * 64, G > 8 ? 1 : 8 / G * 2) void dw5_kernel(DwParams p) {
+__global__ __launch_bounds__(G * 64, 8 / G * 2) void dw5_kernel(DwParams p) {
     __shared__ uint4 sh[G][kDwHH * kDwHW];
     const int n_groups = p.C / (8 * G);
     const int grp = blockIdx.x % n_groups;
@@ -1297,9 +1297,9 @@ struct DwPwParams {
     int H, W, N, xs, ys, rs, act_dw, act_pw, tiles_w;
 };
 
-template <int C, int TW>
+template <int C, int TH_, int TW>
 struct DwPwCfg {
-    static constexpr int TH = 8, P = TH * TW, OUTS = P / 64;  // dw outputs per lane
+    static constexpr int TH = TH_, P = TH * TW, OUTS = P / 64;  // dw outputs per lane
     static constexpr int HH = TH + 4, HWD = TW + 4;           // halo rows / columns
     static constexpr int Q = C / 32, NCH = C / 8;             // K steps, 8-channel chunks
     static constexpr int FP = P / 16, NT = C / 16;            // pixel fragments, cout tiles
@@ -1311,9 +1311,9 @@ struct DwPwCfg {
     static_assert(FP % PWV == 0 && NT % CWV == 0 && (OUTS == 1 || OUTS == 2), "dwpw tiling");
 };
 
-template <int C, int TW>
-__global__ __launch_bounds__(512, C <= 96 ? 2 : 1) void dwpw_kernel(DwPwParams p) {
-    using G = DwPwCfg<C, TW>;
+template <int C, int TH, int TW>
+__global__ __launch_bounds__(512, TH == 4 ? 3 : 2) void dwpw_kernel(DwPwParams p) {
+    using G = DwPwCfg<C, TH, TW>;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint8_t* Bt = lds;                        // [Q][P rows][4 slots]
     uint8_t* At = lds + G::B_BYTES;           // 2 x [C rows][4 slots]
@@ -1341,20 +1341,53 @@ __global__ __launch_bounds__(512, C <= 96 ? 2 : 1) void dwpw_kernel(DwPwParams p
         }
     };
     load_w(0);
+    // the epilogue's residual, loaded now so that it lands under the depthwise phase
+    const int wp = wave % G::PWV, wc = wave / G::PWV;
+    const int kg = lane >> 4, r16 = lane & 15;
+    uint2 rsd[G::FPW][G::TPW];
+    if (p.res) {
+#pragma unroll
+        for (int i = 0; i < G::FPW; i++) {
+            const int px = (wp * G::FPW + i) * 16 + r16;
+            const int h = h0 + px / TW, w = w0 + px % TW;
+#pragma unroll
+            for (int j = 0; j < G::TPW; j++) {
+                const int co = (wc * G::TPW + j) * 16 + kg * 4;
+                rsd[i][j] = (h < p.H && w < p.W && co < p.N)
+                                ? *reinterpret_cast<const uint2*>(p.res + (((size_t)n * p.H + h) * p.W + w) * p.rs + co)
+                                : uint2{0u, 0u};
+            }
+        }
+    }
     // ---- depthwise phase
     const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
     typedef float f32x2v __attribute__((ext_vector_type(2)));
 #pragma unroll 1
     for (int c0 = 0; c0 < G::NCH; c0 += 8) {
         const int g = min(8, G::NCH - c0);   // chunks this round
-        for (int i = tid; i < G::HH * G::HWD * g; i += 512) {
-            const int pix = i / g, q = i - pix * g;
-            const int r = pix / G::HWD, c = pix - r * G::HWD;
-            const int hi = h0 - 2 + r, wi = w0 - 2 + c;
-            halo[q * G::HH * G::HWD + pix] =
-                (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
-                    ? *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + (c0 + q) * 8)
-                    : uint4{0u, 0u, 0u, 0u};
+        {   // every load of the round in flight before the first LDS write
+            constexpr int HR = (G::HH * G::HWD * 8 + 511) / 512;
+            uint4 hv[HR];
+#pragma unroll
+            for (int j = 0; j < HR; j++) {
+                const int i = tid + j * 512;
+                hv[j] = uint4{0u, 0u, 0u, 0u};
+                if (i < G::HH * G::HWD * g) {
+                    const int pix = i / g, q = i - pix * g;
+                    const int r = pix / G::HWD, c = pix - r * G::HWD;
+                    const int hi = h0 - 2 + r, wi = w0 - 2 + c;
+                    if (hi >= 0 && hi < p.H && wi >= 0 && wi < p.W)
+                        hv[j] = *reinterpret_cast<const uint4*>(xb + ((size_t)hi * p.W + wi) * p.xs + (c0 + q) * 8);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < HR; j++) {
+                const int i = tid + j * 512;
+                if (i < G::HH * G::HWD * g) {
+                    const int pix = i / g, q = i - pix * g;
+                    halo[q * G::HH * G::HWD + pix] = hv[j];
+                }
+            }
         }
         __syncthreads();
         if (wave < g) {
@@ -1430,8 +1463,6 @@ __global__ __launch_bounds__(512, C <= 96 ? 2 : 1) void dwpw_kernel(DwPwParams p
     if (G::Q > 1) load_w(1);
     __syncthreads();
     // ---- pointwise phase
-    const int wp = wave % G::PWV, wc = wave / G::PWV;
-    const int kg = lane >> 4, r16 = lane & 15;
     const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
     f32x4 acc[G::FPW][G::TPW];
 #pragma unroll
@@ -1477,7 +1508,7 @@ __global__ __launch_bounds__(512, C <= 96 ? 2 : 1) void dwpw_kernel(DwPwParams p
 #pragma unroll
                 for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
             if (p.res) {
-                const uint2 r = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                const uint2 r = rsd[i][j];
                 v[0] += bf(r.x & 0xffff), v[1] += bf(r.x >> 16), v[2] += bf(r.y & 0xffff), v[3] += bf(r.y >> 16);
             }
             if (p.act_pw == 1)
@@ -1537,18 +1568,17 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
                     int C, int act, hipStream_t s) {
     MVP_REQUIRE(C % 32 == 0 && xs % 8 == 0 && ys % 8 == 0, "dw5: channels must be a multiple of 32");
     DwParams p{x, y, w, b, H, W, C, xs, ys, act, (W + kDwTW - 1) / kDwTW};
-    // G chunks of 8 channels per workgroup: 8 (128 B of every pixel, one cache line); the
-    // 96-channel planes take all 12 chunks (the whole 192-B pixel) — with G = 4 each workgroup
-    // read a 64-B third of every pixel and the PMC showed 2.07x the algorithmic bytes
-    // (gpurun_out/detbd: 509 us per 80x80x96 layer of 512 frames)
-    const int G = C % 64 == 0 ? 8 : C == 96 ? 12 : 4;
+    // G chunks of 8 channels per workgroup: 8 (128 B of every pixel, one cache line), else 4.
+    // (Measured: the 96-channel planes with all 12 chunks per workgroup read 1.37x the
+    // algorithmic bytes instead of 2.07x but ran 555 vs 509 us per 80x80 layer of 512 frames,
+    // gpurun_out/detbd3: 768-thread workgroups halve the occupancy.  Those planes now run fused,
+    // dwpw_kernel.)
+    const int G = C % 64 == 0 ? 8 : 4;
     const long blocks = (long)p.tiles_w * ((H + kDwTH - 1) / kDwTH) * (C / (8 * G));
     if (n == 0 || blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31) && n < 65536, "dw5: grid too large");
     if (G == 8)
         hipLaunchKernelGGL(dw5_kernel<8>, dim3((unsigned)blocks, (unsigned)n), dim3(512), 0, s, p);
-    else if (G == 12)
-        hipLaunchKernelGGL(dw5_kernel<12>, dim3((unsigned)blocks, (unsigned)n), dim3(768), 0, s, p);
     else
         hipLaunchKernelGGL(dw5_kernel<4>, dim3((unsigned)blocks, (unsigned)n), dim3(256), 0, s, p);
     MVP_HIP(hipGetLastError());
@@ -1705,16 +1735,17 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     MVP_HIP(hipGetLastError());
 }
 
-template <int C, int TW>
+template <int C, int TH, int TW>
 void launch_dwpw_t(const DwPwParams& p, int n, hipStream_t s) {
-    using G = DwPwCfg<C, TW>;
+    using G = DwPwCfg<C, TH, TW>;
     static bool attr = false;
     if (!attr) {
-        MVP_HIP(hipFuncSetAttribute((const void*)dwpw_kernel<C, TW>, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+        MVP_HIP(hipFuncSetAttribute((const void*)dwpw_kernel<C, TH, TW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    G::LDS));
         attr = true;
     }
     const int tiles = ((p.H + G::TH - 1) / G::TH) * p.tiles_w;
-    hipLaunchKernelGGL((dwpw_kernel<C, TW>), dim3((unsigned)tiles, (unsigned)n), dim3(512), G::LDS, s, p);
+    hipLaunchKernelGGL((dwpw_kernel<C, TH, TW>), dim3((unsigned)tiles, (unsigned)n), dim3(512), G::LDS, s, p);
 }
 
 void launch_det_dwpw(const uint16_t* x, int xs, const float* dw_w, const float* dw_b, const uint16_t* wimg,
@@ -1724,16 +1755,20 @@ void launch_det_dwpw(const uint16_t* x, int xs, const float* dw_w, const float* 
                 "dwpw: C=%d cout=%d strides %d/%d", C, N, xs, ys);
     if (n == 0) return;
     MVP_REQUIRE(n < 65536 && (long)H * W < (1L << 26), "dwpw: grid too large");
-    const int TW = C <= 96 ? 16 : 8;
+    constexpr int TW = 16;
     DwPwParams p{x, dw_w, dw_b, wimg, pw_b, res, y, H, W, N, xs, ys, rs, act_dw, act_pw, (W + TW - 1) / TW};
-    if (C == 64) launch_dwpw_t<64, 16>(p, n, s);
-    else if (C == 96) launch_dwpw_t<96, 16>(p, n, s);
-    else if (C == 192) launch_dwpw_t<192, 8>(p, n, s);
-    else launch_dwpw_t<384, 8>(p, n, s);
+    // 4 x 16 tiles: 36-44 KB of LDS, 3 workgroups per CU (8 x 16 tiles: 2 per CU, 83.5 vs 82.0 ms
+    // per 512-frame forward same-box, gpurun_out/r06g)
+    if (C == 64) launch_dwpw_t<64, 4, TW>(p, n, s);
+    else launch_dwpw_t<96, 4, TW>(p, n, s);
     MVP_HIP(hipGetLastError());
 }
 
-bool det_dwpw_supported(int C) { return C == 64 || C == 96 || C == 192 || C == 384; }
+// Measured per block, 512 frames (gpurun_out/detbd2, detbd3): 64 channels on 160x160 1.93 ms fused
+// (4 x 16 tiles) vs 2.73 for dw5 + GEMM; 96 on 80x80 0.90 vs 1.20 (with the identity); with 8 x 8
+// tiles 192 on 40x40 1.00 vs 0.68 and 384 on 20x20 1.12 vs 0.38 — the tile re-reads the whole
+// C x C weight matrix and too few tiles hide the serial phases — so only 64 and 96 are fused.
+bool det_dwpw_supported(int C) { return C == 64 || C == 96; }
 
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
                    hipStream_t s) {

@@ -48,7 +48,9 @@ NECK_OUT = 192
 FEAT = 192
 TEST_CFG = dict(nms_pre=1000, min_bbox_size=0, score_thr=0.05, iou_threshold=0.6, max_per_img=100)
 DET_STEM, DET_CONV, DET_DW, DET_CA, DET_SPP, DET_UP2, DET_HEAD, DET_DWPW = range(8)
-DWPW_CHANNELS = (64, 96, 192, 384)   # stored channel counts the fused dw5 + pw kernel is built for
+# stored channel counts where the fused dw5 + pw kernel runs (the 160x160 / 80x80 planes: CSPNeXt
+# stages 1-2 and the last top-down block); on the 40x40 / 20x20 planes it measured slower (det.hip)
+DWPW_CHANNELS = (64, 96)
 ACT_NONE, ACT_RELU, ACT_SILU = 0, 1, 2
 
 

@@ -134,8 +134,8 @@ def test_halo_rows_bitwise(sd, size, n, monkeypatch):
 
 @pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
 def test_dwpw_fused_bitwise(sd, size, n, monkeypatch):
-    """Every CSPNeXtBlock's conv2 as ONE launch (DET_DWPW: 5x5 depthwise + 1x1 pointwise, the
-    depthwise output kept in LDS; det.hip dwpw_kernel) against the unfused pair (dw5_kernel +
+    """The CSPNeXt stage-1/2 blocks' conv2 as ONE launch (DET_DWPW: 5x5 depthwise + 1x1 pointwise,
+    the depthwise output kept in LDS; det.hip dwpw_kernel) against the unfused pair (dw5_kernel +
     the 1x1 GEMM, MVPOSE_DET_DWPW=0): the same fma chains, bf16 rounding of the intermediate, MFMA
     operands and K order, so the candidates of every prior and the selected boxes are
     bit-identical (at 128 the 4x4 .. 32x32 planes exercise the partial tiles)."""
@@ -145,7 +145,7 @@ def test_dwpw_fused_bitwise(sd, size, n, monkeypatch):
         monkeypatch.setenv("MVPOSE_DET_DWPW", fuse)
         det = D.RTMDetector(sd, max_batch=n, size=size)
         kinds = [op.kind for op in det.spec.ops]
-        assert (D.DET_DWPW in kinds) == (fuse == "1") and (D.DET_DW in kinds) == (fuse == "0")
+        assert (D.DET_DWPW in kinds) == (fuse == "1")
         r = det.detect(frames)
         torch.cuda.synchronize()
         out[fuse] = (r["cand"].cpu(), r["best"].cpu())

@@ -13,7 +13,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "multi-camera_3d_pose_estimation_amd")]
-KIND = {0: "stem", 1: "conv", 2: "dw5", 3: "ca", 4: "spp", 5: "up2", 6: "head"}
+KIND = {0: "stem", 1: "conv", 2: "dw5", 3: "ca", 4: "spp", 5: "up2", 6: "head", 7: "dwpw"}
 
 
 def plan(batch):
@@ -33,6 +33,9 @@ def plan(batch):
             byts = hi * wi * op.in_.c * 2 + ho * wo * op.out.c * 2 * (2 if op.res.t >= 0 else 1)
         elif k == "stem":
             macs, byts = ho * wo * 32 * 27, hi * wi * 8 + ho * wo * 64
+        elif k == "dwpw":
+            macs = hi * wi * op.in_.c * 25 + ho * wo * op.out.c * op.in_.c
+            byts = hi * wi * op.in_.c * 2 + ho * wo * op.out.c * 2 * (2 if op.res.t >= 0 else 1)
         elif k == "dw5":
             macs, byts = hi * wi * op.in_.c * 25, hi * wi * op.in_.c * 4
         elif k in ("spp", "up2"):
