@@ -59,13 +59,26 @@ struct SgdArgs {
     float* cams_best;          // [M][n_learn][12]
 };
 
-struct Proj {
-    float u, v;                 // pixel
-    float x, y;                 // normalised (undistorted) coordinates
-    float P2;                   // camera-frame depth
-    float r2, rad, h2;
-    float xd, yd;
+// The projection and its adjoint are templates over the lane's value type: float (one point)
+// or f2v (two points per lane, the trajectory-only pass A): every operation is the same in the
+// same order, so the two-point form issues v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32 — one
+// instruction for both points, the same roundings (contraction stays off) — where the one-point
+// form issues two.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float rcp_v(float b) { return __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ f2v rcp_v(f2v b) { return f2v{__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)}; }
+__device__ __forceinline__ float fma_v(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+__device__ __forceinline__ f2v fma_v(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <class V>
+struct ProjT {
+    V u, v;                     // pixel
+    V x, y;                     // normalised (undistorted) coordinates
+    V P2;                       // camera-frame depth
+    V r2, rad, h2;
+    V xd, yd;
 };
+using Proj = ProjT<float>;
 
 // (a0 / b, a1 / b) for finite normal operands: one v_rcp_f32 and a Markstein correction
 // step per quotient (q = a·r, e = a − q·b, q + e·r): the correctly rounded quotient except in
@@ -81,35 +94,36 @@ struct Proj {
 // the reference's own runs produce stays many orders of magnitude inside that range; a per-lane
 // range guard with an IEEE fallback measured +4.5-8 % per SGD iteration
 // (profiles/r04_sgd_guard_ab.txt), so there is none.
-__device__ __forceinline__ void div2_fast(float a0, float a1, float b, float& q0, float& q1) {
-    const float r = __builtin_amdgcn_rcpf(b);
-    const float p0 = a0 * r, p1 = a1 * r;
-    q0 = __builtin_fmaf(__builtin_fmaf(-p0, b, a0), r, p0);
-    q1 = __builtin_fmaf(__builtin_fmaf(-p1, b, a1), r, p1);
+template <class V>
+__device__ __forceinline__ void div2_fast(V a0, V a1, V b, V& q0, V& q1) {
+    const V r = rcp_v(b);
+    const V p0 = a0 * r, p1 = a1 * r;
+    q0 = fma_v(fma_v(-p0, b, a0), r, p0);
+    q1 = fma_v(fma_v(-p1, b, a1), r, p1);
 }
 
 // project_points_torch (pose_refinement.py:118-177) for one point, torch op order.  kstd: K's
 // last row is (0, 0, 1) (camera-uniform), so h2 = xd·0 + yd·0 + 1 is exactly 1 for finite xd, yd
 // and u = h0 / 1 = h0: the division is skipped with identical results (a non-finite xd or yd
 // gives a non-finite cost either way, which the likelihood's finite mask drops).
-__device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, float X1, float X2, bool ign,
-                                        bool kstd) {
+template <class V>
+__device__ __forceinline__ ProjT<V> project(const float* __restrict__ c, V X0, V X1, V X2, bool ign, bool kstd) {
     const float* K = c;
     const float* R = c + 9;
     const float* T = c + 18;
     const float* d = c + 21;
-    Proj o;
-    const float P0 = X0 * R[0] + X1 * R[1] + X2 * R[2] + T[0];
-    const float P1 = X0 * R[3] + X1 * R[4] + X2 * R[5] + T[1];
-    const float P2 = X0 * R[6] + X1 * R[7] + X2 * R[8] + T[2];
+    ProjT<V> o;
+    const V P0 = X0 * R[0] + X1 * R[1] + X2 * R[2] + T[0];
+    const V P1 = X0 * R[3] + X1 * R[4] + X2 * R[5] + T[1];
+    const V P2 = X0 * R[6] + X1 * R[7] + X2 * R[8] + T[2];
     o.P2 = P2;
     div2_fast(P0, P1, P2, o.x, o.y);
     if (!ign) {
-        const float x = o.x, y = o.y;
-        const float r2 = x * x + y * y;
+        const V x = o.x, y = o.y;
+        const V r2 = x * x + y * y;
         const float k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3], k3 = d[4];
-        const float rad = 1.f + k1 * r2 + k2 * (r2 * r2) + k3 * (r2 * r2 * r2);
-        float xd = x * rad, yd = y * rad;
+        const V rad = 1.f + k1 * r2 + k2 * (r2 * r2) + k3 * (r2 * r2 * r2);
+        V xd = x * rad, yd = y * rad;
         xd = xd + (2.f * p1 * x * y + p2 * (r2 + 2.f * (x * x)));
         yd = yd + (p1 * (r2 + 2.f * (y * y)) + 2.f * p2 * x * y);
         o.r2 = r2;
@@ -117,19 +131,19 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
         o.xd = xd;
         o.yd = yd;
     } else {
-        o.r2 = 0.f;
-        o.rad = 1.f;
+        o.r2 = V(0.f);
+        o.rad = V(1.f);
         o.xd = o.x;
         o.yd = o.y;
     }
-    const float h0 = o.xd * K[0] + o.yd * K[1] + K[2];
-    const float h1 = o.xd * K[3] + o.yd * K[4] + K[5];
+    const V h0 = o.xd * K[0] + o.yd * K[1] + K[2];
+    const V h1 = o.xd * K[3] + o.yd * K[4] + K[5];
     if (kstd) {
-        o.h2 = 1.f;
+        o.h2 = V(1.f);
         o.u = h0;
         o.v = h1;
     } else {
-        const float h2 = o.xd * K[6] + o.yd * K[7] + K[8];
+        const V h2 = o.xd * K[6] + o.yd * K[7] + K[8];
         o.h2 = h2;
         div2_fast(h0, h1, h2, o.u, o.v);
     }
@@ -137,38 +151,38 @@ __device__ __forceinline__ Proj project(const float* __restrict__ c, float X0, f
 }
 
 // d(u,v)/dX transposed applied to (gu, gv): the adjoint of project().
-__device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const Proj& o, bool ign, bool kstd,
-                                                float gu, float gv, float& g0, float& g1, float& g2,
-                                                float (&dP)[3]) {
+template <class V>
+__device__ __forceinline__ void project_adjoint(const float* __restrict__ c, const ProjT<V>& o, bool ign, bool kstd,
+                                                V gu, V gv, V& g0, V& g1, V& g2, V (&dP)[3]) {
     const float* K = c;
     const float* R = c + 9;
     const float* d = c + 21;
     // (u, v) = (h0, h1) / h2, h = K·[xd, yd, 1].  The adjoint's reciprocals are v_rcp_f32
     // (1 ulp): only the forward value needs torch's correctly rounded divisions, the gradient
     // already differs from autograd's by f32 summation order (an IEEE 1/x is ~10 VALU ops)
-    float gxd, gyd;
+    V gxd, gyd;
     if (kstd) {  // K6 = K7 = 0, h2 = 1: the same values without the zero terms
         gxd = K[0] * gu + K[3] * gv;
         gyd = K[1] * gu + K[4] * gv;
     } else {
-        const float ih2 = __builtin_amdgcn_rcpf(o.h2);
+        const V ih2 = rcp_v(o.h2);
         gxd = ((K[0] - o.u * K[6]) * gu + (K[3] - o.v * K[6]) * gv) * ih2;
         gyd = ((K[1] - o.u * K[7]) * gu + (K[4] - o.v * K[7]) * gv) * ih2;
     }
-    float gx = gxd, gy = gyd;
+    V gx = gxd, gy = gyd;
     if (!ign) {
-        const float x = o.x, y = o.y, r2 = o.r2, rad = o.rad;
+        const V x = o.x, y = o.y, r2 = o.r2, rad = o.rad;
         const float k1 = d[0], k2 = d[1], p1 = d[2], p2 = d[3], k3 = d[4];
-        const float drad = k1 + 2.f * k2 * r2 + 3.f * k3 * r2 * r2;
-        const float dxx = rad + 2.f * x * x * drad + 2.f * p1 * y + 6.f * p2 * x;
-        const float dxy = 2.f * x * y * drad + 2.f * p1 * x + 2.f * p2 * y;
-        const float dyy = rad + 2.f * y * y * drad + 6.f * p1 * y + 2.f * p2 * x;
+        const V drad = k1 + 2.f * k2 * r2 + 3.f * k3 * r2 * r2;
+        const V dxx = rad + 2.f * x * x * drad + 2.f * p1 * y + 6.f * p2 * x;
+        const V dxy = 2.f * x * y * drad + 2.f * p1 * x + 2.f * p2 * y;
+        const V dyy = rad + 2.f * y * y * drad + 6.f * p1 * y + 2.f * p2 * x;
         gx = dxx * gxd + dxy * gyd;   // d(xd,yd)/dx is symmetric in its off-diagonal
         gy = dxy * gxd + dyy * gyd;
     }
     // x = P0/P2, y = P1/P2, P = R·X + T
-    const float iP2 = __builtin_amdgcn_rcpf(o.P2);
-    const float a = gx * iP2, b = gy * iP2, cz = -(gx * o.x + gy * o.y) * iP2;
+    const V iP2 = rcp_v(o.P2);
+    const V a = gx * iP2, b = gy * iP2, cz = -(gx * o.x + gy * o.y) * iP2;
     dP[0] = a;  // d/dP of the camera-frame point (the learnable extrinsics' chain)
     dP[1] = b;
     dP[2] = cz;
@@ -377,6 +391,78 @@ __global__ __launch_bounds__(BS) void sgd_kernel(SgdArgs a) {
                 for (int k = 0; k < kCamGrad; k++) cg0[k] = cg1[k] = 0.f;
             // likelihood value AND its (not yet 1/n-scaled) gradient: one projection per
             // (point, camera) per step; the scale needs the global finite count.
+            if constexpr (!LEARN && kU == 1) {
+                // two points per lane (q0 and q0 + BS, the order the one-point loop visits them
+                // in, so every sum is the same): the projection and its adjoint on f2v, packed
+                // VALU instructions for both points
+                for (int q0 = tid; q0 < nq; q0 += 2 * BS) {
+                    const bool hb = q0 + BS < nq;
+                    const int qa = q0, qb = hb ? q0 + BS : q0;
+                    int ia, ja, ib, jb;
+                    divmod_small(qa, J, rJ, ia, ja);
+                    divmod_small(qb, J, rJ, ib, jb);
+                    const int ta = t0 + ia, tb = t0 + ib;
+                    const float* pa = X + 3 * (ta * J + ja);
+                    const float* pb = X + 3 * (tb * J + jb);
+                    const f2v X0 = {pa[0], pb[0]}, X1 = {pa[1], pb[1]}, X2 = {pa[2], pb[2]};
+                    const Target tga = load_target(tgt + ((size_t)ta * Vg * J + ja) * 6);
+                    const Target tgb = load_target(tgt + ((size_t)tb * Vg * J + jb) * 6);
+                    float lsa = 0.f, lsb = 0.f;
+                    int lca = 0, lcb = 0;
+                    f2v g0 = {0.f, 0.f}, g1 = {0.f, 0.f}, g2 = {0.f, 0.f};
+                    for (int c = 0; c < V; c++) {
+                        const float* cam = cam_s + c * MVP_SGD_CAM_FLOATS;
+                        const bool kstd = cam_kstd[c] != 0;  // camera-uniform
+                        const ProjT<f2v> o = project(cam, X0, X1, X2, ign, kstd);
+                        const Target gA = own ? load_target(tgt + (((size_t)ta * Vg + c) * J + ja) * 6) : tga;
+                        const Target gB = own ? load_target(tgt + (((size_t)tb * Vg + c) * J + jb) * 6) : tgb;
+                        const f2v a00 = {gA.a00, gB.a00}, a01 = {gA.a01, gB.a01};
+                        const f2v a10 = {gA.a10, gB.a10}, a11 = {gA.a11, gB.a11};
+                        const f2v d0 = o.u - f2v{gA.m0, gB.m0}, d1 = o.v - f2v{gA.m1, gB.m1};
+                        const f2v val = 0.5f * ((d0 * a00 + d1 * a10) * d0 + (d0 * a01 + d1 * a11) * d1);
+                        const bool fa = finite(val.x), fb = finite(val.y);
+                        if (!fa && !fb) continue;
+                        const f2v s01 = a01 + a10;
+                        const f2v gu = 0.5f * (2.f * a00 * d0 + s01 * d1);
+                        const f2v gv = 0.5f * (s01 * d0 + 2.f * a11 * d1);
+                        f2v h0, h1, h2, dP[3];
+                        project_adjoint(cam, o, ign, kstd, gu, gv, h0, h1, h2, dP);
+                        if (fa && fb) {
+                            lsa += val.x;
+                            lsb += val.y;
+                            lca++;
+                            lcb++;
+                            g0 += h0;
+                            g1 += h1;
+                            g2 += h2;
+                        } else if (fa) {
+                            lsa += val.x;
+                            lca++;
+                            g0.x += h0.x;
+                            g1.x += h1.x;
+                            g2.x += h2.x;
+                        } else {
+                            lsb += val.y;
+                            lcb++;
+                            g0.y += h0.y;
+                            g1.y += h1.y;
+                            g2.y += h2.y;
+                        }
+                    }
+                    acc[0] += lsa;
+                    acc[1] += lca;
+                    gb[3 * qa + 0] = g0.x;
+                    gb[3 * qa + 1] = g1.x;
+                    gb[3 * qa + 2] = g2.x;
+                    if (hb) {
+                        acc[0] += lsb;
+                        acc[1] += lcb;
+                        gb[3 * qb + 0] = g0.y;
+                        gb[3 * qb + 1] = g1.y;
+                        gb[3 * qb + 2] = g2.y;
+                    }
+                }
+            } else
             for (int q0 = tid; q0 < nq; q0 += kU * BS) {
                 float xs[kU][3];
                 Target tg[kU];
