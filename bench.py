@@ -497,9 +497,10 @@ def video_decode_line(gops=48, gop=12, threads=16):
             "device_split_decode": {
                 "frames_per_s": len(samples) / best, "threads": threads, "bit_identical_to_host": same,
                 "host_phases_ms": {k: (1e3 * v if isinstance(v, float) else v) for k, v in phases.items()},
-                "path": "mvpose.video.decode_mp4v_device: host entropy decoding (mvp_mp4v_parse) on the thread pool, "
-                        "one H2D of records + coefficients, reconstruction (IDCT, half-pel MC, BGR) by "
-                        "mvp_mp4v_reconstruct on the GPU; frames end in HBM"}}
+                "path": "mvpose.video.decode_mp4v_device: host entropy decoding (mvp_mp4v_parse_many, one call per "
+                        "GOP) on the thread pool, each GOP's records + coefficients to the device on a copy stream as "
+                        "it is parsed, reconstruction (IDCT, half-pel MC, BGR) by mvp_mp4v_reconstruct on the GPU, one "
+                        "launch per GOP position; frames end in HBM"}}
 
 
 def detector_line(dev, est, cams_params, V, batch=None, reps=5):
