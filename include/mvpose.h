@@ -268,7 +268,9 @@ int mvp_graph_plan(void* handle, int batch, int64_t* rec_out, int max_records, i
  *   MVP_DET_STEM : 3x3/s2 conv of the 4-channel letterboxed input to 32 channels,
  *                  f32 weights [32][3][3][4] + bias [32], act.
  *   MVP_DET_CONV : y = act(conv(x) + bias [+ res]), ks 1|3, stride 1|2, bf16 weights
- *                  [cout_pad][ks][ks][cin] (cout_pad as mvp_graph), f32 bias.
+ *                  [cout_pad][ks][ks][cin] (cout_pad as mvp_graph), f32 bias.  aux = the live
+ *                  couts L (0 = all): the caller guarantees zero weights and bias for couts
+ *                  >= L, whose outputs are then stored as 0 without being computed.
  *   MVP_DET_DW   : 5x5 depthwise conv + bias + act, f32 weights [c/8][25][8], bias [c].
  *   MVP_DET_CA   : channel attention in place on `in`: x *= hardsigmoid(W·mean(x) + b),
  *                  f32 W^T [c][c] (w_off) and b [c].

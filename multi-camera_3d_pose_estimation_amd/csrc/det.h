@@ -23,7 +23,8 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
 // before the residual, 1 = ReLU after it)
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s, const uint16_t* wimg = nullptr, const uint16_t* wband = nullptr);
+                          hipStream_t s, const uint16_t* wimg = nullptr, const uint16_t* wband = nullptr,
+                          int live = 0);  // live: couts with non-zero weights or bias (0 = all N)
 // A CSPNeXtBlock's depthwise 5x5 (dw_w [C/8][25][8] f32, dw_b [C]) and pointwise 1x1 (wimg: the
 // GEMM weight image of the [det_cout_pad(N) == C][C] weights, pw_b [C]) in one launch, the
 // intermediate kept in LDS; bit-identical to launch_det_dw5 + launch_det_conv_gemm (ks 1).

@@ -514,17 +514,25 @@ det_conv_gemm_kernel(GParams p) {
 // TR output rows per tile (2 or 4): wave (wp, wc) computes rows wp, wp + 2, ... of cout half
 // wc.  4 rows spread each tile's weight DMA over twice the pixels (62.5 KB of LDS, 2
 // workgroups per CU, against 54 KB and 3 for 2 rows); the K order per output is the same.
-template <int BN, int NCK, int TR = 2>  // NCK 32-channel input chunks, one DMA + compute phase each
+// LT > 0 (round 6): only the first LT 16-cout tiles carry real channels (RTMDet-m's 48-channel
+// stem / stage-1 convs stored as 64: the last tile's weights and biases are zero, so its outputs
+// are SiLU(0) = +0).  Each of the 4 waves then takes one output row of a 4-row tile and all LT
+// tiles (12 MFMAs per tap instead of 16: the zero tile is not multiplied) and stores zeros for
+// the padding couts — the real couts' K order and epilogue are unchanged: bit-identical.
+template <int BN, int NCK, int TR = 2, int LT = 0>  // NCK 32-channel input chunks, one DMA + compute phase each
 __global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GParams p) {
+    constexpr bool ROWS = LT > 0;
+    static_assert(!ROWS || (TR % 4 == 0 && LT < BN / 16), "live-tile halo: 4-row tiles");
     constexpr int TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;  // halo pixels
-    constexpr int NRW = TR / 2;                                // output rows per wave
+    constexpr int RS = ROWS ? 4 : 2;                           // row stride between a wave's rows
+    constexpr int NRW = TR / RS;                               // output rows per wave
     constexpr int A_SLOTS = 9 * 4 * BN, A_R64 = A_SLOTS / 64;
     constexpr int B_R64 = (HP * 4 + 63) / 64;
-    constexpr int WCT = BN / 32;
+    constexpr int WCT = ROWS ? LT : BN / 32;                   // 16-cout tiles per wave
     __shared__ __attribute__((aligned(1024))) uint8_t lds[(A_SLOTS + B_R64 * 64) * 16];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wp = wave & 1, wc = wave >> 1;  // output row of the tile, cout half
+    const int wp = ROWS ? wave : wave & 1, wc = ROWS ? 0 : wave >> 1;  // output row of the tile, cout half
     const int tiles_w = (p.W + TW - 1) / TW, tiles_h = (p.H + TR - 1) / TR;
     const int per = tiles_w * tiles_h;
     const int n = blockIdx.x / per, t = blockIdx.x - n * per;
@@ -572,7 +580,7 @@ __global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GPa
         for (int rw = 0; rw < NRW; rw++)
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const int hp = (wp + 2 * rw + dy) * HW_ + i * 16 + r16 + dx;
+                const int hp = (wp + RS * rw + dy) * HW_ + i * 16 + r16 + dx;
                 b[rw][i] = *reinterpret_cast<const bf16x8*>(lds + A_SLOTS * 16 + hp * 64 + ((kg ^ swz(hp)) * 16));
             }
 #pragma unroll
@@ -587,8 +595,21 @@ __global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GPa
     }
 #pragma unroll
     for (int rw = 0; rw < NRW; rw++) {
-    const int ho = ho0 + wp + 2 * rw;
+    const int ho = ho0 + wp + RS * rw;
     if (ho >= p.H) break;
+    if constexpr (ROWS) {   // the zero tiles' couts
+#pragma unroll
+        for (int c = LT; c < BN / 16; c++) {
+            const int co = c * 16 + kg * 4;
+            if (co >= p.N) continue;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int wo = wo0 + i * 16 + r16;
+                if (wo >= p.W) continue;
+                *reinterpret_cast<uint2*>(p.y + (((long)n * p.H + ho) * p.W + wo) * p.ys + co) = uint2{0u, 0u};
+            }
+        }
+    }
 #pragma unroll
     for (int c = 0; c < WCT; c++) {
         const int co = wc * (BN / 2) + c * 16 + kg * 4;
@@ -1644,7 +1665,8 @@ void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
 
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s, const uint16_t* wimg, const uint16_t* wband) {
+                          hipStream_t s, const uint16_t* wimg, const uint16_t* wband, int live) {
+    if (live <= 0 || live > N) live = N;
     MVP_REQUIRE(cin % 32 == 0 && N % 4 == 0 && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
                 "det conv: cin=%d cout=%d strides %d/%d", cin, N, xs, ys);
     MVP_REQUIRE((ks == 1 && stride == 1) || (ks == 3 && (stride == 1 || stride == 2)), "det conv: ks %d stride %d", ks,
@@ -1655,7 +1677,10 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     // cout tile: the widest of 192 / 128 / 96 / 64 dividing the padded couts.  Measured
     // alternatives, all slower on RTMDet-m (profiles/r03detcfg.txt, 128 frames, same box):
     // 128-cout tiles 27.2-27.5 vs 25.9 ms, 256-pixel tiles of 8 waves 27.7, of 4 waves 32.6,
-    // a 4-slot ring level; removed with their environment switches in round 3.
+    // a 4-slot ring level; removed with their environment switches in round 3.  Round 6
+    // re-measured 256-pixel tiles on the <= 40x40 planes' 192-cout convs only (their 128-pixel
+    // tiles re-read each weight slice 1.7-6.6x): 84.5 vs 81.2 ms per 512 frames, removed again
+    // (profiles/r06_det_wide_live_ab.txt).
     const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, 0, H, W, Ho, Wo, wimg};
@@ -1698,6 +1723,11 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
             else if (cin == 64) go(det_conv_halo_kernel<32, 2, 2>);
             else if (npad == 64) go(det_conv_halo_kernel<64, 1, 2>);
             else go(det_conv_halo_kernel<32, 1, 2>);
+        } else if (npad == 64 && live <= 48 && live > 32 && !res && DET_HALO_TR % 4 == 0 &&
+                   !(getenv("MVPOSE_DET_LIVE") && getenv("MVPOSE_DET_LIVE")[0] == '0')) {
+            // 48 real couts in 64 (RTMDet-m stem.2, stage-1 conv1): 3 live tiles
+            if (cin == 64) go(det_conv_halo_kernel<64, 2, DET_HALO_TR, 3>);
+            else go(det_conv_halo_kernel<64, 1, DET_HALO_TR, 3>);
         } else {
             if (cin == 64 && npad == 64) go(det_conv_halo_kernel<64, 2, DET_HALO_TR>);
             else if (cin == 64) go(det_conv_halo_kernel<32, 2, DET_HALO_TR>);

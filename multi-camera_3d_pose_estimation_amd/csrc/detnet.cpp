@@ -82,6 +82,7 @@ void validate(DetNet& g, int64_t w_elems, int64_t f_elems) {
                 MVP_REQUIRE(y.h == (x.h + 2 * pad - op.ks) / op.stride + 1 && y.w == (x.w + 2 * pad - op.ks) / op.stride + 1,
                             "det conv %zu: output plane", k);
                 MVP_REQUIRE(op.in.t != op.out.t, "det conv %zu: a conv cannot write its input tensor", k);
+                MVP_REQUIRE(op.aux >= 0 && op.aux <= op.out.c, "det conv %zu: live couts %lld", k, (long long)op.aux);
                 if (op.res.t >= 0) {
                     const mvp_tensor_desc& r = view_ok(op.res, "res", k);
                     MVP_REQUIRE(r.h == y.h && r.w == y.w && op.res.c == op.out.c, "det conv %zu: residual shape", k);
@@ -296,7 +297,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
                                      op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
                                      vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                     op.act, s, g->wimg[k], g->wband[k]);
+                                     op.act, s, g->wimg[k], g->wband[k], (int)op.aux);
                 break;
             }
             case MVP_DET_DW: {

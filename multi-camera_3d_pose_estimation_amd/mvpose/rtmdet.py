@@ -323,7 +323,10 @@ class DetSpec:
         w_off = self._push_w(to_bf16_bits(ws))
         if self.f32_weights is not None:
             self.f32_weights[w_off] = ws.astype(np.float32)
-        self._op("+".join(names), DET_CONV, x, out, res, ks=k, stride=stride, w_off=w_off, b_off=self._push_f(bs))
+        # aux: the live couts (stored channels past the last real one have zero weights and
+        # bias, so their outputs are SiLU(0) = 0 and kernels may skip them)
+        self._op("+".join(names), DET_CONV, x, out, res, ks=k, stride=stride, w_off=w_off, b_off=self._push_f(bs),
+                 aux=int(out.cmap.max()) + 1)
         self.macs += ho * wo * cout * cin * k * k
         return out
 

@@ -154,6 +154,30 @@ def test_dwpw_fused_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(out["0"][1].view(torch.int32), out["1"][1].view(torch.int32))
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_live_couts_bitwise(sd, size, n, monkeypatch):
+    """The 48-of-64-cout 3x3 convs (stem.2, stage-1 conv1: DetOp.aux = 48 live couts) on the
+    halo kernel's live-tile form (det_conv_halo_kernel<64, *, 4, 3>: one output row per wave,
+    the zero tile stored, not multiplied) against the full 64-cout form (MVPOSE_DET_LIVE=0):
+    every tensor of the forward, padding channels included, is bit-identical."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=21)).cuda()
+    outs = []
+    for live in ("0", "1"):
+        monkeypatch.setenv("MVPOSE_DET_LIVE", live)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        live_ops = [k for k, op in enumerate(det.spec.ops) if op.kind == D.DET_CONV and 32 < op.aux < op.out.c]
+        assert len(live_ops) >= 2, live_ops
+        det.run_ops(frames, 0, len(det.spec.ops))
+        torch.cuda.synchronize()
+        ts = [det.tensor(t, n).cpu() for t in range(len(det.spec.tensors))]
+        outs.append((ts, det.cand[:n].cpu()))
+        det.close()
+    (ta, ca), (tb, cb) = outs
+    for t, (x, y) in enumerate(zip(ta, tb)):
+        assert torch.equal(x.view(torch.int16), y.view(torch.int16)), (size, t)
+    assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
+
+
 def test_band_conv_vs_gemm(sd, monkeypatch):
     """The 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40 planes run on the
     band-halo kernel (det_conv_band_kernel, the default): each one, on the forward's own input,
