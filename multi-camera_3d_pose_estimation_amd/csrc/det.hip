@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "conv.h"
 #include "det.h"
@@ -500,6 +501,272 @@ det_conv_gemm_kernel(GParams p) {
                 uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
         }
     }
+}
+
+constexpr int kPersMaxN = 1024;  // couts whose biases the persistent 1x1 kernel stages in LDS
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    typedef __attribute__((address_space(3))) const uint8_t lds_u8;
+    return (uint32_t)(uintptr_t)(lds_u8*)p;
+}
+// LDS write / read-back of the epilogue staging as asm: the compiler would otherwise put a
+// vmcnt(0) (the in-flight ring DMAs) in front of them; the read waits for the wave's writes
+__device__ __forceinline__ void lds_write_u2(void* p, uint2 v) {
+    asm volatile("ds_write_b64 %0, %1\n\ts_nop 1" : : "v"(lds_addr(p)), "v"(v) : "memory");
+}
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+// raw buffer resource (stride 0, num_records bytes; gfx9 dword 3)
+__device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
+    const uint64_t a = (uint64_t)(uintptr_t)base;
+    return i32x4{__builtin_amdgcn_readfirstlane((int)(uint32_t)a), __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)),
+                 __builtin_amdgcn_readfirstlane(bytes), 0x00020000};
+}
+// a weight-fragment load the compiler does not see (its waitcnt pass, seeing the LDS-DMAs and these
+// loads as mixed event kinds, put vmcnt(0) in front of every third K step's MFMAs); the kernel's
+// own end-of-step wait covers it
+__device__ __forceinline__ bf16x8 buffer_load_frag(i32x4 r, int off) {
+#ifdef PERS_BUILTIN_LOAD
+    __amdgpu_buffer_rsrc_t rr;
+    __builtin_memcpy(&rr, &r, 16);
+    return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rr, off, 0, 0));
+#else
+    bf16x8 v;
+    // s_nop 4: the descriptor may be fresh from v_readfirstlane and the offset from a VALU op
+    asm volatile("s_nop 4\n\tbuffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(r) : "memory");
+    return v;
+#endif
+}
+// a buffer store the compiler does not see: its waitcnt pass would otherwise count it among the
+// pending vector-memory events, see reads and writes mixed, and put vmcnt(0) in front of the next
+// use of any load (the weight fragments two K steps ahead); the kernel's own waits count loads only
+__device__ __forceinline__ void buffer_store_u4(u32x4 v, i32x4 r, int off) {
+#ifdef PERS_BUILTIN_STORE
+    __amdgpu_buffer_rsrc_t rr;
+    __builtin_memcpy(&rr, &r, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rr, off, 0, 0);
+#else
+    // s_nop 4 as the load; s_nop 1 after: the store reads its data registers late, and the
+    // compiler's next instruction may overwrite them
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" : : "v"(v), "v"(off), "s"(r) : "memory");
+#endif
+}
+__device__ __forceinline__ u32x4 lds_read_u4_sync(const void* p) {
+    u32x4 v;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+    return v;
+}
+
+// ds_read_b128 + its own lgkmcnt(0) in one asm block: the compiler cannot see it, so it inserts
+// no vmcnt wait for the LDS-DMAs in flight (it assumes they may alias any LDS read it emits)
+__device__ __forceinline__ float4 lds_read_f4_sync(const float* p) {
+    typedef __attribute__((address_space(3))) float lds_float;
+    const uint32_t a = (uint32_t)(uintptr_t)(const lds_float*)p;
+    float4 v;
+    asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+    return v;
+}
+
+// Persistent 1x1 GEMM (round 6).  det_conv_gemm_kernel moves both operands by LDS-DMA; on the
+// 1x1 convs (~17 ms of the 512-frame forward) that is ~114 cycles per 1-KiB DMA instruction per
+// CU (24.6 GB/s per CU, 6.3 TB/s chip-wide: neck.top_down_blocks.1's main+short conv, 20
+// instructions per K step of which 12 are the re-fetched weight slice), the kernels' bound.
+// Here the pixel operand (B) still arrives by LDS-DMA into a 3-slot ring, but each wave loads
+// its own weight fragments (A) straight into VGPRs with buffer loads (L2-resident, no
+// redundancy: PW = 1 puts the 4 waves side by side along the couts, each over all 128 pixels),
+// two K steps ahead.  A workgroup per (CU, slot) walks a strided list of (tile, cout block)
+// items and the pipeline runs across items.  The epilogue stages each wave's 16-pixel rows in
+// LDS and writes whole pixel runs with buffer stores.  Same MFMA operands and sequence (K steps
+// 0 .. nq - 1 from zero) and epilogue arithmetic as det_conv_gemm_kernel<BN, 1, 1, ...>:
+// bit-identical outputs.
+template <int B, int E, typename F>
+__device__ __forceinline__ void det_static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        det_static_for<B + 1, E>(f);
+    }
+}
+
+template <int BN, int PW, int NBUF>
+__global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
+    constexpr int NT = 256, NWV = 4, BMP = 128, D = NBUF - 1;
+    constexpr int CWV = NWV / PW;        // waves along the couts
+    constexpr int WCO = BN / CWV;        // couts per wave
+    constexpr int WCT = WCO / 16;        // 16-cout tiles per wave
+    constexpr int FP = BMP / (16 * PW);  // 16-pixel fragments per wave
+    constexpr int B_SLOTS = 4 * BMP, SUB = B_SLOTS * 16, BR = B_SLOTS / NT;
+    constexpr int ROWB = WCO * 2;        // staged bytes per pixel
+    constexpr int OFF_BIAS = NBUF * SUB, OFF_STAGE = OFF_BIAS + kPersMaxN * 4;
+    static_assert(WCO % 16 == 0 && FP * 16 * PW == BMP && B_SLOTS % NT == 0, "tiling");
+    // one LDS object: with a second __shared__ array the compiler's LDS-DMA alias check put
+    // vmcnt(0) in front of every fragment read
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[OFF_STAGE + NWV * 16 * ROWB];
+    float* bias_s = reinterpret_cast<float*>(lds + OFF_BIAS);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wp = wave % PW, wc = wave / PW;
+    const int nq = p.cin / 32;
+    // items: logical blocks (tile, cout block; couts fastest) split into 8 contiguous XCD ranges
+    // (the dispatcher deals blockIdx round-robin over the XCDs); XCD x's gx workgroups take its
+    // range round-robin, so the cout blocks of a tile run side by side on one XCD
+    const long nblk = (p.M + BMP - 1) / BMP * p.n_nb;
+    const int G = gridDim.x, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int gx = G / 8 + (xcd < (G & 7) ? 1 : 0);
+    const long qx = nblk >> 3, rx = nblk & 7;
+    const long x0 = xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx;
+    const long x1 = x0 + qx + (xcd < rx ? 1 : 0);
+    const long n_items = x1 - x0 > loc ? (x1 - x0 - loc + gx - 1) / gx : 0;
+    const long S = n_items * nq;  // K steps of this workgroup
+    if (S == 0) return;           // workgroup-uniform
+    for (int i = tid; i < p.N; i += NT) bias_s[i] = p.bias[i];
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    const int kg = lane >> 4, r16 = lane & 15;
+    int b_row[BR], b_kg[BR];
+#pragma unroll
+    for (int j = 0; j < BR; j++) {
+        const int slot = j * NT + tid;
+        b_row[j] = slot >> 2;
+        b_kg[j] = (slot & 3) ^ swz(b_row[j]);
+    }
+    // A: lane (kg, r16) of tile c holds chunk kg of cout co0 + wc * WCO + 16c + r16 (the packed
+    // image's slot (q * npad + co) * 4 + (kg ^ swz(co)))
+    const i32x4 wr = make_rsrc(p.wimg, (int)std::min<long>((long)p.npad * nq * 64, 0x7fffffffL));
+    const int a_step = p.npad * 64;  // bytes between K steps of the image
+    int a_lane[WCT];                 // this lane's byte offset per tile for co0 = 0 (step 0)
+#pragma unroll
+    for (int c = 0; c < WCT; c++) {
+        const int co = wc * WCO + c * 16 + r16;
+        a_lane[c] = co * 64 + ((kg ^ swz(co)) * 16);
+    }
+    bf16x8 areg[NBUF][WCT];
+    // issue K step g (item g / nq, step g % nq): its pixel image into ring slot ST, its weight
+    // fragments into areg[ST]
+    auto issue = [&](long g, auto Ss) {
+        constexpr int ST = decltype(Ss)::value;
+        const long it = g / nq;
+        const int k = (int)(g - it * nq);
+        const long lb = x0 + loc + it * gx;
+        const long tile = lb / p.n_nb;
+        const int co0 = (int)(lb - tile * p.n_nb) * BN;
+        uint8_t* base = lds + ST * SUB;
+#pragma unroll
+        for (int j = 0; j < BR; j++) {
+            const long m = tile * BMP + b_row[j];
+            const void* src = m < p.M ? (const void*)(p.x + m * p.xs + k * 32 + b_kg[j] * 8)
+                                      : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
+            glds16_det(src, base + (j * NT + wave * 64) * 16);
+        }
+#pragma unroll
+        for (int c = 0; c < WCT; c++) {
+            // couts past npad: an out-of-range offset (the load returns zeros)
+            const int off = co0 + wc * WCO + c * 16 < p.npad ? k * a_step + co0 * 64 + a_lane[c] : 0x7ff00000;
+            areg[ST][c] = buffer_load_frag(wr, off);
+        }
+    };
+    constexpr int OPS = BR + WCT;  // vector memory instructions per issued step (this wave)
+    f32x4 acc[FP][WCT];
+#pragma unroll
+    for (int i = 0; i < FP; i++)
+#pragma unroll
+        for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    det_static_for<0, D>([&](auto J) {
+        if (J < S) issue(J, J);
+    });
+    wait_vm(OPS * (int)(std::min<long>(D, S) - 1));
+    __builtin_amdgcn_s_barrier();
+    const int soff = r16 * 64 + ((kg ^ ((-(r16 >> 2)) & 3)) * 16);
+    uint8_t* stage = lds + OFF_STAGE + wave * 16 * ROWB;  // this wave's epilogue rows
+    int k = 0;
+    long it = 0;
+    unsigned ends = 0;  // bit t: iteration g - 1 - t ran an epilogue
+    constexpr int kStores = FP * ((2 * WCO + 63) / 64);  // store instructions per epilogue (this wave)
+    auto step = [&](long g, auto Ss) {
+        constexpr int ST = decltype(Ss)::value;
+        if (g + D < S) issue(g + D, std::integral_constant<int, (ST + D) % NBUF>{});
+        {
+            // this step's weight fragments landed at the previous step's wait (the asm loads are
+            // invisible to the compiler): tell it so here, before their first use
+#pragma unroll
+            for (int c = 0; c < WCT; c++) asm volatile("" : "+v"(areg[ST][c]));
+            const uint8_t* base = lds + ST * SUB;
+            bf16x8 b[FP];
+#pragma unroll
+            for (int i = 0; i < FP; i++) b[i] = *reinterpret_cast<const bf16x8*>(base + (wp * 16 * FP + i * 16) * 64 + soff);
+#pragma unroll
+            for (int i = 0; i < FP; i++)
+#pragma unroll
+                for (int c = 0; c < WCT; c++)
+                    acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(areg[ST][c], b[i], acc[i][c], 0, 0, 0);
+        }
+        // step g + 1 landed (pixels and weights): younger are the later steps' operations and
+        // the stores of the epilogues run since its issue (iterations g + 1 - D .. g - 1).  Loads,
+        // stores and LDS-DMA retire in issue order, so counting the stores keeps their slow write
+        // acknowledgements off this wait.
+        wait_vm(OPS * (int)(std::min<long>(g + D, S - 1) - g - 1) + kStores * __builtin_popcount(ends & ((1u << (D - 1)) - 1)));
+        ends <<= 1;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (++k < nq) return;
+        // ---- the item's epilogue (det_conv_gemm_kernel's arithmetic), a fresh accumulator
+        const long lb = x0 + loc + it * gx;
+        const long tile = lb / p.n_nb;
+        const int co0 = (int)(lb - tile * p.n_nb) * BN;
+        const long m0 = tile * BMP;
+        float4 bb[WCT];
+#pragma unroll
+        for (int c = 0; c < WCT; c++) {
+            const int co = co0 + wc * WCO + c * 16 + kg * 4;
+            bb[c] = lds_read_f4_sync(bias_s + (co < p.N ? co : 0));
+        }
+        // buffer stores: lanes past the couts / pixels get an out-of-range offset and are dropped
+        const long mv = p.M - m0;
+        const i32x4 yr = make_rsrc(p.y + m0 * p.ys, (int)((mv < BMP ? mv : BMP) * p.ys * 2));
+#pragma unroll
+        for (int i = 0; i < FP; i++) {
+            const long mi = m0 + wp * 16 * FP + i * 16;
+#pragma unroll
+            for (int c = 0; c < WCT; c++) {
+                const int co = co0 + wc * WCO + c * 16 + kg * 4;
+                const long m = mi + r16;
+                float v[4] = {acc[i][c][0] + bb[c].x, acc[i][c][1] + bb[c].y, acc[i][c][2] + bb[c].z,
+                              acc[i][c][3] + bb[c].w};
+                acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (p.act == 2)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = act_f(v[e], 2);
+                if (p.res && co < p.N && m < p.M) {
+                    const uint2 r = *reinterpret_cast<const uint2*>(p.res + m * p.rs + co);
+                    v[0] += bf(r.x & 0xffff), v[1] += bf(r.x >> 16), v[2] += bf(r.y & 0xffff), v[3] += bf(r.y >> 16);
+                }
+                if (p.act == 1)
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = fmaxf(v[e], 0.f);
+                lds_write_u2(stage + r16 * ROWB + (c * 16 + kg * 4) * 2,
+                             uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)});
+            }
+            // the wave's 16 pixels x WCO couts back as 16-B row chunks: a store instruction writes
+            // whole ROWB-byte pixel runs instead of 16 runs of 32 B
+            constexpr int NCH = 16 * ROWB / 16;
+#pragma unroll
+            for (int q0 = 0; q0 < NCH; q0 += 64) {
+                const int q = min(q0 + lane, NCH - 1);
+                const int px = q / (ROWB / 16), ch = q - px * (ROWB / 16);
+                const u32x4 o = lds_read_u4_sync(stage + q * 16);
+                const int co = co0 + wc * WCO + ch * 8;
+                const bool ok = q0 + lane < NCH && co < p.N;
+                const int off = ok ? ((wp * 16 * FP + i * 16 + px) * p.ys + co) * 2 : 0x7ff00000;
+                buffer_store_u4(o, yr, off);
+            }
+        }
+        ends |= 1;
+        k = 0;
+        it++;
+    };
+    for (long g = 0; g < S; g += NBUF)
+        det_static_for<0, NBUF>([&](auto J) {
+            if (g + J < S) step(g + J, J);
+        });
 }
 
 // 3x3/s1 convs with one 32-channel input chunk (the 320x320 stem / stage-1 planes, 24 -> 32
@@ -1741,6 +2008,29 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const long blocks = (p.M + kPx - 1) / kPx * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
+    if (ks == 1 && wimg && N <= kPersMaxN) {  // persistent 1x1 GEMM: 2 workgroups per CU
+        const char* e = getenv("MVPOSE_DET_PERS");  // A/B and tests: 0 = one tile per workgroup
+        if (!(e && e[0] == '0')) {
+            // all blocks, or a multiple of 8 (the kernel's per-XCD split needs one of the two)
+            const char* eo = getenv("MVPOSE_DET_PERS_OCC");  // A/B: workgroups per CU (default 2)
+            const long occ = eo ? std::max(1, atoi(eo)) : 2;
+            const long grid = blocks <= occ * det_band_grid() ? blocks : occ * det_band_grid() / 8 * 8;
+            MVP_REQUIRE(grid > 0, "det conv: persistent grid");
+            const dim3 gp((unsigned)grid), tp(256);
+            const bool deep = e && e[0] == '4';  // A/B: a 4-slot ring
+            auto go = [&](auto k3, auto k4) {
+                if (deep) hipLaunchKernelGGL(k4, gp, tp, 0, s, p);
+                else hipLaunchKernelGGL(k3, gp, tp, 0, s, p);
+            };
+            if (bn == 192) go(det_conv1x1_pers_kernel<192, 1, 3>, det_conv1x1_pers_kernel<192, 1, 4>);
+            else if (bn == 128) go(det_conv1x1_pers_kernel<128, 1, 3>, det_conv1x1_pers_kernel<128, 1, 4>);
+            else if (bn == 96) go(det_conv1x1_pers_kernel<96, 2, 3>, det_conv1x1_pers_kernel<96, 2, 4>);
+            else if (bn == 64) go(det_conv1x1_pers_kernel<64, 1, 3>, det_conv1x1_pers_kernel<64, 1, 4>);
+            else go(det_conv1x1_pers_kernel<32, 2, 3>, det_conv1x1_pers_kernel<32, 2, 4>);
+            MVP_HIP(hipGetLastError());
+            return;
+        }
+    }
     const dim3 g((unsigned)blocks), t(256);
 #define MVP_DET_CONV_BN(KS, S)                                                                         \
     do {                                                                                              \

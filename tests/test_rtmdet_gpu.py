@@ -178,6 +178,29 @@ def test_live_couts_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_persistent_1x1_bitwise(sd, size, n, monkeypatch):
+    """The 1x1 convs on the persistent GEMM (det_conv1x1_pers_kernel: 2 workgroups per CU walk
+    (tile, cout block) items with the DMA ring running across items, the default) against one
+    tile per workgroup (det_conv_gemm_kernel<*, 1, 1>, MVPOSE_DET_PERS=0): the same operand
+    images and MFMA sequence per output, so every tensor of the forward is bit-identical (the
+    128 size: ragged last tiles and workgroups with no item)."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=23)).cuda()
+    outs = []
+    for pers in ("0", "1"):
+        monkeypatch.setenv("MVPOSE_DET_PERS", pers)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        det.run_ops(frames, 0, len(det.spec.ops))
+        torch.cuda.synchronize()
+        ts = [det.tensor(t, n).cpu() for t in range(len(det.spec.tensors))]
+        outs.append((ts, det.cand[:n].cpu()))
+        det.close()
+    (ta, ca), (tb, cb) = outs
+    for t, (x, y) in enumerate(zip(ta, tb)):
+        assert torch.equal(x.view(torch.int16), y.view(torch.int16)), (size, t)
+    assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
+
+
 def test_band_conv_vs_gemm(sd, monkeypatch):
     """The 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40 planes run on the
     band-halo kernel (det_conv_band_kernel, the default): each one, on the forward's own input,
