@@ -587,7 +587,7 @@ __device__ __forceinline__ void det_static_for(F&& f) {
     }
 }
 
-template <int BN, int PW, int NBUF>
+template <int BN, int PW, int NBUF, int KS = 1, int STR = 1>
 __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     constexpr int NT = 256, NWV = 4, BMP = 128, D = NBUF - 1;
     constexpr int CWV = NWV / PW;        // waves along the couts
@@ -605,7 +605,8 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wp = wave % PW, wc = wave / PW;
-    const int nq = p.cin / 32;
+    const int kc = p.cin / 32;        // 32-channel chunks per tap
+    const int nq = KS * KS * kc;      // K steps per item: (tap, chunk), chunks fastest
     // items: logical blocks (tile, cout block; couts fastest) split into 8 contiguous XCD ranges
     // (the dispatcher deals blockIdx round-robin over the XCDs); XCD x's gx workgroups take its
     // range round-robin, so the cout blocks of a tile run side by side on one XCD
@@ -641,27 +642,62 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     bf16x8 areg[NBUF][WCT];
     // issue K step g (item g / nq, step g % nq): its pixel image into ring slot ST, its weight
     // fragments into areg[ST]
-    auto issue = [&](long g, auto Ss) {
+    // the issue stream (steps are issued in order): its item, step in the item and, for 3x3, the
+    // tap and chunk of that step and the output pixels (frame, row, column) of this thread's B
+    // rows -- advanced per step, so no division in the per-step path
+    long i_it = 0, i_tile = 0;
+    int i_k = 0, i_co0 = 0, i_ch = 0, i_kw = 0, i_kh = 0;
+    int b_n[BR], b_ho[BR], b_wo[BR];
+    auto issue = [&](auto Ss) {
         constexpr int ST = decltype(Ss)::value;
-        const long it = g / nq;
-        const int k = (int)(g - it * nq);
-        const long lb = x0 + loc + it * gx;
-        const long tile = lb / p.n_nb;
-        const int co0 = (int)(lb - tile * p.n_nb) * BN;
-        uint8_t* base = lds + ST * SUB;
+        if (i_k == 0) {  // a new item
+            const long lb = x0 + loc + i_it * gx;
+            i_tile = lb / p.n_nb;
+            i_co0 = (int)(lb - i_tile * p.n_nb) * BN;
+            if constexpr (KS > 1) {
+                const long hw = (long)p.Ho * p.Wo;
 #pragma unroll
-        for (int j = 0; j < BR; j++) {
-            const long m = tile * BMP + b_row[j];
-            const void* src = m < p.M ? (const void*)(p.x + m * p.xs + k * 32 + b_kg[j] * 8)
-                                      : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
-            glds16_det(src, base + (j * NT + wave * 64) * 16);
+                for (int j = 0; j < BR; j++) {
+                    const long m = i_tile * BMP + b_row[j];
+                    b_n[j] = m < p.M ? (int)(m / hw) : -1;
+                    const int r = m < p.M ? (int)(m - (long)b_n[j] * hw) : 0;
+                    b_ho[j] = r / p.Wo;
+                    b_wo[j] = r - b_ho[j] * p.Wo;
+                }
+            }
+        }
+        const int k = i_k;
+        uint8_t* base = lds + ST * SUB;
+        if constexpr (KS == 1) {
+#pragma unroll
+            for (int j = 0; j < BR; j++) {
+                const long m = i_tile * BMP + b_row[j];
+                const void* src = m < p.M ? (const void*)(p.x + m * p.xs + k * 32 + b_kg[j] * 8)
+                                          : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
+                glds16_det(src, base + (j * NT + wave * 64) * 16);
+            }
+        } else {
+            // the GEMM kernel's K order: chunk fastest, then the tap column, then the tap row
+#pragma unroll
+            for (int j = 0; j < BR; j++) {
+                const int hi = b_ho[j] * STR + i_kh - KS / 2, wi = b_wo[j] * STR + i_kw - KS / 2;
+                const bool in = b_n[j] >= 0 && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W;
+                const void* src = in ? (const void*)(p.x + (((long)b_n[j] * p.H + hi) * p.W + wi) * p.xs + i_ch * 32 + b_kg[j] * 8)
+                                     : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
+                glds16_det(src, base + (j * NT + wave * 64) * 16);
+            }
+            if (++i_ch == kc) {
+                i_ch = 0;
+                if (++i_kw == KS) i_kw = 0, i_kh++;
+            }
         }
 #pragma unroll
         for (int c = 0; c < WCT; c++) {
             // couts past npad: an out-of-range offset (the load returns zeros)
-            const int off = co0 + wc * WCO + c * 16 < p.npad ? k * a_step + co0 * 64 + a_lane[c] : 0x7ff00000;
+            const int off = i_co0 + wc * WCO + c * 16 < p.npad ? k * a_step + i_co0 * 64 + a_lane[c] : 0x7ff00000;
             areg[ST][c] = buffer_load_frag(wr, off);
         }
+        if (++i_k == nq) i_k = 0, i_it++, i_kh = 0;
     };
     constexpr int OPS = BR + WCT;  // vector memory instructions per issued step (this wave)
     f32x4 acc[FP][WCT];
@@ -670,7 +706,7 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
 #pragma unroll
         for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     det_static_for<0, D>([&](auto J) {
-        if (J < S) issue(J, J);
+        if (J < S) issue(J);
     });
     wait_vm(OPS * (int)(std::min<long>(D, S) - 1));
     __builtin_amdgcn_s_barrier();
@@ -682,7 +718,7 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     constexpr int kStores = FP * ((2 * WCO + 63) / 64);  // store instructions per epilogue (this wave)
     auto step = [&](long g, auto Ss) {
         constexpr int ST = decltype(Ss)::value;
-        if (g + D < S) issue(g + D, std::integral_constant<int, (ST + D) % NBUF>{});
+        if (g + D < S) issue(std::integral_constant<int, (ST + D) % NBUF>{});
         {
             // this step's weight fragments landed at the previous step's wait (the asm loads are
             // invisible to the compiler): tell it so here, before their first use
@@ -2008,25 +2044,28 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const long blocks = (p.M + kPx - 1) / kPx * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
-    if (ks == 1 && wimg && N <= kPersMaxN) {  // persistent 1x1 GEMM: 2 workgroups per CU
-        const char* e = getenv("MVPOSE_DET_PERS");  // A/B and tests: 0 = one tile per workgroup
-        if (!(e && e[0] == '0')) {
+    if (wimg && N <= kPersMaxN) {  // persistent GEMM: 2 workgroups per CU
+        // A/B and tests: 0 = one tile per workgroup everywhere; 3 = the 3x3 GEMM convs too
+        const char* e = getenv("MVPOSE_DET_PERS");
+        if (!(e && e[0] == '0') && (ks == 1 || (e && e[0] == '3'))) {
             // all blocks, or a multiple of 8 (the kernel's per-XCD split needs one of the two)
             const char* eo = getenv("MVPOSE_DET_PERS_OCC");  // A/B: workgroups per CU (default 2)
             const long occ = eo ? std::max(1, atoi(eo)) : 2;
             const long grid = blocks <= occ * det_band_grid() ? blocks : occ * det_band_grid() / 8 * 8;
             MVP_REQUIRE(grid > 0, "det conv: persistent grid");
             const dim3 gp((unsigned)grid), tp(256);
-            const bool deep = e && e[0] == '4';  // A/B: a 4-slot ring
-            auto go = [&](auto k3, auto k4) {
-                if (deep) hipLaunchKernelGGL(k4, gp, tp, 0, s, p);
-                else hipLaunchKernelGGL(k3, gp, tp, 0, s, p);
+            auto go = [&](auto kern) { hipLaunchKernelGGL(kern, gp, tp, 0, s, p); };
+            auto by_bn = [&](auto ks_tag, auto st_tag) {
+                constexpr int K = decltype(ks_tag)::value, T = decltype(st_tag)::value;
+                if (bn == 192) go(det_conv1x1_pers_kernel<192, 1, 3, K, T>);
+                else if (bn == 128) go(det_conv1x1_pers_kernel<128, 1, 3, K, T>);
+                else if (bn == 96) go(det_conv1x1_pers_kernel<96, 2, 3, K, T>);
+                else if (bn == 64) go(det_conv1x1_pers_kernel<64, 1, 3, K, T>);
+                else go(det_conv1x1_pers_kernel<32, 2, 3, K, T>);
             };
-            if (bn == 192) go(det_conv1x1_pers_kernel<192, 1, 3>, det_conv1x1_pers_kernel<192, 1, 4>);
-            else if (bn == 128) go(det_conv1x1_pers_kernel<128, 1, 3>, det_conv1x1_pers_kernel<128, 1, 4>);
-            else if (bn == 96) go(det_conv1x1_pers_kernel<96, 2, 3>, det_conv1x1_pers_kernel<96, 2, 4>);
-            else if (bn == 64) go(det_conv1x1_pers_kernel<64, 1, 3>, det_conv1x1_pers_kernel<64, 1, 4>);
-            else go(det_conv1x1_pers_kernel<32, 2, 3>, det_conv1x1_pers_kernel<32, 2, 4>);
+            if (ks == 1) by_bn(std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{});
+            else if (stride == 1) by_bn(std::integral_constant<int, 3>{}, std::integral_constant<int, 1>{});
+            else by_bn(std::integral_constant<int, 3>{}, std::integral_constant<int, 2>{});
             MVP_HIP(hipGetLastError());
             return;
         }

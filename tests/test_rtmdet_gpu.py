@@ -178,17 +178,19 @@ def test_live_couts_bitwise(sd, size, n, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
-@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
-def test_persistent_1x1_bitwise(sd, size, n, monkeypatch):
-    """The 1x1 convs on the persistent GEMM (det_conv1x1_pers_kernel: 2 workgroups per CU walk
-    (tile, cout block) items with the DMA ring running across items, the default) against one
-    tile per workgroup (det_conv_gemm_kernel<*, 1, 1>, MVPOSE_DET_PERS=0): the same operand
-    images and MFMA sequence per output, so every tensor of the forward is bit-identical (the
-    128 size: ragged last tiles and workgroups with no item)."""
+@pytest.mark.parametrize("size,n,pers", [(128, 3, "1"), (640, 2, "1"), (128, 3, "3"), (640, 2, "3")])
+def test_persistent_1x1_bitwise(sd, size, n, pers, monkeypatch):
+    """The 1x1 and the GEMM-path 3x3 (s1 and s2) convs on the persistent GEMM
+    (det_conv1x1_pers_kernel: 2 workgroups per CU walk (tile, cout block) items, weight
+    fragments loaded into VGPRs, the pixel ring running across items; the default) against one
+    tile per workgroup (det_conv_gemm_kernel, MVPOSE_DET_PERS=0): the same operands and MFMA
+    sequence per output (K steps in (tap row, tap column, chunk) order), so every tensor of the
+    forward is bit-identical (the 128 size: ragged last tiles, zero-padded taps at the borders,
+    workgroups with no item)."""
     frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=23)).cuda()
     outs = []
-    for pers in ("0", "1"):
-        monkeypatch.setenv("MVPOSE_DET_PERS", pers)
+    for mode in ("0", pers):  # pers "1": the 1x1 convs (the default); "3": the 3x3 GEMM convs too
+        monkeypatch.setenv("MVPOSE_DET_PERS", mode)
         det = D.RTMDetector(sd, max_batch=n, size=size)
         det.run_ops(frames, 0, len(det.spec.ops))
         torch.cuda.synchronize()
