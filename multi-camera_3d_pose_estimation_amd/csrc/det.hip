@@ -516,6 +516,7 @@ __device__ __forceinline__ void lds_write_u2(void* p, uint2 v) {
 }
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 // raw buffer resource (stride 0, num_records bytes; gfx9 dword 3)
 __device__ __forceinline__ i32x4 make_rsrc(const void* base, int bytes) {
     const uint64_t a = (uint64_t)(uintptr_t)base;
@@ -939,6 +940,180 @@ __global__ __launch_bounds__(256, TR == 2 ? 3 : 2) void det_conv_halo_kernel(GPa
                 uint2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
         }
     }
+    }
+}
+
+// Persistent halo conv (round 6) for the 64-cout 3x3/s1 convs with one or two input chunks (the
+// 320x320 stem.2 and the 160x160 stage-1 block conv1s: ~6.6 ms of the 512-frame forward).
+// det_conv_halo_kernel re-DMAs the conv's whole weight set (36 KB per chunk) with every
+// 256-pixel tile: 60 % of its LDS-DMA bytes, and without them the forward ran 3.2 ms faster
+// (timing diagnostic, profiles/r06_det_halo_pers.txt).  Here one workgroup per CU (8 waves)
+// keeps the weights of every chunk resident in LDS for the launch and walks 8-row x 64-column
+// tiles (a contiguous per-XCD range, so neighbouring tiles' halo rows meet in that L2); each
+// (tile, chunk) step's 10 x 66 halo arrives by LDS-DMA into one of two buffers while the
+// previous step computes.  Wave w computes output row w of the tile for the LT live 16-cout
+// tiles (4 pixel fragments each); the padding couts are stored as zeros (their weights and
+// biases are zero).  The DMA and the stores are asm the compiler does not track (no vmcnt it
+// would put in front of LDS reads); the kernel counts its own waits.  Same operand images and
+// K order (chunk, tap, channel) as det_conv_halo_kernel: bit-identical.
+__device__ __forceinline__ void glds16_raw(const void* src, uint32_t lds_off) {
+    uint32_t saved;  // m0 is the compiler's: restored after the issue (the DMA reads it at issue)
+    asm volatile("s_nop 4\n\ts_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(saved)
+                 : "v"(src), "s"(lds_off)
+                 : "memory");
+}
+__device__ __forceinline__ void buffer_store_u2v(u32x2 v, i32x4 r, int off) {
+    asm volatile("s_nop 4\n\tbuffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 1" : : "v"(v), "v"(off), "s"(r) : "memory");
+}
+
+template <int NCK, int LT>
+struct HaloPersCfg {
+    static constexpr int BN = 64, TR = 8, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;
+    static constexpr int NWV = 8, NT = 64 * NWV;
+    static constexpr int A_SLOTS = 9 * 4 * BN;              // one chunk's weights, [tap][cout][4]
+    static constexpr int B_R64 = (HP * 4 + 63) / 64;        // halo DMA rounds (1 KiB each)
+    static constexpr int BUF = B_R64 * 64 * 16;             // one halo buffer
+    static constexpr int OFF_B = NCK * A_SLOTS * 16;
+    static constexpr int LDS = OFF_B + 2 * BUF;
+    static_assert(LDS <= 160 * 1024, "halo pers: LDS budget");
+    static_assert(LT >= 1 && LT <= 4, "live tiles");
+};
+
+template <int NCK, int LT>
+__global__ __launch_bounds__(512, 1) void det_conv_halo_pers_kernel(GParams p) {
+    using G = HaloPersCfg<NCK, LT>;
+    constexpr int BN = G::BN, TR = G::TR, TW = G::TW, HW_ = G::HW_, NWV = G::NWV;
+    extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    auto swz = [](int r) { return (-(r >> 2)) & 3; };
+    const int tiles_w = (p.W + TW - 1) / TW, tiles_h = (p.H + TR - 1) / TR, per = tiles_w * tiles_h;
+    const long T = p.M / ((long)p.H * p.W) * per;
+    const int NG = gridDim.x, xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
+    const int gx = NG / 8 + (xcd < (NG & 7) ? 1 : 0);
+    const long qx = T >> 3, rx = T & 7;
+    const long x0 = xcd < rx ? xcd * (qx + 1) : rx * (qx + 1) + (xcd - rx) * qx;
+    const long x1 = x0 + qx + (xcd < rx ? 1 : 0);
+    const long n_tiles = x1 - x0 > loc ? (x1 - x0 - loc + gx - 1) / gx : 0;
+    if (n_tiles == 0) return;  // workgroup-uniform
+    const long S = n_tiles * NCK;
+    // the weights of every chunk, once: slot s of chunk q = tap * 4BN + 4co + (kq ^ swz(co))
+    for (int i = tid; i < NCK * G::A_SLOTS; i += G::NT) {
+        const int q = i / G::A_SLOTS, sl = i - q * G::A_SLOTS, tp = sl / (4 * BN), rem = sl - tp * (4 * BN);
+        const int co = rem >> 2, kq = (rem & 3) ^ swz(co);
+        *reinterpret_cast<uint4*>(lds + i * 16) =
+            *reinterpret_cast<const uint4*>(p.w + (size_t)co * (288 * NCK) + tp * (32 * NCK) + q * 32 + kq * 8);
+    }
+    const int kg = lane >> 4, r16 = lane & 15;
+    // the lane's biases, complete before the loop (a load the compiler still counted as pending
+    // there would put a vmcnt wait, covering the next step's DMA, into every epilogue)
+    f32x4 bb[LT];
+#pragma unroll
+    for (int c = 0; c < LT; c++) {
+        bb[c] = *reinterpret_cast<const f32x4*>(p.bias + c * 16 + kg * 4);
+        asm volatile("" : "+v"(bb[c]));
+    }
+    // this wave's halo DMA rounds (r = wave + NWV j < B_R64)
+    const int ops = (G::B_R64 - wave + NWV - 1) / NWV;
+    auto tile_of = [&](long t, int& n, int& ho0, int& wo0) {
+        const long lt = x0 + loc + t * gx;
+        n = (int)(lt / per);
+        const int r = (int)(lt - (long)n * per), th = r / tiles_w;
+        ho0 = th * TR;
+        wo0 = (r - th * tiles_w) * TW;
+    };
+    auto issue = [&](long st, int buf) {
+        const long t = st / NCK;
+        const int q = (int)(st - t * NCK);
+        int n, ho0, wo0;
+        tile_of(t, n, ho0, wo0);
+        const uint16_t* xb = p.x + (size_t)n * p.H * p.W * p.xs;
+#pragma unroll
+        for (int j = 0; j < (G::B_R64 + NWV - 1) / NWV; j++) {
+            const int r = wave + NWV * j;
+            if (r < G::B_R64) {  // wave-uniform
+                const int sl = r * 64 + lane, hp = sl >> 2, kq = (sl & 3) ^ swz(hp);
+                const int hy = hp / HW_, hx = hp - hy * HW_;
+                const int gy = ho0 + hy - 1, gx2 = wo0 + hx - 1;
+                const bool in = hp < G::HP && (unsigned)gy < (unsigned)p.H && (unsigned)gx2 < (unsigned)p.W;
+                const void* src = in ? (const void*)(xb + ((size_t)gy * p.W + gx2) * p.xs + q * 32 + kq * 8)
+                                     : (const void*)(p.zero + (sl & 1023) * 8);
+                glds16_raw(src, (uint32_t)(G::OFF_B + buf * G::BUF + r * 1024));
+            }
+        }
+    };
+    constexpr int kStores = 4 * (BN / 16);  // per wave and tile: 4 fragments x every 16-cout tile
+    const int soff = r16 * 64 + ((kg ^ swz(r16)) * 16);
+    f32x4 acc[4][LT];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+        for (int c = 0; c < LT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    issue(0, 0);
+    __syncthreads();  // the weights (plain stores) are visible
+    int st_after = 0;  // store instructions issued since the last DMA issue
+    for (long st = 0; st < S; st++) {
+        const int buf = (int)(st & 1);
+        wait_vm(st_after);  // this wave's DMA of step st landed (only the later stores may be pending)
+        __builtin_amdgcn_s_barrier();  // every wave's; the other buffer is free
+        asm volatile("" ::: "memory");
+        if (st + 1 < S) {
+            issue(st + 1, buf ^ 1);
+            st_after = 0;
+        }
+        const long t = st / NCK;
+        const int q = (int)(st - t * NCK);
+        const uint8_t* wa = lds + q * G::A_SLOTS * 16;
+        const uint8_t* hb = lds + G::OFF_B + buf * G::BUF;
+#pragma unroll
+        for (int tp = 0; tp < 9; tp++) {
+            const int dy = tp / 3, dx = tp % 3;
+            bf16x8 a[LT], b[4];
+#pragma unroll
+            for (int c = 0; c < LT; c++) a[c] = *reinterpret_cast<const bf16x8*>(wa + tp * 4 * BN * 16 + (c * 16) * 64 + soff);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int hp = (wave + dy) * HW_ + i * 16 + r16 + dx;
+                b[i] = *reinterpret_cast<const bf16x8*>(hb + hp * 64 + ((kg ^ swz(hp)) * 16));
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int c = 0; c < LT; c++) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[c], b[i], acc[i][c], 0, 0, 0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (q + 1 < NCK) continue;
+        // ---- the tile's epilogue: row `wave` of the tile, every 16-cout tile (zeros past LT)
+        int n, ho0, wo0;
+        tile_of(t, n, ho0, wo0);
+        const int ho = ho0 + wave;
+        const uint16_t* yb = p.y + (((size_t)n * p.H + (ho < p.H ? ho : 0)) * p.W + wo0) * p.ys;
+        const i32x4 yr = make_rsrc(yb, (int)std::min<long>((long)TW * p.ys * 2, 0x7fffffffL));
+#pragma unroll
+        for (int c = 0; c < BN / 16; c++) {
+            const int co = c * 16 + kg * 4;
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int wo = wo0 + i * 16 + r16;
+                u32x2 o = {0u, 0u};
+                if (c < LT) {
+                    const f32x4 ac = acc[i][c < LT ? c : 0];
+                    const f32x4 bc = bb[c < LT ? c : 0];
+                    float v[4] = {ac[0] + bc[0], ac[1] + bc[1], ac[2] + bc[2], ac[3] + bc[3]};
+#pragma unroll
+                    for (int e = 0; e < 4; e++) v[e] = act_f(v[e], p.act);
+                    o = u32x2{tobf(v[0]) | (tobf(v[1]) << 16), tobf(v[2]) | (tobf(v[3]) << 16)};
+                }
+                const bool ok = ho < p.H && wo < p.W && co < p.N;
+                buffer_store_u2v(o, yr, ok ? ((i * 16 + r16) * p.ys + co) * 2 : 0x7ff00000);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int c = 0; c < LT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st_after = kStores;
     }
 }
 
@@ -1966,6 +2141,12 @@ void launch_band(const GParams& p, const uint16_t* wband, hipStream_t s) {
 }
 }  // namespace
 
+// the persistent halo kernel (A/B and tests: MVPOSE_DET_HALO_PERS=0 = det_conv_halo_kernel)
+bool halo_pers_on() {
+    const char* e = getenv("MVPOSE_DET_HALO_PERS");
+    return !(e && e[0] == '0');
+}
+
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
                           hipStream_t s, const uint16_t* wimg, const uint16_t* wband, int live) {
@@ -2026,6 +2207,23 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
             else if (cin == 64) go(det_conv_halo_kernel<32, 2, 2>);
             else if (npad == 64) go(det_conv_halo_kernel<64, 1, 2>);
             else go(det_conv_halo_kernel<32, 1, 2>);
+        } else if (npad == 64 && (live == 48 || live == 64) && !res && halo_pers_on()) {
+            // persistent, weights resident (det_conv_halo_pers_kernel)
+            auto go_p = [&](auto kern, int lds_bytes) {
+                static int attr_done[4] = {0, 0, 0, 0};
+                const int slot = (cin == 64) * 2 + (live == 64);
+                if (!attr_done[slot]) {
+                    MVP_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+                    attr_done[slot] = 1;
+                }
+                const long T = (long)n * ((H + 7) / 8) * ((W + 63) / 64), cap = det_band_grid();
+                const long grid = T <= cap ? T : cap / 8 * 8;
+                hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds_bytes, s, p);
+            };
+            if (cin == 64 && live == 48) go_p(det_conv_halo_pers_kernel<2, 3>, HaloPersCfg<2, 3>::LDS);
+            else if (cin == 64) go_p(det_conv_halo_pers_kernel<2, 4>, HaloPersCfg<2, 4>::LDS);
+            else if (live == 48) go_p(det_conv_halo_pers_kernel<1, 3>, HaloPersCfg<1, 3>::LDS);
+            else go_p(det_conv_halo_pers_kernel<1, 4>, HaloPersCfg<1, 4>::LDS);
         } else if (npad == 64 && live <= 48 && live > 32 && !res && DET_HALO_TR % 4 == 0 &&
                    !(getenv("MVPOSE_DET_LIVE") && getenv("MVPOSE_DET_LIVE")[0] == '0')) {
             // 48 real couts in 64 (RTMDet-m stem.2, stage-1 conv1): 3 live tiles

@@ -203,6 +203,29 @@ def test_persistent_1x1_bitwise(sd, size, n, pers, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
+@pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])
+def test_halo_persistent_bitwise(sd, size, n, monkeypatch):
+    """The 64-cout 3x3/s1 convs with one or two input chunks (stem.2, the stage-1 block conv1s)
+    on the persistent halo kernel (det_conv_halo_pers_kernel: weights resident in LDS, 8-row
+    tiles, the next step's halo DMA under the current one; the default) against the tile
+    kernel (det_conv_halo_kernel, MVPOSE_DET_HALO_PERS=0): same operands and K order, so every
+    tensor of the forward is bit-identical (128: planes narrower than a 64-column tile)."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=29)).cuda()
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MVPOSE_DET_HALO_PERS", mode)
+        det = D.RTMDetector(sd, max_batch=n, size=size)
+        det.run_ops(frames, 0, len(det.spec.ops))
+        torch.cuda.synchronize()
+        ts = [det.tensor(t, n).cpu() for t in range(len(det.spec.tensors))]
+        outs.append((ts, det.cand[:n].cpu()))
+        det.close()
+    (ta, ca), (tb, cb) = outs
+    for t, (x, y) in enumerate(zip(ta, tb)):
+        assert torch.equal(x.view(torch.int16), y.view(torch.int16)), (size, t)
+    assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
+
+
 def test_band_conv_vs_gemm(sd, monkeypatch):
     """The 3x3/s1 convs with >= 96 input channels on the 80x80 / 40x40 planes run on the
     band-halo kernel (det_conv_band_kernel, the default): each one, on the forward's own input,
