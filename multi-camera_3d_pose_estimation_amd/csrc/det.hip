@@ -967,9 +967,9 @@ __device__ __forceinline__ void buffer_store_u2v(u32x2 v, i32x4 r, int off) {
     asm volatile("s_nop 4\n\tbuffer_store_dwordx2 %0, %1, %2, 0 offen\n\ts_nop 1" : : "v"(v), "v"(off), "s"(r) : "memory");
 }
 
-template <int NCK, int LT>
+template <int BN_, int NCK, int LT>
 struct HaloPersCfg {
-    static constexpr int BN = 64, TR = 8, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;
+    static constexpr int BN = BN_, TR = 8, TW = 64, HW_ = TW + 2, HP = (TR + 2) * HW_;
     static constexpr int NWV = 8, NT = 64 * NWV;
     static constexpr int A_SLOTS = 9 * 4 * BN;              // one chunk's weights, [tap][cout][4]
     static constexpr int B_R64 = (HP * 4 + 63) / 64;        // halo DMA rounds (1 KiB each)
@@ -977,12 +977,12 @@ struct HaloPersCfg {
     static constexpr int OFF_B = NCK * A_SLOTS * 16;
     static constexpr int LDS = OFF_B + 2 * BUF;
     static_assert(LDS <= 160 * 1024, "halo pers: LDS budget");
-    static_assert(LT >= 1 && LT <= 4, "live tiles");
+    static_assert(LT >= 1 && LT <= BN / 16 && (BN == 32 || BN == 64), "live tiles");
 };
 
-template <int NCK, int LT>
+template <int BN_, int NCK, int LT>
 __global__ __launch_bounds__(512, 1) void det_conv_halo_pers_kernel(GParams p) {
-    using G = HaloPersCfg<NCK, LT>;
+    using G = HaloPersCfg<BN_, NCK, LT>;
     constexpr int BN = G::BN, TR = G::TR, TW = G::TW, HW_ = G::HW_, NWV = G::NWV;
     extern __shared__ __attribute__((aligned(1024))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2220,10 +2220,22 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
                 const long grid = T <= cap ? T : cap / 8 * 8;
                 hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(512), lds_bytes, s, p);
             };
-            if (cin == 64 && live == 48) go_p(det_conv_halo_pers_kernel<2, 3>, HaloPersCfg<2, 3>::LDS);
-            else if (cin == 64) go_p(det_conv_halo_pers_kernel<2, 4>, HaloPersCfg<2, 4>::LDS);
-            else if (live == 48) go_p(det_conv_halo_pers_kernel<1, 3>, HaloPersCfg<1, 3>::LDS);
-            else go_p(det_conv_halo_pers_kernel<1, 4>, HaloPersCfg<1, 4>::LDS);
+            if (cin == 64 && live == 48) go_p(det_conv_halo_pers_kernel<64, 2, 3>, HaloPersCfg<64, 2, 3>::LDS);
+            else if (cin == 64) go_p(det_conv_halo_pers_kernel<64, 2, 4>, HaloPersCfg<64, 2, 4>::LDS);
+            else if (live == 48) go_p(det_conv_halo_pers_kernel<64, 1, 3>, HaloPersCfg<64, 1, 3>::LDS);
+            else go_p(det_conv_halo_pers_kernel<64, 1, 4>, HaloPersCfg<64, 1, 4>::LDS);
+        } else if (npad == 32 && cin == 32 && live > 16 && !res && halo_pers_on()) {
+            // RTMDet-m stem.1 (24 -> 24 couts stored as 32): both 16-cout tiles live
+            static bool attr32 = false;
+            using G32 = HaloPersCfg<32, 1, 2>;
+            if (!attr32) {
+                MVP_HIP(hipFuncSetAttribute((const void*)det_conv_halo_pers_kernel<32, 1, 2>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, G32::LDS));
+                attr32 = true;
+            }
+            const long T = (long)n * ((H + 7) / 8) * ((W + 63) / 64), cap = det_band_grid();
+            const long grid = T <= cap ? T : cap / 8 * 8;
+            hipLaunchKernelGGL((det_conv_halo_pers_kernel<32, 1, 2>), dim3((unsigned)grid), dim3(512), G32::LDS, s, p);
         } else if (npad == 64 && live <= 48 && live > 32 && !res && DET_HALO_TR % 4 == 0 &&
                    !(getenv("MVPOSE_DET_LIVE") && getenv("MVPOSE_DET_LIVE")[0] == '0')) {
             // 48 real couts in 64 (RTMDet-m stem.2, stage-1 conv1): 3 live tiles
