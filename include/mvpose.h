@@ -343,6 +343,12 @@ int mvp_det_arena_bytes(void* handle, int64_t* bytes_out);
 int mvp_det_run_ops(void* handle, const uint8_t* frames_dev, int n, int h, int w, int op_begin, int op_end,
                     float* cand_dev, void* stream);
 int mvp_det_tensor_copy(void* handle, int t, int n, void* buf_dev, int to_arena, void* stream);
+/* Producer passes folded into their consumer 1x1 conv at create time (the neck's nearest-2x
+ * upsamples; the channel-attention scale pass): folded_out[k] = 1 when op k's pass runs inside
+ * the next conv reading its tensor (a DET_UP2 then launches nothing and leaves its output slice
+ * unwritten; a DET_CA computes its scales and leaves its tensor unscaled), else 0.  Off with
+ * MVPOSE_DET_FOLD=0 in the environment at create time.  Results are bit-identical either way. */
+int mvp_det_folded_ops(void* handle, int* folded_out, int n_ops);
 int mvp_det_destroy(void* handle);
 
 /* ---------------------------------------------------------------------------

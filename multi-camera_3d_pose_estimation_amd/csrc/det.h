@@ -21,10 +21,24 @@ void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float*
 // conv (1x1, or 3x3 stride 1 / 2, pad ks/2) as a GEMM over the flat output pixels with the
 // im2col gathered by DMA; w [det_cout_pad(N)][ks][ks][cin] bf16; act as ConvLaunch.relu (2 = SiLU
 // before the residual, 1 = ReLU after it)
+// Producer passes folded into a 1x1 conv's pixel DMA on the persistent GEMM (round 6), the
+// producer's own launch skipped: `up` = input channels [0, up_c) are the nearest-2x upsample of
+// an H/2 x W/2 plane at up (pixel stride up_s; the neck's DET_UP2); `ca` = [n][cin] f32 scales
+// applied to every input channel as it lands (DET_CA's in-place pass).  Bit-identical to running
+// the producer.
+struct DetConvFold {
+    const uint16_t* up = nullptr;
+    int up_s = 0, up_c = 0;
+    const float* ca = nullptr;
+};
+// whether a conv of this shape runs on the persistent 1x1 GEMM with folds (`ca`: the scale
+// fold, whose tables hold 8 frames per 128-pixel tile); MVPOSE_DET_FOLD=0 turns folding off
+bool det_conv_fold_ok(int H, int W, int cin, int N, int ks, bool ca);
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
                           hipStream_t s, const uint16_t* wimg = nullptr, const uint16_t* wband = nullptr,
-                          int live = 0);  // live: couts with non-zero weights or bias (0 = all N)
+                          int live = 0,  // live: couts with non-zero weights or bias (0 = all N)
+                          const DetConvFold* fold = nullptr);
 // A CSPNeXtBlock's depthwise 5x5 (dw_w [C/8][25][8] f32, dw_b [C]) and pointwise 1x1 (wimg: the
 // GEMM weight image of the [det_cout_pad(N) == C][C] weights, pw_b [C]) in one launch, the
 // intermediate kept in LDS; bit-identical to launch_det_dw5 + launch_det_conv_gemm (ks 1).
@@ -41,7 +55,9 @@ int det_band_rows(int npad);  // cout rows of the band image (npad rounded up to
 void det_pack_band_weights(const uint16_t* w, uint16_t* img, int npad, int cin, hipStream_t s);
 // channel attention in place; scratch: [n][17][C] f32 (per-split partial sums + scales)
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
-                   hipStream_t s);
+                   hipStream_t s, bool scale_pass = true);
+// the [n][C] scales launch_det_ca leaves in its scratch
+inline const float* det_ca_scales(const float* scratch, int n, int C) { return scratch + (size_t)n * 16 * C; }
 void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s);
 void launch_det_up2(const uint16_t* x, int xs, uint16_t* y, int ys, int n, int H, int W, int C, hipStream_t s);
 void launch_det_head(const uint16_t* x, int xs, int F, const float* w, const float* b, float* cand, int n, int H, int W,

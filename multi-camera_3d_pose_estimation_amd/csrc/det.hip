@@ -293,6 +293,11 @@ struct GParams {
     // four swizzled 16-B chunks in LDS slot order: a weight DMA instruction reads 1 KB
     // contiguous instead of 16 rows x 64 B); nullptr: gather from w
     const uint16_t* wimg = nullptr;
+    // persistent 1x1 GEMM folds (DetConvFold, det.h): input channels [0, up_c) from the nearest-2x
+    // upsample of `up` (an H/2 x W/2 plane, pixel stride up_s); `ca`: [n][cin] f32 channel scales
+    const uint16_t* up = nullptr;
+    const float* ca = nullptr;
+    int up_s = 0, up_c = 0;
 };
 
 // s_waitcnt vmcnt(n') for the largest level n' <= n (wave-uniform n): at most n' of this
@@ -552,6 +557,20 @@ __device__ __forceinline__ void buffer_store_u4(u32x4 v, i32x4 r, int off) {
     asm volatile("s_nop 4\n\tbuffer_store_dwordx4 %0, %1, %2, 0 offen\n\ts_nop 1" : : "v"(v), "v"(off), "s"(r) : "memory");
 #endif
 }
+// this thread's two landed pixel chunks (16 B each) and their 4 scale quads in one wait (early
+// clobber: a result register must not alias an address the later reads still need)
+__device__ __forceinline__ void lds_read_ca6(const void* d0, const void* d1, const void* t0, const void* t1, u32x4& v0,
+                                             u32x4& v1, f32x4& s00, f32x4& s01, f32x4& s10, f32x4& s11) {
+    asm volatile(
+        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %7\n\tds_read_b128 %2, %8\n\tds_read_b128 %3, %8 offset:16\n\t"
+        "ds_read_b128 %4, %9\n\tds_read_b128 %5, %9 offset:16\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(v0), "=&v"(v1), "=&v"(s00), "=&v"(s01), "=&v"(s10), "=&v"(s11)
+        : "v"(lds_addr(d0)), "v"(lds_addr(d1)), "v"(lds_addr(t0)), "v"(lds_addr(t1))
+        : "memory");
+}
+__device__ __forceinline__ void lds_write_u4(void* p, u32x4 v) {
+    asm volatile("ds_write_b128 %0, %1\n\ts_nop 1" : : "v"(lds_addr(p)), "v"(v) : "memory");
+}
 __device__ __forceinline__ u32x4 lds_read_u4_sync(const void* p) {
     u32x4 v;
     asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(p)) : "memory");
@@ -580,6 +599,12 @@ __device__ __forceinline__ float4 lds_read_f4_sync(const float* p) {
 // LDS and writes whole pixel runs with buffer stores.  Same MFMA operands and sequence (K steps
 // 0 .. nq - 1 from zero) and epilogue arithmetic as det_conv_gemm_kernel<BN, 1, 1, ...>:
 // bit-identical outputs.
+// FM (fold mode): 1 = K channels [0, up_c) read from the nearest-2x upsample's source (the
+// neck's DET_UP2 op is not run: the pixel DMA addresses the half-resolution pixel); 2 = the
+// channel-attention scale (the DET_CA op's in-place pass is not run): wave 0 DMAs each step's
+// table of scales (8 frames x 32 channels, f32) one step ahead, and every thread scales its own
+// landed pixel chunks in LDS (f32 product, bf16 round: ca_scale_kernel's arithmetic) before the
+// barrier that publishes the step.
 template <int B, int E, typename F>
 __device__ __forceinline__ void det_static_for(F&& f) {
     if constexpr (B < E) {
@@ -588,7 +613,7 @@ __device__ __forceinline__ void det_static_for(F&& f) {
     }
 }
 
-template <int BN, int PW, int NBUF, int KS = 1, int STR = 1>
+template <int BN, int PW, int NBUF, int KS = 1, int STR = 1, int FM = 0>
 __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     constexpr int NT = 256, NWV = 4, BMP = 128, D = NBUF - 1;
     constexpr int CWV = NWV / PW;        // waves along the couts
@@ -598,10 +623,13 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     constexpr int B_SLOTS = 4 * BMP, SUB = B_SLOTS * 16, BR = B_SLOTS / NT;
     constexpr int ROWB = WCO * 2;        // staged bytes per pixel
     constexpr int OFF_BIAS = NBUF * SUB, OFF_STAGE = OFF_BIAS + kPersMaxN * 4;
+    constexpr int OFF_CA = OFF_STAGE + NWV * 16 * ROWB;  // FM & 2: NBUF 1-KiB scale tables
     static_assert(WCO % 16 == 0 && FP * 16 * PW == BMP && B_SLOTS % NT == 0, "tiling");
+    static_assert(KS == 1 || FM == 0, "folds: 1x1 only");
+    static_assert(!(FM & 2) || BR == 2, "lds_read_ca6: two chunks per thread");
     // one LDS object: with a second __shared__ array the compiler's LDS-DMA alias check put
     // vmcnt(0) in front of every fragment read
-    __shared__ __attribute__((aligned(1024))) uint8_t lds[OFF_STAGE + NWV * 16 * ROWB];
+    __shared__ __attribute__((aligned(1024))) uint8_t lds[OFF_CA + ((FM & 2) ? NBUF * 1024 : 0)];
     float* bias_s = reinterpret_cast<float*>(lds + OFF_BIAS);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -649,6 +677,16 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
     long i_it = 0, i_tile = 0;
     int i_k = 0, i_co0 = 0, i_ch = 0, i_kw = 0, i_kh = 0;
     int b_n[BR], b_ho[BR], b_wo[BR];
+    long b_up[BR];  // FM & 1: the half-resolution source pixel of each B row
+    const long hw = (long)p.Ho * p.Wo;
+    // FM & 2: first frame of the scale table of the next issued step; its DMA (wave 0): lane l
+    // holds the scales of channels 4 (l & 7) .. + 3 of the step's 32, frame n0 + (l >> 3)
+    long ca_n0 = 0;
+    auto ca_table = [&](int slot, long n0, int kk) {
+        const long nfr = p.M / hw;
+        const long fr = std::min<long>(n0 + (lane >> 3), nfr - 1);
+        glds16_det(p.ca + fr * p.cin + kk * 32 + (lane & 7) * 4, lds + OFF_CA + slot * 1024);
+    };
     auto issue = [&](auto Ss) {
         constexpr int ST = decltype(Ss)::value;
         if (i_k == 0) {  // a new item
@@ -666,6 +704,18 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
                     b_wo[j] = r - b_ho[j] * p.Wo;
                 }
             }
+            if constexpr ((FM & 1) != 0) {
+#pragma unroll
+                for (int j = 0; j < BR; j++) {
+                    const long m = i_tile * BMP + b_row[j];
+                    b_up[j] = 0;
+                    if (m < p.M) {
+                        const long n = m / hw;
+                        const int r = (int)(m - n * hw), h = r / p.W, w = r - h * p.W;
+                        b_up[j] = (n * (p.H >> 1) + (h >> 1)) * (p.W >> 1) + (w >> 1);
+                    }
+                }
+            }
         }
         const int k = i_k;
         uint8_t* base = lds + ST * SUB;
@@ -673,7 +723,10 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
 #pragma unroll
             for (int j = 0; j < BR; j++) {
                 const long m = i_tile * BMP + b_row[j];
-                const void* src = m < p.M ? (const void*)(p.x + m * p.xs + k * 32 + b_kg[j] * 8)
+                const uint16_t* px = p.x + m * p.xs;
+                if constexpr ((FM & 1) != 0)
+                    if (k * 32 < p.up_c) px = p.up + b_up[j] * p.up_s;
+                const void* src = m < p.M ? (const void*)(px + k * 32 + b_kg[j] * 8)
                                           : (const void*)(p.zero + ((j * NT + tid) & 1023) * 8);
                 glds16_det(src, base + (j * NT + wave * 64) * 16);
             }
@@ -699,17 +752,64 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
             areg[ST][c] = buffer_load_frag(wr, off);
         }
         if (++i_k == nq) i_k = 0, i_it++, i_kh = 0;
+        if constexpr ((FM & 2) != 0) {  // the next step's scale table (wave 0; clamped past the end)
+            if (i_k == 0) ca_n0 = (x0 + loc + i_it * gx) / p.n_nb * BMP / hw;
+            if (wave == 0) ca_table((ST + 1) % NBUF, ca_n0, i_k);
+        }
     };
-    constexpr int OPS = BR + WCT;  // vector memory instructions per issued step (this wave)
+    // vector memory instructions per issued step (this wave)
+    const int OPS = BR + WCT + ((FM & 2) != 0 && wave == 0 ? 1 : 0);
+    // FM & 2: scale this thread's two landed chunks of the step in ring slot `slot` (its own
+    // DMAs; the step's table landed one barrier earlier), in the consumption order of the steps
+    int sc_k = 0, sc_fs[BR];
+    long sc_it = 0;
+    auto ca_scale = [&](int slot) {
+        if (sc_k == 0) {
+            const long tile = (x0 + loc + sc_it * gx) / p.n_nb;
+            const long n0 = tile * BMP / hw;
+#pragma unroll
+            for (int j = 0; j < BR; j++) {
+                const long m = tile * BMP + b_row[j];
+                sc_fs[j] = m < p.M ? (int)(m / hw - n0) : 0;
+            }
+        }
+        uint8_t* d0 = lds + slot * SUB + tid * 16;
+        uint8_t* d1 = d0 + NT * 16;
+        const uint8_t* tb = lds + OFF_CA + slot * 1024;
+        u32x4 v[2];
+        f32x4 sc[2][2];
+        lds_read_ca6(d0, d1, tb + sc_fs[0] * 128 + b_kg[0] * 32, tb + sc_fs[1] * 128 + b_kg[1] * 32, v[0], v[1],
+                     sc[0][0], sc[0][1], sc[1][0], sc[1][1]);
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            float f[8];
+            unpack8(uint4{v[j][0], v[j][1], v[j][2], v[j][3]}, f);
+#pragma unroll
+            for (int e = 0; e < 4; e++) f[e] *= sc[j][0][e], f[4 + e] *= sc[j][1][e];
+            const uint4 o = pack8(f);
+            lds_write_u4(j ? d1 : d0, u32x4{o.x, o.y, o.z, o.w});
+        }
+        if (++sc_k == nq) sc_k = 0, sc_it++;
+    };
     f32x4 acc[FP][WCT];
 #pragma unroll
     for (int i = 0; i < FP; i++)
 #pragma unroll
         for (int c = 0; c < WCT; c++) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr ((FM & 2) != 0) {  // step 0's scale table, published before the first issue
+        ca_n0 = (x0 + loc) / p.n_nb * BMP / hw;
+        if (wave == 0) ca_table(0, ca_n0, 0);
+        wait_vm(0);
+        __builtin_amdgcn_s_barrier();
+    }
     det_static_for<0, D>([&](auto J) {
         if (J < S) issue(J);
     });
     wait_vm(OPS * (int)(std::min<long>(D, S) - 1));
+    if constexpr ((FM & 2) != 0) {
+        ca_scale(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     const int soff = r16 * 64 + ((kg ^ ((-(r16 >> 2)) & 3)) * 16);
     uint8_t* stage = lds + OFF_STAGE + wave * 16 * ROWB;  // this wave's epilogue rows
@@ -741,6 +841,8 @@ __global__ __launch_bounds__(256, 2) void det_conv1x1_pers_kernel(GParams p) {
         // acknowledgements off this wait.
         wait_vm(OPS * (int)(std::min<long>(g + D, S - 1) - g - 1) + kStores * __builtin_popcount(ends & ((1u << (D - 1)) - 1)));
         ends <<= 1;
+        if constexpr ((FM & 2) != 0)
+            if (g + 1 < S) ca_scale((ST + 1) % NBUF);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
@@ -1156,6 +1258,9 @@ struct BandCfg {
 // gpurun_out/detband4: four times the DMA pieces cost more than the address arithmetic saved.)
 // NWV waves: 4 (one per SIMD, each 80 pixels x the 64 couts) or 8 (two per SIMD, each 80 pixels
 // x 32 couts: more LDS reads, but a second wave to hide each one's waits).
+// (Measured and dropped, round 6: the 20x20 planes as whole-frame items of 400 pixels = 5 pixel
+// groups x 2 cout groups, 10 waves: 24 % of the MFMA peak against the GEMM kernel's 31 % there —
+// the SIMDs hold 3, 3, 2, 2 waves — 5.58 vs 4.47 ms for the 8 convs, profiles/r06_det_folds.txt.)
 template <int W, int TR, int NWV>
 __global__ __launch_bounds__(64 * NWV, 1) void det_conv_band_kernel(GParams p, const uint16_t* __restrict__ wband) {
     using C = BandCfg<W, TR>;
@@ -2147,10 +2252,45 @@ bool halo_pers_on() {
     return !(e && e[0] == '0');
 }
 
+namespace {
+bool det_pers_1x1_on() {
+    const char* e = getenv("MVPOSE_DET_PERS");
+    return !(e && e[0] == '0');
+}
+int det_conv_bn(int npad) {
+    return npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
+}
+}  // namespace
+
+namespace {
+// the shapes the fold kernels take (no environment: the graph decided at create time)
+bool fold_shape_ok(int H, int W, int cin, int N, int ks, bool ca) {
+    if (ks != 1 || N > kPersMaxN || cin % 32 != 0) return false;
+    const int bn = det_conv_bn(det_cout_pad(N));
+    if (bn != 192 && bn != 96) return false;  // the instantiated fold kernels
+    // a 128-pixel tile's rows span at most 8 frames (the scale table)
+    const long hw = (long)H * W;
+    return hw > 0 && (!ca || (127 + hw - 1) / hw + 1 <= 8);
+}
+}  // namespace
+
+bool det_conv_fold_ok(int H, int W, int cin, int N, int ks, bool ca) {
+    const char* e = getenv("MVPOSE_DET_FOLD");
+    return !(e && e[0] == '0') && det_pers_1x1_on() && fold_shape_ok(H, W, cin, N, ks, ca);
+}
+
 void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const float* bias, const uint16_t* res, int rs,
                           uint16_t* y, int ys, int n, int H, int W, int cin, int N, int ks, int stride, int act,
-                          hipStream_t s, const uint16_t* wimg, const uint16_t* wband, int live) {
+                          hipStream_t s, const uint16_t* wimg, const uint16_t* wband, int live, const DetConvFold* fold) {
     if (live <= 0 || live > N) live = N;
+    const int fm = fold ? (fold->up ? 1 : 0) | (fold->ca ? 2 : 0) : 0;
+    if (fm) {
+        MVP_REQUIRE(wimg && fold_shape_ok(H, W, cin, N, ks, fm & 2), "det conv: fold on a conv the fold kernels do not take");
+        MVP_REQUIRE(fm != 3, "det conv: one fold per conv");
+        MVP_REQUIRE(!(fm & 1) || (H % 2 == 0 && W % 2 == 0 && fold->up_c % 32 == 0 && fold->up_c <= cin &&
+                                  fold->up_s % 8 == 0),
+                    "det conv: upsample fold shape");
+    }
     MVP_REQUIRE(cin % 32 == 0 && N % 4 == 0 && xs % 8 == 0 && ys % 4 == 0 && (!res || rs % 4 == 0),
                 "det conv: cin=%d cout=%d strides %d/%d", cin, N, xs, ys);
     MVP_REQUIRE((ks == 1 && stride == 1) || (ks == 3 && (stride == 1 || stride == 2)), "det conv: ks %d stride %d", ks,
@@ -2165,9 +2305,10 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     // re-measured 256-pixel tiles on the <= 40x40 planes' 192-cout convs only (their 128-pixel
     // tiles re-read each weight slice 1.7-6.6x): 84.5 vs 81.2 ms per 512 frames, removed again
     // (profiles/r06_det_wide_live_ab.txt).
-    const int bn = npad % 192 == 0 ? 192 : npad % 128 == 0 ? 128 : npad % 96 == 0 ? 96 : npad % 64 == 0 ? 64 : 32;
+    const int bn = det_conv_bn(npad);
     GParams p{x, w, bias, res, y, conv_zero_region(), (long)n * Ho * Wo, cin, N, npad, xs, ys, rs, act,
               (npad + bn - 1) / bn, 0, H, W, Ho, Wo, wimg};
+    if (fm) p.up = fold->up, p.up_s = fold->up_s, p.up_c = fold->up_c, p.ca = fold->ca;
     {
         const char* e = getenv("MVPOSE_DET_XCD");  // A/B: 0 = blockIdx order
         p.xcd_order = !(e && e[0] == '0');
@@ -2254,10 +2395,22 @@ void launch_det_conv_gemm(const uint16_t* x, int xs, const uint16_t* w, const fl
     const long blocks = (p.M + kPx - 1) / kPx * p.n_nb;
     if (blocks == 0) return;
     MVP_REQUIRE(blocks < (1L << 31), "det conv: grid too large");
+    if (fm) {  // folds: the persistent 1x1 GEMM, whatever MVPOSE_DET_PERS now says (decided at create)
+        const char* eo = getenv("MVPOSE_DET_PERS_OCC");
+        const long occ = eo ? std::max(1, atoi(eo)) : 2;
+        const long grid = blocks <= occ * det_band_grid() ? blocks : occ * det_band_grid() / 8 * 8;
+        const dim3 gp((unsigned)grid), tp(256);
+        if (fm == 1 && bn == 192) hipLaunchKernelGGL((det_conv1x1_pers_kernel<192, 1, 3, 1, 1, 1>), gp, tp, 0, s, p);
+        else if (fm == 1) hipLaunchKernelGGL((det_conv1x1_pers_kernel<96, 2, 3, 1, 1, 1>), gp, tp, 0, s, p);
+        else if (bn == 192) hipLaunchKernelGGL((det_conv1x1_pers_kernel<192, 1, 3, 1, 1, 2>), gp, tp, 0, s, p);
+        else hipLaunchKernelGGL((det_conv1x1_pers_kernel<96, 2, 3, 1, 1, 2>), gp, tp, 0, s, p);
+        MVP_HIP(hipGetLastError());
+        return;
+    }
     if (wimg && N <= kPersMaxN) {  // persistent GEMM: 2 workgroups per CU
         // A/B and tests: 0 = one tile per workgroup everywhere; 3 = the 3x3 GEMM convs too
         const char* e = getenv("MVPOSE_DET_PERS");
-        if (!(e && e[0] == '0') && (ks == 1 || (e && e[0] == '3'))) {
+        if (det_pers_1x1_on() && (ks == 1 || (e && e[0] == '3'))) {
             // all blocks, or a multiple of 8 (the kernel's per-XCD split needs one of the two)
             const char* eo = getenv("MVPOSE_DET_PERS_OCC");  // A/B: workgroups per CU (default 2)
             const long occ = eo ? std::max(1, atoi(eo)) : 2;
@@ -2340,7 +2493,8 @@ void launch_det_dwpw(const uint16_t* x, int xs, const float* dw_w, const float* 
 bool det_dwpw_supported(int C) { return C == 64 || C == 96; }
 
 void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, const float* b, float* scratch,
-                   hipStream_t s) {
+                   hipStream_t s, bool scale_pass) {
+    static_assert(kCaSplit == 16, "det_ca_scales (det.h)");
     MVP_REQUIRE(C % 8 == 0 && C / 8 <= 256 && xs % 8 == 0, "ca: C=%d", C);
     const int rows = 256 / (C / 8);
     const size_t lds = (size_t)rows * C * sizeof(float);
@@ -2354,6 +2508,7 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
     hipLaunchKernelGGL(ca_fc_kernel, dim3((unsigned)((C + 63) / 64), (unsigned)n), dim3(64), (size_t)C * sizeof(float),
                        s, p);
     MVP_HIP(hipGetLastError());
+    if (!scale_pass) return;  // folded into the consumer conv (DetConvFold::ca)
     const long work = (long)HW * (C / 8);
     hipLaunchKernelGGL(ca_scale_kernel, dim3((unsigned)((work + 255) / 256), (unsigned)n), dim3(256), 0, s, x, sc, HW,
                        C, xs);

@@ -26,6 +26,9 @@ struct DetNet {
     float* ca_scratch = nullptr;
     std::vector<uint16_t*> wimg;   // per conv op: the GEMM kernel's weight image (owned)
     std::vector<uint16_t*> wband;  // per band-eligible conv op: the band kernel's weight image (owned)
+    // producer passes folded into their consumer 1x1 conv (det.h DetConvFold; plan_folds)
+    std::vector<int> fold_src;  // per conv op: the DET_UP2 / DET_CA op folded into it, or -1
+    std::vector<char> folded;   // per op: its pass runs inside its consumer (UP2: not launched; CA: no scale pass)
 };
 
 void free_det(DetNet& g) {
@@ -207,6 +210,67 @@ void plan(DetNet& g) {
     g.arena_bytes = top;
 }
 
+// Folds (round 6), decided once per graph: a DET_UP2 whose output slice only the next 1x1 conv
+// reading that tensor consumes (the neck's top-down joins: the conv's pixel DMA addresses the
+// half-resolution source instead), and a DET_CA directly followed by the 1x1 conv on its tensor
+// (every CSP layer's final_conv: the scales are applied as the pixels land in LDS).  Each stays
+// unfolded unless nothing else reads the bytes the fold leaves unwritten or unscaled.
+// MVPOSE_DET_FOLD=0 (read here) keeps every producer pass.
+void plan_folds(DetNet& g) {
+    const int no = (int)g.ops.size();
+    g.fold_src.assign(no, -1);
+    g.folded.assign(no, 0);
+    auto reads = [&](const mvp_det_op& op, int t) {
+        if (op.in.t == t) return true;
+        return (op.kind == MVP_DET_CONV || op.kind == MVP_DET_DWPW) && op.res.t == t;
+    };
+    auto writes = [&](const mvp_det_op& op, int t, int c0, int c1) {
+        const bool w = op.kind == MVP_DET_STEM || op.kind == MVP_DET_CONV || op.kind == MVP_DET_DW ||
+                       op.kind == MVP_DET_UP2 || op.kind == MVP_DET_DWPW;
+        if (w && op.out.t == t && op.out.coff < c1 && c0 < op.out.coff + op.out.c) return true;
+        // in-place passes on their input view
+        return (op.kind == MVP_DET_CA || op.kind == MVP_DET_SPP) && op.in.t == t;
+    };
+    for (int k = 0; k < no; k++) {
+        const mvp_det_op& u = g.ops[k];
+        if (u.kind == MVP_DET_UP2) {
+            const int t = u.out.t;
+            int j = k + 1;
+            while (j < no && !reads(g.ops[j], t)) j++;
+            if (j == no) continue;
+            const mvp_det_op& c = g.ops[j];
+            const mvp_tensor_desc& x = g.tensors[c.in.t];
+            if (c.kind != MVP_DET_CONV || c.ks != 1 || c.in.t != t || c.in.coff != 0 || u.out.coff != 0 ||
+                u.out.c % 32 != 0 || u.out.c > c.in.c || c.res.t == t || g.tensors[u.in.t].c % 8 != 0 ||
+                !det_conv_fold_ok(x.h, x.w, c.in.c, c.out.c, 1, false))
+                continue;
+            bool ok = true;
+            for (int m = 0; m < no && ok; m++) {
+                if (m == k || m == j) continue;
+                if (reads(g.ops[m], t) && m > k) ok = false;  // another reader of the upsample
+                // the source must not change between the upsample and its consumer
+                if (m > k && m < j && writes(g.ops[m], u.in.t, u.in.coff, u.in.coff + u.in.c)) ok = false;
+                if (m > k && m < j && writes(g.ops[m], t, 0, u.out.c)) ok = false;
+            }
+            if (!ok) continue;
+            g.folded[k] = 1;
+            g.fold_src[j] = k;
+        } else if (u.kind == MVP_DET_CA && k + 1 < no) {
+            const mvp_det_op& c = g.ops[k + 1];
+            const mvp_tensor_desc& x = g.tensors[u.in.t];
+            if (c.kind != MVP_DET_CONV || c.ks != 1 || c.in.t != u.in.t || c.in.coff != u.in.coff || c.in.c != u.in.c ||
+                c.res.t == u.in.t || !det_conv_fold_ok(x.h, x.w, c.in.c, c.out.c, 1, true))
+                continue;
+            bool ok = true;
+            for (int m = k + 2; m < no && ok; m++)
+                if (reads(g.ops[m], u.in.t)) ok = false;  // a later reader would see unscaled channels
+            if (!ok) continue;
+            g.folded[k] = 1;
+            g.fold_src[k + 1] = k;
+        }
+    }
+}
+
 }  // namespace
 }  // namespace mvp
 
@@ -235,6 +299,7 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
         g->fb = f_dev;
         mvp::validate(*g, w_elems, f_elems);
         mvp::plan(*g);
+        mvp::plan_folds(*g);
         hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
         if (e != hipSuccess)
             mvp::fail(MVP_ERR_NOMEM, "mvp_det_create: arena of %lld bytes: %s", (long long)g->arena_bytes,
@@ -294,10 +359,22 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 break;
             case MVP_DET_CONV: {
                 const mvp_tensor_desc& x = T(op.in.t);
+                DetConvFold fold;
+                if (g->fold_src[k] >= 0) {
+                    const mvp_det_op& u = g->ops[g->fold_src[k]];
+                    if (u.kind == MVP_DET_UP2) {
+                        fold.up = vp(u.in);
+                        fold.up_s = T(u.in.t).c;
+                        fold.up_c = u.out.c;
+                    } else {
+                        fold.ca = det_ca_scales(g->ca_scratch, n, op.in.c);
+                    }
+                }
                 launch_det_conv_gemm(vp(op.in), x.c, g->wb + op.w_off, g->fb + op.b_off,
                                      op.res.t >= 0 ? vp(op.res) : nullptr, op.res.t >= 0 ? T(op.res.t).c : 0,
                                      vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, op.out.c, op.ks, op.stride,
-                                     op.act, s, g->wimg[k], g->wband[k], (int)op.aux);
+                                     op.act, s, g->wimg[k], g->wband[k], (int)op.aux,
+                                     g->fold_src[k] >= 0 ? &fold : nullptr);
                 break;
             }
             case MVP_DET_DW: {
@@ -317,7 +394,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
             case MVP_DET_CA: {
                 const mvp_tensor_desc& x = T(op.in.t);
                 launch_det_ca(vp(op.in), x.c, n, x.h * x.w, op.in.c, g->fb + op.w_off, g->fb + op.b_off, g->ca_scratch,
-                              s);
+                              s, !g->folded[k]);
                 break;
             }
             case MVP_DET_SPP: {
@@ -326,6 +403,7 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
                 break;
             }
             case MVP_DET_UP2: {
+                if (g->folded[k]) break;  // its consumer reads the source (plan_folds)
                 const mvp_tensor_desc& x = T(op.in.t);
                 launch_det_up2(vp(op.in), x.c, vp(op.out), T(op.out.t).c, n, x.h, x.w, op.in.c, s);
                 break;
@@ -375,6 +453,15 @@ extern "C" int mvp_det_run_ops(void* handle, const uint8_t* frames, int n, int h
     if (n == 0 || op_begin == op_end) return MVP_OK;
     MVP_REQUIRE((op_begin > 0 || frames) && cand, "mvp_det_run_ops: NULL buffer");
     mvp::run_ops(g, frames, n, h, w, op_begin, op_end, cand, nullptr, reinterpret_cast<hipStream_t>(stream));
+    MVP_ABI_END
+}
+
+extern "C" int mvp_det_folded_ops(void* handle, int* folded_out, int n_ops) {
+    MVP_ABI_BEGIN
+    DetNet* g = static_cast<DetNet*>(handle);
+    MVP_REQUIRE(g != nullptr && folded_out != nullptr, "mvp_det_folded_ops: NULL argument");
+    MVP_REQUIRE(n_ops == (int)g->ops.size(), "mvp_det_folded_ops: %d ops, the graph has %zu", n_ops, g->ops.size());
+    for (int k = 0; k < n_ops; k++) folded_out[k] = g->folded[k];
     MVP_ABI_END
 }
 

@@ -81,6 +81,7 @@ SIGNATURES = {
     "mvp_det_arena_bytes": (c_int, None),
     "mvp_det_run_ops": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     "mvp_det_tensor_copy": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p]),
+    "mvp_det_folded_ops": (c_int, [c_void_p, c_void_p, c_int]),
     "mvp_det_destroy": (c_int, [c_void_p]),
     "mvp_sgd_workspace_floats": (c_int, [c_int, c_int, c_int, c_int, P(c_int64)]),
     # mvp_sgd_params struct pointer declared in mvpose/refine.py

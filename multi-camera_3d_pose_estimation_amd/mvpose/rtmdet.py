@@ -560,6 +560,12 @@ class RTMDetector:
         call("mvp_det_run_ops", self._h, ctypes.c_void_p(frames.data_ptr()), n, h, w, begin, end,
              ctypes.c_void_p(self.cand.data_ptr()), ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
 
+    def folded_ops(self) -> list[int]:
+        """Per op: 1 when its pass runs inside its consumer conv (mvp_det_folded_ops)."""
+        out = (ctypes.c_int * len(self.spec.ops))()
+        call("mvp_det_folded_ops", self._h, out, len(self.spec.ops))
+        return list(out)
+
     def tensor(self, t: int, n: int) -> torch.Tensor:
         """Copy of arena tensor t (first n images) as (n, h, w, c) bf16."""
         h, w, c, _ = self.spec.tensors[t]

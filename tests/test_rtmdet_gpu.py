@@ -66,9 +66,12 @@ def test_letterbox_bit_exact(shape):
 
 
 @pytest.mark.parametrize("size,n", [(128, 2), (640, 1)])
-def test_layer_by_layer(sd, size, n):
+def test_layer_by_layer(sd, size, n, monkeypatch):
     """Each op of the graph on the GPU's own inputs vs the interpreter (every kernel alone,
-    at a small size with 2 frames and at the reference's 640)."""
+    at a small size with 2 frames and at the reference's 640).  The producer passes folded into
+    their consumer convs are kept as launches here (MVPOSE_DET_FOLD=0: each op alone); the folds
+    are test_folds_bitwise's."""
+    monkeypatch.setenv("MVPOSE_DET_FOLD", "0")
     det = D.RTMDetector(sd, max_batch=n, size=size)
     spec = det.spec
     frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=5)).cuda()
@@ -189,6 +192,7 @@ def test_persistent_1x1_bitwise(sd, size, n, pers, monkeypatch):
     workgroups with no item)."""
     frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=23)).cuda()
     outs = []
+    monkeypatch.setenv("MVPOSE_DET_FOLD", "0")  # mode 0 has no folds (they need the persistent GEMM)
     for mode in ("0", pers):  # pers "1": the 1x1 convs (the default); "3": the 3x3 GEMM convs too
         monkeypatch.setenv("MVPOSE_DET_PERS", mode)
         det = D.RTMDetector(sd, max_batch=n, size=size)
@@ -201,6 +205,59 @@ def test_persistent_1x1_bitwise(sd, size, n, pers, monkeypatch):
     for t, (x, y) in enumerate(zip(ta, tb)):
         assert torch.equal(x.view(torch.int16), y.view(torch.int16)), (size, t)
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
+
+
+@pytest.mark.parametrize("size,n", [(160, 3), (640, 2)])
+def test_folds_bitwise(sd, size, n, monkeypatch):
+    """The neck's nearest-2x upsamples and the CSP layers' channel-attention scale pass folded into
+    their consumer 1x1 convs (det_conv1x1_pers_kernel FM 1 / 2: the pixel DMA reads the
+    half-resolution source; the scales are applied to the landed pixels in LDS with
+    ca_scale_kernel's f32 product and bf16 rounding) against the unfolded launches
+    (MVPOSE_DET_FOLD=0): the output of every op, run from the start up to it, and the candidates
+    are bit-identical.  And the folds happened: the upsample slices stay unwritten and the
+    attention tensors unscaled (160: 5x5 stride-32 planes, a 128-pixel tile over 7 frames)."""
+    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=31)).cuda()
+    dets = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MVPOSE_DET_FOLD", mode)
+        dets[mode] = D.RTMDetector(sd, max_batch=n, size=size)
+    spec = dets["0"].spec
+    ops = spec.ops
+    up_ops = [k for k, op in enumerate(ops) if op.kind == D.DET_UP2]
+    ca_ops = [k for k, op in enumerate(ops) if op.kind == D.DET_CA]
+    assert len(up_ops) == 2 and len(ca_ops) == 4, (up_ops, ca_ops)
+    f0, f1 = dets["0"].folded_ops(), dets["1"].folded_ops()
+    assert not any(f0) and [k for k, f in enumerate(f1) if f] == sorted(up_ops + ca_ops), f1
+
+    def view(det, v):
+        return det.tensor(v.t, n)[..., v.coff:v.coff + v.c].cpu()
+
+    def upto(det, k, v):
+        det.run_ops(frames, 0, k)
+        torch.cuda.synchronize()
+        return view(det, v)
+
+    for k in ca_ops:  # folded: the op leaves its tensor unscaled; unfolded: it scales it
+        v = ops[k].in_
+        b0, a0 = upto(dets["0"], k, v), upto(dets["0"], k + 1, v)
+        b1, a1 = upto(dets["1"], k, v), upto(dets["1"], k + 1, v)
+        assert torch.equal(b0.view(torch.int16), b1.view(torch.int16)), k
+        assert torch.equal(a1.view(torch.int16), b1.view(torch.int16)), (k, "scale pass ran")
+        assert not torch.equal(a0.view(torch.int16), b0.view(torch.int16)), k
+    for k in up_ops:  # folded: the upsample slice is never written
+        a0, a1 = upto(dets["0"], k + 1, ops[k].out), upto(dets["1"], k + 1, ops[k].out)
+        assert not torch.equal(a0.view(torch.int16), a1.view(torch.int16)), (k, "upsample ran")
+    for k, op in enumerate(ops):
+        if op.kind in (D.DET_UP2, D.DET_CA, D.DET_HEAD, D.DET_SPP):
+            continue
+        a0, a1 = upto(dets["0"], k + 1, op.out), upto(dets["1"], k + 1, op.out)
+        assert torch.equal(a0.view(torch.int16), a1.view(torch.int16)), (size, k, spec.names[k])
+    r0, r1 = dets["0"].detect(frames), dets["1"].detect(frames)
+    torch.cuda.synchronize()
+    assert torch.equal(r0["cand"].cpu().view(torch.int32), r1["cand"].cpu().view(torch.int32))
+    assert torch.equal(r0["best"].cpu().view(torch.int32), r1["best"].cpu().view(torch.int32))
+    for d in dets.values():
+        d.close()
 
 
 @pytest.mark.parametrize("size,n", [(128, 3), (640, 2)])

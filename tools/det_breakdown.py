@@ -1,7 +1,8 @@
 """Per-op breakdown of one RTMDet-m forward from a kernel trace (+ optional PMC traffic):
     python tools/det_breakdown.py run BATCH PLAN.npz          # on the GPU (under rocprofv3): 3 detects, saves the op plan
     python tools/det_breakdown.py report TRACE.csv PLAN.npz [PMC_FETCH.csv PMC_WRITE.csv]
-Each graph op launches one kernel (channel attention three: pool, fc, scale), the letterbox one in
+Each graph op launches one kernel (channel attention three: pool, fc, scale; a folded upsample none,
+a folded attention no scale pass: mvp_det_folded_ops), the letterbox one in
 front and the per-frame selection one after; the last forward's kernels pair with the op list
 in order.  Per op: us, algorithmic HBM bytes (input read once + output + residual, the stored
 channel counts) and MACs, so the roofline each op is held to is visible."""
@@ -22,8 +23,11 @@ def plan(batch):
     sp = det.spec
     rows = [("letterbox", "letterbox", 0.0, batch * (720 * 1280 * 3 + 640 * 640 * 4 * 2))]
     T = sp.tensors
-    for name, op in zip(sp.names, sp.ops):
+    folded = det.folded_ops()
+    for name, op, fo in zip(sp.names, sp.ops, folded):
         k = KIND[op.kind]
+        if fo and k == "up2":  # runs inside its consumer conv's pixel DMA: no launch
+            continue
         hi, wi, ci, _ = T[op.in_.t]
         if op.out.t >= 0:
             ho, wo, _, _ = T[op.out.t]
@@ -44,8 +48,9 @@ def plan(batch):
             macs, byts = hi * wi * 5 * op.in_.c // 2, hi * wi * op.in_.c * 2
         if k == "ca":
             c = op.in_.c
-            rows += [(name + ".pool", "ca", 0.0, batch * hi * wi * c * 2.0), (name + ".fc", "ca", 0.0, batch * c * c * 4.0),
-                     (name + ".scale", "ca", 0.0, batch * hi * wi * c * 4.0)]
+            rows += [(name + ".pool", "ca", 0.0, batch * hi * wi * c * 2.0), (name + ".fc", "ca", 0.0, batch * c * c * 4.0)]
+            if not fo:  # folded: the scales are applied in the final conv's LDS
+                rows.append((name + ".scale", "ca", 0.0, batch * hi * wi * c * 4.0))
         else:
             rows.append((name, k, batch * float(macs), batch * float(byts)))
     rows.append(("select", "select", 0.0, 0.0))
