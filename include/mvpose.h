@@ -346,7 +346,9 @@ int mvp_det_tensor_copy(void* handle, int t, int n, void* buf_dev, int to_arena,
 /* Producer passes folded into their consumer 1x1 conv at create time (the neck's nearest-2x
  * upsamples; the channel-attention scale pass): folded_out[k] = 1 when op k's pass runs inside
  * the next conv reading its tensor (a DET_UP2 then launches nothing and leaves its output slice
- * unwritten; a DET_CA computes its scales and leaves its tensor unscaled), else 0.  Off with
+ * unwritten; a DET_CA computes its scales and leaves its tensor unscaled); folded_out[0] = 2
+ * when the letterbox runs inside the stem (op 0 stages its rows from the raw frames; the input
+ * tensor stays unwritten unless mvp_det_forward is given letterboxed_dev); else 0.  Off with
  * MVPOSE_DET_FOLD=0 in the environment at create time.  Results are bit-identical either way. */
 int mvp_det_folded_ops(void* handle, int* folded_out, int n_ops);
 int mvp_det_destroy(void* handle);

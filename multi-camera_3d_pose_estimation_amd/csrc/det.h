@@ -16,6 +16,10 @@ void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, con
 // 3x3/s2 conv 4 -> 32 channels on the letterboxed [n][S][S][4] input, w f32 [32][9][4].
 void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act,
                      hipStream_t s);
+// the letterbox folded into the stem: the stem stages its input rows letterboxed from the raw
+// [n][H][W][3] uint8 frames (bit-identical to launch_det_letterbox + launch_det_stem)
+void launch_det_letterbox_stem(const uint8_t* frames, int H, int W, const float* mean3, const float* std3,
+                               const float* w, const float* b, uint16_t* y, int n, int S, int act, hipStream_t s);
 void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,
                     int C, int act, hipStream_t s);
 // conv (1x1, or 3x3 stride 1 / 2, pad ks/2) as a GEMM over the flat output pixels with the

@@ -73,11 +73,8 @@ __device__ __forceinline__ void lin_coef(int d, double scale, int n_src, int& s0
     s1 = min(sx + 1, n_src - 1);
 }
 
-__global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
-    const int n = blockIdx.y;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= p.S * p.S) return;
-    const int y = i / p.S, x = i - y * p.S;
+// letterboxed pixel (y, x) of frame n: 3 normalised bf16 channels + a zero 4th
+__device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x) {
     int v[3] = {114, 114, 114};
     const uint8_t* fr = p.f + (size_t)n * p.H * p.W * 3;
     if (y < p.nh && x < p.nw) {
@@ -104,8 +101,15 @@ __global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
     float o[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) o[c] = ((float)v[c] - p.mean[c]) / p.stdv[c];
-    uint32_t* dst = p.out + ((size_t)n * p.S * p.S + i) * 2;
-    *reinterpret_cast<uint2*>(dst) = uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
+    return uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
+    const int n = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= p.S * p.S) return;
+    const int y = i / p.S, x = i - y * p.S;
+    *reinterpret_cast<uint2*>(p.out + ((size_t)n * p.S * p.S + i) * 2) = lb_pixel(p, n, y, x);
 }
 
 // ------------------------------------------------------------------ stem conv
@@ -114,9 +118,13 @@ __global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
 // five input rows they read are staged in LDS with a one-pixel zero border.  A row r of
 // cout tile c is cout (r >> 2) * 8 + 4c + (r & 3), so lane group g owns the 8 consecutive
 // couts 8g..8g+7 of its pixel (one 16-B store).
+// LB (round 6): the five input rows are letterboxed from the raw frames as they are staged
+// (lb_pixel: letterbox_kernel's arithmetic), so the letterboxed image is never written or read
+// back (the letterbox pass folded into the stem; bit-identical).
+template <bool LB>
 __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, uint16_t* __restrict__ y,
-                                                       int S, int act, long n_tiles) {
+                                                       int S, int act, long n_tiles, LbParams lb) {
     extern __shared__ uint2 sx[];  // [5][S + 2]
     const int Wo = S / 2, LW = S + 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
@@ -144,7 +152,9 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restric
         for (int i = tid; i < 5 * LW; i += 256) {
             const int r = i / LW, c = i - r * LW;
             const int hi = 2 * ho0 - 1 + r, wi = c - 1;
-            sx[i] = (hi >= 0 && hi < S && wi >= 0 && wi < S) ? xin[(size_t)hi * S + wi] : uint2{0u, 0u};
+            const bool in = hi >= 0 && hi < S && wi >= 0 && wi < S;
+            if constexpr (LB) sx[i] = in ? lb_pixel(lb, (int)n, hi, wi) : uint2{0u, 0u};
+            else sx[i] = in ? xin[(size_t)hi * S + wi] : uint2{0u, 0u};
         }
         __syncthreads();
         for (int pt = wave; pt < n_pt; pt += 4) {
@@ -2127,8 +2137,8 @@ __global__ __launch_bounds__(512, TH == 4 ? 3 : 2) void dwpw_kernel(DwPwParams p
 }  // namespace
 
 // ---------------------------------------------------------------------------- launchers
-void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, const float* mean3, const float* std3,
-                          void* out, hipStream_t s) {
+namespace {
+LbParams lb_params(const uint8_t* frames, int H, int W, int S, const float* mean3, const float* std3, void* out) {
     int nh, nw;
     det_rescale_size(H, W, S, nh, nw);
     MVP_REQUIRE(nh >= 1 && nw >= 1 && nh <= S && nw <= S, "letterbox: bad size");
@@ -2140,6 +2150,13 @@ void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, con
     p.scale_y = 1.0 / ((double)nh / H);
     p.area2 = p.scale_x == 2.0 && p.scale_y == 2.0 && W == 2 * nw && H == 2 * nh;
     for (int c = 0; c < 3; c++) p.mean[c] = mean3[c], p.stdv[c] = std3[c];
+    return p;
+}
+}  // namespace
+
+void launch_det_letterbox(const uint8_t* frames, int n, int H, int W, int S, const float* mean3, const float* std3,
+                          void* out, hipStream_t s) {
+    const LbParams p = lb_params(frames, H, W, S, mean3, std3, out);
     if (n == 0) return;
     hipLaunchKernelGGL(letterbox_kernel, dim3((unsigned)((S * S + 255) / 256), (unsigned)n), dim3(256), 0, s, p);
     MVP_HIP(hipGetLastError());
@@ -2151,8 +2168,9 @@ void det_rescale_size(int H, int W, int S, int& nh, int& nw) {
     nw = (int)(W * sc + 0.5);
 }
 
-void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act,
-                     hipStream_t s) {
+namespace {
+void stem_launch(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act, hipStream_t s,
+                 const LbParams* lb) {
     MVP_REQUIRE(S % 16 == 0, "det stem: size %d must be a multiple of 16", S);
     const long n_tiles = (long)n * (S / 4);
     if (n_tiles == 0) return;
@@ -2164,8 +2182,24 @@ void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t
     }
     const size_t lds = (size_t)5 * (S + 2) * sizeof(uint2);
     const long grid = std::min<long>(n_tiles, (long)cus * 8);
-    hipLaunchKernelGGL(det_stem_kernel, dim3((unsigned)grid), dim3(256), lds, s, x, w, b, y, S, act, n_tiles);
+    if (lb)
+        hipLaunchKernelGGL(det_stem_kernel<true>, dim3((unsigned)grid), dim3(256), lds, s, x, w, b, y, S, act, n_tiles, *lb);
+    else
+        hipLaunchKernelGGL(det_stem_kernel<false>, dim3((unsigned)grid), dim3(256), lds, s, x, w, b, y, S, act, n_tiles,
+                           LbParams{});
     MVP_HIP(hipGetLastError());
+}
+}  // namespace
+
+void launch_det_stem(const uint16_t* x, const float* w, const float* b, uint16_t* y, int n, int S, int act,
+                     hipStream_t s) {
+    stem_launch(x, w, b, y, n, S, act, s, nullptr);
+}
+
+void launch_det_letterbox_stem(const uint8_t* frames, int H, int W, const float* mean3, const float* std3,
+                               const float* w, const float* b, uint16_t* y, int n, int S, int act, hipStream_t s) {
+    const LbParams lb = lb_params(frames, H, W, S, mean3, std3, nullptr);
+    stem_launch(nullptr, w, b, y, n, S, act, s, &lb);
 }
 
 void launch_det_dw5(const uint16_t* x, int xs, uint16_t* y, int ys, const float* w, const float* b, int n, int H, int W,

@@ -29,6 +29,7 @@ struct DetNet {
     // producer passes folded into their consumer 1x1 conv (det.h DetConvFold; plan_folds)
     std::vector<int> fold_src;  // per conv op: the DET_UP2 / DET_CA op folded into it, or -1
     std::vector<char> folded;   // per op: its pass runs inside its consumer (UP2: not launched; CA: no scale pass)
+    bool lb_folded = false;     // the letterbox runs inside op 0 (the stem stages its rows from the frames)
 };
 
 void free_det(DetNet& g) {
@@ -220,6 +221,18 @@ void plan_folds(DetNet& g) {
     const int no = (int)g.ops.size();
     g.fold_src.assign(no, -1);
     g.folded.assign(no, 0);
+    g.lb_folded = false;
+    {
+        const char* e = getenv("MVPOSE_DET_FOLD");
+        if (e && e[0] == '0') return;
+    }
+    // the letterbox into the stem: op 0 is the only reader of the letterboxed input
+    g.lb_folded = g.ops[0].kind == MVP_DET_STEM;
+    for (int k = 1; k < no; k++) {
+        const mvp_det_op& op = g.ops[k];
+        if (op.in.t == g.input || ((op.kind == MVP_DET_CONV || op.kind == MVP_DET_DWPW) && op.res.t == g.input))
+            g.lb_folded = false;
+    }
     auto reads = [&](const mvp_det_op& op, int t) {
         if (op.in.t == t) return true;
         return (op.kind == MVP_DET_CONV || op.kind == MVP_DET_DWPW) && op.res.t == t;
@@ -350,12 +363,18 @@ void run_ops(DetNet* g, const uint8_t* frames, int n, int h, int w, int begin, i
     auto T = [&](int t) -> const mvp_tensor_desc& { return g->tensors[t]; };
     static const float kMean[3] = {103.53f, 116.28f, 123.675f};
     static const float kStd[3] = {57.375f, 57.12f, 58.395f};
-    if (begin == 0) launch_det_letterbox(frames, n, h, w, g->size, kMean, kStd, base(g->input), s);
+    // the letterbox folded into the stem (plan_folds) unless the caller wants the letterboxed image
+    const bool lb_fused = begin == 0 && g->lb_folded && !letterboxed;
+    if (begin == 0 && !lb_fused) launch_det_letterbox(frames, n, h, w, g->size, kMean, kStd, base(g->input), s);
     for (int k = begin; k < end; k++) {
         const mvp_det_op& op = g->ops[k];
         switch (op.kind) {
             case MVP_DET_STEM:
-                launch_det_stem(vp(op.in), g->fb + op.w_off, g->fb + op.b_off, vp(op.out), n, g->size, op.act, s);
+                if (lb_fused && k == 0)
+                    launch_det_letterbox_stem(frames, h, w, kMean, kStd, g->fb + op.w_off, g->fb + op.b_off, vp(op.out), n,
+                                              g->size, op.act, s);
+                else
+                    launch_det_stem(vp(op.in), g->fb + op.w_off, g->fb + op.b_off, vp(op.out), n, g->size, op.act, s);
                 break;
             case MVP_DET_CONV: {
                 const mvp_tensor_desc& x = T(op.in.t);
@@ -462,6 +481,7 @@ extern "C" int mvp_det_folded_ops(void* handle, int* folded_out, int n_ops) {
     MVP_REQUIRE(g != nullptr && folded_out != nullptr, "mvp_det_folded_ops: NULL argument");
     MVP_REQUIRE(n_ops == (int)g->ops.size(), "mvp_det_folded_ops: %d ops, the graph has %zu", n_ops, g->ops.size());
     for (int k = 0; k < n_ops; k++) folded_out[k] = g->folded[k];
+    if (g->lb_folded && n_ops > 0) folded_out[0] = 2;
     MVP_ABI_END
 }
 

@@ -207,16 +207,18 @@ def test_persistent_1x1_bitwise(sd, size, n, pers, monkeypatch):
     assert torch.equal(ca.view(torch.int32), cb.view(torch.int32))
 
 
-@pytest.mark.parametrize("size,n", [(160, 3), (640, 2)])
-def test_folds_bitwise(sd, size, n, monkeypatch):
+@pytest.mark.parametrize("size,n,shape", [(160, 3, (180, 320)), (640, 2, (720, 1280)), (160, 2, (301, 499))])
+def test_folds_bitwise(sd, size, n, shape, monkeypatch):
     """The neck's nearest-2x upsamples and the CSP layers' channel-attention scale pass folded into
     their consumer 1x1 convs (det_conv1x1_pers_kernel FM 1 / 2: the pixel DMA reads the
     half-resolution source; the scales are applied to the landed pixels in LDS with
     ca_scale_kernel's f32 product and bf16 rounding) against the unfolded launches
     (MVPOSE_DET_FOLD=0): the output of every op, run from the start up to it, and the candidates
     are bit-identical.  And the folds happened: the upsample slices stay unwritten and the
-    attention tensors unscaled (160: 5x5 stride-32 planes, a 128-pixel tile over 7 frames)."""
-    frames = torch.from_numpy(_frames(n, size * 9 // 8, 2 * size, seed=31)).cuda()
+    attention tensors unscaled (160: 5x5 stride-32 planes, a 128-pixel tile over 7 frames).  The
+    letterbox is folded into the stem too (det_stem_kernel<true> stages its input rows from the
+    raw frames): 2x frames take the INTER_AREA fast path, 301 x 499 the bilinear one."""
+    frames = torch.from_numpy(_frames(n, *shape, seed=31)).cuda()
     dets = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("MVPOSE_DET_FOLD", mode)
@@ -227,7 +229,8 @@ def test_folds_bitwise(sd, size, n, monkeypatch):
     ca_ops = [k for k, op in enumerate(ops) if op.kind == D.DET_CA]
     assert len(up_ops) == 2 and len(ca_ops) == 4, (up_ops, ca_ops)
     f0, f1 = dets["0"].folded_ops(), dets["1"].folded_ops()
-    assert not any(f0) and [k for k, f in enumerate(f1) if f] == sorted(up_ops + ca_ops), f1
+    assert not any(f0) and [k for k, f in enumerate(f1) if f] == sorted([0] + up_ops + ca_ops), f1
+    assert f1[0] == 2 and ops[0].kind == D.DET_STEM  # the letterbox inside the stem
 
     def view(det, v):
         return det.tensor(v.t, n)[..., v.coff:v.coff + v.c].cpu()
