@@ -1126,8 +1126,6 @@ __global__ __launch_bounds__(512, 1) void det_conv_halo_pers_kernel(GParams p) {
         bb[c] = *reinterpret_cast<const f32x4*>(p.bias + c * 16 + kg * 4);
         asm volatile("" : "+v"(bb[c]));
     }
-    // this wave's halo DMA rounds (r = wave + NWV j < B_R64)
-    const int ops = (G::B_R64 - wave + NWV - 1) / NWV;
     auto tile_of = [&](long t, int& n, int& ho0, int& wo0) {
         const long lt = x0 + loc + t * gx;
         n = (int)(lt / per);

@@ -180,6 +180,8 @@ void plan(DetNet& g) {
             op.kind == MVP_DET_DWPW)
             touch(op.out.t, k);
         if (op.kind == MVP_DET_CONV || op.kind == MVP_DET_DWPW) touch(op.res.t, k);
+        // a fold's consumer reads its producer's input in its own launch (plan_folds runs first)
+        if (!g.fold_src.empty() && g.fold_src[k] >= 0) touch(g.ops[g.fold_src[k]].in.t, k);
     }
     std::vector<int> order;
     for (int t = 0; t < nt; t++)
@@ -311,8 +313,8 @@ extern "C" int mvp_det_create(const mvp_tensor_desc* tensors, int n_tensors, con
         g->wb = w_dev;
         g->fb = f_dev;
         mvp::validate(*g, w_elems, f_elems);
-        mvp::plan(*g);
         mvp::plan_folds(*g);
+        mvp::plan(*g);
         hipError_t e = hipMalloc(&g->arena, g->arena_bytes);
         if (e != hipSuccess)
             mvp::fail(MVP_ERR_NOMEM, "mvp_det_create: arena of %lld bytes: %s", (long long)g->arena_bytes,
