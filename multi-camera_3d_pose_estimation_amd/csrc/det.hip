@@ -1559,50 +1559,53 @@ __global__ __launch_bounds__(256) void ca_scale_kernel(uint16_t* x, const float*
 
 // ------------------------------------------------------------------ SPP max pools
 // maxpool 9 = maxpool 5 twice, 13 = three times (stride 1, -inf padding: exact), so one
-// workgroup per (image, 8-channel group) keeps the plane in LDS and applies the 5x5 max
-// three times, writing each result into its slice.
+// workgroup per (image, G 8-channel groups) keeps the plane in LDS and applies the 5x5 max three
+// times, writing each result into its slice.  The 5x5 max is a 5-wide row max, then a 5-tall
+// column max of those (max is exact and order-free; every value is bf16, so the packed row
+// maxima are exact too); the column max overwrites the plane it started from (the row maxima
+// are a plane of their own).  G = 4 (round 6): a thread item is one 16-B chunk of a pixel, so a
+// pixel's 64 B load and store coalesce and each phase has 6 items per thread instead of 1.6
+// (one 8-channel group per workgroup ran 515 us for the 20x20 x 384 SPP of 512 frames).
+template <int G>
 __global__ __launch_bounds__(256) void spp_kernel(uint16_t* buf, int H, int W, int C, int xs) {
-    extern __shared__ uint4 pl[];  // three planes [H*W] of 8 channels: input, row maxima, output
-    const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, HW = H * W;
-    uint16_t* base = buf + (size_t)n * HW * xs + cg * 8;
+    extern __shared__ uint4 pl[];  // two planes [H*W][G]: the pooled input, its row maxima
+    const int cg = blockIdx.x, n = blockIdx.y, tid = threadIdx.x, HW = H * W, NI = HW * G;
+    uint16_t* base = buf + (size_t)n * HW * xs + cg * 8 * G;
     uint4* a = pl;
-    uint4* r = pl + HW;
-    uint4* b = pl + 2 * HW;
-    for (int i = tid; i < HW; i += 256) a[i] = *reinterpret_cast<const uint4*>(base + (size_t)i * xs);
-    // the 5x5 max as a 5-wide row max, then a 5-tall column max of those (max is exact and
-    // order-free; every value is bf16, so the packed row maxima are exact too)
+    uint4* r = pl + NI;
+    for (int i = tid; i < NI; i += 256) {
+        const int px = i / G, g = i - px * G;
+        a[i] = *reinterpret_cast<const uint4*>(base + (size_t)px * xs + g * 8);
+    }
     for (int k = 1; k <= 3; k++) {
         __syncthreads();
-        for (int i = tid; i < HW; i += 256) {
-            const int y = i / W, x = i - y * W;
+        for (int i = tid; i < NI; i += 256) {
+            const int px = i / G, g = i - px * G, y = px / W, x = px - y * W;
             float m[8];
             for (int c = 0; c < 8; c++) m[c] = -__builtin_inff();
             for (int xx = max(x - 2, 0); xx <= min(x + 2, W - 1); xx++) {
                 float v[8];
-                unpack8(a[y * W + xx], v);
+                unpack8(a[(y * W + xx) * G + g], v);
 #pragma unroll
                 for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
             }
             r[i] = pack8(m);
         }
         __syncthreads();
-        for (int i = tid; i < HW; i += 256) {
-            const int y = i / W, x = i - y * W;
+        for (int i = tid; i < NI; i += 256) {
+            const int px = i / G, g = i - px * G, y = px / W, x = px - y * W;
             float m[8];
             for (int c = 0; c < 8; c++) m[c] = -__builtin_inff();
             for (int yy = max(y - 2, 0); yy <= min(y + 2, H - 1); yy++) {
                 float v[8];
-                unpack8(r[yy * W + x], v);
+                unpack8(r[(yy * W + x) * G + g], v);
 #pragma unroll
                 for (int c = 0; c < 8; c++) m[c] = fmaxf(m[c], v[c]);
             }
             const uint4 o = pack8(m);
-            b[i] = o;
-            *reinterpret_cast<uint4*>(base + (size_t)i * xs + k * C) = o;
+            a[i] = o;
+            *reinterpret_cast<uint4*>(base + (size_t)px * xs + k * C + g * 8) = o;
         }
-        uint4* t = a;
-        a = b;
-        b = t;
     }
 }
 
@@ -2549,12 +2552,17 @@ void launch_det_ca(uint16_t* x, int xs, int n, int HW, int C, const float* wt, c
 
 void launch_det_spp(uint16_t* buf, int xs, int n, int H, int W, int C, hipStream_t s) {
     MVP_REQUIRE(C % 8 == 0 && xs >= 4 * C && xs % 8 == 0, "spp: C=%d stride=%d", C, xs);
-    // three 16-B planes of the SPP input in LDS: H * W <= 1365 (the stride-32 plane of a detector
-    // input up to 1,184 x 1,184; 20 x 20 = 400 at the model's 640)
-    const size_t lds = (size_t)3 * H * W * sizeof(uint4);
-    MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large (H * W <= 1365)", H, W);
+    // two planes of G 16-B chunks per pixel in LDS: with G = 4, H * W <= 1024 (20 x 20 = 400 at the
+    // model's 640; 1,024 = the stride-32 plane of a 1,024 x 1,024 input); larger planes or
+    // channel counts not a multiple of 32 take G = 1 (H * W <= 2048)
+    const int G = (C % 32 == 0 && H * W <= 1024) ? 4 : 1;
+    const size_t lds = (size_t)2 * H * W * G * sizeof(uint4);
+    MVP_REQUIRE(lds <= 64 * 1024, "spp: %dx%d plane too large (H * W <= 2048)", H, W);
     if (n == 0) return;
-    hipLaunchKernelGGL(spp_kernel, dim3((unsigned)(C / 8), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
+    if (G == 4)
+        hipLaunchKernelGGL(spp_kernel<4>, dim3((unsigned)(C / 32), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
+    else
+        hipLaunchKernelGGL(spp_kernel<1>, dim3((unsigned)(C / 8), (unsigned)n), dim3(256), lds, s, buf, H, W, C, xs);
     MVP_HIP(hipGetLastError());
 }
 
