@@ -548,6 +548,10 @@ class RTMDetector:
                     or not best_out.is_cuda):
                 raise ValueError(f"best_out must be a contiguous float32 ({n}, 6) CUDA tensor")
             best = best_out
+        if letterboxed is not None and (letterboxed.dtype != torch.bfloat16 or not letterboxed.is_cuda or
+                                        not letterboxed.is_contiguous() or
+                                        tuple(letterboxed.shape) != (n, self.size, self.size, 4)):
+            raise ValueError(f"letterboxed must be a contiguous bfloat16 ({n}, {self.size}, {self.size}, 4) CUDA tensor")
         lb = ctypes.c_void_p(letterboxed.data_ptr()) if letterboxed is not None else None
         call("mvp_det_forward", self._h, ctypes.c_void_p(frames.data_ptr()), n, h, w,
              ctypes.c_float(self.cfg["score_thr"]), ctypes.c_void_p(cand.data_ptr()),

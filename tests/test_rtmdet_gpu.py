@@ -261,8 +261,18 @@ def test_folds_bitwise(sd, size, n, shape, monkeypatch):
         assert torch.equal(a0.view(torch.int16), a1.view(torch.int16)), (size, k, spec.names[k])
     r0, r1 = dets["0"].detect(frames), dets["1"].detect(frames)
     torch.cuda.synchronize()
-    assert torch.equal(r0["cand"].cpu().view(torch.int32), r1["cand"].cpu().view(torch.int32))
-    assert torch.equal(r0["best"].cpu().view(torch.int32), r1["best"].cpu().view(torch.int32))
+    c0, b0 = r0["cand"].cpu(), r0["best"].cpu()
+    assert torch.equal(c0.view(torch.int32), r1["cand"].cpu().view(torch.int32))
+    assert torch.equal(b0.view(torch.int32), r1["best"].cpu().view(torch.int32))
+    # asked for the letterboxed image, the folded graph letterboxes apart (the stem reads it back)
+    dets["0"].run_ops(frames, 0, 1)  # the unfolded letterbox (+ the stem, which does not write its input)
+    torch.cuda.synchronize()
+    img0 = dets["0"].tensor(ops[0].in_.t, n).cpu()
+    lb = torch.empty((n, size, size, 4), dtype=torch.bfloat16, device="cuda")
+    r1b = dets["1"].detect(frames, letterboxed=lb)
+    torch.cuda.synchronize()
+    assert torch.equal(lb.cpu().view(torch.int16), img0.view(torch.int16))
+    assert torch.equal(c0.view(torch.int32), r1b["cand"].cpu().view(torch.int32))
     for d in dets.values():
         d.close()
 
