@@ -73,6 +73,14 @@ __device__ __forceinline__ void lin_coef(int d, double scale, int n_src, int& s0
     s1 = min(sx + 1, n_src - 1);
 }
 
+// normalised bf16 channels of a letterboxed u8 pixel (+ a zero 4th)
+__device__ __forceinline__ uint2 lb_pack(const LbParams& p, const int* v) {
+    float o[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) o[c] = ((float)v[c] - p.mean[c]) / p.stdv[c];
+    return uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
+}
+
 // letterboxed pixel (y, x) of frame n: 3 normalised bf16 channels + a zero 4th
 __device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x) {
     int v[3] = {114, 114, 114};
@@ -98,10 +106,32 @@ __device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x
             }
         }
     }
-    float o[3];
+    return lb_pack(p, v);
+}
+
+// letterboxed pixels (y, x) and (y, x + 1), x even, of frame n on the INTER_AREA fast path (the
+// stem's staging, round 6): their 2 x 2 source blocks are 12 contiguous bytes per source row,
+// read as 3 dwords instead of 12 bytes each (needs the row start 4-byte aligned: W % 4 == 0);
+// the same integer arithmetic as lb_pixel
+__device__ __forceinline__ void lb_pair(const LbParams& p, int n, int y, int x, uint2& o0, uint2& o1) {
+    if (!p.area2 || (p.W & 3) || y >= p.nh || x + 1 >= p.nw) {
+        o0 = lb_pixel(p, n, y, x);
+        o1 = lb_pixel(p, n, y, x + 1);
+        return;
+    }
+    const uint8_t* r0 = p.f + ((size_t)n * p.H * p.W + (size_t)(2 * y) * p.W + 2 * x) * 3;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(r0);
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(r0 + (size_t)p.W * 3);
+    const uint32_t a[3] = {w0[0], w0[1], w0[2]}, b[3] = {w1[0], w1[1], w1[2]};
+    auto byte = [](const uint32_t* w, int i) { return (int)((w[i >> 2] >> ((i & 3) * 8)) & 0xff); };
+    int v0[3], v1[3];
 #pragma unroll
-    for (int c = 0; c < 3; c++) o[c] = ((float)v[c] - p.mean[c]) / p.stdv[c];
-    return uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
+    for (int c = 0; c < 3; c++) {
+        v0[c] = (byte(a, c) + byte(a, 3 + c) + byte(b, c) + byte(b, 3 + c) + 2) >> 2;
+        v1[c] = (byte(a, 6 + c) + byte(a, 9 + c) + byte(b, 6 + c) + byte(b, 9 + c) + 2) >> 2;
+    }
+    o0 = lb_pack(p, v0);
+    o1 = lb_pack(p, v1);
 }
 
 __global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
@@ -149,12 +179,25 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restric
         const int ho0 = (int)(t - n * tiles) * 2;
         const uint2* xin = reinterpret_cast<const uint2*>(x) + (size_t)n * S * S;
         __syncthreads();
-        for (int i = tid; i < 5 * LW; i += 256) {
-            const int r = i / LW, c = i - r * LW;
-            const int hi = 2 * ho0 - 1 + r, wi = c - 1;
-            const bool in = hi >= 0 && hi < S && wi >= 0 && wi < S;
-            if constexpr (LB) sx[i] = in ? lb_pixel(lb, (int)n, hi, wi) : uint2{0u, 0u};
-            else sx[i] = in ? xin[(size_t)hi * S + wi] : uint2{0u, 0u};
+        if constexpr (LB) {
+            // pixel pairs (wi, wi + 1), wi even, of the five rows; the zero border columns apart
+            const int PR = S / 2;
+            for (int i = tid; i < 5 * PR; i += 256) {
+                const int r = i / PR, wi = 2 * (i - r * PR);
+                const int hi = 2 * ho0 - 1 + r;
+                uint2 o0 = {0u, 0u}, o1 = {0u, 0u};
+                if (hi >= 0 && hi < S) lb_pair(lb, (int)n, hi, wi, o0, o1);
+                sx[r * LW + wi + 1] = o0;
+                sx[r * LW + wi + 2] = o1;
+            }
+            if (tid < 10) sx[(tid >> 1) * LW + (tid & 1) * (LW - 1)] = uint2{0u, 0u};
+        } else {
+            for (int i = tid; i < 5 * LW; i += 256) {
+                const int r = i / LW, c = i - r * LW;
+                const int hi = 2 * ho0 - 1 + r, wi = c - 1;
+                const bool in = hi >= 0 && hi < S && wi >= 0 && wi < S;
+                sx[i] = in ? xin[(size_t)hi * S + wi] : uint2{0u, 0u};
+            }
         }
         __syncthreads();
         for (int pt = wave; pt < n_pt; pt += 4) {
