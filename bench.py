@@ -71,7 +71,7 @@ def spawn_ranks(n):
 
 # The committed PMC traffic pass the roofline lines cite (tools/pmc_traffic.py): named explicitly —
 # a newest-file rule picked r04zz_ over r04zz2_ by lexicographic order in round 4.
-TRAFFIC_FILE = "profiles/r06s_traffic.json"
+TRAFFIC_FILE = "profiles/r06u_traffic.json"
 # per-kernel-family breakdown of one 1,024-crop forward (tools/fwd_breakdown.sh: a kernel trace of
 # backbone forwards only, paired with the graph's launch plan for each launch's MACs)
 BREAKDOWN_FILE = "profiles/r06a_forward_breakdown.json"
