@@ -57,14 +57,35 @@ __global__ __launch_bounds__(kBlock) void preprocess_kernel(PreParams p) {
     const int w[4] = {(32 - ty) * (32 - tx) * 32, (32 - ty) * tx * 32, ty * (32 - tx) * 32, ty * tx * 32};
     int acc[3] = {0, 0, 0};
     const uint8_t* img = p.frames + (size_t)n * p.H * p.W * 3;
+    // each source row's two pixels are 6 contiguous bytes: away from the right edge (and with
+    // 4-byte-aligned rows) 3 dword loads and two byte alignments instead of 6 byte loads (round 6);
+    // the integer sums are exact, so the order of the terms does not matter
+    const bool fast = (p.W & 3) == 0 && sx >= 0 && sx + 3 < p.W;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int xx = sx + (q & 1), yy = sy + (q >> 1);
-        if (xx >= 0 && xx < p.W && yy >= 0 && yy < p.H) {
-            const uint8_t* px = img + ((size_t)yy * p.W + xx) * 3;
-            acc[0] += px[0] * w[q];
-            acc[1] += px[1] * w[q];
-            acc[2] += px[2] * w[q];
+    for (int r = 0; r < 2; r++) {
+        const int yy = sy + r;
+        if (yy < 0 || yy >= p.H) continue;
+        const uint8_t* row = img + (size_t)yy * p.W * 3;
+        if (fast) {
+            const int b0 = 3 * sx, sh = b0 & 3;
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(row + (b0 & ~3));
+            const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+            const uint32_t d0 = __builtin_amdgcn_alignbyte(w1, w0, sh), d1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            const int wl = w[2 * r], wr = w[2 * r + 1];
+            acc[0] += (int)(d0 & 0xff) * wl + (int)((d0 >> 24) & 0xff) * wr;
+            acc[1] += (int)((d0 >> 8) & 0xff) * wl + (int)(d1 & 0xff) * wr;
+            acc[2] += (int)((d0 >> 16) & 0xff) * wl + (int)((d1 >> 8) & 0xff) * wr;
+            continue;
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int xx = sx + h;
+            if (xx >= 0 && xx < p.W) {
+                const uint8_t* px = row + (size_t)xx * 3;
+                acc[0] += px[0] * w[2 * r + h];
+                acc[1] += px[1] * w[2 * r + h];
+                acc[2] += px[2] * w[2 * r + h];
+            }
         }
     }
     float v[3];
