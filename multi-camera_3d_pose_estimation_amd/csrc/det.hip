@@ -81,9 +81,9 @@ __device__ __forceinline__ uint2 lb_pack(const LbParams& p, const int* v) {
     return uint2{tobf(o[0]) | (tobf(o[1]) << 16), tobf(o[2])};
 }
 
-// letterboxed pixel (y, x) of frame n: 3 normalised bf16 channels + a zero 4th
-__device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x) {
-    int v[3] = {114, 114, 114};
+// the u8 channels of letterboxed pixel (y, x) of frame n (114 in the padding)
+__device__ __forceinline__ void lb_u8(const LbParams& p, int n, int y, int x, int* v) {
+    v[0] = v[1] = v[2] = 114;
     const uint8_t* fr = p.f + (size_t)n * p.H * p.W * 3;
     if (y < p.nh && x < p.nw) {
         if (p.area2) {
@@ -106,17 +106,33 @@ __device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x
             }
         }
     }
+}
+
+// letterboxed pixel (y, x) of frame n: 3 normalised bf16 channels + a zero 4th
+__device__ __forceinline__ uint2 lb_pixel(const LbParams& p, int n, int y, int x) {
+    int v[3];
+    lb_u8(p, n, y, x, v);
     return lb_pack(p, v);
+}
+
+// lb_pack through a table of the 3 x 256 normalised values (the stem's staging: the same
+// division, done once per value instead of three times per pixel)
+__device__ __forceinline__ uint2 lb_pack_lut(const uint16_t* lut, const int* v) {
+    return uint2{(uint32_t)lut[v[0]] | ((uint32_t)lut[256 + v[1]] << 16), (uint32_t)lut[512 + v[2]]};
 }
 
 // letterboxed pixels (y, x) and (y, x + 1), x even, of frame n on the INTER_AREA fast path (the
 // stem's staging, round 6): their 2 x 2 source blocks are 12 contiguous bytes per source row,
 // read as 3 dwords instead of 12 bytes each (needs the row start 4-byte aligned: W % 4 == 0);
 // the same integer arithmetic as lb_pixel
-__device__ __forceinline__ void lb_pair(const LbParams& p, int n, int y, int x, uint2& o0, uint2& o1) {
+__device__ __forceinline__ void lb_pair(const LbParams& p, int n, int y, int x, uint2& o0, uint2& o1,
+                                        const uint16_t* lut) {
     if (!p.area2 || (p.W & 3) || y >= p.nh || x + 1 >= p.nw) {
-        o0 = lb_pixel(p, n, y, x);
-        o1 = lb_pixel(p, n, y, x + 1);
+        int v0[3], v1[3];
+        lb_u8(p, n, y, x, v0);
+        lb_u8(p, n, y, x + 1, v1);
+        o0 = lb_pack_lut(lut, v0);
+        o1 = lb_pack_lut(lut, v1);
         return;
     }
     const uint8_t* r0 = p.f + ((size_t)n * p.H * p.W + (size_t)(2 * y) * p.W + 2 * x) * 3;
@@ -130,8 +146,8 @@ __device__ __forceinline__ void lb_pair(const LbParams& p, int n, int y, int x, 
         v0[c] = (byte(a, c) + byte(a, 3 + c) + byte(b, c) + byte(b, 3 + c) + 2) >> 2;
         v1[c] = (byte(a, 6 + c) + byte(a, 9 + c) + byte(b, 6 + c) + byte(b, 9 + c) + 2) >> 2;
     }
-    o0 = lb_pack(p, v0);
-    o1 = lb_pack(p, v1);
+    o0 = lb_pack_lut(lut, v0);
+    o1 = lb_pack_lut(lut, v1);
 }
 
 __global__ __launch_bounds__(256) void letterbox_kernel(LbParams p) {
@@ -156,8 +172,14 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restric
                                                        const float* __restrict__ bias, uint16_t* __restrict__ y,
                                                        int S, int act, long n_tiles, LbParams lb) {
     extern __shared__ uint2 sx[];  // [5][S + 2]
+    __shared__ uint16_t lut[LB ? 3 * 256 : 1];  // LB: the normalised bf16 of every u8 value
     const int Wo = S / 2, LW = S + 2;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+    if constexpr (LB)
+        for (int i = tid; i < 3 * 256; i += 256) {
+            const int c = i >> 8;
+            lut[i] = (uint16_t)tobf(((float)(i & 255) - lb.mean[c]) / lb.stdv[c]);
+        }
     bf16x8 afr[2][2];
     float4 b4[2];
 #pragma unroll
@@ -186,7 +208,7 @@ __global__ __launch_bounds__(256) void det_stem_kernel(const uint16_t* __restric
                 const int r = i / PR, wi = 2 * (i - r * PR);
                 const int hi = 2 * ho0 - 1 + r;
                 uint2 o0 = {0u, 0u}, o1 = {0u, 0u};
-                if (hi >= 0 && hi < S) lb_pair(lb, (int)n, hi, wi, o0, o1);
+                if (hi >= 0 && hi < S) lb_pair(lb, (int)n, hi, wi, o0, o1, lut);
                 sx[r * LW + wi + 1] = o0;
                 sx[r * LW + wi + 2] = o1;
             }
